@@ -1,0 +1,677 @@
+// ark_ddgi.cpp — the C-ABI context of the MI355X DDGI path (include/ark_ddgi.h).
+//
+// Owns all device memory of one DDGI node instance on one GPU: the persistent
+// atlases/offsets (the DDGISamplingSet, DDGINode.cpp:101-105), the per-update
+// working set (slot table, hit records, surfels) and the scene (BVH + RT mesh
+// data + materials + lights). Every update is enqueued on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ark_ddgi.h"
+#include "../../include/ark_ddgi_debug.h"
+#include "ark_fmath.h"
+#include "bvh_builder.h"
+#include "ddgi_kernels.h"
+
+using namespace ark;
+
+namespace {
+
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t alloc(size_t n)
+    {
+        release();
+        bytes = n;
+        if (n == 0) return hipSuccess;
+        return hipMalloc(&ptr, n);
+    }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template<typename T> T* as() const { return static_cast<T*>(ptr); }
+};
+
+uint16_t f32_to_f16_host(float f)
+{
+    // host-side RNE conversion for the clear values (matches v_cvt_f16_f32)
+    _Float16 h = static_cast<_Float16>(f);
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+}
+
+} // namespace
+
+struct ArkDdgiCtx {
+    ArkDdgiDesc desc {};
+    std::string lastError;
+    hipStream_t stream = nullptr;
+    int device = 0;
+    int cuCount = 0;
+    int X = 0, Y = 0, Z = 0, N = 0;
+    int Wi = 0, Hi = 0, Wv = 0, Hv = 0;
+    int Kmax = 0, Rmax = 0;
+    int slabZ0 = 0, slabZ1 = 0;
+    // persistent resources
+    DeviceBuffer irr, vis, offsets;
+    // working set
+    DeviceBuffer slots, fib, hits, surfels, spill, rayCounter, counters;
+    uint32_t spillEntries = 0;
+    uint32_t traceBlocks = 0, shadeBlocks = 0;
+    // scene
+    bool hasScene = false;
+    DeviceBuffer nodes, tris, indices, vertices, meshes, materials, instances, texInfos, texels, spots;
+    SceneArgs scene {};
+    ArkDdgiBvhStats bvhStats {};
+    uint32_t bvhMaxDepth = 0;
+    // instrumentation
+    bool counting = false;
+    bool timing = false;
+    hipEvent_t ev[6] = {};
+    float lastMs[5] = {};
+    bool timingValid = false;
+    ArkDdgiCounters lastCounters {};
+    bool countersPending = false;
+    uint64_t lastRays = 0, lastProbes = 0;
+
+    int fail(int code, const char* fmt, ...)
+    {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        std::vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        lastError = buf;
+        return code;
+    }
+    int hipFail(hipError_t e, const char* what)
+    {
+        return fail(ARK_DDGI_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+#define ARK_HIP(expr)                                                   \
+    do {                                                                \
+        hipError_t _e = (expr);                                         \
+        if (_e != hipSuccess) return ctx->hipFail(_e, #expr);           \
+    } while (0)
+
+namespace {
+
+int clearHistory(ArkDdgiCtx* ctx)
+{
+    // DDGINode.cpp:89-94: irradiance cleared to 0, visibility to (zFar, zFar^2) in RG16F;
+    // zFar^2 = 1e8 overflows fp16: +inf by RNE, or 65504 if saturating.
+    uint16_t zf = f32_to_f16_host(ctx->desc.z_far);
+    uint16_t zf2 = f32_to_f16_host(ctx->desc.z_far * ctx->desc.z_far);
+    if (ctx->desc.clear_overflow_mode == ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE) {
+        if ((zf & 0x7fffu) == 0x7c00u) zf = static_cast<uint16_t>((zf & 0x8000u) | 0x7bffu);
+        if ((zf2 & 0x7fffu) == 0x7c00u) zf2 = static_cast<uint16_t>((zf2 & 0x8000u) | 0x7bffu);
+    }
+    ARK_HIP(hipMemsetAsync(ctx->irr.ptr, 0, ctx->irr.bytes, ctx->stream));
+    ARK_HIP(launch_fill_u32(ctx->vis.ptr, ctx->vis.bytes / 4, static_cast<uint32_t>(zf) | (static_cast<uint32_t>(zf2) << 16), ctx->stream));
+    ARK_HIP(hipMemsetAsync(ctx->offsets.ptr, 0, ctx->offsets.bytes, ctx->stream));
+    ARK_HIP(hipMemsetAsync(ctx->surfels.ptr, 0, ctx->surfels.bytes, ctx->stream));
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    return ARK_DDGI_OK;
+}
+
+int ensureSpill(ArkDdgiCtx* ctx)
+{
+    uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
+    uint32_t threads = std::max(ctx->traceBlocks * kTraceBlock, ctx->shadeBlocks * kShadeBlock);
+    size_t bytes = static_cast<size_t>(need) * threads * sizeof(int32_t);
+    if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
+    ARK_HIP(ctx->spill.alloc(bytes));
+    ctx->spillEntries = need;
+    return ARK_DDGI_OK;
+}
+
+template<typename T>
+int upload(ArkDdgiCtx* ctx, DeviceBuffer& buf, const T* data, size_t count)
+{
+    size_t bytes = count * sizeof(T);
+    ARK_HIP(buf.alloc(std::max<size_t>(bytes, 16)));
+    if (bytes) ARK_HIP(hipMemcpy(buf.ptr, data, bytes, hipMemcpyHostToDevice));
+    return ARK_DDGI_OK;
+}
+
+// sRGB EOTF applied per texel before filtering (Vulkan sRGB formats).
+float srgbToLinear(float c)
+{
+    return c <= 0.04045f ? c / 12.92f : powf_((c + 0.055f) / 1.055f, 2.4f);
+}
+
+} // namespace
+
+extern "C" {
+
+int32_t ark_ddgi_abi_version(void) { return ARK_DDGI_ABI_VERSION; }
+
+int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
+{
+    if (!desc || !outCtx || desc->struct_size != sizeof(ArkDdgiDesc)) return ARK_DDGI_E_INVALID_ARGUMENT;
+    *outCtx = nullptr;
+    if (desc->grid_dims[0] <= 0 || desc->grid_dims[1] <= 0 || desc->grid_dims[2] <= 0) return ARK_DDGI_E_NO_PROBE_GRID;
+    auto* ctx = new ArkDdgiCtx();
+    ctx->desc = *desc;
+    ctx->X = desc->grid_dims[0];
+    ctx->Y = desc->grid_dims[1];
+    ctx->Z = desc->grid_dims[2];
+    ctx->N = ctx->X * ctx->Y * ctx->Z;
+    ctx->Rmax = desc->max_rays_per_probe > 0 ? desc->max_rays_per_probe : ARK_DDGI_MAX_RAYS_PER_PROBE;
+    ctx->Kmax = desc->max_probe_updates > 0 ? desc->max_probe_updates : ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES;
+    const int shards = desc->shard_count > 0 ? desc->shard_count : 1;
+    if (ctx->Rmax > ARK_DDGI_MAX_RAYS_PER_PROBE || ctx->Z % shards != 0 || desc->shard_rank < 0 || desc->shard_rank >= shards) {
+        delete ctx;
+        return ARK_DDGI_E_INVALID_ARGUMENT;
+    }
+    ctx->desc.shard_count = shards;
+    ctx->slabZ0 = desc->shard_rank * (ctx->Z / shards);
+    ctx->slabZ1 = ctx->slabZ0 + ctx->Z / shards;
+    const int si = ARK_DDGI_IRRADIANCE_RES + 2 * ARK_DDGI_ATLAS_PADDING;
+    const int sv = ARK_DDGI_VISIBILITY_RES + 2 * ARK_DDGI_ATLAS_PADDING;
+    ctx->Wi = ctx->X * si * ctx->Y;
+    ctx->Hi = ctx->Z * si;
+    ctx->Wv = ctx->X * sv * ctx->Y;
+    ctx->Hv = ctx->Z * sv;
+    auto bad = [&](hipError_t e, const char* what) {
+        std::fprintf(stderr, "ark_ddgi_create: %s: %s\n", what, hipGetErrorString(e));
+        delete ctx;
+        return ARK_DDGI_E_DEVICE;
+    };
+    hipError_t e = hipSetDevice(desc->device);
+    if (e != hipSuccess) return bad(e, "hipSetDevice");
+    ctx->device = desc->device;
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, desc->device);
+    if (e != hipSuccess) return bad(e, "hipGetDeviceProperties");
+    ctx->cuCount = prop.multiProcessorCount;
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (auto& ev : ctx->ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
+    const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
+    if ((e = ctx->irr.alloc(static_cast<size_t>(ctx->Wi) * ctx->Hi * 8)) != hipSuccess) return bad(e, "alloc irradiance");
+    if ((e = ctx->vis.alloc(static_cast<size_t>(ctx->Wv) * ctx->Hv * 4)) != hipSuccess) return bad(e, "alloc visibility");
+    if ((e = ctx->offsets.alloc(static_cast<size_t>(ctx->N) * 16)) != hipSuccess) return bad(e, "alloc offsets");
+    if ((e = ctx->slots.alloc(K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
+    if ((e = ctx->fib.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib");
+    if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
+    if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
+    if ((e = ctx->rayCounter.alloc(256)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
+    // persistent grids: as many workgroups as are co-resident
+    int occT = 0, occS = 0;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_primary_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occS, kernel_shade_ptr(false), kShadeBlock, 0)) != hipSuccess) return bad(e, "occupancy shade");
+    ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
+    ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
+    if (clearHistory(ctx) != ARK_DDGI_OK) {
+        std::fprintf(stderr, "ark_ddgi_create: %s\n", ctx->lastError.c_str());
+        delete ctx;
+        return ARK_DDGI_E_DEVICE;
+    }
+    *outCtx = ctx;
+    return ARK_DDGI_OK;
+}
+
+void ark_ddgi_destroy(ArkDdgiCtx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter,
+                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
+                             &ctx->texInfos, &ctx->texels, &ctx->spots })
+        b->release();
+    for (auto& ev : ctx->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx) { return ctx ? ctx->lastError.c_str() : "null context"; }
+
+int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!s || s->struct_size != sizeof(ArkDdgiScene)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiScene");
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    // validate
+    for (uint32_t i = 0; i < s->instance_count; ++i) {
+        const ArkRTInstance& inst = s->instances[i];
+        if (inst.rt_mesh_index >= s->mesh_count) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "instance %u: rt_mesh_index out of range", i);
+        const ArkRTTriangleMesh& m = s->meshes[inst.rt_mesh_index];
+        if (m.material_index < 0 || static_cast<uint32_t>(m.material_index) >= s->material_count)
+            return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "mesh %u: material_index out of range", inst.rt_mesh_index);
+        if (static_cast<uint64_t>(m.first_index) + 3ull * inst.triangle_count > s->index_count)
+            return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "instance %u: indices out of range", i);
+    }
+    // World-space triangles per hit-mask class (GpuScene.cpp:883-929: one TLAS
+    // instance per mesh segment; flattened here into one BVH per class).
+    std::vector<BuildTriangle> cls[3];
+    std::vector<GpuInstance> ginst(s->instance_count);
+    for (uint32_t ii = 0; ii < s->instance_count; ++ii) {
+        const ArkRTInstance& inst = s->instances[ii];
+        const ArkRTTriangleMesh& m = s->meshes[inst.rt_mesh_index];
+        const float* M = inst.object_to_world;
+        const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
+        GpuInstance& g = ginst[ii];
+        std::memset(&g, 0, sizeof(g));
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) g.normal_matrix[r * 4 + c] = M[r * 4 + c];
+        g.rt_mesh_index = static_cast<int32_t>(inst.rt_mesh_index);
+        g.flip_facing = det < 0.0f ? 1 : 0;
+        g.hit_mask = static_cast<int32_t>(inst.hit_mask);
+        const int c = (inst.hit_mask & ARK_RT_HIT_MASK_OPAQUE) ? 0 : (inst.hit_mask & ARK_RT_HIT_MASK_MASKED) ? 1 : 2;
+        for (uint32_t p = 0; p < inst.triangle_count; ++p) {
+            BuildTriangle t;
+            float* w[3] = { t.v0, t.v1, t.v2 };
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t idx = s->indices[static_cast<size_t>(m.first_index) + 3u * p + k];
+                const uint64_t vi = static_cast<uint64_t>(m.first_vertex) + idx;
+                if (vi >= s->vertex_count) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "instance %u prim %u: vertex out of range", ii, p);
+                const float* P = &s->positions[vi * 3];
+                w[k][0] = M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3];
+                w[k][1] = M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7];
+                w[k][2] = M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11];
+            }
+            t.instance = ii;
+            t.primitive = p;
+            cls[c].push_back(t);
+        }
+    }
+    BvhBuildOptions opt;
+    std::vector<GpuBvhNode> allNodes;
+    std::vector<GpuTriangle> allTris;
+    int32_t roots[3] = { -1, -1, -1 };
+    uint32_t maxDepth = 0, maxLeaf = 0;
+    float sah = 0.0f;
+    for (int c = 0; c < 3; ++c) {
+        if (cls[c].empty()) continue;
+        BvhBuildResult r = build_bvh(cls[c], opt, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()));
+        roots[c] = static_cast<int32_t>(allNodes.size());
+        if (c == 0) sah = r.sah_cost;
+        maxDepth = std::max(maxDepth, r.max_depth);
+        maxLeaf = std::max(maxLeaf, r.max_leaf);
+        allNodes.insert(allNodes.end(), r.nodes.begin(), r.nodes.end());
+        allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
+        std::vector<BuildTriangle>().swap(cls[c]);
+    }
+    if (allTris.size() >= (1ull << (31 - kLeafCountBits))) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "too many triangles for the leaf encoding");
+    // Structural check before anything reaches the GPU: every node is referenced
+    // at most once from a root-reachable parent (no cycles, no sharing), every
+    // leaf range lies inside the triangle array and every triangle is covered once.
+    {
+        std::vector<uint8_t> seenNode(allNodes.size(), 0);
+        std::vector<uint8_t> seenTri(allTris.size(), 0);
+        std::vector<int32_t> work;
+        for (int c = 0; c < 3; ++c)
+            if (roots[c] >= 0) work.push_back(roots[c]);
+        while (!work.empty()) {
+            int32_t n = work.back();
+            work.pop_back();
+            if (n < 0 || static_cast<size_t>(n) >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %d", n);
+            seenNode[n] = 1;
+            for (int k = 0; k < 2; ++k) {
+                int32_t ch = allNodes[n].child[k];
+                if (ch >= 0) {
+                    work.push_back(ch);
+                } else {
+                    const float lo = allNodes[n].n0[0];
+                    uint32_t code = static_cast<uint32_t>(~ch);
+                    uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
+                    const bool farSentinel = (k == 0 ? lo : allNodes[n].n1[0]) > 1e29f;
+                    if (farSentinel) continue;
+                    if (static_cast<uint64_t>(first) + cnt > allTris.size()) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
+                    for (uint32_t t = first; t < first + cnt; ++t) {
+                        if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
+                        seenTri[t] = 1;
+                    }
+                }
+            }
+        }
+        for (size_t t = 0; t < seenTri.size(); ++t)
+            if (!seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
+    }
+    // textures: decoded to float4 texels (sRGB EOTF per texel), + trailing 1x1 white
+    std::vector<GpuTextureInfo> infos;
+    std::vector<float> texels;
+    for (uint32_t i = 0; i <= s->texture_count; ++i) {
+        GpuTextureInfo ti {};
+        ti.texel_offset = texels.size() / 4;
+        if (i == s->texture_count) {
+            ti.width = ti.height = 1;
+            ti.wrap = ARK_WRAP_REPEAT;
+            texels.insert(texels.end(), { 1.0f, 1.0f, 1.0f, 1.0f });
+        } else {
+            const ArkTexture& t = s->textures[i];
+            if (t.width <= 0 || t.height <= 0 || !t.data) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "texture %u invalid", i);
+            ti.width = t.width;
+            ti.height = t.height;
+            ti.wrap = t.wrap;
+            const size_t n = static_cast<size_t>(t.width) * t.height;
+            for (size_t p = 0; p < n; ++p)
+                for (int c = 0; c < 4; ++c) {
+                    float v = 0.0f;
+                    switch (t.format) {
+                    case ARK_TEX_RGBA8_UNORM: v = static_cast<float>(static_cast<const uint8_t*>(t.data)[p * 4 + c]) / 255.0f; break;
+                    case ARK_TEX_RGBA8_SRGB:
+                        v = static_cast<float>(static_cast<const uint8_t*>(t.data)[p * 4 + c]) / 255.0f;
+                        if (c < 3) v = srgbToLinear(v);
+                        break;
+                    case ARK_TEX_R32F: v = c == 0 ? static_cast<const float*>(t.data)[p] : (c == 3 ? 1.0f : 0.0f); break;
+                    case ARK_TEX_RGBA32F: v = static_cast<const float*>(t.data)[p * 4 + c]; break;
+                    default: return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "texture %u: unknown format", i);
+                    }
+                    texels.push_back(v);
+                }
+        }
+        infos.push_back(ti);
+    }
+    std::vector<GpuSpotLight> gspots(s->spot_light_count);
+    for (uint32_t i = 0; i < s->spot_light_count; ++i) {
+        const ArkSpotLight& sl = s->spot_lights[i];
+        GpuSpotLight& g = gspots[i];
+        std::memset(&g, 0, sizeof(g));
+        for (int k = 0; k < 3; ++k) {
+            g.color[k] = sl.color[k];
+            g.direction[k] = sl.world_space_direction[k];
+            g.right[k] = sl.world_space_right[k];
+            g.up[k] = sl.world_space_up[k];
+            g.position[k] = sl.world_space_position[k];
+        }
+        g.position[3] = sl.outer_cone_half_angle;
+        g.ies_texture = sl.ies_profile_index;
+    }
+    int rc;
+    if ((rc = upload(ctx, ctx->nodes, allNodes.data(), allNodes.size())) != 0) return rc;
+    if ((rc = upload(ctx, ctx->tris, allTris.data(), allTris.size())) != 0) return rc;
+    if ((rc = upload(ctx, ctx->indices, s->indices, s->index_count)) != 0) return rc;
+    if ((rc = upload(ctx, ctx->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
+    if ((rc = upload(ctx, ctx->meshes, s->meshes, s->mesh_count)) != 0) return rc;
+    if ((rc = upload(ctx, ctx->materials, s->materials, s->material_count)) != 0) return rc;
+    if ((rc = upload(ctx, ctx->instances, ginst.data(), ginst.size())) != 0) return rc;
+    if ((rc = upload(ctx, ctx->texInfos, infos.data(), infos.size())) != 0) return rc;
+    if ((rc = upload(ctx, ctx->texels, texels.data(), texels.size())) != 0) return rc;
+    if ((rc = upload(ctx, ctx->spots, gspots.data(), gspots.size())) != 0) return rc;
+    SceneArgs& sc = ctx->scene;
+    sc.nodes = ctx->nodes.as<GpuBvhNode>();
+    sc.tris = ctx->tris.as<GpuTriangle>();
+    sc.root_opaque = roots[0];
+    sc.root_masked = roots[1];
+    sc.root_blend = roots[2];
+    sc.texture_count = static_cast<int32_t>(s->texture_count);
+    sc.indices = ctx->indices.as<uint32_t>();
+    sc.vertices = ctx->vertices.as<float>();
+    sc.meshes = ctx->meshes.as<ArkRTTriangleMesh>();
+    sc.materials = ctx->materials.as<ArkShaderMaterial>();
+    sc.instances = ctx->instances.as<GpuInstance>();
+    sc.tex_infos = ctx->texInfos.as<GpuTextureInfo>();
+    sc.texels = ctx->texels.as<float4>();
+    sc.white_texture = static_cast<int32_t>(s->texture_count);
+    sc.env_texture = (s->environment_texture >= 0 && static_cast<uint32_t>(s->environment_texture) < s->texture_count) ? s->environment_texture : sc.white_texture;
+    sc.has_sun = s->has_directional_light ? 1 : 0;
+    for (int k = 0; k < 3; ++k) {
+        sc.sun_color[k] = s->directional_light.color[k];
+        sc.sun_dir[k] = s->directional_light.world_space_direction[k];
+    }
+    sc.spot_count = static_cast<int32_t>(s->spot_light_count);
+    sc.spots = ctx->spots.as<GpuSpotLight>();
+    ctx->bvhMaxDepth = maxDepth;
+    if ((rc = ensureSpill(ctx)) != 0) return rc;
+    ctx->hasScene = true;
+    const auto t1 = std::chrono::steady_clock::now();
+    ctx->bvhStats.node_count = allNodes.size();
+    ctx->bvhStats.triangle_count = allTris.size();
+    ctx->bvhStats.max_depth = maxDepth;
+    ctx->bvhStats.max_leaf_size = maxLeaf;
+    ctx->bvhStats.sah_cost = sah;
+    ctx->bvhStats.build_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    ctx->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvhNode);
+    ctx->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
+    return ARK_DDGI_OK;
+}
+
+static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t K)
+{
+    if (ctx->desc.shard_count <= 1) return K;
+    uint32_t n = 0;
+    const uint32_t N = static_cast<uint32_t>(ctx->N), XZ = static_cast<uint32_t>(ctx->X * ctx->Z);
+    for (uint32_t s = 0; s < K; ++s) {
+        uint32_t p = (first + s) % N;
+        int z = static_cast<int>((p % XZ) / static_cast<uint32_t>(ctx->X));
+        if (z >= ctx->slabZ0 && z < ctx->slabZ1) n++;
+    }
+    return n;
+}
+
+int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!p || p->struct_size != sizeof(ArkDdgiFrameParams)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiFrameParams");
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_update before ark_ddgi_set_scene");
+    const uint32_t N = static_cast<uint32_t>(ctx->N);
+    const uint32_t K = std::min(p->probe_updates, N);
+    const uint32_t R = p->rays_per_probe;
+    if (K == 0 || R == 0 || K > static_cast<uint32_t>(ctx->Kmax) || R > static_cast<uint32_t>(ctx->Rmax))
+        return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "probe_updates %u / rays_per_probe %u outside [1,%d] / [1,%d]", K, R, ctx->Kmax, ctx->Rmax);
+    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    ARK_HIP(hipSetDevice(ctx->device));
+    FrameArgs f {};
+    f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
+    f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
+    for (int k = 0; k < 3; ++k) {
+        f.spacing[k] = ctx->desc.probe_spacing[k];
+        f.origin[k] = ctx->desc.offset_to_first[k];
+    }
+    f.z_far = ctx->desc.z_far;
+    f.frame = p->frame_index;
+    f.first = p->first_probe_index % N;
+    f.window = K;
+    f.sharded = ctx->desc.shard_count > 1 ? 1 : 0;
+    f.slab_z0 = ctx->slabZ0;
+    f.slab_z1 = ctx->slabZ1;
+    f.window_probes = countSlabProbes(ctx, f.first, K);
+    f.R = R;
+    f.Rmax = static_cast<uint32_t>(ctx->Rmax);
+    f.window_rays = f.window_probes * R;
+    f.hysteresis_irradiance = p->hysteresis_irradiance;
+    f.hysteresis_visibility = p->hysteresis_visibility;
+    f.visibility_sharpness = p->visibility_sharpness;
+    f.ambient_amount = p->ambient_amount;
+    f.environment_multiplier = p->environment_multiplier;
+    f.delta_time = p->delta_time;
+    f.update_offsets = p->update_offsets;
+    f.irr = ctx->irr.as<uint16_t>();
+    f.vis = ctx->vis.as<uint16_t>();
+    f.offsets = ctx->offsets.as<float4>();
+    f.slots = ctx->slots.as<GpuProbeSlot>();
+    f.fib = ctx->fib.as<float4>();
+    f.hits = ctx->hits.as<GpuHit>();
+    f.surfels = ctx->surfels.as<uint16_t>();
+    f.spill = ctx->spill.as<int32_t>();
+    f.ray_counter = ctx->rayCounter.as<uint32_t>();
+    f.counters = ctx->counters.as<unsigned long long>();
+    const bool timing = ctx->timing;
+    const bool count = ctx->counting;
+    if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
+    ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, 4, s));
+    if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
+    ARK_HIP(launch_probe_slots(f, s));
+    if (f.window_probes > 0) {
+        ARK_HIP(launch_trace_primary(ctx->scene, f, ctx->traceBlocks, count, s));
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
+        ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
+        ARK_HIP(launch_probe_update(f, s));
+    } else if (timing) {
+        ARK_HIP(hipEventRecord(ctx->ev[1], s));
+        ARK_HIP(hipEventRecord(ctx->ev[2], s));
+    }
+    if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
+    ctx->timingValid = timing;
+    ctx->countersPending = count;
+    ctx->lastRays = f.window_rays;
+    ctx->lastProbes = f.window_probes;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_synchronize(ArkDdgiCtx* ctx)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    ARK_HIP(hipDeviceSynchronize());
+    return ARK_DDGI_OK;
+}
+
+static int resourceInfo(const ArkDdgiCtx* ctx, int which, void** ptr, uint64_t* bytes)
+{
+    switch (which) {
+    case ARK_DDGI_ATLAS_IRRADIANCE: *ptr = ctx->irr.ptr; *bytes = ctx->irr.bytes; return 0;
+    case ARK_DDGI_ATLAS_VISIBILITY: *ptr = ctx->vis.ptr; *bytes = ctx->vis.bytes; return 0;
+    case ARK_DDGI_SURFELS: *ptr = ctx->surfels.ptr; *bytes = ctx->surfels.bytes; return 0;
+    case ARK_DDGI_PROBE_OFFSETS: *ptr = ctx->offsets.ptr; *bytes = ctx->offsets.bytes; return 0;
+    default: return ARK_DDGI_E_INVALID_ARGUMENT;
+    }
+}
+
+int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* outBytes)
+{
+    if (!ctx || !outBytes) return ARK_DDGI_E_INVALID_ARGUMENT;
+    void* p;
+    return resourceInfo(ctx, which, &p, outBytes);
+}
+
+int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* dst, uint64_t bytes)
+{
+    if (!ctx || !dst) return ARK_DDGI_E_INVALID_ARGUMENT;
+    void* p;
+    uint64_t n;
+    if (resourceInfo(ctx, which, &p, &n) != 0) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "unknown resource %d", which);
+    if (bytes != n) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "resource %d is %llu bytes, got %llu", which, (unsigned long long)n, (unsigned long long)bytes);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemcpy(dst, p, n, hipMemcpyDeviceToHost));
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_write(ArkDdgiCtx* ctx, int which, const void* src, uint64_t bytes)
+{
+    if (!ctx || !src) return ARK_DDGI_E_INVALID_ARGUMENT;
+    void* p;
+    uint64_t n;
+    if (resourceInfo(ctx, which, &p, &n) != 0) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "unknown resource %d", which);
+    if (bytes != n) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "resource %d is %llu bytes, got %llu", which, (unsigned long long)n, (unsigned long long)bytes);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemcpy(p, src, n, hipMemcpyHostToDevice));
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_device_views(ArkDdgiCtx* ctx, ArkDdgiDeviceViews* v)
+{
+    if (!ctx || !v) return ARK_DDGI_E_INVALID_ARGUMENT;
+    std::memset(v, 0, sizeof(*v));
+    v->irradiance_atlas = ctx->irr.ptr;
+    v->irradiance_bytes = ctx->irr.bytes;
+    v->irradiance_width = ctx->Wi;
+    v->irradiance_height = ctx->Hi;
+    v->visibility_atlas = ctx->vis.ptr;
+    v->visibility_bytes = ctx->vis.bytes;
+    v->visibility_width = ctx->Wv;
+    v->visibility_height = ctx->Hv;
+    v->probe_offsets = ctx->offsets.ptr;
+    v->probe_offsets_bytes = ctx->offsets.bytes;
+    // Z-slab = contiguous texel-row band of both atlases (tile row = z, ddgi/common.glsl:58-61)
+    const uint64_t rowI = static_cast<uint64_t>(ctx->Wi) * 8, rowV = static_cast<uint64_t>(ctx->Wv) * 4;
+    const int si = ARK_DDGI_IRRADIANCE_RES + 2, sv = ARK_DDGI_VISIBILITY_RES + 2;
+    v->irradiance_slab_offset = static_cast<uint64_t>(ctx->slabZ0) * si * rowI;
+    v->irradiance_slab_bytes = static_cast<uint64_t>(ctx->slabZ1 - ctx->slabZ0) * si * rowI;
+    v->visibility_slab_offset = static_cast<uint64_t>(ctx->slabZ0) * sv * rowV;
+    v->visibility_slab_bytes = static_cast<uint64_t>(ctx->slabZ1 - ctx->slabZ0) * sv * rowV;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_reset_history(ArkDdgiCtx* ctx)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    return clearHistory(ctx);
+}
+
+int ark_ddgi_set_counting(ArkDdgiCtx* ctx, int enabled)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->counting = enabled != 0;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out)
+{
+    if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    out->rays = ctx->lastRays;
+    out->probes = ctx->lastProbes;
+    if (ctx->countersPending) {
+        unsigned long long c[8];
+        ARK_HIP(hipSetDevice(ctx->device));
+        ARK_HIP(hipDeviceSynchronize());
+        ARK_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof(c), hipMemcpyDeviceToHost));
+        out->node_visits = c[0];
+        out->tri_tests = c[1];
+        out->hits = c[2];
+        out->shadow_rays = c[3];
+    }
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->timing = enabled != 0;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out, int count)
+{
+    if (!ctx || !out || count <= 0) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!ctx->timingValid) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "timing not enabled for the last update");
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipEventSynchronize(ctx->ev[3]));
+    float ms[5] = {};
+    ARK_HIP(hipEventElapsedTime(&ms[0], ctx->ev[0], ctx->ev[3]));
+    ARK_HIP(hipEventElapsedTime(&ms[1], ctx->ev[0], ctx->ev[1]));
+    ARK_HIP(hipEventElapsedTime(&ms[2], ctx->ev[1], ctx->ev[2]));
+    ARK_HIP(hipEventElapsedTime(&ms[3], ctx->ev[2], ctx->ev[3]));
+    ms[4] = 0.0f; // borders + offsets are fused into the probe-update kernel
+    for (int i = 0; i < count && i < 5; ++i) out[i] = ms[i];
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out)
+{
+    if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    *out = ctx->bvhStats;
+    return ARK_DDGI_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,305 @@
+// bvh_builder.cpp — binned SAH BVH2 over world-space triangles (host, C++ threads).
+#include "bvh_builder.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace ark {
+namespace {
+
+struct Aabb {
+    float lo[3] = { INFINITY, INFINITY, INFINITY };
+    float hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    void grow(const float p[3])
+    {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], p[a]);
+            hi[a] = std::max(hi[a], p[a]);
+        }
+    }
+    void grow(const Aabb& b)
+    {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], b.lo[a]);
+            hi[a] = std::max(hi[a], b.hi[a]);
+        }
+    }
+    float area() const
+    {
+        float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+        if (!(d0 >= 0.0f)) return 0.0f;
+        return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+};
+
+struct Ref {
+    Aabb box;
+    float c[3];
+};
+
+struct Range {
+    int32_t code; // >= 0 node index, < 0 leaf code
+    Aabb box;
+};
+
+class Builder {
+public:
+    Builder(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t nodeBase, uint32_t triBase)
+        : m_opt(opt), m_nodeBase(nodeBase), m_triBase(triBase)
+    {
+        const size_t n = tris.size();
+        m_refs.resize(n);
+        m_idx.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            Ref& r = m_refs[i];
+            r.box.grow(tris[i].v0);
+            r.box.grow(tris[i].v1);
+            r.box.grow(tris[i].v2);
+            for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (r.box.lo[a] + r.box.hi[a]);
+            m_idx[i] = static_cast<uint32_t>(i);
+        }
+        m_nodes.resize(2 * n + 2);
+        int hw = opt.threads > 0 ? opt.threads : static_cast<int>(std::thread::hardware_concurrency());
+        m_threadsAvail = std::max(0, hw - 1);
+    }
+
+    BvhBuildResult run(const std::vector<BuildTriangle>& tris)
+    {
+        BvhBuildResult res;
+        const uint32_t n = static_cast<uint32_t>(m_refs.size());
+        m_nodeCount = 1; // node 0 = root
+        Range root = buildRange(0, n, 1, 0);
+        if (root.code < 0) {
+            // whole set fits one leaf: root with the leaf + an unreachable far child
+            Aabb far;
+            const float p[3] = { 1e30f, 1e30f, 1e30f };
+            far.grow(p);
+            writeNode(0, root.box, root.code, far, ~0);
+        }
+        m_nodes.resize(m_nodeCount);
+        res.nodes = std::move(m_nodes);
+        res.tris.resize(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            const BuildTriangle& t = tris[m_idx[i]];
+            GpuTriangle& g = res.tris[i];
+            float e1[3], e2[3];
+            for (int a = 0; a < 3; ++a) {
+                e1[a] = t.v1[a] - t.v0[a];
+                e2[a] = t.v2[a] - t.v0[a];
+            }
+            g.t0[0] = t.v0[0]; g.t0[1] = t.v0[1]; g.t0[2] = t.v0[2]; g.t0[3] = e1[0];
+            g.t1[0] = e1[1]; g.t1[1] = e1[2]; g.t1[2] = e2[0]; g.t1[3] = e2[1];
+            g.t2[0] = e2[2];
+            std::memcpy(&g.t2[1], &t.instance, 4);
+            std::memcpy(&g.t2[2], &t.primitive, 4);
+            g.t2[3] = 0.0f;
+        }
+        res.max_depth = m_maxDepth.load();
+        res.max_leaf = m_maxLeaf.load();
+        res.sah_cost = sahCost(res.nodes, root.box);
+        return res;
+    }
+
+private:
+    float sahCost(const std::vector<GpuBvhNode>& nodes, const Aabb& rootBox) const
+    {
+        const float ra = rootBox.area();
+        if (!(ra > 0.0f)) return 0.0f;
+        double cost = 0.0;
+        for (const GpuBvhNode& nd : nodes) {
+            Aabb b[2];
+            b[0].lo[0] = nd.n0[0]; b[0].hi[0] = nd.n0[1]; b[0].lo[1] = nd.n0[2]; b[0].hi[1] = nd.n0[3];
+            b[1].lo[0] = nd.n1[0]; b[1].hi[0] = nd.n1[1]; b[1].lo[1] = nd.n1[2]; b[1].hi[1] = nd.n1[3];
+            b[0].lo[2] = nd.n2[0]; b[0].hi[2] = nd.n2[1]; b[1].lo[2] = nd.n2[2]; b[1].hi[2] = nd.n2[3];
+            for (int c = 0; c < 2; ++c) {
+                if (b[c].lo[0] > 1e29f) continue;
+                double a = b[c].area() / ra;
+                if (nd.child[c] >= 0) cost += m_opt.traversal_cost * a;
+                else cost += m_opt.intersection_cost * a * ((static_cast<uint32_t>(~nd.child[c]) & (kMaxLeafSize - 1)) + 1);
+            }
+        }
+        return static_cast<float>(cost + m_opt.traversal_cost);
+    }
+
+    void writeNode(uint32_t local, const Aabb& b0, int32_t c0, const Aabb& b1, int32_t c1)
+    {
+        GpuBvhNode& nd = m_nodes[local];
+        Aabb bb[2] = { b0, b1 };
+        for (int c = 0; c < 2; ++c) {
+            Aabb& b = bb[c];
+            if (b.lo[0] > 1e29f) continue; // far sentinel stays exact
+            float m = 0.0f, e = 0.0f;
+            for (int a = 0; a < 3; ++a) {
+                m = std::max(m, std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])));
+                e = std::max(e, b.hi[a] - b.lo[a]);
+            }
+            const float eps = m * 2e-6f + e * 1e-5f + 1e-7f;
+            for (int a = 0; a < 3; ++a) {
+                b.lo[a] -= eps;
+                b.hi[a] += eps;
+            }
+        }
+        nd.n0[0] = bb[0].lo[0]; nd.n0[1] = bb[0].hi[0]; nd.n0[2] = bb[0].lo[1]; nd.n0[3] = bb[0].hi[1];
+        nd.n1[0] = bb[1].lo[0]; nd.n1[1] = bb[1].hi[0]; nd.n1[2] = bb[1].lo[1]; nd.n1[3] = bb[1].hi[1];
+        nd.n2[0] = bb[0].lo[2]; nd.n2[1] = bb[0].hi[2]; nd.n2[2] = bb[1].lo[2]; nd.n2[3] = bb[1].hi[2];
+        nd.child[0] = c0;
+        nd.child[1] = c1;
+        nd.child[2] = 0;
+        nd.child[3] = 0;
+    }
+
+    int32_t leafCode(uint32_t first, uint32_t count) const
+    {
+        uint32_t v = ((m_triBase + first) << kLeafCountBits) | (count - 1u);
+        return ~static_cast<int32_t>(v);
+    }
+
+    Range buildRange(uint32_t first, uint32_t count, int depth, int forcedLocal = -1)
+    {
+        {
+            int md = m_maxDepth.load();
+            while (depth > md && !m_maxDepth.compare_exchange_weak(md, depth)) {}
+        }
+        Aabb box, cbox;
+        for (uint32_t i = first; i < first + count; ++i) {
+            const Ref& r = m_refs[m_idx[i]];
+            box.grow(r.box);
+            cbox.grow(r.c);
+        }
+        const int maxLeaf = std::min(m_opt.max_leaf_size, kMaxLeafSize);
+        if (count == 1 || (count <= 2 && maxLeaf >= 2)) return makeLeaf(first, count, box);
+
+        // split: binned SAH over 3 axes, object-median fallback near the depth cap
+        const int log2n = static_cast<int>(std::ceil(std::log2(std::max(1.0, static_cast<double>(count) / maxLeaf))));
+        const bool forceMedian = depth + log2n + 2 >= m_opt.max_depth;
+        uint32_t mid = first + count / 2;
+        bool split = true;
+        if (!forceMedian) {
+            const int B = std::max(4, std::min(m_opt.bins, 64));
+            float bestCost = INFINITY;
+            int bestAxis = -1, bestBin = -1;
+            for (int a = 0; a < 3; ++a) {
+                const float ext = cbox.hi[a] - cbox.lo[a];
+                if (!(ext > 0.0f)) continue;
+                Aabb bb[64];
+                uint32_t bc[64] = {};
+                const float scale = static_cast<float>(B) / ext;
+                for (uint32_t i = first; i < first + count; ++i) {
+                    const Ref& r = m_refs[m_idx[i]];
+                    int k = std::min(B - 1, std::max(0, static_cast<int>((r.c[a] - cbox.lo[a]) * scale)));
+                    bc[k]++;
+                    bb[k].grow(r.box);
+                }
+                float leftArea[64];
+                uint32_t leftCount[64];
+                Aabb acc;
+                uint32_t n = 0;
+                for (int k = 0; k < B - 1; ++k) {
+                    acc.grow(bb[k]);
+                    n += bc[k];
+                    leftArea[k] = acc.area();
+                    leftCount[k] = n;
+                }
+                Aabb accR;
+                uint32_t nr = 0;
+                for (int k = B - 1; k > 0; --k) {
+                    accR.grow(bb[k]);
+                    nr += bc[k];
+                    const uint32_t nl = leftCount[k - 1];
+                    if (nl == 0 || nr == 0) continue;
+                    const float cost = leftArea[k - 1] * nl + accR.area() * nr;
+                    if (cost < bestCost) {
+                        bestCost = cost;
+                        bestAxis = a;
+                        bestBin = k;
+                    }
+                }
+            }
+            const float area = box.area();
+            const float splitCost = m_opt.traversal_cost + (area > 0.0f ? bestCost / area : 0.0f) * m_opt.intersection_cost;
+            const float leafCost = m_opt.intersection_cost * count;
+            if (static_cast<int>(count) <= maxLeaf && (bestAxis < 0 || leafCost <= splitCost)) split = false;
+            if (split && bestAxis >= 0) {
+                const int a = bestAxis;
+                const float ext = cbox.hi[a] - cbox.lo[a];
+                const float scale = static_cast<float>(B) / ext;
+                const float lo = cbox.lo[a];
+                auto it = std::partition(m_idx.begin() + first, m_idx.begin() + first + count, [&](uint32_t id) {
+                    int k = std::min(B - 1, std::max(0, static_cast<int>((m_refs[id].c[a] - lo) * scale)));
+                    return k < bestBin;
+                });
+                mid = static_cast<uint32_t>(it - m_idx.begin());
+            }
+            if (split && (bestAxis < 0 || mid == first || mid == first + count)) {
+                medianSplit(first, count, cbox);
+                mid = first + count / 2;
+            }
+        } else {
+            if (static_cast<int>(count) <= maxLeaf) split = false;
+            else medianSplit(first, count, cbox);
+        }
+        if (!split) return makeLeaf(first, count, box);
+
+        const uint32_t local = forcedLocal >= 0 ? static_cast<uint32_t>(forcedLocal) : m_nodeCount.fetch_add(1);
+        Range l, r;
+        const uint32_t nl = mid - first, nr = first + count - mid;
+        bool spawned = false;
+        if (count > 65536) {
+            int avail = m_threadsAvail.fetch_sub(1);
+            if (avail > 0) {
+                spawned = true;
+                std::thread t([&] { l = buildRange(first, nl, depth + 1); });
+                r = buildRange(mid, nr, depth + 1);
+                t.join();
+            }
+            m_threadsAvail.fetch_add(1);
+        }
+        if (!spawned) {
+            l = buildRange(first, nl, depth + 1);
+            r = buildRange(mid, nr, depth + 1);
+        }
+        writeNode(local, l.box, l.code, r.box, r.code);
+        return Range { static_cast<int32_t>(m_nodeBase + local), box };
+    }
+
+    void medianSplit(uint32_t first, uint32_t count, const Aabb& cbox)
+    {
+        int a = 0;
+        float e0 = cbox.hi[0] - cbox.lo[0], e1 = cbox.hi[1] - cbox.lo[1], e2 = cbox.hi[2] - cbox.lo[2];
+        if (e1 > e0 && e1 >= e2) a = 1;
+        else if (e2 > e0 && e2 > e1) a = 2;
+        std::nth_element(m_idx.begin() + first, m_idx.begin() + first + count / 2, m_idx.begin() + first + count,
+                         [&](uint32_t x, uint32_t y) { return m_refs[x].c[a] < m_refs[y].c[a]; });
+    }
+
+    Range makeLeaf(uint32_t first, uint32_t count, const Aabb& box)
+    {
+        uint32_t ml = m_maxLeaf.load();
+        while (count > ml && !m_maxLeaf.compare_exchange_weak(ml, count)) {}
+        return Range { leafCode(first, count), box };
+    }
+
+    const BvhBuildOptions m_opt;
+    const uint32_t m_nodeBase, m_triBase;
+    std::vector<Ref> m_refs;
+    std::vector<uint32_t> m_idx;
+    std::vector<GpuBvhNode> m_nodes;
+    std::atomic<uint32_t> m_nodeCount { 0 };
+    std::atomic<int> m_maxDepth { 0 };
+    std::atomic<uint32_t> m_maxLeaf { 0 };
+    std::atomic<int> m_threadsAvail { 0 };
+};
+
+} // namespace
+
+BvhBuildResult build_bvh(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t node_base, uint32_t tri_base)
+{
+    if (tris.empty()) return {};
+    Builder b(tris, opt, node_base, tri_base);
+    return b.run(tris);
+}
+
+} // namespace ark

@@ -1,0 +1,42 @@
+// bvh_builder.h — binned-SAH BVH2 builder producing the 64 B node / 48 B triangle
+// HBM layout consumed by the traversal kernels (ddgi_types.h). Replaces the
+// acceleration structure build the Vulkan driver performs for the reference
+// (VulkanAccelerationStructureKHR.cpp, build flag PREFER_FAST_TRACE).
+#pragma once
+
+#include <stdint.h>
+#include <vector>
+
+#include "ddgi_types.h"
+
+namespace ark {
+
+struct BuildTriangle {
+    float v0[3], v1[3], v2[3]; // world space
+    uint32_t instance;
+    uint32_t primitive;
+};
+
+struct BvhBuildOptions {
+    int max_leaf_size = 4;   // <= kMaxLeafSize
+    int bins = 32;
+    int max_depth = 60;      // hard cap: splits fall back to object median near it
+    int threads = 0;         // 0 = hardware concurrency
+    float traversal_cost = 1.0f;
+    float intersection_cost = 1.0f;
+};
+
+struct BvhBuildResult {
+    std::vector<GpuBvhNode> nodes; // node 0 is the root (always an internal node)
+    std::vector<GpuTriangle> tris; // leaf order
+    uint32_t max_depth = 0;
+    uint32_t max_leaf = 0;
+    float sah_cost = 0.0f;
+};
+
+// Builds one BVH over `tris` (all of one hit-mask class). Node indices and
+// triangle indices are offset by node_base / tri_base so several BVHs can share
+// one node array and one triangle array.
+BvhBuildResult build_bvh(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t node_base, uint32_t tri_base);
+
+} // namespace ark

@@ -1,0 +1,867 @@
+// ddgi_kernels.hip — the DDGI probe-update hot path as HIP kernels for gfx950.
+//
+// One update (DDGINode.cpp:171-298) is four launches on one stream:
+//   1. k_probe_slots    window -> slot table (probe position + offset, per-probe
+//                       ray rotation) and the spherical-Fibonacci table.
+//   2. k_trace_primary  persistent traversal of all K*R probe rays: opaque pass
+//                       (closest hit) then masked pass (alpha-tested any-hit),
+//                       software BVH2 with a per-lane LDS ring stack (spilling to
+//                       HBM only beyond kStackLds entries) and wave64 ballot
+//                       refill of finished lanes (raygen.rgen:114-171).
+//   3. k_shade          closest-hit shading (opaque.rchit:105-176) with shadow
+//                       rays (any-hit traversal), environment on miss
+//                       (raygen.rgen:149-158), indirect from the previous frame's
+//                       atlases (probeSampling.glsl:64-163) -> fp16 surfels.
+//   4. k_probe_update   one workgroup per probe: irradiance + visibility blend
+//                       (probeUpdateIrradiance.comp, probeUpdateVisibility.comp),
+//                       tile border copy (probeBorderCopy*.comp), probe offsets
+//                       (probeUpdateOffset.comp).
+// No MFMA: the path is traversal/gather, HBM/latency bound.
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/ark_ddgi.h"
+#include "ddgi_device.h"
+#include "ddgi_kernels.h"
+
+namespace ark {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// 1. window -> slots
+// ---------------------------------------------------------------------------
+// sphericalFibonacciSample (common.glsl:121-130)
+__device__ V3 sphericalFibonacciSample(uint32_t i, uint32_t n)
+{
+    float theta = kTwoPi * static_cast<float>(i) / kGoldenRatio;
+    float phi = acosf_(2.0f * (static_cast<float>(i) / static_cast<float>(n)) - 1.0f);
+    float sinPhi = sinf_(phi);
+    float st, ct;
+    sincosf_(theta, &st, &ct);
+    return { ct * sinPhi, st * sinPhi, cosf_(phi) };
+}
+
+// Writes slot `slot` for probe `probeIdx` (ddgi/common.glsl:12-25 seed/rotation,
+// :69-77 position, raygen.rgen:196-197 offset).
+__device__ void writeSlot(const FrameArgs& f, uint32_t slot, uint32_t probeIdx)
+{
+    uint32_t tilesPerSheet = static_cast<uint32_t>(f.X * f.Z);
+    uint32_t sheetProbeIdx = probeIdx % tilesPerSheet;
+    int y = static_cast<int>(probeIdx / tilesPerSheet);
+    int x = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(f.X));
+    int z = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X));
+    V3 c = { static_cast<float>(x), static_cast<float>(y), static_cast<float>(z) };
+    V3 pos = v3(f.origin[0], f.origin[1], f.origin[2]) + c * v3(f.spacing[0], f.spacing[1], f.spacing[2]);
+    float4 off = f.offsets[probeIdx];
+    pos = pos + v3(off.x, off.y, off.z);
+    uint32_t st = wang_hash(512u * probeIdx + f.frame % 512u);
+    // randomPointOnSphere (random.glsl:63-74)
+    float theta = kTwoPi * randomFloat(st);
+    float u = 2.0f * randomFloat(st) - 1.0f;
+    float sr = sqrtf_(1.0f - u * u);
+    float s, cth;
+    sincosf_(theta, &s, &cth);
+    V3 axis = { sr * cth, sr * s, u };
+    float angle = kTwoPi * randomFloat(st);
+    float as, ac;
+    sincosf_(angle, &as, &ac);
+    GpuProbeSlot ps;
+    ps.pos[0] = pos.x;
+    ps.pos[1] = pos.y;
+    ps.pos[2] = pos.z;
+    ps.probe_index = probeIdx;
+    ps.axis[0] = axis.x;
+    ps.axis[1] = axis.y;
+    ps.axis[2] = axis.z;
+    ps.angle_sin = as;
+    ps.angle_cos = ac;
+    ps._pad[0] = ps._pad[1] = ps._pad[2] = 0.0f;
+    f.slots[slot] = ps;
+}
+
+__device__ __forceinline__ bool inSlab(const FrameArgs& f, uint32_t probeIdx)
+{
+    uint32_t sheetProbeIdx = probeIdx % static_cast<uint32_t>(f.X * f.Z);
+    int z = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X));
+    return z >= f.slab_z0 && z < f.slab_z1;
+}
+
+// Unsharded: slot s <-> probe (first + s) % N (raygen.rgen:192). Sharded (Z-slab):
+// a single workgroup compacts the window in order, so slots are deterministic.
+__global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
+{
+    const uint32_t N = static_cast<uint32_t>(f.X * f.Y * f.Z);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid < f.R) {
+        V3 d = sphericalFibonacciSample(tid, f.R);
+        f.fib[tid] = make_float4(d.x, d.y, d.z, 0.0f);
+    }
+    if (f.sharded) return;
+    if (tid < f.window) writeSlot(f, tid, (tid + f.first) % N);
+}
+
+__global__ void __launch_bounds__(1024) k_probe_slots_sharded(FrameArgs f)
+{
+    __shared__ uint32_t waveCount[16];
+    __shared__ uint32_t base;
+    const uint32_t N = static_cast<uint32_t>(f.X * f.Y * f.Z);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < f.window; c0 += 1024u) {
+        uint32_t s = c0 + threadIdx.x;
+        uint32_t probeIdx = (s + f.first) % N;
+        bool keep = s < f.window && inSlab(f, probeIdx);
+        uint64_t m = __ballot(keep);
+        if (lane == 0) waveCount[wave] = static_cast<uint32_t>(__popcll(m));
+        __syncthreads();
+        uint32_t before = base;
+        for (uint32_t w = 0; w < wave; ++w) before += waveCount[w];
+        uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+        if (keep) writeSlot(f, before + rank, probeIdx);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < 16; ++w) tot += waveCount[w];
+            base += tot;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal
+// ---------------------------------------------------------------------------
+// Per-lane traversal stack: the top kStackLds entries live in an LDS ring
+// (slot-major, so the 64 lanes of a wave hit distinct banks), deeper entries
+// spill to a per-lane HBM area [entry][lane] that only deep descents touch.
+template<int BLOCK>
+struct Stack {
+    int32_t* lds;
+    int32_t* spill;
+    uint32_t spillStride;
+    int depth;
+    __device__ __forceinline__ void push(int32_t v)
+    {
+        int slot = depth & (kStackLds - 1);
+        if (depth >= kStackLds) spill[static_cast<size_t>(depth - kStackLds) * spillStride] = lds[slot * BLOCK];
+        lds[slot * BLOCK] = v;
+        depth++;
+    }
+    __device__ __forceinline__ int32_t pop()
+    {
+        depth--;
+        int slot = depth & (kStackLds - 1);
+        int32_t v = lds[slot * BLOCK];
+        if (depth >= kStackLds) lds[slot * BLOCK] = spill[static_cast<size_t>(depth - kStackLds) * spillStride];
+        return v;
+    }
+};
+
+struct RayHit {
+    float t;      // best t so far (tmax of the query)
+    float u, v;
+    uint32_t tri; // leaf-order triangle index, kNoHit = none
+    uint32_t inst, prim;
+    bool backface;
+};
+
+__device__ __forceinline__ V3 safeInv(V3 d)
+{
+    auto f = [](float x) { return 1.0f / (fabsf_(x) < 1e-20f ? (x < 0.0f ? -1e-20f : 1e-20f) : x); };
+    return { f(d.x), f(d.y), f(d.z) };
+}
+
+// Möller–Trumbore, identical op order to the oracle's intersectTri.
+__device__ __forceinline__ bool intersectTri(V3 o, V3 d, float tmin, float tmax, const GpuTriangle& tr, float* outT, float* outU, float* outV, bool* backfaceDet)
+{
+    V3 v0 = { tr.t0[0], tr.t0[1], tr.t0[2] };
+    V3 e1 = { tr.t0[3], tr.t1[0], tr.t1[1] };
+    V3 e2 = { tr.t1[2], tr.t1[3], tr.t2[0] };
+    V3 p = cross(d, e2);
+    float det = dot(e1, p);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    V3 s = o - v0;
+    float u = dot(s, p) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return false;
+    V3 q = cross(s, e1);
+    float v = dot(d, q) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+    float tt = dot(e2, q) * inv;
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    *outT = tt;
+    *outU = u;
+    *outV = v;
+    *backfaceDet = det < 0.0f;
+    return true;
+}
+
+__device__ __forceinline__ GpuTriangle loadTri(const GpuTriangle* __restrict__ tris, uint32_t i)
+{
+    const float4* p = reinterpret_cast<const float4*>(tris + i);
+    float4 a = p[0], b = p[1], c = p[2];
+    GpuTriangle t;
+    t.t0[0] = a.x; t.t0[1] = a.y; t.t0[2] = a.z; t.t0[3] = a.w;
+    t.t1[0] = b.x; t.t1[1] = b.y; t.t1[2] = b.z; t.t1[3] = b.w;
+    t.t2[0] = c.x; t.t2[1] = c.y; t.t2[2] = c.z; t.t2[3] = c.w;
+    return t;
+}
+
+// masked.rahit:16-37 — any-hit alpha test of a masked candidate.
+__device__ bool alphaAccept(const SceneArgs& sc, uint32_t inst, uint32_t prim, float u, float v)
+{
+    const GpuInstance& gi = sc.instances[inst];
+    const ArkRTTriangleMesh mesh = sc.meshes[gi.rt_mesh_index];
+    const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
+    float bx = 1.0f - u - v, by = u, bz = v;
+    float uv[2][3];
+    for (int k = 0; k < 3; ++k) {
+        uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + k];
+        const float* vx = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+        uv[0][k] = vx[0];
+        uv[1][k] = vx[1];
+    }
+    float uvx = uv[0][0] * bx + uv[0][1] * by + uv[0][2] * bz;
+    float uvy = uv[1][0] * bx + uv[1][1] * by + uv[1][2] * bz;
+    float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
+    return !(c.w < mat.mask_cutoff);
+}
+
+// Closest-hit (ANY=false) or first-hit (ANY=true) traversal of one BVH root.
+// Box tests use the fma slab form; boxes are inflated at build time and the
+// comparison keeps a relative margin, so an exact triangle hit is never culled.
+template<bool ANY, bool ALPHA, bool COUNT, int BLOCK>
+__device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tmin, RayHit& h, Stack<BLOCK>& st, uint32_t& cNodes, uint32_t& cTris)
+{
+    if (root < 0) return false;
+    const V3 idir = safeInv(d);
+    const V3 ooeo = o * idir;
+    int32_t node = root;
+    st.depth = 0;
+    for (;;) {
+        while (node >= 0) {
+            const float4* np = reinterpret_cast<const float4*>(sc.nodes + node);
+            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+            const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+            if (COUNT) cNodes++;
+            const float tmax = h.t;
+            float c0lox = fmaf_(n0.x, idir.x, -ooeo.x), c0hix = fmaf_(n0.y, idir.x, -ooeo.x);
+            float c0loy = fmaf_(n0.z, idir.y, -ooeo.y), c0hiy = fmaf_(n0.w, idir.y, -ooeo.y);
+            float c0loz = fmaf_(n2.x, idir.z, -ooeo.z), c0hiz = fmaf_(n2.y, idir.z, -ooeo.z);
+            float c1lox = fmaf_(n1.x, idir.x, -ooeo.x), c1hix = fmaf_(n1.y, idir.x, -ooeo.x);
+            float c1loy = fmaf_(n1.z, idir.y, -ooeo.y), c1hiy = fmaf_(n1.w, idir.y, -ooeo.y);
+            float c1loz = fmaf_(n2.z, idir.z, -ooeo.z), c1hiz = fmaf_(n2.w, idir.z, -ooeo.z);
+            float t0n = fmaxf(fmaxf(fminf(c0lox, c0hix), fminf(c0loy, c0hiy)), fmaxf(fminf(c0loz, c0hiz), tmin));
+            float t0f = fminf(fminf(fmaxf(c0lox, c0hix), fmaxf(c0loy, c0hiy)), fminf(fmaxf(c0loz, c0hiz), tmax));
+            float t1n = fmaxf(fmaxf(fminf(c1lox, c1hix), fminf(c1loy, c1hiy)), fmaxf(fminf(c1loz, c1hiz), tmin));
+            float t1f = fminf(fminf(fmaxf(c1lox, c1hix), fmaxf(c1loy, c1hiy)), fminf(fmaxf(c1loz, c1hiz), tmax));
+            const bool hit0 = t0n <= fmaf_(t0f, 1.00001f, 1e-7f);
+            const bool hit1 = t1n <= fmaf_(t1f, 1.00001f, 1e-7f);
+            if (hit0 && hit1) {
+                int32_t nearC = n3.x, farC = n3.y;
+                if (t1n < t0n) { nearC = n3.y; farC = n3.x; }
+                st.push(farC);
+                node = nearC;
+            } else if (hit0) {
+                node = n3.x;
+            } else if (hit1) {
+                node = n3.y;
+            } else {
+                if (st.depth == 0) return h.tri != kNoHit;
+                node = st.pop();
+            }
+        }
+        // leaf
+        const int32_t code = ~node;
+        const uint32_t first = static_cast<uint32_t>(code) >> kLeafCountBits;
+        const uint32_t count = (static_cast<uint32_t>(code) & (kMaxLeafSize - 1)) + 1u;
+        for (uint32_t i = first; i < first + count; ++i) {
+            const GpuTriangle tr = loadTri(sc.tris, i);
+            if (COUNT) cTris++;
+            float tt, uu, vv;
+            bool bf;
+            if (!intersectTri(o, d, tmin, h.t, tr, &tt, &uu, &vv, &bf)) continue;
+            const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
+            const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
+            if (ANY) {
+                h.tri = i;
+                return true;
+            }
+            if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
+            if (ALPHA && !alphaAccept(sc, inst, prim, uu, vv)) continue;
+            h.t = tt;
+            h.u = uu;
+            h.v = vv;
+            h.tri = i;
+            h.inst = inst;
+            h.prim = prim;
+            h.backface = bf;
+        }
+        if (st.depth == 0) return h.tri != kNoHit;
+        node = st.pop();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2. primary traversal (persistent, wave64 ballot refill)
+// ---------------------------------------------------------------------------
+template<bool COUNT>
+__global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, FrameArgs f)
+{
+    __shared__ int32_t ldsStack[kStackLds * kTraceBlock];
+    const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * kTraceBlock;
+    Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
+    const uint32_t total = f.window_rays;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t cNodes = 0, cTris = 0, cHits = 0;
+    for (;;) {
+        // wave64 refill: one atomic per wave hands out 64 consecutive rays; rays of
+        // one probe share an origin, so a wave starts its descent coherently.
+        uint32_t rayBase = 0;
+        if (lane == 0) rayBase = atomicAdd(f.ray_counter, 64u);
+        rayBase = __shfl(rayBase, 0);
+        if (rayBase >= total) break;
+        const uint32_t ray = rayBase + lane;
+        if (ray < total) {
+            const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+            const GpuProbeSlot ps = f.slots[slot];
+            const float4 fb = f.fib[sample];
+            const V3 o = { ps.pos[0], ps.pos[1], ps.pos[2] };
+            const V3 d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+            const float tmin = 0.0001f; // raygen.rgen:116
+            RayHit h { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+            // opaque pass: RayFlags_Opaque, cullMask 0x01, tmax = zFar (raygen.rgen:122-134)
+            traverse<false, false, COUNT>(sc, sc.root_opaque, o, d, tmin, h, st, cNodes, cTris);
+            if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
+            float tmaxSigned = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
+            // masked pass: RayFlags_NoOpaque, cullMask 0x02, tmax = previous hit T
+            // (raygen.rgen:136-147); a negative tmax (backface) is an empty interval.
+            if (sc.root_masked >= 0 && tmaxSigned >= tmin) {
+                RayHit m { tmaxSigned, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                traverse<false, true, COUNT>(sc, sc.root_masked, o, d, tmin, m, st, cNodes, cTris);
+                if (m.tri != kNoHit) {
+                    m.backface = m.backface != (sc.instances[m.inst].flip_facing != 0);
+                    h = m;
+                }
+            }
+            GpuHit out;
+            if (h.tri == kNoHit) {
+                out.t = __builtin_bit_cast(float, 0x7f800000u);
+                out.u = out.v = 0.0f;
+                out.tri = kNoHit;
+            } else {
+                out.t = h.backface ? -h.t : h.t;
+                out.u = h.u;
+                out.v = h.v;
+                out.tri = h.tri;
+                if (COUNT) cHits++;
+            }
+            f.hits[ray] = out;
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
+        atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
+        atomicAdd(&f.counters[2], static_cast<unsigned long long>(cHits));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3. shading
+// ---------------------------------------------------------------------------
+template<bool COUNT>
+__device__ float traceShadowRay(const SceneArgs& sc, V3 X, V3 L, float maxDistance, Stack<kShadeBlock>& st, uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow)
+{
+    // opaque.rchit:35-54: TerminateOnFirstHit|SkipClosestHit|Opaque, cullMask 0xff, tmin 0.025
+    const float tmin = 0.025f;
+    if (!(maxDistance >= tmin)) return 1.0f;
+    if (COUNT) cShadow++;
+    RayHit h { maxDistance, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+    if (traverse<true, false, COUNT>(sc, sc.root_opaque, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
+    if (traverse<true, false, COUNT>(sc, sc.root_masked, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
+    if (traverse<true, false, COUNT>(sc, sc.root_blend, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
+    return 1.0f;
+}
+
+// probeSampling.glsl:9-27
+__device__ __forceinline__ void atlasSampleUV(const FrameArgs& f, int px, int py, int pz, V3 dir, int res, float invW, float invH, float* u, float* v)
+{
+    const int pad = ARK_DDGI_ATLAS_PADDING;
+    int tileX = px + py * f.X, tileY = pz;
+    int firstX = pad + tileX * (res + 2 * pad), firstY = pad + tileY * (res + 2 * pad);
+    float ex, ey;
+    octahedralEncode(dir, &ex, &ey);
+    float tx = (ex * 0.5f + 0.5f) * static_cast<float>(res);
+    float ty = (ey * 0.5f + 0.5f) * static_cast<float>(res);
+    float ax = static_cast<float>(firstX) + tx, ay = static_cast<float>(firstY) + ty;
+    *u = ax * invW;
+    *v = ay * invH;
+}
+
+// Linear filter, clamp to edge, over an fp16 atlas (DDGINode.cpp:313).
+template<int CH, int NOUT>
+__device__ __forceinline__ void sampleAtlas(const uint16_t* __restrict__ atlas, int W, int H, float u, float v, float* out)
+{
+    float x = u * static_cast<float>(W) - 0.5f;
+    float y = v * static_cast<float>(H) - 0.5f;
+    float x0f = floorf_(x), y0f = floorf_(y);
+    float fx = x - x0f, fy = y - y0f;
+    int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
+    int xa = min(max(x0, 0), W - 1), xb = min(max(x0 + 1, 0), W - 1);
+    int ya = min(max(y0, 0), H - 1), yb = min(max(y0 + 1, 0), H - 1);
+    uint16_t q[4][CH];
+    auto load = [&](int k, int xx, int yy) {
+        const uint16_t* p = atlas + (static_cast<size_t>(yy) * W + xx) * CH;
+        if (CH == 4) {
+            uint2 w = *reinterpret_cast<const uint2*>(p);
+            q[k][0] = static_cast<uint16_t>(w.x & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(w.x >> 16);
+            q[k][2 % CH] = static_cast<uint16_t>(w.y & 0xffffu);
+            q[k][3 % CH] = static_cast<uint16_t>(w.y >> 16);
+        } else {
+            uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+            q[k][0] = static_cast<uint16_t>(w & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(w >> 16);
+        }
+    };
+    load(0, xa, ya);
+    load(1, xb, ya);
+    load(2, xa, yb);
+    load(3, xb, yb);
+    for (int c = 0; c < NOUT; ++c) {
+        float t00 = f16_to_f32(q[0][c]), t10 = f16_to_f32(q[1][c]);
+        float t01 = f16_to_f32(q[2][c]), t11 = f16_to_f32(q[3][c]);
+        out[c] = lerpf(lerpf(t00, t10, fx), lerpf(t01, t11, fx), fy);
+    }
+}
+
+// probeSampling.glsl:64-163
+__device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
+{
+    const V3 spacing = v3(f.spacing[0], f.spacing[1], f.spacing[2]);
+    const V3 origin = v3(f.origin[0], f.origin[1], f.origin[2]);
+    V3 rel = (P - origin) / spacing;
+    int bx = min(max(static_cast<int>(rel.x), 0), f.X - 1);
+    int by = min(max(static_cast<int>(rel.y), 0), f.Y - 1);
+    int bz = min(max(static_cast<int>(rel.z), 0), f.Z - 1);
+    V3 baseProbePos = origin + v3(static_cast<float>(bx), static_cast<float>(by), static_cast<float>(bz)) * spacing;
+    V3 sumIrradiance = splat(0.0f);
+    float sumWeight = 0.0f;
+    V3 al = (P - baseProbePos) / spacing;
+    V3 alpha = { clampf(al.x, 0.0f, 1.0f), clampf(al.y, 0.0f, 1.0f), clampf(al.z, 0.0f, 1.0f) };
+    const float invWi = 1.0f / static_cast<float>(f.Wi), invHi = 1.0f / static_cast<float>(f.Hi);
+    const float invWv = 1.0f / static_cast<float>(f.Wv), invHv = 1.0f / static_cast<float>(f.Hv);
+    const float minDistanceBetweenProbes = fminf_(spacing.x, fminf_(spacing.y, spacing.z));
+    const V3 nN = normalize(N);
+    for (int i = 0; i < 8; ++i) {
+        int ox = i & 1, oy = (i >> 1) & 1, oz = (i >> 2) & 1;
+        int px = min(max(bx + ox, 0), f.X - 1);
+        int py = min(max(by + oy, 0), f.Y - 1);
+        int pz = min(max(bz + oz, 0), f.Z - 1);
+        V3 tri = { fmaxf_(0.001f, mixf(1.0f - alpha.x, alpha.x, static_cast<float>(ox))),
+                   fmaxf_(0.001f, mixf(1.0f - alpha.y, alpha.y, static_cast<float>(oy))),
+                   fmaxf_(0.001f, mixf(1.0f - alpha.z, alpha.z, static_cast<float>(oz))) };
+        float trilinearWeight = tri.x * tri.y * tri.z;
+        float weight = 1.0f;
+        const float tunableShadowBias = 0.3f;
+        V3 selfShadowBias = (N * 0.2f + Vw * 0.8f) * (0.75f * minDistanceBetweenProbes) * tunableShadowBias;
+        V3 biasedPosition = P + selfShadowBias;
+        V3 probePos = origin + v3(static_cast<float>(px), static_cast<float>(py), static_cast<float>(pz)) * spacing;
+        V3 pointToProbe = probePos - biasedPosition;
+        V3 directionToProbe = normalize(pointToProbe);
+        V3 unbiasedDirectionToProbe = normalize(probePos - P);
+        const float smoothFloor = 0.02f, additionalSmoothening = 0.25f;
+        weight *= smoothFloor + (1.0f - smoothFloor) * powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
+        {
+            float u, v;
+            atlasSampleUV(f, px, py, pz, -directionToProbe, ARK_DDGI_VISIBILITY_RES, invWv, invHv, &u, &v);
+            float vis[2];
+            sampleAtlas<2, 2>(f.vis, f.Wv, f.Hv, u, v, vis);
+            float meanDistanceToOccluder = vis[0];
+            float variance = fabsf_(vis[1] - square(vis[0]));
+            float distToProbe = length(pointToProbe);
+            float chebychevWeight = 1.0f;
+            if (distToProbe > meanDistanceToOccluder) {
+                chebychevWeight = variance / (variance + square(distToProbe - meanDistanceToOccluder));
+                chebychevWeight = chebychevWeight * chebychevWeight * chebychevWeight;
+            }
+            chebychevWeight = fmaxf_(0.05f, chebychevWeight);
+            weight *= chebychevWeight;
+        }
+        weight = fmaxf_(0.000001f, weight);
+        const float crushThreshold = 0.2f;
+        if (weight < crushThreshold) weight *= square(weight) * (1.0f / square(crushThreshold));
+        weight *= trilinearWeight;
+        float u, v;
+        atlasSampleUV(f, px, py, pz, nN, ARK_DDGI_IRRADIANCE_RES, invWi, invHi, &u, &v);
+        float irr[3];
+        sampleAtlas<4, 3>(f.irr, f.Wi, f.Hi, u, v, irr);
+        V3 probeIrradiance = pow3(v3(irr[0], irr[1], irr[2]), 5.0f * 0.5f);
+        sumIrradiance = sumIrradiance + weight * probeIrradiance;
+        sumWeight += weight;
+    }
+    V3 irradiance = sumIrradiance / sumWeight;
+    irradiance = irradiance * irradiance;
+    irradiance = irradiance * (0.5f * kPi);
+    return irradiance;
+}
+
+template<bool COUNT>
+__global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f)
+{
+    __shared__ int32_t ldsStack[kStackLds * kShadeBlock];
+    const uint32_t gtid = blockIdx.x * kShadeBlock + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * kShadeBlock;
+    Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
+    uint32_t cNodes = 0, cTris = 0, cShadow = 0;
+    for (uint32_t ray = gtid; ray < f.window_rays; ray += nthreads) {
+        const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+        const GpuHit hit = f.hits[ray];
+        const GpuProbeSlot ps = f.slots[slot];
+        const float4 fb = f.fib[sample];
+        const V3 origin = { ps.pos[0], ps.pos[1], ps.pos[2] };
+        const V3 dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+        V3 color;
+        float dist;
+        if (hit.tri == kNoHit) {
+            // miss (raygen.rgen:149-158)
+            dist = f.z_far;
+            float u, v;
+            sphericalUvFromDirection(dir, &u, &v);
+            float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.env_texture, u, v);
+            color = f.environment_multiplier * v3(c.x, c.y, c.z);
+        } else if (hit.t < 0.0f) {
+            // backface: colour 0, depth x 0.2 (raygen.rgen:208-213); the closest-hit
+            // colour and the indirect term are overwritten, so they are not evaluated.
+            color = splat(0.0f);
+            dist = hit.t * 0.2f;
+        } else {
+            const float T = hit.t;
+            const GpuTriangle tr = loadTri(sc.tris, hit.tri);
+            const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
+            const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
+            const GpuInstance gi = sc.instances[inst];
+            const ArkRTTriangleMesh mesh = sc.meshes[gi.rt_mesh_index];
+            const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
+            float bx = 1.0f - hit.u - hit.v, by = hit.u, bz = hit.v;
+            const float* vx[3];
+            for (int k = 0; k < 3; ++k) {
+                uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + k];
+                vx[k] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+            }
+            // opaque.rchit:118-131 (front face: no flip)
+            V3 N = normalize(v3(vx[0][2], vx[0][3], vx[0][4]) * bx + v3(vx[1][2], vx[1][3], vx[1][4]) * by + v3(vx[2][2], vx[2][3], vx[2][4]) * bz);
+            const float* M = gi.normal_matrix;
+            V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
+            N = normalize(Nw);
+            float uvx = vx[0][0] * bx + vx[1][0] * by + vx[2][0] * bz;
+            float uvy = vx[0][1] * bx + vx[1][1] * by + vx[2][1] * bz;
+            float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
+            V3 baseColor = v3(c.x, c.y, c.z) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
+            c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.emissive), uvx, uvy);
+            V3 emissive = v3(c.x, c.y, c.z) * v3(mat.emissive_factor[0], mat.emissive_factor[1], mat.emissive_factor[2]);
+            c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.metallic_roughness), uvx, uvy);
+            float metallic = c.z * mat.metallic_factor;
+            float roughness = c.y * mat.roughness_factor;
+            const float clearcoat = mat.clearcoat, ccRough = mat.clearcoat_roughness;
+            const V3 V = -dir;
+            V3 ambient = f.ambient_amount * baseColor;
+            color = emissive + ambient;
+            const V3 hitPoint = origin + T * dir;
+            if (sc.has_sun) { // opaque.rchit:56-73
+                V3 L = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+                float LdotN = dot(L, N);
+                if (LdotN > 0.0f) {
+                    float shadowFactor = traceShadowRay<COUNT>(sc, hitPoint, L, 2.0f * f.z_far, st, cNodes, cTris, cShadow);
+                    V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                    V3 directLight = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]) * shadowFactor;
+                    color = color + brdf * LdotN * directLight;
+                }
+            }
+            for (int li = 0; li < sc.spot_count; ++li) { // opaque.rchit:75-103
+                const GpuSpotLight sl = sc.spots[li];
+                V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
+                V3 L = -normalize(sdir);
+                float LdotN = dot(L, N);
+                if (LdotN > 0.0f) {
+                    V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
+                    float distanceToLight = length(toLight);
+                    V3 normalizedToLight = toLight / distanceToLight;
+                    float shadowFactor = traceShadowRay<COUNT>(sc, hitPoint, normalizedToLight, distanceToLight - 0.001f, st, cNodes, cTris, cShadow);
+                    float distanceAttenuation = 1.0f / square(distanceToLight);
+                    // evaluateIESLookupTable (lighting.glsl:20-39)
+                    V3 lrd = -normalizedToLight;
+                    float iesValue = 0.0f;
+                    float angleV = dot(lrd, sdir);
+                    if (!(angleV <= 0.0f)) {
+                        float hx = dot(lrd, v3(sl.right[0], sl.right[1], sl.right[2]));
+                        float hy = dot(lrd, v3(sl.up[0], sl.up[1], sl.up[2]));
+                        float angleH = atan2f_(hy, hx) + kPi;
+                        float lx = acosf_(angleV) / (2.0f * sl.position[3]);
+                        float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
+                        iesValue = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(sl.ies_texture), lx, ly).x;
+                    }
+                    V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                    V3 directLight = v3(sl.color[0], sl.color[1], sl.color[2]) * shadowFactor * distanceAttenuation * iesValue;
+                    color = color + brdf * LdotN * directLight;
+                }
+            }
+            // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
+            dist = T;
+            const V3 hitPos = origin + dist * dir;
+            const V3 Vi = -dir;
+            V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
+            V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
+            V3 irradiance = sampleDDGI(f, hitPos, N, Vi);
+            V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
+            color = color + baseColor * indirect;
+        }
+        // imageStore(surfelImage, (slot, sample), vec4(color, dist)) -> fp16
+        uint2 packed;
+        packed.x = static_cast<uint32_t>(f32_to_f16(color.x)) | (static_cast<uint32_t>(f32_to_f16(color.y)) << 16);
+        packed.y = static_cast<uint32_t>(f32_to_f16(color.z)) | (static_cast<uint32_t>(f32_to_f16(dist)) << 16);
+        reinterpret_cast<uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + sample] = packed;
+    }
+    if (COUNT) {
+        atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
+        atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
+        atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 4. probe update: irradiance + visibility + borders + offsets, one WG per probe
+// ---------------------------------------------------------------------------
+// probeBorderCopyCorners.comp / probeBorderCopyEdges.comp for one tile of side
+// res+2, as a (dst <- src) map over the 4*res+4 border texels (tile-local).
+__device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, int* sx, int* sy)
+{
+    const int side = res + 2;
+    if (b < 4) { // corners (probeBorderCopyCorners.comp:20-51)
+        int cx = b & 1, cy = b >> 1;
+        int scx = (cx + 1) % 2, scy = (cy + 1) % 2;
+        *dx = cx * (side - 1);
+        *dy = cy * (side - 1);
+        *sx = scx * (side - 1) + (scx == 0 ? 1 : -1);
+        *sy = scy * (side - 1) + (scy == 0 ? 1 : -1);
+        return;
+    }
+    // edges (probeBorderCopyEdges.comp:20-56)
+    b -= 4;
+    const int sideIdx = b / res, step = b % res;
+    const int cornerX[4] = { 0, 1, 1, 0 }, cornerY[4] = { 0, 0, 1, 1 };
+    const int stepX[4] = { 1, 0, -1, 0 }, stepY[4] = { 0, 1, 0, -1 };
+    const int inIdx = (sideIdx + 1) % 4;
+    int cX = cornerX[sideIdx] * (side - 1), cY = cornerY[sideIdx] * (side - 1);
+    *dx = cX + (step + 1) * stepX[sideIdx];
+    *dy = cY + (step + 1) * stepY[sideIdx];
+    *sx = (cX + stepX[inIdx]) + (res - step) * stepX[sideIdx];
+    *sy = (cY + stepY[inIdx]) + (res - step) * stepY[sideIdx];
+}
+
+__global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
+{
+    constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
+    __shared__ float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
+    __shared__ uint2 sSurf[ARK_DDGI_MAX_RAYS_PER_PROBE];
+    __shared__ uint2 sIrrTile[(IR + 2) * (IR + 2)];
+    __shared__ uint32_t sVisTile[(VR + 2) * (VR + 2)];
+    const uint32_t slot = blockIdx.x;
+    if (slot >= f.window_probes) return;
+    const GpuProbeSlot ps = f.slots[slot];
+    const uint32_t probeIdx = ps.probe_index;
+    const uint32_t R = f.R;
+    const int tid = threadIdx.x;
+    const V3 axis = v3(ps.axis[0], ps.axis[1], ps.axis[2]);
+    for (uint32_t s = tid; s < R; s += kUpdateBlock) {
+        float4 fb = f.fib[s];
+        V3 d = rotate(v3(fb.x, fb.y, fb.z), axis, ps.angle_sin, ps.angle_cos);
+        sDir[0][s] = d.x;
+        sDir[1][s] = d.y;
+        sDir[2][s] = d.z;
+        sSurf[s] = reinterpret_cast<const uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + s];
+    }
+    __syncthreads();
+    // tile origin (ddgi/common.glsl:53-67)
+    const uint32_t tilesPerSheet = static_cast<uint32_t>(f.X * f.Z);
+    const uint32_t sheetProbeIdx = probeIdx % tilesPerSheet;
+    const int py = static_cast<int>(probeIdx / tilesPerSheet);
+    const int px = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(f.X));
+    const int pz = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X));
+    const int tileX = px + py * f.X, tileY = pz;
+    const float epsilon = 1e-9f * static_cast<float>(R);
+    if (tid < VR * VR) {
+        // probeUpdateVisibility.comp:24-63
+        const int tx = tid % VR, ty = tid / VR;
+        float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(VR);
+        float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(VR);
+        const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
+        const float gridMaxSpacing = fmaxf_(f.spacing[0], fmaxf_(f.spacing[1], f.spacing[2]));
+        const float maxDistance = 1.5f * gridMaxSpacing;
+        float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
+        for (uint32_t s = 0; s < R; ++s) {
+            V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+            float weight = powf_(fmaxf_(0.0f, dot(texelDirection, rd)), f.visibility_sharpness);
+            float d = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
+            d = fminf_(fabsf_(d), maxDistance);
+            nv0 += weight * d;
+            nv1 += weight * square(d);
+            totalWeight += weight;
+        }
+        float den = fmaxf_(totalWeight, epsilon);
+        nv0 = nv0 / den;
+        nv1 = nv1 / den;
+        const int ax = 1 + tileX * (VR + 2) + tx, ay = 1 + tileY * (VR + 2) + ty;
+        uint32_t* t = reinterpret_cast<uint32_t*>(f.vis) + static_cast<size_t>(ay) * f.Wv + ax;
+        uint32_t old = *t;
+        nv0 = mixf(nv0, f16_to_f32(static_cast<uint16_t>(old & 0xffffu)), f.hysteresis_visibility);
+        nv1 = mixf(nv1, f16_to_f32(static_cast<uint16_t>(old >> 16)), f.hysteresis_visibility);
+        uint32_t nw = static_cast<uint32_t>(f32_to_f16(nv0)) | (static_cast<uint32_t>(f32_to_f16(nv1)) << 16);
+        *t = nw;
+        sVisTile[(ty + 1) * (VR + 2) + tx + 1] = nw;
+    } else {
+        const int i = tid - VR * VR;
+        if (i < IR * IR) {
+            // probeUpdateIrradiance.comp:22-79
+            const int tx = i % IR, ty = i / IR;
+            float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(IR);
+            float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(IR);
+            const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
+            V3 newIrr = splat(0.0f);
+            float totalWeight = 0.0f;
+            for (uint32_t s = 0; s < R; ++s) {
+                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+                float weight = fmaxf_(0.0f, dot(texelDirection, rd));
+                uint2 sv = sSurf[s];
+                V3 rad = v3(f16_to_f32(static_cast<uint16_t>(sv.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.x >> 16)),
+                            f16_to_f32(static_cast<uint16_t>(sv.y & 0xffffu)));
+                newIrr = newIrr + weight * rad;
+                totalWeight += weight;
+            }
+            newIrr = newIrr / fmaxf_(totalWeight, epsilon);
+            newIrr = pow3(newIrr, 1.0f / 5.0f);
+            const int ax = 1 + tileX * (IR + 2) + tx, ay = 1 + tileY * (IR + 2) + ty;
+            uint2* t = reinterpret_cast<uint2*>(f.irr) + static_cast<size_t>(ay) * f.Wi + ax;
+            uint2 old = *t;
+            V3 o = v3(f16_to_f32(static_cast<uint16_t>(old.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(old.x >> 16)),
+                      f16_to_f32(static_cast<uint16_t>(old.y & 0xffffu)));
+            newIrr = mix3(newIrr, o, f.hysteresis_irradiance);
+            uint2 nw;
+            nw.x = static_cast<uint32_t>(f32_to_f16(newIrr.x)) | (static_cast<uint32_t>(f32_to_f16(newIrr.y)) << 16);
+            nw.y = static_cast<uint32_t>(f32_to_f16(newIrr.z)) | (static_cast<uint32_t>(f32_to_f16(0.0f)) << 16);
+            *t = nw;
+            sIrrTile[(ty + 1) * (IR + 2) + tx + 1] = nw;
+        }
+    }
+    __syncthreads();
+    // Border texels of this (updated) tile. Tiles not updated this frame already
+    // hold border == f(interior) since their last update (or the uniform clear), so
+    // copying borders of updated tiles only equals the reference's all-tile pass.
+    if (tid < 4 * VR + 4) {
+        int dx, dy, sx, sy;
+        borderSource(VR, tid, &dx, &dy, &sx, &sy);
+        uint32_t val = sVisTile[sy * (VR + 2) + sx];
+        reinterpret_cast<uint32_t*>(f.vis)[static_cast<size_t>(tileY * (VR + 2) + dy) * f.Wv + tileX * (VR + 2) + dx] = val;
+    } else if (tid - (4 * VR + 4) < 4 * IR + 4) {
+        int dx, dy, sx, sy;
+        borderSource(IR, tid - (4 * VR + 4), &dx, &dy, &sx, &sy);
+        uint2 val = sIrrTile[sy * (IR + 2) + sx];
+        reinterpret_cast<uint2*>(f.irr)[static_cast<size_t>(tileY * (IR + 2) + dy) * f.Wi + tileX * (IR + 2) + dx] = val;
+    }
+    // probe offsets (probeUpdateOffset.comp:27-96), one lane, full barrier semantics
+    if (f.update_offsets && tid == kUpdateBlock - 1) {
+        const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
+        const float maxOffset = minAxialSpacing / 2.0f;
+        float4 cur = f.offsets[probeIdx];
+        V3 currentOffset = v3(cur.x, cur.y, cur.z);
+        V3 offset = splat(0.0f);
+        uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
+        V3 accumBackfaceDir = splat(0.0f), accumNearFrontfaceDir = splat(0.0f);
+        for (uint32_t s = 0; s < R; ++s) {
+            V3 d = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+            float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
+            if (a > 0.0f && a < maxOffset) {
+                accumNearFrontfaceDir = accumNearFrontfaceDir + d;
+                nearFrontfaceCount += 1;
+            } else if (a < 0.0f) {
+                backfaceCount += 1;
+                accumBackfaceDir = accumBackfaceDir + d;
+            }
+        }
+        const float stepSize = 0.125f, lerpSpeed = 10.0f;
+        if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
+            offset = offset + normalize(accumBackfaceDir) * stepSize;
+        else if (nearFrontfaceCount >= 1)
+            offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
+        else
+            offset = offset - currentOffset * stepSize;
+        V3 newOffset = currentOffset + offset;
+        if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
+        newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
+        f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
+    }
+}
+
+// Atlas clears (DDGINode.cpp:89-94) as 32-bit fills.
+__global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t value)
+{
+    for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        p[i] = value;
+}
+
+} // namespace dev
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
+{
+    uint32_t n = f.sharded ? f.R : (f.window > f.R ? f.window : f.R);
+    uint32_t blocks = (n + 255u) / 256u;
+    hipLaunchKernelGGL(dev::k_probe_slots, dim3(blocks), dim3(256), 0, s, f);
+    if (f.sharded) hipLaunchKernelGGL(dev::k_probe_slots_sharded, dim3(1), dim3(1024), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
+{
+    if (count) hipLaunchKernelGGL(dev::k_trace_primary<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL(dev::k_trace_primary<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
+{
+    if (count) hipLaunchKernelGGL(dev::k_shade<true>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL(dev::k_shade<false>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s)
+{
+    if (f.window_probes == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_probe_update, dim3(f.window_probes), dim3(kUpdateBlock), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s)
+{
+    if (count == 0) return hipSuccess;
+    uint64_t blocks = (count + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(dev::k_fill_u32, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, static_cast<uint32_t*>(p), count, value);
+    return hipGetLastError();
+}
+
+const void* kernel_trace_primary_ptr(bool count)
+{
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_primary<true>) : reinterpret_cast<const void*>(&dev::k_trace_primary<false>);
+}
+const void* kernel_shade_ptr(bool count)
+{
+    return count ? reinterpret_cast<const void*>(&dev::k_shade<true>) : reinterpret_cast<const void*>(&dev::k_shade<false>);
+}
+
+} // namespace ark

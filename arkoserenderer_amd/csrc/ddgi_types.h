@@ -1,0 +1,83 @@
+// ddgi_types.h — HBM layouts shared by the HIP kernels and the host side of
+// libark_ddgi (BVH builder, context). Plain structs, no HIP types.
+#pragma once
+
+#include <stdint.h>
+
+namespace ark {
+
+// BVH2 node, 64 B = 4 x 16 B (one half of a 128 B line). Child boxes are stored in
+// the parent ("Aila–Laine" layout) so one node fetch tests both children:
+//   n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//   n1 = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//   n2 = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//   n3 = (child0, child1, 0, 0) as int32: >= 0 internal node index,
+//        < 0 leaf: ~((firstTri << kLeafCountBits) | (count - 1)).
+struct alignas(16) GpuBvhNode {
+    float n0[4];
+    float n1[4];
+    float n2[4];
+    int32_t child[4];
+};
+static_assert(sizeof(GpuBvhNode) == 64, "node is 64 B");
+
+constexpr int kLeafCountBits = 3;           // up to 8 triangles per leaf
+constexpr int kMaxLeafSize = 1 << kLeafCountBits;
+
+// World-space triangle record, 48 B = 3 x 16 B, in leaf order:
+//   t0 = (v0.x, v0.y, v0.z, e1.x)   t1 = (e1.y, e1.z, e2.x, e2.y)
+//   t2 = (e2.z, instance, primitive, 0)     (e1 = v1 - v0, e2 = v2 - v0)
+// Closest-hit ties are broken on (instance, primitive), i.e. the global triangle
+// id, so the hit does not depend on the BVH shape (same rule in the oracle).
+struct alignas(16) GpuTriangle {
+    float t0[4];
+    float t1[4];
+    float t2[4];
+};
+static_assert(sizeof(GpuTriangle) == 48, "triangle is 48 B");
+
+// Per-instance shading data (TLAS instance + RT mesh), 64 B.
+struct alignas(16) GpuInstance {
+    float normal_matrix[12]; // mat3(ObjectToWorld) as 3 rows of 4 (w unused)
+    int32_t rt_mesh_index;
+    int32_t flip_facing;     // det(ObjectToWorld) < 0
+    int32_t hit_mask;
+    int32_t _pad;
+};
+
+struct GpuTextureInfo {
+    int32_t width, height, wrap, _pad;
+    uint64_t texel_offset; // in float4 texels into the texel pool
+};
+
+// Spot light as consumed by the closest hit (LightData.h:19-40 subset), 80 B.
+struct alignas(16) GpuSpotLight {
+    float color[4];
+    float direction[4];
+    float right[4];
+    float up[4];
+    float position[4]; // w = outer cone half angle
+    int32_t ies_texture;
+    int32_t _pad[3];
+};
+
+// One probe of the current window (slot), 32 B: position (+offset), rotation.
+struct alignas(16) GpuProbeSlot {
+    float pos[3];
+    uint32_t probe_index;
+    float axis[3];
+    float angle_sin;
+    float angle_cos;
+    float _pad[3];
+};
+
+// Hit record of the primary pass, 16 B: signed t (negative = backface, +inf =
+// miss), barycentrics (u, v) and the leaf-order triangle index.
+struct alignas(16) GpuHit {
+    float t;
+    float u;
+    float v;
+    uint32_t tri;
+};
+
+} // namespace ark

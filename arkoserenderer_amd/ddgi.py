@@ -1,0 +1,232 @@
+"""Python host for the MI355X DDGI path, mirroring the reference node's
+interface (arkose/rendering/nodes/DDGINode.h/.cpp) over the C-ABI.
+
+* ``ProbeGrid``   — arkcore/scene/ProbeGrid.h:6-15 (+ Scene::generateProbeGridFromBoundingBox,
+                    arkose/scene/Scene.cpp:534-583).
+* ``DDGIConfig``  — the node's private members and their defaults (DDGINode.h:25-38).
+* ``DDGIContext`` — one ark_ddgi context (device resources of one node on one GPU).
+* ``DDGINode``    — name() == "DDGI"; ``execute(app_state)`` is the execute lambda
+                    (DDGINode.cpp:171-298): rolling window, first-frame hysteresis,
+                    push-constant values. The native C++ node
+                    (arkoserenderer_amd/host/rendering/nodes/DDGINode.cpp) is the
+                    drop-in for the engine; this mirror drives tests and bench.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+from .scene import SceneData
+
+
+@dataclass
+class ProbeGrid:
+    grid_dimensions: tuple  # (x=width, y=height, z=depth)
+    probe_spacing: tuple
+    offset_to_first: tuple
+
+    def probe_count(self) -> int:
+        x, y, z = self.grid_dimensions
+        return int(x * y * z)
+
+    @staticmethod
+    def from_bounding_box(lo, hi, counts=(16, 16, 16), largest_axis_count=32, margin=1.0):
+        """Scene::generateProbeGridFromBoundingBox (Scene.cpp:534-583): the largest
+        axis gets `largest_axis_count` probes, AABB grown by `margin` metres."""
+        lo = np.asarray(lo, np.float32) - margin
+        hi = np.asarray(hi, np.float32) + margin
+        ext = hi - lo
+        c = list(counts)
+        c[int(np.argmax(ext))] = largest_axis_count
+        spacing = ext / np.asarray(c, np.float32)
+        return ProbeGrid(tuple(int(v) for v in c), tuple(float(v) for v in spacing), tuple(float(v) for v in lo))
+
+
+@dataclass
+class DDGIConfig:
+    rays_per_probe: int = 256            # m_raysPerProbeInt
+    hysteresis_irradiance: float = 0.93  # m_hysteresisIrradiance
+    hysteresis_visibility: float = 0.93  # m_hysteresisVisibility
+    visibility_sharpness: float = 50.0   # m_visibilitySharpness
+    probe_updates_per_frame: int = 2048  # m_probeUpdatesPerFrame
+    compute_probe_offsets: bool = True   # m_computeProbeOffsets
+    apply_probe_offsets: bool = True     # m_applyProbeOffsets
+    use_scene_ambient: bool = True       # m_useSceneAmbient
+    injected_ambient_lx: float = 100.0   # m_injectedAmbientLx
+    max_rays_per_probe: int = abi.ARK_DDGI_MAX_RAYS_PER_PROBE        # DDGINode.h:22
+    max_probe_updates: int = abi.ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES  # DDGINode.h:23
+    clear_overflow_mode: int = abi.ARK_DDGI_CLEAR_OVERFLOW_INF
+
+
+@dataclass
+class AppState:
+    """arkose/rendering/AppState.h:5-29"""
+    frame_index: int = 0
+    delta_time: float = 1.0 / 60.0
+
+    def is_first_frame(self) -> bool:
+        return self.frame_index == 0
+
+
+def _check(lib, ctx, rc, what):
+    if rc != 0:
+        msg = lib.ark_ddgi_last_error(ctx)
+        raise abi.ArkDdgiError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+
+class DDGIContext:
+    """Owns one ark_ddgi context (device memory of one DDGI node on one GPU)."""
+
+    def __init__(self, grid: ProbeGrid, z_far: float, config: DDGIConfig | None = None, device: int = 0,
+                 shard_rank: int = 0, shard_count: int = 1):
+        self.lib = abi.load_library()
+        self.grid = grid
+        self.config = config or DDGIConfig()
+        d = abi.ArkDdgiDesc()
+        d.struct_size = C.sizeof(abi.ArkDdgiDesc)
+        for k in range(3):
+            d.grid_dims[k] = int(grid.grid_dimensions[k])
+            d.probe_spacing[k] = float(grid.probe_spacing[k])
+            d.offset_to_first[k] = float(grid.offset_to_first[k])
+        d.z_far = float(z_far)
+        d.max_rays_per_probe = int(self.config.max_rays_per_probe)
+        d.max_probe_updates = int(self.config.max_probe_updates)
+        d.device = int(device)
+        d.clear_overflow_mode = int(self.config.clear_overflow_mode)
+        d.shard_rank = int(shard_rank)
+        d.shard_count = int(shard_count)
+        self.desc = d
+        h = C.c_void_p()
+        rc = self.lib.ark_ddgi_create(C.byref(d), C.byref(h))
+        if rc != 0:
+            raise abi.ArkDdgiError(rc, "ark_ddgi_create")
+        self.h = h
+        self._scene = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ark_ddgi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def check(self, rc, what):
+        _check(self.lib, self.h, rc, what)
+
+    def set_scene(self, scene: SceneData):
+        s = scene.to_abi()
+        self.check(self.lib.ark_ddgi_set_scene(self.h, C.byref(s)), "ark_ddgi_set_scene")
+        self._scene = scene
+
+    def update(self, params: abi.ArkDdgiFrameParams, stream: int | None = None):
+        self.check(self.lib.ark_ddgi_update(self.h, C.byref(params), C.c_void_p(stream) if stream else None), "ark_ddgi_update")
+
+    def synchronize(self):
+        self.check(self.lib.ark_ddgi_synchronize(self.h), "ark_ddgi_synchronize")
+
+    def size(self, which: int) -> int:
+        n = C.c_uint64()
+        self.check(self.lib.ark_ddgi_resource_size(self.h, which, C.byref(n)), "ark_ddgi_resource_size")
+        return int(n.value)
+
+    def read(self, which: int) -> np.ndarray:
+        n = self.size(which)
+        dt = np.float32 if which == abi.ARK_DDGI_PROBE_OFFSETS else np.uint16
+        out = np.empty(n // np.dtype(dt).itemsize, dtype=dt)
+        self.check(self.lib.ark_ddgi_read(self.h, which, out.ctypes.data, n), "ark_ddgi_read")
+        return out
+
+    def write(self, which: int, data: np.ndarray):
+        data = np.ascontiguousarray(data)
+        self.check(self.lib.ark_ddgi_write(self.h, which, data.ctypes.data, data.nbytes), "ark_ddgi_write")
+
+    def device_views(self) -> abi.ArkDdgiDeviceViews:
+        v = abi.ArkDdgiDeviceViews()
+        self.check(self.lib.ark_ddgi_get_device_views(self.h, C.byref(v)), "ark_ddgi_get_device_views")
+        return v
+
+    def reset_history(self):
+        self.check(self.lib.ark_ddgi_reset_history(self.h), "ark_ddgi_reset_history")
+
+    def set_counting(self, on: bool):
+        self.check(self.lib.ark_ddgi_set_counting(self.h, int(on)), "ark_ddgi_set_counting")
+
+    def counters(self) -> abi.ArkDdgiCounters:
+        c = abi.ArkDdgiCounters()
+        self.check(self.lib.ark_ddgi_get_counters(self.h, C.byref(c)), "ark_ddgi_get_counters")
+        return c
+
+    def set_timing(self, on: bool):
+        self.check(self.lib.ark_ddgi_set_timing(self.h, int(on)), "ark_ddgi_set_timing")
+
+    def last_timings(self):
+        out = (C.c_float * 5)()
+        self.check(self.lib.ark_ddgi_get_last_timings(self.h, out, 5), "ark_ddgi_get_last_timings")
+        return list(out)
+
+    def bvh_stats(self) -> abi.ArkDdgiBvhStats:
+        s = abi.ArkDdgiBvhStats()
+        self.check(self.lib.ark_ddgi_get_bvh_stats(self.h, C.byref(s)), "ark_ddgi_get_bvh_stats")
+        return s
+
+
+def frame_params(config: DDGIConfig, grid: ProbeGrid, app: AppState, first_probe_index: int,
+                 light_pre_exposure: float = 1.0, ambient_illuminance: float = 0.0,
+                 environment_brightness: float = 1.0) -> abi.ArkDdgiFrameParams:
+    """Push-constant values of the execute lambda (DDGINode.cpp:171-292)."""
+    p = abi.ArkDdgiFrameParams()
+    p.struct_size = C.sizeof(abi.ArkDdgiFrameParams)
+    p.frame_index = int(app.frame_index) & 0xFFFFFFFF
+    p.first_probe_index = int(first_probe_index)
+    p.probe_updates = min(int(config.probe_updates_per_frame), grid.probe_count())
+    p.rays_per_probe = int(config.rays_per_probe)
+    p.hysteresis_irradiance = 0.0 if app.is_first_frame() else config.hysteresis_irradiance
+    p.hysteresis_visibility = 0.0 if app.is_first_frame() else config.hysteresis_visibility
+    p.visibility_sharpness = config.visibility_sharpness
+    ambient_lx = ambient_illuminance if config.use_scene_ambient else config.injected_ambient_lx
+    p.ambient_amount = float(np.float32(ambient_lx) * np.float32(light_pre_exposure))
+    p.environment_multiplier = float(np.float32(environment_brightness) * np.float32(light_pre_exposure))
+    p.delta_time = float(app.delta_time)
+    p.update_offsets = int(config.compute_probe_offsets and config.apply_probe_offsets)
+    return p
+
+
+class DDGINode:
+    """Python mirror of DDGINode (name "DDGI") driving a DDGIContext."""
+
+    def __init__(self, config: DDGIConfig | None = None):
+        self.config = config or DDGIConfig()
+        self.probe_update_idx = 0  # m_probeUpdateIdx (DDGINode.h:32)
+        self.ctx: DDGIContext | None = None
+        self.grid: ProbeGrid | None = None
+        self.exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+
+    def name(self) -> str:
+        return "DDGI"
+
+    def construct(self, scene: SceneData, grid: ProbeGrid | None, z_far: float, device: int = 0,
+                  shard_rank: int = 0, shard_count: int = 1, **exposure) -> bool:
+        """DDGINode::construct (DDGINode.cpp:76-169). Returns False (no-op node)
+        when there is no probe grid, like NullExecuteCallback (:78-81)."""
+        if grid is None or grid.probe_count() == 0:
+            return False
+        self.grid = grid
+        self.ctx = DDGIContext(grid, z_far, self.config, device, shard_rank, shard_count)
+        self.ctx.set_scene(scene)
+        self.exposure.update(exposure)
+        return True
+
+    def next_params(self, app: AppState) -> abi.ArkDdgiFrameParams:
+        return frame_params(self.config, self.grid, app, self.probe_update_idx, **self.exposure)
+
+    def execute(self, app: AppState, stream: int | None = None) -> abi.ArkDdgiFrameParams:
+        if self.ctx is None:
+            return None
+        p = self.next_params(app)
+        self.ctx.update(p, stream)
+        self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
+        return p

@@ -1,0 +1,331 @@
+"""Scene inputs for the DDGI path: the RT-scene data contract of GpuScene
+(RT mesh table, u32 index pool, vec3 position pool, RTVertex pool, materials,
+TLAS instances, lights, environment) as numpy arrays, plus loaders:
+
+* ``load_gltf`` — minimal glTF 2.0 (+ .bin) reader following the reference's
+  import rules (arkcore/asset/import/GltfLoader.cpp:372-543 geometry,
+  :918-971 materials) for the in-tree sample models (Cornell box).
+* ``cornell_box`` — BASELINE config C2 (CornellBox.arklvl: +90 deg about X,
+  camera f/11 1/125 s ISO 400, no lights, environment = white x brightness).
+* ``soup`` — BASELINE config C4 synthetic triangle-strip soup (C generator in
+  libark_ddgi, include/ark_scene.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+
+def shader_material_dtype():
+    return np.dtype([
+        ("base_color", "<i4"), ("normal_map", "<i4"), ("metallic_roughness", "<i4"), ("emissive", "<i4"),
+        ("occlusion", "<i4"), ("bent_normal_map", "<i4"), ("clearcoat", "<f4"), ("clearcoat_roughness", "<f4"),
+        ("blend_mode", "<i4"), ("mask_cutoff", "<f4"), ("metallic_factor", "<f4"), ("roughness_factor", "<f4"),
+        ("emissive_factor", "<f4", 3), ("brdf", "<i4"), ("dielectric_reflectance", "<f4"), ("_unused", "<f4", 3),
+        ("color_tint", "<f4", 4),
+    ])
+
+
+MATERIAL_DTYPE = shader_material_dtype()
+MESH_DTYPE = np.dtype([("first_vertex", "<i4"), ("first_index", "<i4"), ("material_index", "<i4")])
+INSTANCE_DTYPE = np.dtype([("object_to_world", "<f4", 12), ("rt_mesh_index", "<u4"), ("triangle_count", "<u4"),
+                           ("hit_mask", "<u4"), ("_pad", "<u4")])
+VERTEX_DTYPE = np.dtype([("tex_coord", "<f4", 2), ("normal", "<f4", 3), ("tangent", "<f4", 4)])
+
+
+def default_material() -> np.ndarray:
+    m = np.zeros((), dtype=MATERIAL_DTYPE)
+    for k in ("base_color", "normal_map", "metallic_roughness", "emissive", "occlusion", "bent_normal_map"):
+        m[k] = -1  # -> default textures (white; GpuScene.cpp:1459-1464)
+    m["blend_mode"] = abi.ARK_BLEND_MODE_OPAQUE
+    m["mask_cutoff"] = 1.0
+    m["metallic_factor"] = 1.0
+    m["roughness_factor"] = 1.0
+    m["dielectric_reflectance"] = 0.04
+    m["color_tint"] = (1.0, 1.0, 1.0, 1.0)
+    return m
+
+
+@dataclass
+class Texture:
+    width: int
+    height: int
+    format: int
+    data: np.ndarray
+    wrap: int = abi.ARK_WRAP_REPEAT
+
+
+@dataclass
+class SpotLight:
+    color: tuple
+    direction: tuple
+    right: tuple
+    up: tuple
+    position: tuple
+    outer_cone_half_angle: float
+    ies_profile_index: int = -1
+
+
+@dataclass
+class SceneData:
+    positions: np.ndarray            # (V, 3) float32
+    vertices: np.ndarray             # (V,) VERTEX_DTYPE
+    indices: np.ndarray              # (I,) uint32, local to mesh first_vertex
+    meshes: np.ndarray               # (M,) MESH_DTYPE
+    materials: np.ndarray            # (Mat,) MATERIAL_DTYPE
+    instances: np.ndarray            # (Inst,) INSTANCE_DTYPE
+    textures: list = field(default_factory=list)
+    sun: tuple | None = None         # (color(3), direction(3)), color pre-exposed
+    spots: list = field(default_factory=list)
+    environment_texture: int = -1
+    _keepalive: list = field(default_factory=list, repr=False)
+    _native: object = field(default=None, repr=False)  # owning ArkSoupScene handle
+
+    @property
+    def triangle_count(self) -> int:
+        return int(self.instances["triangle_count"].sum())
+
+    def to_abi(self) -> abi.ArkDdgiScene:
+        """Builds the ArkDdgiScene view. The returned struct references this
+        object's arrays; keep the SceneData alive while it is used."""
+        s = abi.ArkDdgiScene()
+        s.struct_size = C.sizeof(abi.ArkDdgiScene)
+        keep = []
+
+        def ptr(a):
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            return a.ctypes.data
+
+        s.indices = ptr(self.indices.astype(np.uint32, copy=False))
+        s.index_count = int(self.indices.size)
+        s.positions = ptr(self.positions.astype(np.float32, copy=False))
+        s.vertex_count = int(self.positions.shape[0])
+        s.vertices = ptr(self.vertices)
+        s.meshes = ptr(self.meshes)
+        s.mesh_count = int(self.meshes.size)
+        s.materials = ptr(self.materials)
+        s.material_count = int(self.materials.size)
+        tex = (abi.ArkTexture * max(1, len(self.textures)))()
+        for i, t in enumerate(self.textures):
+            tex[i].width, tex[i].height, tex[i].format, tex[i].wrap = t.width, t.height, t.format, t.wrap
+            tex[i].data = ptr(t.data)
+        keep.append(tex)
+        s.textures = C.addressof(tex)
+        s.texture_count = len(self.textures)
+        s.instances = ptr(self.instances)
+        s.instance_count = int(self.instances.size)
+        if self.sun is not None:
+            s.has_directional_light = 1
+            for k in range(3):
+                s.directional_light.color[k] = self.sun[0][k]
+                s.directional_light.world_space_direction[k] = self.sun[1][k]
+        spots = (abi.ArkSpotLight * max(1, len(self.spots)))()
+        for i, sl in enumerate(self.spots):
+            for k in range(3):
+                spots[i].color[k] = sl.color[k]
+                spots[i].world_space_direction[k] = sl.direction[k]
+                spots[i].world_space_right[k] = sl.right[k]
+                spots[i].world_space_up[k] = sl.up[k]
+                spots[i].world_space_position[k] = sl.position[k]
+            spots[i].outer_cone_half_angle = sl.outer_cone_half_angle
+            spots[i].ies_profile_index = sl.ies_profile_index
+        keep.append(spots)
+        s.spot_lights = C.addressof(spots)
+        s.spot_light_count = len(self.spots)
+        s.environment_texture = self.environment_texture
+        self._keepalive = keep
+        return s
+
+    def bounds(self):
+        lo = np.full(3, np.inf, np.float32)
+        hi = np.full(3, -np.inf, np.float32)
+        for inst in self.instances:
+            mesh = self.meshes[inst["rt_mesh_index"]]
+            idx = self.indices[mesh["first_index"]: mesh["first_index"] + 3 * inst["triangle_count"]]
+            p = self.positions[mesh["first_vertex"] + idx.astype(np.int64)]
+            M = inst["object_to_world"].reshape(3, 4)
+            w = p @ M[:, :3].T + M[:, 3]
+            lo = np.minimum(lo, w.min(0))
+            hi = np.maximum(hi, w.max(0))
+        return lo, hi
+
+
+def quat_to_matrix(x, y, z, w) -> np.ndarray:
+    """Rotation matrix (3x3, float32) of a unit quaternion (x, y, z, w)."""
+    m = np.array([
+        [1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+        [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+        [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+    ], dtype=np.float64)
+    return m.astype(np.float32)
+
+
+_COMPONENT = {5120: np.int8, 5121: np.uint8, 5122: np.int16, 5123: np.uint16, 5125: np.uint32, 5126: np.float32}
+_NCOMP = {"SCALAR": 1, "VEC2": 2, "VEC3": 3, "VEC4": 4, "MAT4": 16}
+
+
+def _accessor(g, buffers, idx):
+    acc = g["accessors"][idx]
+    view = g["bufferViews"][acc["bufferView"]]
+    dt = np.dtype(_COMPONENT[acc["componentType"]])
+    n = _NCOMP[acc["type"]]
+    offset = view.get("byteOffset", 0) + acc.get("byteOffset", 0)
+    stride = view.get("byteStride", 0) or dt.itemsize * n
+    buf = buffers[view["buffer"]]
+    count = acc["count"]
+    if stride == dt.itemsize * n:
+        arr = np.frombuffer(buf, dtype=dt, count=count * n, offset=offset).reshape(count, n)
+    else:
+        arr = np.stack([np.frombuffer(buf, dtype=dt, count=n, offset=offset + i * stride) for i in range(count)])
+    return arr
+
+
+def load_gltf(path: str, transform: np.ndarray | None = None) -> SceneData:
+    """Loads a .gltf + .bin without textures (factors only): one RT mesh +
+    instance per primitive (mesh segment), CCW winding as stored, material
+    mapping as GltfLoader.cpp:918-971 (alphaMode -> blend mode, alphaCutoff,
+    emissiveFactor, metallic/roughness factors, baseColorFactor -> colorTint)."""
+    with open(path) as fh:
+        g = json.load(fh)
+    base = os.path.dirname(path)
+    buffers = [open(os.path.join(base, b["uri"]), "rb").read() for b in g["buffers"]]
+    materials = []
+    for gm in g.get("materials", []):
+        m = default_material()
+        mode = gm.get("alphaMode", "OPAQUE")
+        if mode == "BLEND":
+            m["blend_mode"] = abi.ARK_BLEND_MODE_TRANSLUCENT
+        elif mode == "MASK":
+            m["blend_mode"] = abi.ARK_BLEND_MODE_MASKED
+            m["mask_cutoff"] = float(gm.get("alphaCutoff", 0.5))
+        m["emissive_factor"] = gm.get("emissiveFactor", [0.0, 0.0, 0.0])
+        pbr = gm.get("pbrMetallicRoughness", {})
+        m["metallic_factor"] = float(pbr.get("metallicFactor", 1.0))
+        m["roughness_factor"] = float(pbr.get("roughnessFactor", 1.0))
+        m["color_tint"] = pbr.get("baseColorFactor", [1.0, 1.0, 1.0, 1.0])
+        materials.append(m)
+    if not materials:
+        materials.append(default_material())
+    M = np.eye(3, 4, dtype=np.float32) if transform is None else np.asarray(transform, np.float32).reshape(3, 4)
+    pos_l, vtx_l, idx_l, meshes, instances = [], [], [], [], []
+    nv = ni = 0
+    for mesh in g["meshes"]:
+        for prim in mesh["primitives"]:
+            attrs = prim["attributes"]
+            P = _accessor(g, buffers, attrs["POSITION"]).astype(np.float32)
+            n = P.shape[0]
+            vx = np.zeros(n, dtype=VERTEX_DTYPE)
+            if "NORMAL" in attrs:
+                vx["normal"] = _accessor(g, buffers, attrs["NORMAL"])
+            if "TEXCOORD_0" in attrs:
+                vx["tex_coord"] = _accessor(g, buffers, attrs["TEXCOORD_0"])
+            if "TANGENT" in attrs:
+                vx["tangent"] = _accessor(g, buffers, attrs["TANGENT"])
+            idx = _accessor(g, buffers, prim["indices"]).reshape(-1).astype(np.uint32)
+            pos_l.append(P)
+            vtx_l.append(vx)
+            idx_l.append(idx)
+            mat = prim.get("material", 0)
+            meshes.append((nv, ni, mat))
+            inst = np.zeros((), dtype=INSTANCE_DTYPE)
+            inst["object_to_world"] = M.reshape(-1)
+            inst["rt_mesh_index"] = len(meshes) - 1
+            inst["triangle_count"] = idx.size // 3
+            bm = int(materials[mat]["blend_mode"])
+            inst["hit_mask"] = {abi.ARK_BLEND_MODE_OPAQUE: abi.ARK_RT_HIT_MASK_OPAQUE,
+                                abi.ARK_BLEND_MODE_MASKED: abi.ARK_RT_HIT_MASK_MASKED}.get(bm, abi.ARK_RT_HIT_MASK_BLEND)
+            instances.append(inst)
+            nv += n
+            ni += idx.size
+    return SceneData(
+        positions=np.concatenate(pos_l),
+        vertices=np.concatenate(vtx_l),
+        indices=np.concatenate(idx_l),
+        meshes=np.array(meshes, dtype=MESH_DTYPE),
+        materials=np.array(materials, dtype=MATERIAL_DTYPE),
+        instances=np.array(instances, dtype=INSTANCE_DTYPE),
+    )
+
+
+def manual_exposure(f_number: float, shutter: float, iso: float) -> float:
+    """Camera::calculateManualExposure (arkose/scene/camera/Camera.cpp:203-214)."""
+    ev100 = math.log2((f_number * f_number) / shutter * 100.0 / iso)
+    return 1.0 / (1.2 * 2.0 ** ev100)
+
+
+ASSET_DIRS = [
+    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "assets"),
+]
+
+
+def find_asset(*parts) -> str | None:
+    for d in ASSET_DIRS:
+        p = os.path.join(d, *parts)
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def cornell_box() -> tuple[SceneData, dict]:
+    """BASELINE config C2 scene: CornellBox.gltf under the CornellBox.arklvl
+    transform (+90 deg about X). Returns (scene, exposure info)."""
+    path = find_asset("CornellBox", "CornellBox.gltf")
+    if path is None:
+        raise FileNotFoundError("tests/assets/CornellBox/CornellBox.gltf missing")
+    R = quat_to_matrix(0.7071068286895752, 0.0, 0.0, 0.7071067094802856)
+    T = np.zeros((3, 4), np.float32)
+    T[:, :3] = R
+    scene = load_gltf(path, T)
+    pre = manual_exposure(11.0, 0.008, 400.0)
+    return scene, {"light_pre_exposure": pre, "environment_brightness": 3000.0, "z_far": 10000.0}
+
+
+def soup(triangle_count: int = 10_000_000, **overrides) -> SceneData:
+    """BASELINE config C4 synthetic triangle-strip soup (PCG32 seed 0xA2C05E00)."""
+    lib = abi.load_library()
+    p = abi.ArkSoupParams()
+    lib.ark_soup_default_params(C.byref(p))
+    p.triangle_count = int(triangle_count)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    h = C.c_void_p()
+    rc = lib.ark_soup_generate(C.byref(p), C.byref(h))
+    if rc != 0:
+        raise abi.ArkDdgiError(rc, "ark_soup_generate failed")
+    v = lib.ark_soup_scene_view(h).contents
+    V = int(v.vertex_count)
+
+    def arr(addr, dtype, count):
+        buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(addr)
+        return np.frombuffer(buf, dtype=dtype, count=count)
+
+    scene = SceneData(
+        positions=arr(v.positions, np.float32, V * 3).reshape(V, 3),
+        vertices=arr(v.vertices, VERTEX_DTYPE, V),
+        indices=arr(v.indices, np.uint32, int(v.index_count)),
+        meshes=arr(v.meshes, MESH_DTYPE, int(v.mesh_count)),
+        materials=arr(v.materials, MATERIAL_DTYPE, int(v.material_count)),
+        instances=arr(v.instances, INSTANCE_DTYPE, int(v.instance_count)),
+        sun=(tuple(v.directional_light.color), tuple(v.directional_light.world_space_direction)) if v.has_directional_light else None,
+    )
+    scene._native = _SoupHandle(lib, h)
+    return scene
+
+
+class _SoupHandle:
+    def __init__(self, lib, h):
+        self.lib, self.h = lib, h
+
+    def __del__(self):
+        try:
+            self.lib.ark_soup_free(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,304 @@
+/*
+ * ark_ddgi.h — C-ABI of the MI355X-native DDGI probe-update path.
+ *
+ * This is the drop-in boundary between Arkose's C++ host (the DDGINode that
+ * implements RenderPipelineNode, see arkoserenderer_amd/host/) and the HIP
+ * kernels for gfx950. Plain C structs, explicit sizes, no exceptions and no
+ * torch/HIP types in the signatures: a hipStream_t is passed as `void*`.
+ *
+ * Every entry point replaces a piece of the reference's Vulkan-RT DDGI node:
+ *
+ *   ark_ddgi_create      <- DDGINode::construct resource creation
+ *                           (arkose/rendering/nodes/DDGINode.cpp:76-169): grid CB,
+ *                           atlases + clear values (:89-94), offsets buffer (:96-99),
+ *                           surfel image 4096x512 (:107).
+ *   ark_ddgi_set_scene   <- the scene contract DDGINode binds at construct
+ *                           (DDGINode.cpp:110-142): TLAS (GpuScene.cpp:872-1010),
+ *                           SceneRTMeshDataSet (rayTracing.glsl:9-18), material set
+ *                           (material.glsl:9-14), SceneLightSet (lighting.glsl:8-17),
+ *                           environment map (GpuScene.cpp:1041-1048). The BVH that the
+ *                           Vulkan driver builds is built here instead.
+ *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:171-298):
+ *                           traceRays -> irradiance update -> visibility update ->
+ *                           border copies -> probe offsets.
+ *   ark_ddgi_read, ark_ddgi_write <- the published DDGISamplingSet contents
+ *                           (DDGINode.cpp:101-105) and the Registry texture reuse that
+ *                           carries DDGI history across rebuilds (Registry.cpp:120-150).
+ *
+ * Status convention: 0 = OK, negative = error (ARK_DDGI_E_*); the message of the
+ * last error is available from ark_ddgi_last_error(ctx). This mirrors the
+ * reference's ARKOSE_LOG(Error)+NullExecuteCallback handling (DDGINode.cpp:78-81):
+ * the node maps a negative status to an Error log and a no-op.
+ *
+ * Threading: one context per GPU, used from one host thread. All device work is
+ * enqueued on the caller's stream (or the context's own stream when NULL).
+ */
+#ifndef ARK_DDGI_H
+#define ARK_DDGI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARK_DDGI_ABI_VERSION 1
+
+/* DDGIData.h:4-9 */
+#define ARK_DDGI_IRRADIANCE_RES 8
+#define ARK_DDGI_VISIBILITY_RES 16
+#define ARK_DDGI_ATLAS_PADDING 1
+/* DDGINode.h:22-23 */
+#define ARK_DDGI_MAX_RAYS_PER_PROBE 512
+#define ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES 4096
+
+/* RTData.h:4-6 */
+#define ARK_RT_HIT_MASK_OPAQUE 0x01u
+#define ARK_RT_HIT_MASK_MASKED 0x02u
+#define ARK_RT_HIT_MASK_BLEND 0x04u
+
+/* ShaderBlendMode.h */
+#define ARK_BLEND_MODE_OPAQUE 1
+#define ARK_BLEND_MODE_MASKED 2
+#define ARK_BLEND_MODE_TRANSLUCENT 3
+
+enum {
+    ARK_DDGI_OK = 0,
+    ARK_DDGI_E_INVALID_ARGUMENT = -1,
+    ARK_DDGI_E_NO_PROBE_GRID = -2,
+    ARK_DDGI_E_NO_SCENE = -3,
+    ARK_DDGI_E_OUT_OF_MEMORY = -4,
+    ARK_DDGI_E_DEVICE = -5,
+    ARK_DDGI_E_UNSUPPORTED = -6,
+    ARK_DDGI_E_SIZE_MISMATCH = -7
+};
+
+/* Which DDGI resource an accessor refers to. */
+enum {
+    ARK_DDGI_ATLAS_IRRADIANCE = 0, /* RGBA16F, W_irr x H_irr texels, 8 B/texel */
+    ARK_DDGI_ATLAS_VISIBILITY = 1, /* RG16F,   W_vis x H_vis texels, 4 B/texel */
+    ARK_DDGI_SURFELS = 2,          /* RGBA16F, [slot][rays_per_probe] of the last update */
+    ARK_DDGI_PROBE_OFFSETS = 3     /* float4 per probe (xyz used; std430 vec3 stride 16) */
+};
+
+/* How the visibility atlas clear value (zFar, zFar^2) is stored in RG16F
+ * (DDGINode.cpp:92-94). zFar^2 = 1e8 overflows fp16. */
+enum {
+    ARK_DDGI_CLEAR_OVERFLOW_INF = 0,       /* IEEE RNE: +inf (default) */
+    ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE = 1 /* saturate to 65504 */
+};
+
+/* Texture formats for the bindless material/IES/environment textures. */
+enum {
+    ARK_TEX_RGBA8_UNORM = 0,
+    ARK_TEX_RGBA8_SRGB = 1, /* sRGB decode on fetch (baseColor/emissive/env) */
+    ARK_TEX_R32F = 2,       /* IES LUT (GpuScene.cpp:1101-1124) */
+    ARK_TEX_RGBA32F = 3     /* HDR environment */
+};
+
+enum {
+    ARK_WRAP_REPEAT = 0,
+    ARK_WRAP_CLAMP_TO_EDGE = 1
+};
+
+/* Grid + resource description (ProbeGrid.h:6-15, DDGIProbeGridData DDGIData.h:11-15). */
+typedef struct ArkDdgiDesc {
+    uint32_t struct_size;        /* sizeof(ArkDdgiDesc) */
+    int32_t grid_dims[3];        /* gridDimensions x (width), y (height), z (depth) */
+    float probe_spacing[3];      /* probeSpacing */
+    float offset_to_first[3];    /* offsetToFirst (world position of probe (0,0,0)) */
+    float z_far;                 /* camera far plane: visibility clear + miss distance */
+    int32_t max_rays_per_probe;  /* surfel image height; <= 512 */
+    int32_t max_probe_updates;   /* surfel image width (window capacity); reference: 4096 */
+    int32_t device;              /* HIP device ordinal */
+    int32_t clear_overflow_mode; /* ARK_DDGI_CLEAR_OVERFLOW_* */
+    int32_t shard_rank;          /* Z-slab owned by this context (0 when unsharded) */
+    int32_t shard_count;         /* number of Z-slabs (1 when unsharded); must divide grid_dims[2] */
+    int32_t reserved[4];
+} ArkDdgiDesc;
+
+/* RTVertex, scalar layout, 36 B (RTData.h:9-13 / NonPositionVertex SceneData.h). */
+typedef struct ArkRTVertex {
+    float tex_coord[2];
+    float normal[3];
+    float tangent[4];
+} ArkRTVertex;
+
+/* RTTriangleMesh, 12 B (RTData.h:15-19). */
+typedef struct ArkRTTriangleMesh {
+    int32_t first_vertex;
+    int32_t first_index;
+    int32_t material_index;
+} ArkRTTriangleMesh;
+
+/* ShaderMaterial, std430, 96 B (MaterialData.h:8-33). Texture fields index ArkDdgiScene.textures. */
+typedef struct ArkShaderMaterial {
+    int32_t base_color;
+    int32_t normal_map;
+    int32_t metallic_roughness;
+    int32_t emissive;
+    int32_t occlusion;
+    int32_t bent_normal_map;
+    float clearcoat;
+    float clearcoat_roughness;
+    int32_t blend_mode; /* ARK_BLEND_MODE_* */
+    float mask_cutoff;
+    float metallic_factor;
+    float roughness_factor;
+    float emissive_factor[3];
+    int32_t brdf;
+    float dielectric_reflectance;
+    float _unused[3];
+    float color_tint[4];
+} ArkShaderMaterial;
+
+typedef struct ArkTexture {
+    int32_t width;
+    int32_t height;
+    int32_t format; /* ARK_TEX_* */
+    int32_t wrap;   /* ARK_WRAP_* */
+    const void* data; /* tightly packed rows */
+} ArkTexture;
+
+/* One TLAS instance (GpuScene.cpp:901-928 / VulkanAccelerationStructureKHR.cpp:173-198):
+ * object-to-world 3x4 row-major, customInstanceId = RT mesh index, hit mask
+ * derived from the material blend mode, the BLAS = triangles of that mesh segment. */
+typedef struct ArkRTInstance {
+    float object_to_world[12];
+    uint32_t rt_mesh_index;
+    uint32_t triangle_count;
+    uint32_t hit_mask; /* ARK_RT_HIT_MASK_* */
+    uint32_t _pad;
+} ArkRTInstance;
+
+/* DirectionalLightData subset used by the closest hit (LightData.h:9-17); color is
+ * pre-multiplied by intensity * lightPreExposure as GpuScene does (GpuScene.cpp:811). */
+typedef struct ArkDirectionalLight {
+    float color[3];
+    float world_space_direction[3];
+} ArkDirectionalLight;
+
+/* SpotLightData subset (LightData.h:19-40; GpuScene.cpp:844-858). */
+typedef struct ArkSpotLight {
+    float color[3];
+    float world_space_direction[3];
+    float world_space_right[3];
+    float world_space_up[3];
+    float world_space_position[3];
+    float outer_cone_half_angle;
+    int32_t ies_profile_index; /* index into ArkDdgiScene.textures (R32F LUT) */
+    int32_t _pad;
+} ArkSpotLight;
+
+typedef struct ArkDdgiScene {
+    uint32_t struct_size;
+    const uint32_t* indices;  uint64_t index_count;   /* global u32 index pool, local to first_vertex */
+    const float* positions;   uint64_t vertex_count;  /* vec3 position pool (12 B/vertex) */
+    const ArkRTVertex* vertices;                      /* non-position pool, vertex_count entries */
+    const ArkRTTriangleMesh* meshes; uint32_t mesh_count;
+    const ArkShaderMaterial* materials; uint32_t material_count;
+    const ArkTexture* textures; uint32_t texture_count;
+    const ArkRTInstance* instances; uint32_t instance_count;
+    int32_t has_directional_light;
+    ArkDirectionalLight directional_light;
+    const ArkSpotLight* spot_lights; uint32_t spot_light_count;
+    int32_t environment_texture; /* index into textures; -1 = 1x1 white sRGB (GpuScene.cpp:1041-1048) */
+    int32_t reserved[4];
+} ArkDdgiScene;
+
+/* Per-frame inputs (the push constants of DDGINode.cpp:193-292). */
+typedef struct ArkDdgiFrameParams {
+    uint32_t struct_size;
+    uint32_t frame_index;        /* parameter1 / frameIdx */
+    uint32_t first_probe_index;  /* parameter3 / firstProbeIdx (window start) */
+    uint32_t probe_updates;      /* K = min(updatesPerFrame, N) */
+    uint32_t rays_per_probe;     /* parameter2 / raysPerProbe (R) */
+    float hysteresis_irradiance; /* 0 on the first frame (DDGINode.cpp:215) */
+    float hysteresis_visibility; /* 0 on the first frame (DDGINode.cpp:230) */
+    float visibility_sharpness;  /* default 50 */
+    float ambient_amount;        /* ambientLx * lightPreExposure */
+    float environment_multiplier;/* preExposedEnvironmentBrightnessFactor */
+    float delta_time;            /* AppState::deltaTime */
+    int32_t update_offsets;      /* m_computeProbeOffsets && m_applyProbeOffsets */
+    int32_t reserved[4];
+} ArkDdgiFrameParams;
+
+/* Work/traffic counters of the last update (counters are only collected when
+ * ark_ddgi_set_counting(ctx, 1); the timed path compiles them out). */
+typedef struct ArkDdgiCounters {
+    uint64_t rays;               /* probe rays traced (sum K*R over this context's probes) */
+    uint64_t probes;             /* probes updated */
+    uint64_t node_visits;        /* BVH2 nodes fetched, all traversals */
+    uint64_t tri_tests;          /* triangle records fetched, all traversals */
+    uint64_t hits;               /* probe rays with a hit */
+    uint64_t shadow_rays;        /* shadow rays traced */
+    uint64_t reserved[4];
+} ArkDdgiCounters;
+
+/* Device-side views of the persistent resources, for an external collective
+ * (the Z-slab all-gather) or interop. Pointers are HIP device pointers. */
+typedef struct ArkDdgiDeviceViews {
+    void* irradiance_atlas; uint64_t irradiance_bytes; int32_t irradiance_width, irradiance_height;
+    void* visibility_atlas; uint64_t visibility_bytes; int32_t visibility_width, visibility_height;
+    void* probe_offsets;    uint64_t probe_offsets_bytes;
+    uint64_t irradiance_slab_offset, irradiance_slab_bytes; /* this rank's Z-slab row band */
+    uint64_t visibility_slab_offset, visibility_slab_bytes;
+} ArkDdgiDeviceViews;
+
+typedef struct ArkDdgiCtx ArkDdgiCtx;
+
+int32_t ark_ddgi_abi_version(void);
+
+/* Allocates atlases (cleared as DDGINode.cpp:89-94), offsets (zeros, :96-99) and the
+ * surfel store (max_probe_updates x max_rays_per_probe, :107). Returns
+ * ARK_DDGI_E_NO_PROBE_GRID for an empty grid (DDGINode.cpp:78-81). */
+int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** out_ctx);
+void ark_ddgi_destroy(ArkDdgiCtx* ctx);
+const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx);
+
+/* Copies the scene arrays to HBM and builds the BVH (host arrays are not retained). */
+int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
+
+/* One DDGI update (DDGINode.cpp:171-298) enqueued on `hip_stream` (NULL = ctx stream).
+ * Asynchronous: call ark_ddgi_synchronize or synchronize the stream before reading. */
+int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
+int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
+
+/* Resource geometry and transfers (blocking, for tests / state save-load). */
+int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* out_bytes);
+int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);
+int ark_ddgi_write(ArkDdgiCtx* ctx, int which, const void* host_src, uint64_t bytes);
+int ark_ddgi_get_device_views(ArkDdgiCtx* ctx, ArkDdgiDeviceViews* out_views);
+
+/* Re-applies the creation-time clears (Registry created the textures anew). */
+int ark_ddgi_reset_history(ArkDdgiCtx* ctx);
+
+/* Counter collection (a separate instrumented traversal variant; off by default). */
+int ark_ddgi_set_counting(ArkDdgiCtx* ctx, int enabled);
+int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out_counters);
+
+/* Device time of the last update's kernels, from HIP events on the update stream:
+ * [0] whole update, [1] primary traversal, [2] shading+shadow rays, [3] probe
+ * update (irradiance+visibility), [4] borders+offsets. Milliseconds. */
+int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out_ms, int count);
+int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled);
+
+/* BVH statistics of the last set_scene (node count, leaf triangle count, depth, SAH cost, bytes). */
+typedef struct ArkDdgiBvhStats {
+    uint64_t node_count;
+    uint64_t triangle_count;
+    uint32_t max_depth;
+    uint32_t max_leaf_size;
+    float sah_cost;
+    float build_ms;
+    uint64_t node_bytes;
+    uint64_t triangle_bytes;
+} ArkDdgiBvhStats;
+int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ARK_DDGI_H */

@@ -1,0 +1,32 @@
+/*
+ * ark_ddgi_debug.h — diagnostic entry points of libark_ddgi (not used by the
+ * DDGI node). They exist so tests can pin the device side of the deterministic
+ * math (ark_fmath.h) against the CPU side bit for bit.
+ */
+#ifndef ARK_DDGI_DEBUG_H
+#define ARK_DDGI_DEBUG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Evaluates op (0 sin, 1 cos, 2 acos, 3 atan2(x,y), 4 log2, 5 exp2, 6 pow(x,y),
+ * 7 fp32->fp16->fp32 round trip) on `device` for n inputs (host arrays). */
+int ark_ddgi_debug_fmath(int device, int op, const float* x, const float* y, float* out, uint64_t n);
+
+/* Host-side evaluation of the same functions (for comparison with the device). */
+int ark_ddgi_debug_fmath_host(int op, const float* x, const float* y, float* out, uint64_t n);
+
+/* sizeof() of the ABI structs, in this order: ArkDdgiDesc, ArkRTVertex,
+ * ArkRTTriangleMesh, ArkShaderMaterial, ArkTexture, ArkRTInstance,
+ * ArkDirectionalLight, ArkSpotLight, ArkDdgiScene, ArkDdgiFrameParams,
+ * ArkDdgiCounters, ArkDdgiDeviceViews, ArkDdgiBvhStats. Returns the count written. */
+int ark_ddgi_debug_struct_sizes(uint32_t* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ARK_DDGI_DEBUG_H */

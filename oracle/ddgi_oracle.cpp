@@ -1,0 +1,1425 @@
+// ddgi_oracle.cpp — CPU restatement of Arkose's Vulkan-RT DDGI probe update.
+//
+// *** TEST INFRASTRUCTURE ONLY. ***  Only tests/, __graft_entry__.smoke() and the
+// cpu_baseline leg of bench.py may load this library, and only as the checker
+// (or the timed CPU baseline). The product path (libark_ddgi.so) never calls it.
+//
+// Parity status: the reference path is GLSL for Vulkan KHR ray tracing and cannot
+// be compiled or run in this pipeline (no Vulkan SDK / shader compiler / RT GPU;
+// SURVEY.md §8c), and the reference ships no golden vectors for this path. This
+// oracle is therefore pinned by (1) closed-form known-answer tests derived from the
+// reference formulas (tests/test_oracle_kat.py), (2) the reference's own in-tree
+// fp16 library half.hpp (oracle/_ref, fp16 RNE vectors), and (3) committed golden
+// fixtures it generates (tests/golden/). Against the Vulkan-RT node itself parity
+// is "partially pinned" (helpers + closed forms), not pinned by reference outputs.
+//
+// Every function cites the reference GLSL/C++ it restates. Semantics adopted where
+// the reference is undefined are listed in DESIGN.md §Parity hazards.
+//
+// Arithmetic rules (shared with the HIP kernels so that results are bit-exact):
+//  * compiled with -ffp-contract=off; vector expressions are evaluated per component
+//    left to right exactly as written in GLSL;
+//  * GLSL transcendentals use ark_fmath.h (same algorithm on CPU and GPU; accuracy
+//    vs libm pinned by tests/test_fmath.py);
+//  * max/min/clamp use fmaxf/fminf (IEEE maxNum) semantics;
+//  * every image store rounds fp32 -> fp16 with round-to-nearest-even; NaN is
+//    canonicalised to 0x7e00.
+//  * ray/triangle: Möller–Trumbore in world space (below); closest hit ties are
+//    broken by the smaller global triangle id so the result is BVH-independent.
+
+#include "../include/ark_ddgi.h"
+#include "../arkoserenderer_amd/csrc/ark_fmath.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <thread>
+#include <vector>
+
+using namespace ark;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// fp16 (RNE) — the storage format of the surfel image and both atlases
+// (DDGINode.cpp:90,94,107: RGBA16F / RG16F).
+// ---------------------------------------------------------------------------
+uint16_t f32_to_f16(float f)
+{
+    uint32_t x = f2u(f);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t ax = x & 0x7fffffffu;
+    if (ax > 0x7f800000u) return 0x7e00u;          // NaN (canonical)
+    if (ax >= 0x477ff000u) return sign | 0x7c00u;  // rounds to inf
+    if (ax < 0x33000000u) return sign;             // rounds to zero
+    uint32_t e = ax >> 23;
+    uint32_t m = (ax & 0x7fffffu) | 0x800000u;
+    if (e < 113u) {                                // half subnormal
+        uint32_t shift = 126u - e;
+        uint32_t q = m >> shift;
+        uint32_t rem = m & ((1u << shift) - 1u);
+        uint32_t half = 1u << (shift - 1u);
+        if (rem > half || (rem == half && (q & 1u))) q++;
+        return static_cast<uint16_t>(sign | q);
+    }
+    uint32_t c = ((e - 112u) << 10) | ((m >> 13) & 0x3ffu);
+    uint32_t rem = m & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (c & 1u))) c++;
+    return static_cast<uint16_t>(sign | c);
+}
+
+float f16_to_f32(uint16_t h)
+{
+    uint32_t sign = static_cast<uint32_t>(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1fu;
+    uint32_t m = h & 0x3ffu;
+    if (e == 0) {
+        if (m == 0) return u2f(sign);
+        // subnormal: m * 2^-24
+        float v = static_cast<float>(m) * 0x1p-24f;
+        return sign ? -v : v;
+    }
+    if (e == 31) return u2f(sign | 0x7f800000u | (m << 13));
+    return u2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+
+// ---------------------------------------------------------------------------
+// GLSL-like vector math (component-wise, left-to-right, no contraction)
+// ---------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+inline V3 v3(float x, float y, float z) { return { x, y, z }; }
+inline V3 operator+(V3 a, V3 b) { return { a.x + b.x, a.y + b.y, a.z + b.z }; }
+inline V3 operator-(V3 a, V3 b) { return { a.x - b.x, a.y - b.y, a.z - b.z }; }
+inline V3 operator-(V3 a) { return { -a.x, -a.y, -a.z }; }
+inline V3 operator*(V3 a, V3 b) { return { a.x * b.x, a.y * b.y, a.z * b.z }; }
+inline V3 operator*(V3 a, float s) { return { a.x * s, a.y * s, a.z * s }; }
+inline V3 operator*(float s, V3 a) { return { s * a.x, s * a.y, s * a.z }; }
+inline V3 operator/(V3 a, float s) { return { a.x / s, a.y / s, a.z / s }; }
+inline V3 operator/(V3 a, V3 b) { return { a.x / b.x, a.y / b.y, a.z / b.z }; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 a, V3 b) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x }; }
+inline float length(V3 a) { return sqrtf_(dot(a, a)); }
+// GLSL normalize(v) = v * inversesqrt(dot(v,v)); restated as v * (1/sqrt(dot)).
+inline V3 normalize(V3 a) { float s = 1.0f / sqrtf_(dot(a, a)); return a * s; }
+inline float saturate(float x) { return fminf_(fmaxf_(x, 0.0f), 1.0f); }
+inline float clampf(float x, float lo, float hi) { return fminf_(fmaxf_(x, lo), hi); }
+inline float square(float x) { return x * x; }
+// GLSL mix(x, y, a) = x * (1 - a) + y * a
+inline float mixf(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+inline V3 mix3(V3 x, V3 y, float a) { return { mixf(x.x, y.x, a), mixf(x.y, y.y, a), mixf(x.z, y.z, a) }; }
+inline V3 pow3(V3 v, float e) { return { powf_(v.x, e), powf_(v.y, e), powf_(v.z, e) }; }
+inline V3 splat(float s) { return { s, s, s }; }
+
+// ---------------------------------------------------------------------------
+// RNG + sampling helpers
+// ---------------------------------------------------------------------------
+// common/random.glsl:40-48
+uint32_t wang_hash(uint32_t seed)
+{
+    seed = (seed ^ 61u) ^ (seed >> 16);
+    seed *= 9u;
+    seed = seed ^ (seed >> 4);
+    seed *= 0x27d4eb2du;
+    seed = seed ^ (seed >> 15);
+    return seed;
+}
+// common/random.glsl:25-32
+uint32_t rand_xorshift(uint32_t state)
+{
+    state ^= (state << 13);
+    state ^= (state >> 17);
+    state ^= (state << 5);
+    return state;
+}
+struct Rng {
+    uint32_t state;
+    explicit Rng(uint32_t seed) : state(wang_hash(seed)) {} // seedRandom, random.glsl:53-56
+    float randomFloat() // random.glsl:58-61
+    {
+        state = rand_xorshift(state);
+        return static_cast<float>(state) * (1.0f / 4294967296.0f);
+    }
+    V3 randomPointOnSphere() // random.glsl:63-74
+    {
+        float theta = kTwoPi * randomFloat();
+        float u = 2.0f * randomFloat() - 1.0f;
+        float sr = sqrtf_(1.0f - u * u);
+        float s, c;
+        sincosf_(theta, &s, &c);
+        return { sr * c, sr * s, u };
+    }
+};
+
+// common.glsl:121-130
+V3 sphericalFibonacciSample(uint32_t i, uint32_t n)
+{
+    float theta = kTwoPi * static_cast<float>(i) / kGoldenRatio;
+    float phi = acosf_(2.0f * (static_cast<float>(i) / static_cast<float>(n)) - 1.0f);
+    float sinPhi = sinf_(phi);
+    float st, ct;
+    sincosf_(theta, &st, &ct);
+    return { ct * sinPhi, st * sinPhi, cosf_(phi) };
+}
+
+// common.glsl:133-142 (Rodrigues)
+V3 axisAngleRotate(V3 v, V3 k, float angle)
+{
+    float s, c;
+    sincosf_(angle, &s, &c);
+    return v * c + cross(k, v) * s + k * dot(k, v) * (1.0f - c);
+}
+
+// ddgi/common.glsl:12-25
+V3 calculateRotatedSphericalFibonacciSample(uint32_t probeIdx, uint32_t sampleIdx, uint32_t sampleCount, uint32_t frameIdx)
+{
+    V3 sampleDir = sphericalFibonacciSample(sampleIdx, sampleCount);
+    const uint32_t paramSpacing = 512u;
+    Rng rng(paramSpacing * probeIdx + frameIdx % paramSpacing);
+    V3 axis = rng.randomPointOnSphere();
+    float angle = kTwoPi * rng.randomFloat();
+    return axisAngleRotate(sampleDir, axis, angle);
+}
+
+// common/octahedral.glsl:10-19
+inline float signNotZero(float f) { return (f >= 0.0f) ? 1.0f : -1.0f; }
+
+// common/octahedral.glsl:23-31
+void octahedralEncode(V3 v, float* ox, float* oy)
+{
+    float l1norm = fabsf_(v.x) + fabsf_(v.y) + fabsf_(v.z);
+    float inv = 1.0f / l1norm;
+    float rx = v.x * inv, ry = v.y * inv;
+    if (v.z < 0.0f) {
+        float nx = (1.0f - fabsf_(ry)) * signNotZero(rx);
+        float ny = (1.0f - fabsf_(rx)) * signNotZero(ry);
+        rx = nx;
+        ry = ny;
+    }
+    *ox = rx;
+    *oy = ry;
+}
+
+// common/octahedral.glsl:35-41
+V3 octahedralDecode(float ox, float oy)
+{
+    V3 v = { ox, oy, 1.0f - fabsf_(ox) - fabsf_(oy) };
+    if (v.z < 0.0f) {
+        float nx = (1.0f - fabsf_(v.y)) * signNotZero(v.x);
+        float ny = (1.0f - fabsf_(v.x)) * signNotZero(v.y);
+        v.x = nx;
+        v.y = ny;
+    }
+    return normalize(v);
+}
+
+// common/spherical.glsl:6-13
+void sphericalUvFromDirection(V3 d, float* u, float* v)
+{
+    float phi = atan2f_(d.z, d.x);
+    float theta = acosf_(clampf(d.y, -1.0f, 1.0f));
+    if (phi < 0.0f) phi += kTwoPi;
+    *u = phi / kTwoPi;
+    *v = theta / kPi;
+}
+
+// ---------------------------------------------------------------------------
+// Probe grid addressing (ddgi/common.glsl:36-77)
+// ---------------------------------------------------------------------------
+struct Grid {
+    int X, Y, Z;
+    V3 spacing, origin;
+    int N() const { return X * Y * Z; }
+};
+// ddgi/common.glsl:36-51 : sheetIdx = y, sheetCoord = (x, z)
+inline void probeCoord(const Grid& g, uint32_t probeIdx, int* x, int* y, int* z)
+{
+    uint32_t tilesPerSheet = static_cast<uint32_t>(g.X * g.Z);
+    uint32_t sheetProbeIdx = probeIdx % tilesPerSheet;
+    *y = static_cast<int>(probeIdx / tilesPerSheet);
+    *x = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(g.X));
+    *z = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(g.X));
+}
+// ddgi/common.glsl:53-67
+inline void atlasTexelCoord(const Grid& g, uint32_t probeIdx, int tx, int ty, int res, int pad, int* ax, int* ay)
+{
+    int x, y, z;
+    probeCoord(g, probeIdx, &x, &y, &z);
+    int tileX = x + y * g.X, tileY = z;
+    *ax = pad + tileX * (res + 2 * pad) + tx;
+    *ay = pad + tileY * (res + 2 * pad) + ty;
+}
+// ddgi/common.glsl:69-77
+inline V3 probePosition(const Grid& g, uint32_t probeIdx)
+{
+    int x, y, z;
+    probeCoord(g, probeIdx, &x, &y, &z);
+    V3 c = { static_cast<float>(x), static_cast<float>(y), static_cast<float>(z) };
+    return g.origin + c * g.spacing;
+}
+
+// ---------------------------------------------------------------------------
+// Textures: bilinear, LOD 0, fp32 lerp; sRGB decode per texel before filtering.
+// ---------------------------------------------------------------------------
+struct Tex {
+    int w = 1, h = 1, fmt = ARK_TEX_RGBA8_SRGB, wrap = ARK_WRAP_REPEAT;
+    std::vector<float> rgba; // decoded texels, 4 floats each
+};
+
+float srgbToLinear(float c)
+{
+    return c <= 0.04045f ? c / 12.92f : powf_((c + 0.055f) / 1.055f, 2.4f);
+}
+
+Tex makeTex(const ArkTexture& t)
+{
+    Tex r;
+    r.w = t.width;
+    r.h = t.height;
+    r.fmt = t.format;
+    r.wrap = t.wrap;
+    size_t n = static_cast<size_t>(t.width) * t.height;
+    r.rgba.resize(n * 4);
+    for (size_t i = 0; i < n; ++i) {
+        for (int c = 0; c < 4; ++c) {
+            float v = 0.0f;
+            switch (t.format) {
+            case ARK_TEX_RGBA8_UNORM:
+                v = static_cast<float>(static_cast<const uint8_t*>(t.data)[i * 4 + c]) / 255.0f;
+                break;
+            case ARK_TEX_RGBA8_SRGB:
+                v = static_cast<float>(static_cast<const uint8_t*>(t.data)[i * 4 + c]) / 255.0f;
+                if (c < 3) v = srgbToLinear(v);
+                break;
+            case ARK_TEX_R32F:
+                v = c == 0 ? static_cast<const float*>(t.data)[i] : (c == 3 ? 1.0f : 0.0f);
+                break;
+            case ARK_TEX_RGBA32F:
+                v = static_cast<const float*>(t.data)[i * 4 + c];
+                break;
+            }
+            r.rgba[i * 4 + c] = v;
+        }
+    }
+    return r;
+}
+
+Tex whiteSrgbPixel()
+{
+    Tex r;
+    r.rgba = { 1.0f, 1.0f, 1.0f, 1.0f };
+    return r;
+}
+
+inline int wrapCoord(int i, int n, int wrap)
+{
+    if (wrap == ARK_WRAP_CLAMP_TO_EDGE) return std::min(std::max(i, 0), n - 1);
+    int m = i % n;
+    return m < 0 ? m + n : m;
+}
+inline float lerpf(float a, float b, float t) { return a + (b - a) * t; }
+
+void sampleBilinear(const Tex& t, float u, float v, float out[4])
+{
+    float x = u * static_cast<float>(t.w) - 0.5f;
+    float y = v * static_cast<float>(t.h) - 0.5f;
+    float x0f = floorf_(x), y0f = floorf_(y);
+    float fx = x - x0f, fy = y - y0f;
+    int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
+    int xa = wrapCoord(x0, t.w, t.wrap), xb = wrapCoord(x0 + 1, t.w, t.wrap);
+    int ya = wrapCoord(y0, t.h, t.wrap), yb = wrapCoord(y0 + 1, t.h, t.wrap);
+    const float* t00 = &t.rgba[(static_cast<size_t>(ya) * t.w + xa) * 4];
+    const float* t10 = &t.rgba[(static_cast<size_t>(ya) * t.w + xb) * 4];
+    const float* t01 = &t.rgba[(static_cast<size_t>(yb) * t.w + xa) * 4];
+    const float* t11 = &t.rgba[(static_cast<size_t>(yb) * t.w + xb) * 4];
+    for (int c = 0; c < 4; ++c)
+        out[c] = lerpf(lerpf(t00[c], t10[c], fx), lerpf(t01[c], t11[c], fx), fy);
+}
+
+// Atlas fetch: linear filter, clamp to edge (DDGINode.cpp:313), fp16 texels.
+// `ch` = channels per texel in storage (4 for irradiance, 2 for visibility).
+void sampleAtlas(const std::vector<uint16_t>& atlas, int W, int H, int ch, float u, float v, float* out, int nout)
+{
+    float x = u * static_cast<float>(W) - 0.5f;
+    float y = v * static_cast<float>(H) - 0.5f;
+    float x0f = floorf_(x), y0f = floorf_(y);
+    float fx = x - x0f, fy = y - y0f;
+    int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
+    int xa = std::min(std::max(x0, 0), W - 1), xb = std::min(std::max(x0 + 1, 0), W - 1);
+    int ya = std::min(std::max(y0, 0), H - 1), yb = std::min(std::max(y0 + 1, 0), H - 1);
+    for (int c = 0; c < nout; ++c) {
+        float t00 = f16_to_f32(atlas[(static_cast<size_t>(ya) * W + xa) * ch + c]);
+        float t10 = f16_to_f32(atlas[(static_cast<size_t>(ya) * W + xb) * ch + c]);
+        float t01 = f16_to_f32(atlas[(static_cast<size_t>(yb) * W + xa) * ch + c]);
+        float t11 = f16_to_f32(atlas[(static_cast<size_t>(yb) * W + xb) * ch + c]);
+        out[c] = lerpf(lerpf(t00, t10, fx), lerpf(t01, t11, fx), fy);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Scene (world-space triangles) + BVH (independent of the product's builder)
+// ---------------------------------------------------------------------------
+struct WTri {
+    V3 v0, e1, e2;
+    uint32_t inst, prim, gid;
+    uint32_t flip; // instance transform with negative determinant inverts facing
+};
+
+struct Box {
+    V3 lo, hi;
+};
+inline Box emptyBox() { return { splat(INFINITY), splat(-INFINITY) }; }
+inline void grow(Box& b, V3 p)
+{
+    b.lo = { std::min(b.lo.x, p.x), std::min(b.lo.y, p.y), std::min(b.lo.z, p.z) };
+    b.hi = { std::max(b.hi.x, p.x), std::max(b.hi.y, p.y), std::max(b.hi.z, p.z) };
+}
+inline void grow(Box& b, const Box& o) { grow(b, o.lo); grow(b, o.hi); }
+inline float area(const Box& b)
+{
+    V3 d = b.hi - b.lo;
+    if (d.x < 0) return 0.0f;
+    return 2.0f * (d.x * d.y + d.y * d.z + d.z * d.x);
+}
+
+struct BNode {
+    Box box;
+    int32_t left = -1, right = -1; // internal when left >= 0
+    uint32_t first = 0, count = 0;
+};
+
+struct Bvh {
+    std::vector<BNode> nodes;
+    std::vector<uint32_t> order; // indices into the triangle array
+    bool empty() const { return nodes.empty(); }
+};
+
+struct BuildItem {
+    Box box;
+    V3 c;
+};
+
+struct BuildCtx {
+    Bvh* bvh;
+    std::vector<BuildItem>* items;
+    std::atomic<uint32_t> nodeCounter { 0 };
+    std::atomic<int> threadsLeft { 0 };
+};
+
+void buildNode(BuildCtx& ctx, uint32_t nodeIdx, uint32_t first, uint32_t count)
+{
+    Bvh& bvh = *ctx.bvh;
+    std::vector<BuildItem>& items = *ctx.items;
+    Box b = emptyBox(), cb = emptyBox();
+    for (uint32_t i = first; i < first + count; ++i) {
+        grow(b, items[bvh.order[i]].box);
+        grow(cb, items[bvh.order[i]].c);
+    }
+    BNode& node = bvh.nodes[nodeIdx];
+    node.box = b;
+    if (count <= 4) {
+        node.first = first;
+        node.count = count;
+        return;
+    }
+    // binned SAH on the axis of largest centroid extent
+    V3 ext = cb.hi - cb.lo;
+    int axis = (ext.x >= ext.y && ext.x >= ext.z) ? 0 : (ext.y >= ext.z ? 1 : 2);
+    float lo = axis == 0 ? cb.lo.x : axis == 1 ? cb.lo.y : cb.lo.z;
+    float e = axis == 0 ? ext.x : axis == 1 ? ext.y : ext.z;
+    uint32_t mid = first + count / 2;
+    if (e > 0.0f) {
+        constexpr int NB = 16;
+        Box bb[NB];
+        uint32_t bc[NB] = {};
+        for (int i = 0; i < NB; ++i) bb[i] = emptyBox();
+        float scale = NB / e;
+        auto binOf = [&](uint32_t idx) {
+            const V3& c = items[idx].c;
+            float v = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
+            int k = static_cast<int>((v - lo) * scale);
+            return std::min(std::max(k, 0), NB - 1);
+        };
+        for (uint32_t i = first; i < first + count; ++i) {
+            int k = binOf(bvh.order[i]);
+            bc[k]++;
+            grow(bb[k], items[bvh.order[i]].box);
+        }
+        float best = INFINITY;
+        int bestK = -1;
+        Box accL = emptyBox();
+        uint32_t nL = 0;
+        float leftCost[NB];
+        for (int k = 0; k < NB - 1; ++k) {
+            grow(accL, bb[k]);
+            nL += bc[k];
+            leftCost[k] = area(accL) * static_cast<float>(nL);
+        }
+        Box accR = emptyBox();
+        uint32_t nR = 0;
+        for (int k = NB - 1; k > 0; --k) {
+            grow(accR, bb[k]);
+            nR += bc[k];
+            float cst = leftCost[k - 1] + area(accR) * static_cast<float>(nR);
+            if (nR > 0 && nR < count && cst < best) {
+                best = cst;
+                bestK = k;
+            }
+        }
+        if (bestK > 0) {
+            auto it = std::partition(bvh.order.begin() + first, bvh.order.begin() + first + count,
+                                     [&](uint32_t idx) { return binOf(idx) < bestK; });
+            mid = static_cast<uint32_t>(it - bvh.order.begin());
+        }
+        if (mid == first || mid == first + count) mid = first + count / 2;
+    }
+    uint32_t l = ctx.nodeCounter.fetch_add(2);
+    node.left = static_cast<int32_t>(l);
+    node.right = static_cast<int32_t>(l + 1);
+    uint32_t nl = mid - first, nr = first + count - mid;
+    if (count > 200000 && ctx.threadsLeft.fetch_sub(1) > 0) {
+        std::thread t([&ctx, l, first, nl] { buildNode(ctx, l, first, nl); });
+        buildNode(ctx, l + 1, mid, nr);
+        t.join();
+    } else {
+        buildNode(ctx, l, first, nl);
+        buildNode(ctx, l + 1, mid, nr);
+    }
+}
+
+Bvh buildBvh(const std::vector<WTri>& tris, const std::vector<uint32_t>& subset, int threads)
+{
+    Bvh bvh;
+    if (subset.empty()) return bvh;
+    std::vector<BuildItem> items(tris.size());
+    for (uint32_t idx : subset) {
+        const WTri& t = tris[idx];
+        Box b = emptyBox();
+        V3 v1 = t.v0 + t.e1, v2 = t.v0 + t.e2;
+        grow(b, t.v0);
+        grow(b, v1);
+        grow(b, v2);
+        items[idx].box = b;
+        items[idx].c = (b.lo + b.hi) * 0.5f;
+    }
+    bvh.order = subset;
+    bvh.nodes.resize(2 * subset.size());
+    BuildCtx ctx;
+    ctx.bvh = &bvh;
+    ctx.items = &items;
+    ctx.nodeCounter = 1;
+    ctx.threadsLeft = threads;
+    buildNode(ctx, 0, 0, static_cast<uint32_t>(subset.size()));
+    bvh.nodes.resize(ctx.nodeCounter.load());
+    // conservative inflation so that fp32 slab tests never cull an exact triangle hit
+    for (BNode& n : bvh.nodes) {
+        V3 d = n.box.hi - n.box.lo;
+        float m = std::max(std::max(fabsf(n.box.lo.x), fabsf(n.box.hi.x)), std::max(std::max(fabsf(n.box.lo.y), fabsf(n.box.hi.y)), std::max(fabsf(n.box.lo.z), fabsf(n.box.hi.z))));
+        float eps = m * 1e-6f + 1e-6f + 1e-5f * std::max(d.x, std::max(d.y, d.z));
+        n.box.lo = n.box.lo - splat(eps);
+        n.box.hi = n.box.hi + splat(eps);
+    }
+    return bvh;
+}
+
+struct Ray {
+    V3 o, d;
+    float tmin, tmax;
+};
+
+// Möller–Trumbore (shared exact op order with the HIP kernel ddgi_trace.hip).
+// Front face iff det > 0 (i.e. dot(cross(e1,e2), d) < 0: CCW seen from the ray
+// origin, Vulkan/DXR algebraic convention).
+inline bool intersectTri(const Ray& r, const WTri& t, float tmax, float* outT, float* outU, float* outV, bool* backface)
+{
+    V3 p = cross(r.d, t.e2);
+    float det = dot(t.e1, p);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    V3 s = r.o - t.v0;
+    float u = dot(s, p) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return false;
+    V3 q = cross(s, t.e1);
+    float v = dot(r.d, q) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+    float tt = dot(t.e2, q) * inv;
+    if (!(tt >= r.tmin && tt <= tmax)) return false;
+    *outT = tt;
+    *outU = u;
+    *outV = v;
+    *backface = (det < 0.0f) != (t.flip != 0);
+    return true;
+}
+
+inline bool boxHit(const Box& b, V3 o, V3 inv, float tmin, float tmax)
+{
+    float tx0 = (b.lo.x - o.x) * inv.x, tx1 = (b.hi.x - o.x) * inv.x;
+    float ty0 = (b.lo.y - o.y) * inv.y, ty1 = (b.hi.y - o.y) * inv.y;
+    float tz0 = (b.lo.z - o.z) * inv.z, tz1 = (b.hi.z - o.z) * inv.z;
+    float tn = std::max(std::max(std::min(tx0, tx1), std::min(ty0, ty1)), std::max(std::min(tz0, tz1), tmin));
+    float tf = std::min(std::min(std::max(tx0, tx1), std::max(ty0, ty1)), std::min(std::max(tz0, tz1), tmax));
+    return tn <= tf * 1.00001f + 1e-7f;
+}
+
+inline V3 safeInv(V3 d)
+{
+    auto f = [](float x) { return 1.0f / (fabsf(x) < 1e-20f ? (x < 0 ? -1e-20f : 1e-20f) : x); };
+    return { f(d.x), f(d.y), f(d.z) };
+}
+
+struct Hit {
+    bool hit = false;
+    float t = 0, u = 0, v = 0;
+    uint32_t tri = 0; // index into triangle array
+    bool backface = false;
+};
+
+struct Stats {
+    uint64_t nodes = 0, tris = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Oracle context
+// ---------------------------------------------------------------------------
+struct Oracle {
+    ArkDdgiDesc desc {};
+    Grid g {};
+    int Wi = 0, Hi = 0, Wv = 0, Hv = 0;
+    std::vector<uint16_t> irr, vis;    // atlases (RGBA16F, RG16F)
+    std::vector<float> offsets;        // N x 4
+    std::vector<uint16_t> surfels;     // [slot][R_max] x 4
+    int Rmax = 0, Kmax = 0;
+    // scene
+    bool hasScene = false;
+    std::vector<WTri> tris;
+    Bvh bvhOpaque, bvhMasked, bvhBlend;
+    std::vector<uint32_t> indices;
+    std::vector<ArkRTVertex> vertices;
+    std::vector<ArkRTTriangleMesh> meshes;
+    std::vector<ArkShaderMaterial> materials;
+    std::vector<Tex> textures;
+    std::vector<ArkRTInstance> instances;
+    Tex envWhite;
+    int envTex = -1;
+    bool hasSun = false;
+    ArkDirectionalLight sun {};
+    std::vector<ArkSpotLight> spots;
+    Stats stats;
+};
+
+// Closest-hit traversal within one BVH (mask class), masked pass applies the
+// any-hit alpha test of masked.rahit:16-37.
+void traverseClosest(const Oracle& o, const Bvh& bvh, const Ray& r, Hit& best, bool alphaTest, Stats& st);
+bool traverseAny(const Oracle& o, const Bvh& bvh, const Ray& r, Stats& st);
+
+const Tex& texOf(const Oracle& o, int idx) { return (idx >= 0 && idx < static_cast<int>(o.textures.size())) ? o.textures[idx] : o.envWhite; }
+
+struct Attribs {
+    const ArkRTTriangleMesh* mesh;
+    const ArkShaderMaterial* mat;
+    const ArkRTVertex* v[3];
+};
+Attribs fetchAttribs(const Oracle& o, const WTri& t)
+{
+    Attribs a;
+    const ArkRTInstance& inst = o.instances[t.inst];
+    a.mesh = &o.meshes[inst.rt_mesh_index];
+    a.mat = &o.materials[a.mesh->material_index];
+    for (int k = 0; k < 3; ++k) {
+        uint32_t idx = o.indices[static_cast<size_t>(a.mesh->first_index) + 3u * t.prim + k];
+        a.v[k] = &o.vertices[static_cast<size_t>(a.mesh->first_vertex) + idx];
+    }
+    return a;
+}
+
+// masked.rahit:16-37 — returns true if the candidate is accepted
+bool alphaAccept(const Oracle& o, const WTri& t, float u, float v)
+{
+    Attribs a = fetchAttribs(o, t);
+    float bx = 1.0f - u - v, by = u, bz = v;
+    float uvx = a.v[0]->tex_coord[0] * bx + a.v[1]->tex_coord[0] * by + a.v[2]->tex_coord[0] * bz;
+    float uvy = a.v[0]->tex_coord[1] * bx + a.v[1]->tex_coord[1] * by + a.v[2]->tex_coord[1] * bz;
+    float c[4];
+    sampleBilinear(texOf(o, a.mat->base_color), uvx, uvy, c);
+    return !(c[3] < a.mat->mask_cutoff);
+}
+
+void traverseClosest(const Oracle& o, const Bvh& bvh, const Ray& r, Hit& best, bool alphaTest, Stats& st)
+{
+    if (bvh.empty()) return;
+    V3 inv = safeInv(r.d);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const BNode& n = bvh.nodes[stack[--sp]];
+        st.nodes++;
+        float tmax = best.hit ? best.t : r.tmax;
+        if (!boxHit(n.box, r.o, inv, r.tmin, tmax)) continue;
+        if (n.left < 0) {
+            for (uint32_t i = n.first; i < n.first + n.count; ++i) {
+                uint32_t ti = bvh.order[i];
+                const WTri& t = o.tris[ti];
+                st.tris++;
+                float tt, u, v;
+                bool bf;
+                float cur = best.hit ? best.t : r.tmax;
+                if (!intersectTri(r, t, cur, &tt, &u, &v, &bf)) continue;
+                if (best.hit && tt == best.t && t.gid > o.tris[best.tri].gid) continue; // tie: smaller id wins
+                if (alphaTest && !alphaAccept(o, t, u, v)) continue;
+                best.hit = true;
+                best.t = tt;
+                best.u = u;
+                best.v = v;
+                best.tri = ti;
+                best.backface = bf;
+            }
+        } else {
+            if (sp + 2 > 128) { std::fprintf(stderr, "oracle: BVH stack overflow\n"); std::abort(); }
+            stack[sp++] = static_cast<uint32_t>(n.right);
+            stack[sp++] = static_cast<uint32_t>(n.left);
+        }
+    }
+}
+
+bool traverseAny(const Oracle& o, const Bvh& bvh, const Ray& r, Stats& st)
+{
+    if (bvh.empty()) return false;
+    V3 inv = safeInv(r.d);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const BNode& n = bvh.nodes[stack[--sp]];
+        st.nodes++;
+        if (!boxHit(n.box, r.o, inv, r.tmin, r.tmax)) continue;
+        if (n.left < 0) {
+            for (uint32_t i = n.first; i < n.first + n.count; ++i) {
+                st.tris++;
+                float tt, u, v;
+                bool bf;
+                if (intersectTri(r, o.tris[bvh.order[i]], r.tmax, &tt, &u, &v, &bf)) return true;
+            }
+        } else {
+            if (sp + 2 > 128) { std::fprintf(stderr, "oracle: BVH stack overflow\n"); std::abort(); }
+            stack[sp++] = static_cast<uint32_t>(n.right);
+            stack[sp++] = static_cast<uint32_t>(n.left);
+        }
+    }
+    return false;
+}
+
+// opaque.rchit:35-54 — TerminateOnFirstHit | SkipClosestHit | Opaque, cullMask 0xff,
+// tmin 0.025: any geometry of any hit-mask class occludes.
+float traceShadowRay(const Oracle& o, V3 X, V3 L, float maxDistance, Stats& st)
+{
+    Ray r { X, L, 0.025f, maxDistance };
+    if (!(r.tmax >= r.tmin)) return 1.0f; // empty interval: the miss shader runs
+    if (traverseAny(o, o.bvhOpaque, r, st) || traverseAny(o, o.bvhMasked, r, st) || traverseAny(o, o.bvhBlend, r, st))
+        return 0.0f;
+    return 1.0f;
+}
+
+// --- brdf.glsl:17-148 -------------------------------------------------------
+const float DIELECTRIC_REFLECTANCE = 0.04f; // brdf.glsl:6
+
+float D_GGX(float NdotH, float a) // brdf.glsl:17-22
+{
+    float a2 = a * a;
+    float f = (NdotH * a2 - NdotH) * NdotH + 1.0f;
+    float x = a2 / (kPi * f * f + 1e-20f);
+    return x;
+}
+float F_Schlick1(float VdotH, float f0) { return f0 + (1.0f - f0) * powf_(1.0f - VdotH, 5.0f); } // :24-26
+V3 F_Schlick3(float VdotH, V3 f0) // :28-30
+{
+    float p = powf_(1.0f - VdotH, 5.0f);
+    return f0 + (splat(1.0f) - f0) * p;
+}
+float V_SmithGGXCorrelated(float NdotV, float NdotL, float a) // :43-48
+{
+    float a2 = a * a;
+    float GGXL = NdotV * sqrtf_((-NdotL * a2 + NdotL) * NdotL + a2);
+    float GGXV = NdotL * sqrtf_((-NdotV * a2 + NdotV) * NdotV + a2);
+    return 0.5f / (GGXV + GGXL + 1e-20f);
+}
+float V_Kelemen(float LdotH) { return 0.25f / square(LdotH); } // :50-53
+float clearcoatBRDF(V3 L, V3 V, V3 N, float strength, float rough, float* F) // :55-68
+{
+    V3 H = normalize(L + V);
+    float NdotH = saturate(dot(N, H));
+    float LdotH = saturate(dot(L, H));
+    float a = square(clampf(rough, 0.1f, 1.0f));
+    float D = D_GGX(NdotH, a);
+    float Vv = V_Kelemen(LdotH);
+    *F = F_Schlick1(LdotH, DIELECTRIC_REFLECTANCE) * strength;
+    return D * Vv * *F;
+}
+V3 specularBRDF(V3 L, V3 V, V3 N, V3 baseColor, float roughness, float metallic, V3* F) // :70-89
+{
+    V3 H = normalize(L + V);
+    float NdotV = fabsf_(dot(N, V)) + 1e-5f;
+    float NdotL = clampf(dot(N, L), 0.0f, 1.0f);
+    float NdotH = clampf(dot(N, H), 0.0f, 1.0f);
+    float LdotH = clampf(dot(L, H), 0.0f, 1.0f);
+    float a = square(roughness);
+    V3 f0 = mix3(splat(DIELECTRIC_REFLECTANCE), baseColor, metallic);
+    *F = F_Schlick3(LdotH, f0);
+    float D = D_GGX(NdotH, a);
+    float Vv = V_SmithGGXCorrelated(NdotV, NdotL, a);
+    return *F * D * Vv;
+}
+V3 evaluateDefaultBRDF(V3 L, V3 V, V3 N, V3 baseColor, float roughness, float metallic, float clearcoat, float ccRough) // :132-148
+{
+    float F_c;
+    float Fr_c = clearcoatBRDF(L, V, N, clearcoat, ccRough, &F_c);
+    V3 F_s;
+    V3 Fr_s = specularBRDF(L, V, N, baseColor, roughness, metallic, &F_s);
+    V3 diffuseColor = splat(1.0f - metallic) * baseColor;
+    V3 Fr_d = diffuseColor * splat(1.0f / kPi);
+    V3 brdf = (Fr_d * (splat(1.0f) - F_s) + Fr_s) * (1.0f - F_c) + splat(Fr_c);
+    return brdf;
+}
+
+// lighting.glsl:20-39
+float evaluateIESLookupTable(const Tex& lut, float outerConeHalfAngle, V3 m0, V3 m1, V3 m2, V3 lightRayDir)
+{
+    float angleV = dot(lightRayDir, m2);
+    if (angleV <= 0.0f) return 0.0f;
+    float hx = dot(lightRayDir, m0);
+    float hy = dot(lightRayDir, m1);
+    float angleH = atan2f_(hy, hx) + kPi;
+    float lx = acosf_(angleV) / (2.0f * outerConeHalfAngle);
+    float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
+    float c[4];
+    sampleBilinear(lut, lx, ly, c);
+    return c[0];
+}
+
+struct Surface {
+    V3 color;       // payload.color
+    float hitT;     // payload.hitT (signed: negative for backface)
+    V3 baseColor, normal;
+    float roughness, metallic;
+};
+
+// opaque.rchit:105-176 (RT_EVALUATE_DIRECT_LIGHT=1, RT_USE_EXTENDED_RAY_PAYLOAD=1)
+Surface closestHit(const Oracle& o, const Ray& ray, const Hit& h, float ambientAmount, Stats& st, bool shade)
+{
+    Surface s {};
+    const WTri& t = o.tris[h.tri];
+    s.hitT = h.backface ? -h.t : h.t;
+    if (!shade) return s; // backface: raygen overwrites the colour with 0 (raygen.rgen:208-213)
+    Attribs a = fetchAttribs(o, t);
+    const ArkShaderMaterial& mat = *a.mat;
+    const ArkRTInstance& inst = o.instances[t.inst];
+    float bx = 1.0f - h.u - h.v, by = h.u, bz = h.v;
+    auto n3 = [&](int k) { return v3(a.v[k]->normal[0], a.v[k]->normal[1], a.v[k]->normal[2]); };
+    V3 N = normalize(n3(0) * bx + n3(1) * by + n3(2) * bz);
+    N = h.backface ? -N : N;
+    const float* M = inst.object_to_world; // rows; mat3(ObjectToWorld) * N
+    V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
+    N = normalize(Nw);
+    float uvx = a.v[0]->tex_coord[0] * bx + a.v[1]->tex_coord[0] * by + a.v[2]->tex_coord[0] * bz;
+    float uvy = a.v[0]->tex_coord[1] * bx + a.v[1]->tex_coord[1] * by + a.v[2]->tex_coord[1] * bz;
+    float c[4];
+    sampleBilinear(texOf(o, mat.base_color), uvx, uvy, c);
+    V3 baseColor = v3(c[0], c[1], c[2]) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
+    sampleBilinear(texOf(o, mat.emissive), uvx, uvy, c);
+    V3 emissive = v3(c[0], c[1], c[2]) * v3(mat.emissive_factor[0], mat.emissive_factor[1], mat.emissive_factor[2]);
+    sampleBilinear(texOf(o, mat.metallic_roughness), uvx, uvy, c);
+    float metallic = c[2] * mat.metallic_factor;
+    float roughness = c[1] * mat.roughness_factor;
+    float clearcoat = mat.clearcoat, ccRough = mat.clearcoat_roughness;
+    V3 V = -ray.d;
+    V3 ambient = ambientAmount * baseColor;
+    V3 color = emissive + ambient;
+    V3 hitPoint = ray.o + h.t * ray.d; // rt_WorldRayOrigin + rt_RayHitT * rt_WorldRayDirection
+    float zFar = o.desc.z_far;
+    if (o.hasSun) { // opaque.rchit:56-73
+        V3 L = -normalize(v3(o.sun.world_space_direction[0], o.sun.world_space_direction[1], o.sun.world_space_direction[2]));
+        float LdotN = dot(L, N);
+        if (LdotN > 0.0f) {
+            float shadowFactor = traceShadowRay(o, hitPoint, L, 2.0f * zFar, st);
+            V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+            V3 directLight = v3(o.sun.color[0], o.sun.color[1], o.sun.color[2]) * shadowFactor;
+            color = color + brdf * LdotN * directLight;
+        }
+    }
+    for (const ArkSpotLight& sl : o.spots) { // opaque.rchit:75-103
+        V3 dir = v3(sl.world_space_direction[0], sl.world_space_direction[1], sl.world_space_direction[2]);
+        V3 L = -normalize(dir);
+        float LdotN = dot(L, N);
+        if (LdotN > 0.0f) {
+            V3 toLight = v3(sl.world_space_position[0], sl.world_space_position[1], sl.world_space_position[2]) - hitPoint;
+            float distanceToLight = length(toLight);
+            V3 normalizedToLight = toLight / distanceToLight;
+            float shadowFactor = traceShadowRay(o, hitPoint, normalizedToLight, distanceToLight - 0.001f, st);
+            float distanceAttenuation = 1.0f / square(distanceToLight);
+            V3 right = v3(sl.world_space_right[0], sl.world_space_right[1], sl.world_space_right[2]);
+            V3 up = v3(sl.world_space_up[0], sl.world_space_up[1], sl.world_space_up[2]);
+            float iesValue = evaluateIESLookupTable(texOf(o, sl.ies_profile_index), sl.outer_cone_half_angle, right, up, dir, -normalizedToLight);
+            V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+            V3 directLight = v3(sl.color[0], sl.color[1], sl.color[2]) * shadowFactor * distanceAttenuation * iesValue;
+            color = color + brdf * LdotN * directLight;
+        }
+    }
+    s.color = color;
+    s.baseColor = baseColor;
+    s.normal = N;
+    s.roughness = roughness;
+    s.metallic = metallic;
+    return s;
+}
+
+// ddgi/probeSampling.glsl:9-27
+void atlasSampleUV(const Grid& g, int px, int py, int pz, V3 dir, int res, int pad, float invW, float invH, float* u, float* v)
+{
+    int tileX = px + py * g.X, tileY = pz;
+    int firstX = pad + tileX * (res + 2 * pad), firstY = pad + tileY * (res + 2 * pad);
+    float ex, ey;
+    octahedralEncode(dir, &ex, &ey);
+    float tx = (ex * 0.5f + 0.5f) * static_cast<float>(res);
+    float ty = (ey * 0.5f + 0.5f) * static_cast<float>(res);
+    float ax = static_cast<float>(firstX) + tx, ay = static_cast<float>(firstY) + ty;
+    *u = ax * invW;
+    *v = ay * invH;
+}
+
+// ddgi/probeSampling.glsl:64-163
+V3 sampleDynamicDiffuseGlobalIllumination(const Oracle& o, V3 P, V3 N, V3 Vw)
+{
+    const Grid& g = o.g;
+    V3 rel = (P - g.origin) / g.spacing;
+    int bx = std::min(std::max(static_cast<int>(rel.x), 0), g.X - 1);
+    int by = std::min(std::max(static_cast<int>(rel.y), 0), g.Y - 1);
+    int bz = std::min(std::max(static_cast<int>(rel.z), 0), g.Z - 1);
+    V3 baseProbePos = g.origin + v3(static_cast<float>(bx), static_cast<float>(by), static_cast<float>(bz)) * g.spacing;
+    V3 sumIrradiance = splat(0.0f);
+    float sumWeight = 0.0f;
+    V3 al = (P - baseProbePos) / g.spacing;
+    V3 alpha = { clampf(al.x, 0.0f, 1.0f), clampf(al.y, 0.0f, 1.0f), clampf(al.z, 0.0f, 1.0f) };
+    const float invWi = 1.0f / static_cast<float>(o.Wi), invHi = 1.0f / static_cast<float>(o.Hi);
+    const float invWv = 1.0f / static_cast<float>(o.Wv), invHv = 1.0f / static_cast<float>(o.Hv);
+    for (int i = 0; i < 8; ++i) {
+        int ox = i & 1, oy = (i >> 1) & 1, oz = (i >> 2) & 1;
+        int px = std::min(std::max(bx + ox, 0), g.X - 1);
+        int py = std::min(std::max(by + oy, 0), g.Y - 1);
+        int pz = std::min(std::max(bz + oz, 0), g.Z - 1);
+        V3 tri = { fmaxf_(0.001f, mixf(1.0f - alpha.x, alpha.x, static_cast<float>(ox))),
+                   fmaxf_(0.001f, mixf(1.0f - alpha.y, alpha.y, static_cast<float>(oy))),
+                   fmaxf_(0.001f, mixf(1.0f - alpha.z, alpha.z, static_cast<float>(oz))) };
+        float trilinearWeight = tri.x * tri.y * tri.z;
+        float weight = 1.0f;
+        const float tunableShadowBias = 0.3f;
+        float minDistanceBetweenProbes = fminf_(g.spacing.x, fminf_(g.spacing.y, g.spacing.z));
+        V3 selfShadowBias = (N * 0.2f + Vw * 0.8f) * (0.75f * minDistanceBetweenProbes) * tunableShadowBias;
+        V3 biasedPosition = P + selfShadowBias;
+        V3 probePos = g.origin + v3(static_cast<float>(px), static_cast<float>(py), static_cast<float>(pz)) * g.spacing;
+        V3 pointToProbe = probePos - biasedPosition;
+        V3 directionToProbe = normalize(pointToProbe);
+        V3 unbiasedDirectionToProbe = normalize(probePos - P);
+        const float smoothFloor = 0.02f, additionalSmoothening = 0.25f;
+        weight *= smoothFloor + (1.0f - smoothFloor) * powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
+        {
+            float u, v;
+            atlasSampleUV(g, px, py, pz, -directionToProbe, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, invWv, invHv, &u, &v);
+            float vis[2];
+            sampleAtlas(o.vis, o.Wv, o.Hv, 2, u, v, vis, 2);
+            float meanDistanceToOccluder = vis[0];
+            float variance = fabsf_(vis[1] - square(vis[0]));
+            float distToProbe = length(pointToProbe);
+            float chebychevWeight = 1.0f;
+            if (distToProbe > meanDistanceToOccluder) {
+                chebychevWeight = variance / (variance + square(distToProbe - meanDistanceToOccluder));
+                chebychevWeight = chebychevWeight * chebychevWeight * chebychevWeight;
+            }
+            chebychevWeight = fmaxf_(0.05f, chebychevWeight);
+            weight *= chebychevWeight;
+        }
+        weight = fmaxf_(0.000001f, weight);
+        const float crushThreshold = 0.2f;
+        if (weight < crushThreshold)
+            weight *= square(weight) * (1.0f / square(crushThreshold));
+        weight *= trilinearWeight;
+        float u, v;
+        atlasSampleUV(g, px, py, pz, normalize(N), ARK_DDGI_IRRADIANCE_RES, ARK_DDGI_ATLAS_PADDING, invWi, invHi, &u, &v);
+        float irr[3];
+        sampleAtlas(o.irr, o.Wi, o.Hi, 4, u, v, irr, 3);
+        V3 probeIrradiance = pow3(v3(irr[0], irr[1], irr[2]), 5.0f * 0.5f);
+        sumIrradiance = sumIrradiance + weight * probeIrradiance;
+        sumWeight += weight;
+    }
+    V3 irradiance = sumIrradiance / sumWeight;
+    irradiance = irradiance * irradiance;
+    irradiance = irradiance * (0.5f * kPi);
+    return irradiance;
+}
+
+// raygen.rgen:173-185
+V3 evaluateIndirectLightFromPreviousFrame(const Oracle& o, V3 P, V3 V, V3 N, V3 baseColor, float metallic)
+{
+    V3 H = N;
+    V3 F0 = mix3(splat(DIELECTRIC_REFLECTANCE), baseColor, metallic);
+    V3 F = F_Schlick3(fmaxf_(0.0f, dot(V, H)), F0);
+    V3 irradiance = sampleDynamicDiffuseGlobalIllumination(o, P, N, V);
+    return splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
+}
+
+// raygen.rgen:114-171 (tracePrimaryRay) + :187-218 (main) for one (probe, sample).
+void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const ArkDdgiFrameParams& p, float out[4], Stats& st)
+{
+    const float zFar = o.desc.z_far;
+    float tmin = 0.0001f, tmax = zFar;
+    int numHits = 0;
+    V3 color = splat(0.0f);
+    Ray ray { origin, dir, tmin, tmax };
+    // Opaque pass: RayFlags_Opaque, cullMask RT_HIT_MASK_OPAQUE (raygen.rgen:122-134)
+    Hit hit;
+    traverseClosest(o, o.bvhOpaque, ray, hit, false, st);
+    Hit accepted;
+    if (hit.hit) { // payload.hitT <= tmax
+        accepted = hit;
+        tmax = hit.backface ? -hit.t : hit.t;
+        numHits += 1;
+    }
+    // Masked pass: RayFlags_NoOpaque, cullMask RT_HIT_MASK_MASKED, tmax = previous hit T
+    // (raygen.rgen:136-147). A negative tmax (backface) leaves [tmin,tmax] empty: no hit.
+    if (tmax >= tmin) {
+        Ray r2 { origin, dir, tmin, tmax };
+        Hit mh;
+        traverseClosest(o, o.bvhMasked, r2, mh, true, st);
+        if (mh.hit) {
+            accepted = mh;
+            tmax = mh.backface ? -mh.t : mh.t;
+            numHits += 1;
+        }
+    }
+    float dist;
+    if (numHits == 0) { // raygen.rgen:149-158
+        dist = zFar;
+        float u, v;
+        sphericalUvFromDirection(dir, &u, &v);
+        float c[4];
+        const Tex& env = (o.envTex >= 0) ? o.textures[o.envTex] : o.envWhite;
+        sampleBilinear(env, u, v, c);
+        color = p.environment_multiplier * v3(c[0], c[1], c[2]);
+    } else {
+        Surface s = closestHit(o, ray, accepted, p.ambient_amount, st, !accepted.backface);
+        dist = tmax;
+        if (!accepted.backface) {
+            color = s.color;
+            V3 hitPos = origin + dist * dir;
+            V3 indirect = evaluateIndirectLightFromPreviousFrame(o, hitPos, -dir, s.normal, s.baseColor, s.metallic);
+            color = color + s.baseColor * indirect;
+        } else {
+            color = splat(0.0f); // raygen.rgen:208-213
+            dist = dist * 0.2f;
+        }
+    }
+    out[0] = color.x;
+    out[1] = color.y;
+    out[2] = color.z;
+    out[3] = dist;
+}
+
+template<typename F>
+void parallelFor(int n, int threads, F&& fn)
+{
+    if (threads <= 1 || n <= 1) {
+        for (int i = 0; i < n; ++i) fn(i, 0);
+        return;
+    }
+    std::atomic<int> next { 0 };
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) {
+        ts.emplace_back([&, t] {
+            for (;;) {
+                int i = next.fetch_add(1);
+                if (i >= n) break;
+                fn(i, t);
+            }
+        });
+    }
+    for (auto& t : ts) t.join();
+}
+
+void resetHistory(Oracle& o)
+{
+    // DDGINode.cpp:89-94 clear values; DDGINode.cpp:96-97 zero offsets
+    std::fill(o.irr.begin(), o.irr.end(), 0);
+    uint16_t zf = f32_to_f16(o.desc.z_far);
+    float zf2 = o.desc.z_far * o.desc.z_far;
+    uint16_t zf2h = f32_to_f16(zf2);
+    if (o.desc.clear_overflow_mode == ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE && (zf2h & 0x7fffu) == 0x7c00u) zf2h = 0x7bffu;
+    if (o.desc.clear_overflow_mode == ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE && (zf & 0x7fffu) == 0x7c00u) zf = 0x7bffu;
+    for (size_t i = 0; i < o.vis.size(); i += 2) {
+        o.vis[i] = zf;
+        o.vis[i + 1] = zf2h;
+    }
+    std::fill(o.offsets.begin(), o.offsets.end(), 0.0f);
+    std::fill(o.surfels.begin(), o.surfels.end(), 0);
+}
+
+} // namespace
+
+// ===========================================================================
+// Exported C API (for tests / bench cpu_baseline only)
+// ===========================================================================
+extern "C" {
+
+struct OracleCtx;
+
+void* oracle_create(const ArkDdgiDesc* desc)
+{
+    if (!desc) return nullptr;
+    auto* o = new Oracle();
+    o->desc = *desc;
+    o->g.X = desc->grid_dims[0];
+    o->g.Y = desc->grid_dims[1];
+    o->g.Z = desc->grid_dims[2];
+    if (o->g.X <= 0 || o->g.Y <= 0 || o->g.Z <= 0) { delete o; return nullptr; }
+    o->g.spacing = v3(desc->probe_spacing[0], desc->probe_spacing[1], desc->probe_spacing[2]);
+    o->g.origin = v3(desc->offset_to_first[0], desc->offset_to_first[1], desc->offset_to_first[2]);
+    // DDGINode.cpp:301-320
+    const int si = ARK_DDGI_IRRADIANCE_RES + 2 * ARK_DDGI_ATLAS_PADDING;
+    const int sv = ARK_DDGI_VISIBILITY_RES + 2 * ARK_DDGI_ATLAS_PADDING;
+    o->Wi = o->g.X * si * o->g.Y;
+    o->Hi = o->g.Z * si;
+    o->Wv = o->g.X * sv * o->g.Y;
+    o->Hv = o->g.Z * sv;
+    o->irr.resize(static_cast<size_t>(o->Wi) * o->Hi * 4);
+    o->vis.resize(static_cast<size_t>(o->Wv) * o->Hv * 2);
+    o->offsets.resize(static_cast<size_t>(o->g.N()) * 4);
+    o->Rmax = desc->max_rays_per_probe > 0 ? desc->max_rays_per_probe : ARK_DDGI_MAX_RAYS_PER_PROBE;
+    o->Kmax = desc->max_probe_updates > 0 ? desc->max_probe_updates : ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES;
+    o->surfels.resize(static_cast<size_t>(o->Kmax) * o->Rmax * 4);
+    o->envWhite = whiteSrgbPixel();
+    resetHistory(*o);
+    return o;
+}
+
+void oracle_destroy(void* ctx) { delete static_cast<Oracle*>(ctx); }
+
+int oracle_reset_history(void* ctx)
+{
+    resetHistory(*static_cast<Oracle*>(ctx));
+    return 0;
+}
+
+int oracle_set_scene(void* ctx, const ArkDdgiScene* s, int threads)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!s) return ARK_DDGI_E_INVALID_ARGUMENT;
+    o.indices.assign(s->indices, s->indices + s->index_count);
+    o.vertices.assign(s->vertices, s->vertices + s->vertex_count);
+    o.meshes.assign(s->meshes, s->meshes + s->mesh_count);
+    o.materials.assign(s->materials, s->materials + s->material_count);
+    o.instances.assign(s->instances, s->instances + s->instance_count);
+    o.textures.clear();
+    for (uint32_t i = 0; i < s->texture_count; ++i) o.textures.push_back(makeTex(s->textures[i]));
+    o.envTex = s->environment_texture;
+    o.hasSun = s->has_directional_light != 0;
+    o.sun = s->directional_light;
+    o.spots.assign(s->spot_lights, s->spot_lights + s->spot_light_count);
+    // World-space triangles (GpuScene.cpp:883-929: one instance per mesh segment).
+    o.tris.clear();
+    std::vector<uint32_t> opaque, masked, blend;
+    uint32_t gid = 0;
+    for (uint32_t ii = 0; ii < s->instance_count; ++ii) {
+        const ArkRTInstance& inst = s->instances[ii];
+        const ArkRTTriangleMesh& m = s->meshes[inst.rt_mesh_index];
+        const float* M = inst.object_to_world;
+        float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
+        for (uint32_t p = 0; p < inst.triangle_count; ++p, ++gid) {
+            V3 w[3];
+            for (int k = 0; k < 3; ++k) {
+                uint32_t idx = s->indices[static_cast<size_t>(m.first_index) + 3u * p + k];
+                const float* P = &s->positions[(static_cast<size_t>(m.first_vertex) + idx) * 3];
+                w[k] = { M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3],
+                         M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7],
+                         M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11] };
+            }
+            WTri t { w[0], w[1] - w[0], w[2] - w[0], ii, p, gid, det < 0.0f ? 1u : 0u };
+            uint32_t ti = static_cast<uint32_t>(o.tris.size());
+            o.tris.push_back(t);
+            if (inst.hit_mask & ARK_RT_HIT_MASK_OPAQUE) opaque.push_back(ti);
+            else if (inst.hit_mask & ARK_RT_HIT_MASK_MASKED) masked.push_back(ti);
+            else blend.push_back(ti);
+        }
+    }
+    o.bvhOpaque = buildBvh(o.tris, opaque, threads);
+    o.bvhMasked = buildBvh(o.tris, masked, threads);
+    o.bvhBlend = buildBvh(o.tris, blend, threads);
+    o.hasScene = true;
+    return 0;
+}
+
+// One DDGI update: DDGINode.cpp:171-298. `threads` host threads, parallel over probes.
+int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!p || !o.hasScene) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const Grid& g = o.g;
+    const uint32_t N = static_cast<uint32_t>(g.N());
+    const uint32_t K = std::min(p->probe_updates, N);
+    const uint32_t R = p->rays_per_probe;
+    if (K > static_cast<uint32_t>(o.Kmax) || R > static_cast<uint32_t>(o.Rmax) || R == 0) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const uint32_t first = p->first_probe_index % N;
+    const uint32_t frameIdx = p->frame_index;
+    std::vector<Stats> tstats(std::max(threads, 1));
+
+    // 1. trace rays (raygen.rgen main, launch (K, R))
+    parallelFor(static_cast<int>(K), threads, [&](int slot, int tid) {
+        uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+        V3 pos = probePosition(g, probeIdx);
+        const float* off = &o.offsets[static_cast<size_t>(probeIdx) * 4];
+        pos = pos + v3(off[0], off[1], off[2]);
+        for (uint32_t s = 0; s < R; ++s) {
+            V3 dir = calculateRotatedSphericalFibonacciSample(probeIdx, s, R, frameIdx);
+            float out[4];
+            traceProbeRay(o, probeIdx, pos, dir, *p, out, tstats[tid]);
+            uint16_t* dst = &o.surfels[(static_cast<size_t>(slot) * o.Rmax + s) * 4];
+            for (int c = 0; c < 4; ++c) dst[c] = f32_to_f16(out[c]);
+        }
+    });
+
+    // 2+3. irradiance & visibility update (probeUpdateIrradiance.comp / probeUpdateVisibility.comp)
+    const float gridMaxSpacing = fmaxf_(g.spacing.x, fmaxf_(g.spacing.y, g.spacing.z)); // DDGINode.cpp:187
+    parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
+        uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+        std::vector<V3> dirs(R);
+        for (uint32_t s = 0; s < R; ++s) dirs[s] = calculateRotatedSphericalFibonacciSample(probeIdx, s, R, frameIdx);
+        const uint16_t* sf = &o.surfels[static_cast<size_t>(slot) * o.Rmax * 4];
+        const float epsilon = 1e-9f * static_cast<float>(R);
+        // probeUpdateIrradiance.comp:22-79
+        for (int ty = 0; ty < ARK_DDGI_IRRADIANCE_RES; ++ty)
+            for (int tx = 0; tx < ARK_DDGI_IRRADIANCE_RES; ++tx) {
+                float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(ARK_DDGI_IRRADIANCE_RES);
+                float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(ARK_DDGI_IRRADIANCE_RES);
+                V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
+                int ax, ay;
+                atlasTexelCoord(g, probeIdx, tx, ty, ARK_DDGI_IRRADIANCE_RES, ARK_DDGI_ATLAS_PADDING, &ax, &ay);
+                V3 newIrr = splat(0.0f);
+                float totalWeight = 0.0f;
+                for (uint32_t s = 0; s < R; ++s) {
+                    float weight = fmaxf_(0.0f, dot(texelDirection, dirs[s]));
+                    V3 rad = v3(f16_to_f32(sf[s * 4 + 0]), f16_to_f32(sf[s * 4 + 1]), f16_to_f32(sf[s * 4 + 2]));
+                    newIrr = newIrr + weight * rad;
+                    totalWeight += weight;
+                }
+                newIrr = newIrr / fmaxf_(totalWeight, epsilon);
+                newIrr = pow3(newIrr, 1.0f / 5.0f);
+                uint16_t* t = &o.irr[(static_cast<size_t>(ay) * o.Wi + ax) * 4];
+                V3 old = v3(f16_to_f32(t[0]), f16_to_f32(t[1]), f16_to_f32(t[2]));
+                newIrr = mix3(newIrr, old, p->hysteresis_irradiance);
+                t[0] = f32_to_f16(newIrr.x);
+                t[1] = f32_to_f16(newIrr.y);
+                t[2] = f32_to_f16(newIrr.z);
+                t[3] = f32_to_f16(0.0f);
+            }
+        // probeUpdateVisibility.comp:24-63
+        const float maxDistance = 1.5f * gridMaxSpacing;
+        for (int ty = 0; ty < ARK_DDGI_VISIBILITY_RES; ++ty)
+            for (int tx = 0; tx < ARK_DDGI_VISIBILITY_RES; ++tx) {
+                float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(ARK_DDGI_VISIBILITY_RES);
+                float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(ARK_DDGI_VISIBILITY_RES);
+                V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
+                int ax, ay;
+                atlasTexelCoord(g, probeIdx, tx, ty, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, &ax, &ay);
+                float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
+                for (uint32_t s = 0; s < R; ++s) {
+                    float weight = powf_(fmaxf_(0.0f, dot(texelDirection, dirs[s])), p->visibility_sharpness);
+                    float d = f16_to_f32(sf[s * 4 + 3]);
+                    d = fminf_(fabsf_(d), maxDistance);
+                    nv0 += weight * d;
+                    nv1 += weight * square(d);
+                    totalWeight += weight;
+                }
+                float den = fmaxf_(totalWeight, epsilon);
+                nv0 = nv0 / den;
+                nv1 = nv1 / den;
+                uint16_t* t = &o.vis[(static_cast<size_t>(ay) * o.Wv + ax) * 2];
+                nv0 = mixf(nv0, f16_to_f32(t[0]), p->hysteresis_visibility);
+                nv1 = mixf(nv1, f16_to_f32(t[1]), p->hysteresis_visibility);
+                t[0] = f32_to_f16(nv0);
+                t[1] = f32_to_f16(nv1);
+            }
+    });
+
+    // 5. border copies over all N probe tiles (probeBorderCopyCorners.comp / probeBorderCopyEdges.comp)
+    auto borders = [&](std::vector<uint16_t>& atlas, int W, int ch, int res) {
+        const int side = res + 2 * ARK_DDGI_ATLAS_PADDING;
+        const int tilesX = g.X * g.Y, tilesY = g.Z;
+        for (int ty = 0; ty < tilesY; ++ty)
+            for (int tx = 0; tx < tilesX; ++tx) {
+                auto at = [&](int x, int y) { return &atlas[(static_cast<size_t>(y) * W + x) * ch]; };
+                // corners (probeBorderCopyCorners.comp:20-51)
+                for (int cy = 0; cy < 2; ++cy)
+                    for (int cx = 0; cx < 2; ++cx) {
+                        int sx = (cx + 1) % 2, sy = (cy + 1) % 2;
+                        int dX = tx * side + cx * (side - 1), dY = ty * side + cy * (side - 1);
+                        int sX = tx * side + sx * (side - 1), sY = ty * side + sy * (side - 1);
+                        sX += (sx == 0) ? 1 : -1;
+                        sY += (sy == 0) ? 1 : -1;
+                        std::memcpy(at(dX, dY), at(sX, sY), ch * 2);
+                    }
+                // edges (probeBorderCopyEdges.comp:20-56)
+                static const int cornerIdx[4][2] = { { 0, 0 }, { 1, 0 }, { 1, 1 }, { 0, 1 } };
+                static const int stepDir[4][2] = { { 1, 0 }, { 0, 1 }, { -1, 0 }, { 0, -1 } };
+                for (int sideIdx = 0; sideIdx < 4; ++sideIdx) {
+                    const int* in = stepDir[(sideIdx + 1) % 4];
+                    int cX = tx * side + cornerIdx[sideIdx][0] * (side - 1);
+                    int cY = ty * side + cornerIdx[sideIdx][1] * (side - 1);
+                    for (int step = 0; step < res; ++step) {
+                        int dX = cX + (step + 1) * stepDir[sideIdx][0], dY = cY + (step + 1) * stepDir[sideIdx][1];
+                        int sX = (cX + in[0]) + (res - step) * stepDir[sideIdx][0];
+                        int sY = (cY + in[1]) + (res - step) * stepDir[sideIdx][1];
+                        std::memcpy(at(dX, dY), at(sX, sY), ch * 2);
+                    }
+                }
+            }
+    };
+    borders(o.irr, o.Wi, 4, ARK_DDGI_IRRADIANCE_RES);
+    borders(o.vis, o.Wv, 2, ARK_DDGI_VISIBILITY_RES);
+
+    // 6. probe offsets (probeUpdateOffset.comp:27-96), full barrier semantics
+    if (p->update_offsets) {
+        const float minAxialSpacing = fminf_(g.spacing.x, fminf_(g.spacing.y, g.spacing.z));
+        const float maxOffset = minAxialSpacing / 2.0f; // DDGINode.cpp:287-289
+        parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
+            uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+            const uint16_t* sf = &o.surfels[static_cast<size_t>(slot) * o.Rmax * 4];
+            float* cur = &o.offsets[static_cast<size_t>(probeIdx) * 4];
+            V3 currentOffset = v3(cur[0], cur[1], cur[2]);
+            V3 offset = splat(0.0f);
+            uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
+            V3 accumBackfaceDir = splat(0.0f), accumNearFrontfaceDir = splat(0.0f);
+            for (uint32_t i = 0; i < R; ++i) {
+                V3 d = calculateRotatedSphericalFibonacciSample(probeIdx, i, R, frameIdx);
+                float a = f16_to_f32(sf[i * 4 + 3]);
+                if (a > 0.0f && a < maxOffset) {
+                    accumNearFrontfaceDir = accumNearFrontfaceDir + d;
+                    nearFrontfaceCount += 1;
+                } else if (a < 0.0f) {
+                    backfaceCount += 1;
+                    accumBackfaceDir = accumBackfaceDir + d;
+                }
+            }
+            const float stepSize = 0.125f, lerpSpeed = 10.0f;
+            if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
+                offset = offset + normalize(accumBackfaceDir) * stepSize;
+            else if (nearFrontfaceCount >= 1)
+                offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
+            else
+                offset = offset - currentOffset * stepSize;
+            V3 newOffset = currentOffset + offset;
+            if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
+            newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * p->delta_time));
+            cur[0] = newOffset.x;
+            cur[1] = newOffset.y;
+            cur[2] = newOffset.z;
+        });
+    }
+    Stats tot;
+    for (auto& s : tstats) { tot.nodes += s.nodes; tot.tris += s.tris; }
+    o.stats = tot;
+    return 0;
+}
+
+int oracle_read(void* ctx, int which, void* dst, uint64_t bytes)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    const void* src = nullptr;
+    uint64_t n = 0;
+    switch (which) {
+    case ARK_DDGI_ATLAS_IRRADIANCE: src = o.irr.data(); n = o.irr.size() * 2; break;
+    case ARK_DDGI_ATLAS_VISIBILITY: src = o.vis.data(); n = o.vis.size() * 2; break;
+    case ARK_DDGI_SURFELS: src = o.surfels.data(); n = o.surfels.size() * 2; break;
+    case ARK_DDGI_PROBE_OFFSETS: src = o.offsets.data(); n = o.offsets.size() * 4; break;
+    default: return ARK_DDGI_E_INVALID_ARGUMENT;
+    }
+    if (bytes != n) return ARK_DDGI_E_SIZE_MISMATCH;
+    std::memcpy(dst, src, n);
+    return 0;
+}
+
+int oracle_write(void* ctx, int which, const void* src, uint64_t bytes)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    void* dst = nullptr;
+    uint64_t n = 0;
+    switch (which) {
+    case ARK_DDGI_ATLAS_IRRADIANCE: dst = o.irr.data(); n = o.irr.size() * 2; break;
+    case ARK_DDGI_ATLAS_VISIBILITY: dst = o.vis.data(); n = o.vis.size() * 2; break;
+    case ARK_DDGI_SURFELS: dst = o.surfels.data(); n = o.surfels.size() * 2; break;
+    case ARK_DDGI_PROBE_OFFSETS: dst = o.offsets.data(); n = o.offsets.size() * 4; break;
+    default: return ARK_DDGI_E_INVALID_ARGUMENT;
+    }
+    if (bytes != n) return ARK_DDGI_E_SIZE_MISMATCH;
+    std::memcpy(dst, src, n);
+    return 0;
+}
+
+void oracle_get_stats(void* ctx, uint64_t* nodes, uint64_t* tris)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    *nodes = o.stats.nodes;
+    *tris = o.stats.tris;
+}
+
+// ---- helper KAT exports ----------------------------------------------------
+uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
+uint32_t oracle_rand_xorshift(uint32_t s) { return rand_xorshift(s); }
+
+void oracle_rotated_fib(uint32_t probeIdx, uint32_t sampleIdx, uint32_t n, uint32_t frame, float* out)
+{
+    V3 d = calculateRotatedSphericalFibonacciSample(probeIdx, sampleIdx, n, frame);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+void oracle_fib(uint32_t i, uint32_t n, float* out)
+{
+    V3 d = sphericalFibonacciSample(i, n);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+void oracle_oct_decode(float x, float y, float* out)
+{
+    V3 d = octahedralDecode(x, y);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+void oracle_oct_encode(const float* v, float* out) { octahedralEncode(v3(v[0], v[1], v[2]), &out[0], &out[1]); }
+void oracle_atlas_texel(const int* dims, uint32_t probeIdx, int tx, int ty, int res, int* out)
+{
+    Grid g { dims[0], dims[1], dims[2], splat(1), splat(0) };
+    atlasTexelCoord(g, probeIdx, tx, ty, res, ARK_DDGI_ATLAS_PADDING, &out[0], &out[1]);
+}
+void oracle_f32_to_f16(const float* in, uint16_t* out, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) out[i] = f32_to_f16(in[i]);
+}
+void oracle_f16_to_f32(const uint16_t* in, float* out, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) out[i] = f16_to_f32(in[i]);
+}
+// op: 0 sin 1 cos 2 acos 3 atan2 4 log2 5 exp2 6 pow
+void oracle_fmath(int op, const float* x, const float* y, float* out, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        switch (op) {
+        case 0: out[i] = sinf_(x[i]); break;
+        case 1: out[i] = cosf_(x[i]); break;
+        case 2: out[i] = acosf_(x[i]); break;
+        case 3: out[i] = atan2f_(x[i], y[i]); break;
+        case 4: out[i] = log2f_(x[i]); break;
+        case 5: out[i] = exp2f_(x[i]); break;
+        case 6: out[i] = powf_(x[i], y[i]); break;
+        default: out[i] = 0; break;
+        }
+    }
+}
+
+} // extern "C"

@@ -1,0 +1,129 @@
+"""ctypes binding of the CPU oracle (oracle/build/libddgi_oracle.so).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use this, as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from arkoserenderer_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_PATH = os.path.join(ROOT, "oracle", "build", "libddgi_oracle.so")
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_PATH):
+            raise RuntimeError(f"oracle not built: {ORACLE_PATH} (run __graft_entry__.build())")
+        lib = C.CDLL(ORACLE_PATH)
+        lib.oracle_create.restype = C.c_void_p
+        lib.oracle_create.argtypes = [C.POINTER(abi.ArkDdgiDesc)]
+        lib.oracle_destroy.argtypes = [C.c_void_p]
+        lib.oracle_reset_history.argtypes = [C.c_void_p]
+        lib.oracle_set_scene.argtypes = [C.c_void_p, C.POINTER(abi.ArkDdgiScene), C.c_int]
+        lib.oracle_update.argtypes = [C.c_void_p, C.POINTER(abi.ArkDdgiFrameParams), C.c_int]
+        lib.oracle_read.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]
+        lib.oracle_write.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]
+        lib.oracle_get_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        lib.oracle_wang_hash.restype = C.c_uint32
+        lib.oracle_wang_hash.argtypes = [C.c_uint32]
+        lib.oracle_rand_xorshift.restype = C.c_uint32
+        lib.oracle_rand_xorshift.argtypes = [C.c_uint32]
+        lib.oracle_rotated_fib.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+        lib.oracle_fib.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p]
+        lib.oracle_oct_decode.argtypes = [C.c_float, C.c_float, C.c_void_p]
+        lib.oracle_oct_encode.argtypes = [C.c_void_p, C.c_void_p]
+        lib.oracle_atlas_texel.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.oracle_f32_to_f16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        lib.oracle_f16_to_f32.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        lib.oracle_fmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        _lib = lib
+    return _lib
+
+
+class Oracle:
+    """CPU restatement of the DDGI node; same inputs as the C-ABI."""
+
+    def __init__(self, desc: abi.ArkDdgiDesc):
+        self.lib = load()
+        self.desc = desc
+        self.h = self.lib.oracle_create(C.byref(desc))
+        if not self.h:
+            raise RuntimeError("oracle_create failed")
+        self.sizes = {}
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_scene(self, scene, threads: int = 8):
+        s = scene.to_abi()
+        rc = self.lib.oracle_set_scene(self.h, C.byref(s), threads)
+        assert rc == 0, rc
+        self._scene = scene
+
+    def update(self, params, threads: int = 8):
+        rc = self.lib.oracle_update(self.h, C.byref(params), threads)
+        assert rc == 0, rc
+
+    def _size(self, which):
+        X, Y, Z = self.desc.grid_dims
+        if which == abi.ARK_DDGI_ATLAS_IRRADIANCE:
+            return X * 10 * Y * Z * 10 * 4
+        if which == abi.ARK_DDGI_ATLAS_VISIBILITY:
+            return X * 18 * Y * Z * 18 * 2
+        if which == abi.ARK_DDGI_SURFELS:
+            return self.desc.max_probe_updates * self.desc.max_rays_per_probe * 4
+        return X * Y * Z * 4
+
+    def read(self, which):
+        n = self._size(which)
+        dt = np.float32 if which == abi.ARK_DDGI_PROBE_OFFSETS else np.uint16
+        out = np.empty(n, dtype=dt)
+        rc = self.lib.oracle_read(self.h, which, out.ctypes.data, out.nbytes)
+        assert rc == 0, rc
+        return out
+
+    def write(self, which, data):
+        data = np.ascontiguousarray(data)
+        rc = self.lib.oracle_write(self.h, which, data.ctypes.data, data.nbytes)
+        assert rc == 0, rc
+
+    def stats(self):
+        n, t = C.c_uint64(), C.c_uint64()
+        self.lib.oracle_get_stats(self.h, C.byref(n), C.byref(t))
+        return int(n.value), int(t.value)
+
+
+def f32_to_f16(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.shape, np.uint16)
+    load().oracle_f32_to_f16(x.ctypes.data, out.ctypes.data, x.size)
+    return out
+
+
+def f16_to_f32(h):
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    out = np.empty(h.shape, np.float32)
+    load().oracle_f16_to_f32(h.ctypes.data, out.ctypes.data, h.size)
+    return out
+
+
+def fmath(op: int, x, y=None):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float32)
+    out = np.empty_like(x)
+    load().oracle_fmath(op, x.ctypes.data, y.ctypes.data, out.ctypes.data, x.size)
+    return out
