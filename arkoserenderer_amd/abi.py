@@ -185,11 +185,14 @@ class ArkDdgiCounters(C.Structure):
     _fields_ = [
         ("rays", C.c_uint64),
         ("probes", C.c_uint64),
-        ("node_visits", C.c_uint64),
-        ("tri_tests", C.c_uint64),
+        ("primary_node_visits", C.c_uint64),
+        ("primary_tri_tests", C.c_uint64),
         ("hits", C.c_uint64),
+        ("front_hits", C.c_uint64),
         ("shadow_rays", C.c_uint64),
-        ("reserved", C.c_uint64 * 4),
+        ("shadow_node_visits", C.c_uint64),
+        ("shadow_tri_tests", C.c_uint64),
+        ("reserved", C.c_uint64),
     ]
 
 

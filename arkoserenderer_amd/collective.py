@@ -1,0 +1,59 @@
+"""Z-slab exchange of the DDGI atlases across GPUs (RCCL over xGMI via
+torch.distributed, backend "nccl" = RCCL on ROCm).
+
+A Z-slab of the probe grid is a contiguous texel-row band of both atlases
+(tile row = probe z, ddgi/common.glsl:58-61), so after every update each rank
+contributes its band to an in-place all-gather of the whole atlas. The full
+atlas (not a one-probe halo) is exchanged because the indirect bounce of the
+next frame samples the previous frame's atlases at arbitrary hit points
+(raygen.rgen:127 -> probeSampling.glsl:64-163).
+"""
+from __future__ import annotations
+
+
+class _CudaArray:
+    """Minimal __cuda_array_interface__ view of raw device bytes owned by libark_ddgi."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {
+            "shape": (int(nbytes),),
+            "typestr": "|u1",
+            "data": (int(ptr), False),
+            "version": 3,
+            "strides": None,
+        }
+
+
+def device_bytes(ptr: int, nbytes: int, device):
+    import torch
+
+    return torch.as_tensor(_CudaArray(ptr, nbytes), device=device)
+
+
+class SlabExchange:
+    """In-place all-gather of the irradiance and visibility atlases of one
+    DDGIContext (one Z-slab per rank). Works with any torch.distributed backend
+    whose tensors live where the atlases live (nccl on GPU; gloo for CPU tests)."""
+
+    def __init__(self, views, rank: int, world: int, device, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.bufs = []
+        for ptr, total, off, slab in (
+            (views.irradiance_atlas, views.irradiance_bytes, views.irradiance_slab_offset, views.irradiance_slab_bytes),
+            (views.visibility_atlas, views.visibility_bytes, views.visibility_slab_offset, views.visibility_slab_bytes),
+        ):
+            full = device_bytes(ptr, total, device)
+            assert slab * world == total and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
+            self.bufs.append((full, full[off:off + slab]))
+
+    def exchange(self):
+        import torch.distributed as dist
+
+        for full, mine in self.bufs:
+            dist.all_gather_into_tensor(full, mine, group=self.group)
+
+
+def slab_bands(total_bytes: int, world: int):
+    """(offset, bytes) of every rank's band; used by the CPU (gloo) tests."""
+    slab = total_bytes // world
+    return [(r * slab, slab) for r in range(world)]

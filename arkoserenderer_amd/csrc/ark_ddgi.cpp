@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -298,6 +299,9 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         }
     }
     BvhBuildOptions opt;
+    // host threads for the build: the box's CPU share per GPU is 16 cores
+    opt.threads = 16;
+    if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
     std::vector<GpuBvhNode> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
@@ -636,10 +640,13 @@ int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out)
         ARK_HIP(hipSetDevice(ctx->device));
         ARK_HIP(hipDeviceSynchronize());
         ARK_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof(c), hipMemcpyDeviceToHost));
-        out->node_visits = c[0];
-        out->tri_tests = c[1];
+        out->primary_node_visits = c[0];
+        out->primary_tri_tests = c[1];
         out->hits = c[2];
         out->shadow_rays = c[3];
+        out->shadow_node_visits = c[4];
+        out->shadow_tri_tests = c[5];
+        out->front_hits = c[6];
     }
     return ARK_DDGI_OK;
 }

@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
     const uint32_t gtid = blockIdx.x * kShadeBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kShadeBlock;
     Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
-    uint32_t cNodes = 0, cTris = 0, cShadow = 0;
+    uint32_t cNodes = 0, cTris = 0, cShadow = 0, cFront = 0;
     for (uint32_t ray = gtid; ray < f.window_rays; ray += nthreads) {
         const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
         const GpuHit hit = f.hits[ray];
@@ -539,6 +539,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
             dist = hit.t * 0.2f;
         } else {
             const float T = hit.t;
+            if (COUNT) cFront++;
             const GpuTriangle tr = loadTri(sc.tris, hit.tri);
             const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
             const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
@@ -625,9 +626,10 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
         reinterpret_cast<uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + sample] = packed;
     }
     if (COUNT) {
-        atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
-        atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
+        atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
+        atomicAdd(&f.counters[5], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
+        atomicAdd(&f.counters[6], static_cast<unsigned long long>(cFront));
     }
 }
 

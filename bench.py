@@ -1,0 +1,278 @@
+"""DDGI probe-update benchmark (BASELINE.json metric: Mrays/s + probes-updated/s,
+DDGI 32^3 grid x 256 rays, at 1/2/4/8 MI355X).
+
+Workload (config C4): synthetic 10M-triangle strip soup (PCG32
+seed 0xA2C05E00), 32x32x32 probes (spacing 1 m, origin 0), 256 rays/probe, the
+full grid updated every step (K = N = 32768), sun light. A step = one DDGI
+update (trace -> shade -> irradiance/visibility/border/offset update) of every
+probe; with N GPUs the grid is split in Z-slabs (strong scaling: fixed total
+work) and the atlases are all-gathered over RCCL after each update.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+# Algorithmic bytes (SURVEY.md §8d model, adapted to this build's layouts)
+NODE_BYTES = 64        # GpuBvhNode (two child boxes + child codes)
+TRI_BYTES = 48         # GpuTriangle (v0, e1, e2, instance, primitive)
+HIT_RECORD_BYTES = 16  # GpuHit
+SURFEL_BYTES = 8       # RGBA16F surfel
+# per shaded (front) hit: triangle 48 + instance 64 + RT mesh 12 + material 96 + 3 indices 12
+# + 3 RTVertex 108 + 3 texel fetches 48 + 8-probe DDGI gather 8*(4*4 + 4*8) = 384
+SHADE_HIT_BYTES = 48 + 64 + 12 + 96 + 12 + 108 + 48 + 384
+MISS_BYTES = 16        # environment texel
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--triangles", type=int, default=10_000_000)
+    ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--rays", type=int, default=256)
+    ap.add_argument("--probe-updates", type=int, default=0, help="0 = whole grid per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "latest_pmc.json"),
+                    help="PMC traffic summary written by tools/profile_pmc.py (optional)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from arkoserenderer_amd import abi
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+    from arkoserenderer_amd.collective import SlabExchange
+
+    G = args.grid
+    N = G * G * G
+    K = args.probe_updates or N
+    R = args.rays
+    t_setup = time.time()
+    scene = S.soup(args.triangles)
+    grid = D.ProbeGrid((G, G, G), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=K, max_rays_per_probe=R, max_probe_updates=K,
+                       compute_probe_offsets=True)
+    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    node = D.DDGINode(cfg)
+    assert node.construct(scene, grid, 10000.0, device=local_rank, shard_rank=rank, shard_count=world, **exposure)
+    ctx = node.ctx
+    bvh = ctx.bvh_stats()
+    stream = torch.cuda.current_stream(device)
+    sptr = stream.cuda_stream
+    exch = SlabExchange(ctx.device_views(), rank, world, device) if world > 1 else None
+    setup_s = time.time() - t_setup
+
+    frame = 0
+
+    def step():
+        nonlocal frame
+        node.execute(D.AppState(frame), sptr)
+        if exch is not None:
+            exch.exchange()
+        frame += 1
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+
+    # --- counter-instrumented update (separate kernel variant; not timed) -----
+    ctx.set_counting(True)
+    step()
+    torch.cuda.synchronize(device)
+    cnt = ctx.counters()
+    ctx.set_counting(False)
+
+    # --- per-kernel device time from HIP events on the update stream ----------
+    ctx.set_timing(True)
+    ktimes = []
+    for _ in range(3):
+        step()
+        ktimes.append(ctx.last_timings())
+    ctx.set_timing(False)
+    torch.cuda.synchronize(device)
+
+    # --- timed region: exactly `steps` steps -----------------------------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    total_rays = args.steps * K * R
+    total_probes = args.steps * K
+    mrays = total_rays / dt / 1e6
+
+    # roofline of the dominant kernel (per launch, this rank's share)
+    avg = [sum(k[i] for k in ktimes) / len(ktimes) for i in range(5)]
+    rays_rank = cnt.rays
+    kernel_bytes = {
+        "k_trace_primary": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays_rank,
+        "k_shade": HIT_RECORD_BYTES * rays_rank + NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests
+                   + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays_rank - cnt.hits) + SURFEL_BYTES * rays_rank,
+        "k_probe_update": cnt.probes * (R * SURFEL_BYTES + 2 * (64 * 8 + 256 * 4) + (36 * 8 + 68 * 4) + 32),
+    }
+    kernel_ms = {"k_trace_primary": avg[1], "k_shade": avg[2], "k_probe_update": avg[3]}
+    dom = max(kernel_ms, key=kernel_ms.get)
+    achieved = kernel_bytes[dom] / (kernel_ms[dom] * 1e-3) / 1e9
+    traffic = None
+    pmc_note = None
+    if os.path.exists(args.pmc):
+        try:
+            with open(args.pmc) as fh:
+                pm = json.load(fh)
+            if pm.get("config", {}).get("triangles") == args.triangles and pm.get("config", {}).get("grid") == G and dom in pm.get("kernels", {}):
+                traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
+                pmc_note = pm.get("source")
+        except Exception as e:  # noqa: BLE001
+            pmc_note = f"unreadable: {e}"
+
+    result = {
+        "metric": "Mrays/s + probes-updated/s, DDGI 32^3 grid x 256 rays, at 1/2/4/8 MI355X",
+        "value": round(mrays, 3),
+        "unit": "Mrays/s",
+        "probes_updated_per_s": round(total_probes / dt, 1),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C4: synthetic 10M-triangle strip soup, 32x32x32 probes x 256 rays, whole grid updated per step",
+            "triangles": scene.triangle_count,
+            "grid": G,
+            "rays_per_probe": R,
+            "probe_updates_per_step": K,
+            "parallelism": f"zslab{world}",
+            "bvh_nodes": int(bvh.node_count),
+            "bvh_max_depth": int(bvh.max_depth),
+            "bvh_build_ms": round(bvh.build_ms, 1),
+            "setup_s": round(setup_s, 2),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": pmc_note,
+            "algorithmic_bytes_per_launch": int(kernel_bytes[dom]),
+            "avg_launch_ms": round(kernel_ms[dom], 4),
+        },
+        "kernels_ms": {k: round(v, 4) for k, v in kernel_ms.items()},
+        "update_ms": round(avg[0], 4),
+        "per_ray": {
+            "primary_nodes": round(cnt.primary_node_visits / max(1, rays_rank), 2),
+            "primary_tris": round(cnt.primary_tri_tests / max(1, rays_rank), 2),
+            "hit_frac": round(cnt.hits / max(1, rays_rank), 4),
+            "front_hit_frac": round(cnt.front_hits / max(1, rays_rank), 4),
+            "shadow_rays": round(cnt.shadow_rays / max(1, rays_rank), 4),
+            "shadow_nodes": round(cnt.shadow_node_visits / max(1, rays_rank), 2),
+            "shadow_tris": round(cnt.shadow_tri_tests / max(1, rays_rank), 2),
+        },
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(scene, grid, R, args, exposure)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    node.ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, grid, R, args, exposure):
+    """The CPU oracle (C++ restatement of the reference shaders, `port`) on a
+    bounded sample of the same workload: the first probes of the window of the
+    same scene/grid/R, all stages of the update, `threads` host threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    from arkoserenderer_amd import ddgi as D
+    from parity import make_desc
+
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    kmax = 4096
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=kmax, max_rays_per_probe=R, max_probe_updates=kmax,
+                       compute_probe_offsets=True)
+    orc = O.Oracle(make_desc(grid, 10000.0, cfg))
+    t = time.time()
+    orc.set_scene(scene, threads)
+    build_s = time.time() - t
+    probes = 16
+    spent, rays, done_probes = 0.0, 0, 0
+    first = 0
+    frame = 0
+    while spent < args.cpu_seconds:
+        cfg.probe_updates_per_frame = probes
+        p = D.frame_params(cfg, grid, D.AppState(frame), first, **exposure)
+        t = time.perf_counter()
+        orc.update(p, threads)
+        el = time.perf_counter() - t
+        spent += el
+        rays += probes * R
+        done_probes += probes
+        first += probes
+        frame += 1
+        # grow the chunk towards ~1/4 of the budget
+        rate = probes / max(el, 1e-6)
+        probes = int(min(kmax, max(16, rate * args.cpu_seconds / 4)))
+    orc.close()
+    return {
+        "value": round(rays / spent / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{done_probes} probes x {R} rays of the same C4 workload (probes 0..{done_probes - 1}), full update incl. shading/indirect/blend, {spent:.1f} s; oracle BVH build {build_s:.1f} s excluded",
+        "probes_updated_per_s": round(done_probes / spent, 2),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -227,13 +227,16 @@ typedef struct ArkDdgiFrameParams {
 /* Work/traffic counters of the last update (counters are only collected when
  * ark_ddgi_set_counting(ctx, 1); the timed path compiles them out). */
 typedef struct ArkDdgiCounters {
-    uint64_t rays;               /* probe rays traced (sum K*R over this context's probes) */
-    uint64_t probes;             /* probes updated */
-    uint64_t node_visits;        /* BVH2 nodes fetched, all traversals */
-    uint64_t tri_tests;          /* triangle records fetched, all traversals */
-    uint64_t hits;               /* probe rays with a hit */
-    uint64_t shadow_rays;        /* shadow rays traced */
-    uint64_t reserved[4];
+    uint64_t rays;                /* probe rays traced (sum K*R over this context's probes) */
+    uint64_t probes;              /* probes updated */
+    uint64_t primary_node_visits; /* BVH2 nodes (64 B) fetched by the probe-ray traversals */
+    uint64_t primary_tri_tests;   /* triangle records (48 B) fetched by the probe-ray traversals */
+    uint64_t hits;                /* probe rays with a hit (front or back face) */
+    uint64_t front_hits;          /* probe rays whose hit is shaded (front face) */
+    uint64_t shadow_rays;         /* shadow rays traced */
+    uint64_t shadow_node_visits;  /* BVH2 nodes fetched by shadow rays */
+    uint64_t shadow_tri_tests;    /* triangle records fetched by shadow rays */
+    uint64_t reserved;
 } ArkDdgiCounters;
 
 /* Device-side views of the persistent resources, for an external collective

@@ -68,7 +68,13 @@ def run_pair(scene, grid, cfg, frames, z_far=10000.0, exposure=None, threads=8, 
         orc.update(p, threads)
         node_idx = (node_idx + p.probe_updates) % grid.probe_count()
         if check_each_frame or f == frames - 1:
-            reports.append([diff_report(k, ctx.read(w), orc.read(w)) for k, w in RESOURCES.items()])
+            rep = []
+            for k, w in RESOURCES.items():
+                g, o = ctx.read(w), orc.read(w)
+                r = diff_report(k, g, o)
+                r["nonzero"] = int(np.count_nonzero(o))
+                rep.append(r)
+            reports.append(rep)
     ctx.close()
     orc.close()
     return reports
