@@ -70,7 +70,8 @@ struct ArkDdgiCtx {
     // persistent resources
     DeviceBuffer irr, vis, offsets;
     // working set
-    DeviceBuffer slots, fib, hits, surfels, spill, rayCounter, counters;
+    DeviceBuffer slots, fib, hits, surfels, spill, rayCounter, counters, shadeScratch;
+    uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0;
     // scene
@@ -235,7 +236,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeScratch,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
@@ -439,6 +440,14 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     sc.spot_count = static_cast<int32_t>(s->spot_light_count);
     sc.spots = ctx->spots.as<GpuSpotLight>();
     ctx->bvhMaxDepth = maxDepth;
+    if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
+    ctx->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
+    {
+        int occ = 0;
+        ARK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_shade_ptr(false), kShadeBlock, shade_lds_bytes(ctx->lightCount)));
+        ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occ) * ctx->cuCount);
+        ARK_HIP(ctx->shadeScratch.alloc(shade_scratch_bytes(ctx->shadeBlocks, ctx->lightCount)));
+    }
     if ((rc = ensureSpill(ctx)) != 0) return rc;
     ctx->hasScene = true;
     const auto t1 = std::chrono::steady_clock::now();
@@ -511,6 +520,8 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     f.hits = ctx->hits.as<GpuHit>();
     f.surfels = ctx->surfels.as<uint16_t>();
     f.spill = ctx->spill.as<int32_t>();
+    f.shade_scratch = ctx->shadeScratch.as<float4>();
+    f.light_count = ctx->lightCount;
     f.ray_counter = ctx->rayCounter.as<uint32_t>();
     f.counters = ctx->counters.as<unsigned long long>();
     const bool timing = ctx->timing;
@@ -553,6 +564,7 @@ static int resourceInfo(const ArkDdgiCtx* ctx, int which, void** ptr, uint64_t* 
     case ARK_DDGI_ATLAS_VISIBILITY: *ptr = ctx->vis.ptr; *bytes = ctx->vis.bytes; return 0;
     case ARK_DDGI_SURFELS: *ptr = ctx->surfels.ptr; *bytes = ctx->surfels.bytes; return 0;
     case ARK_DDGI_PROBE_OFFSETS: *ptr = ctx->offsets.ptr; *bytes = ctx->offsets.bytes; return 0;
+    case ARK_DDGI_DEBUG_HITS: *ptr = ctx->hits.ptr; *bytes = ctx->hits.bytes; return 0;
     default: return ARK_DDGI_E_INVALID_ARGUMENT;
     }
 }

@@ -43,6 +43,10 @@ __device__ __forceinline__ float lerpf(float a, float b, float t) { return a + (
 // fp16 storage (RNE, NaN canonicalised to 0x7e00 like the oracle)
 __device__ __forceinline__ uint16_t f32_to_f16(float f)
 {
+    // The empty asm makes the fp32 value opaque: without it the backend may fuse
+    // the producing fmul/fma with the conversion (v_mad_mix* rounds the exact
+    // product to f16 once), which differs from fp32-then-f16 on fp16 ties.
+    asm volatile("" : "+v"(f));
     if (f != f) return 0x7e00u;
     return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));
 }

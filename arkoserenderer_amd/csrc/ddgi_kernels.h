@@ -14,6 +14,8 @@ constexpr int kStackLds = 16;      // traversal stack entries per lane kept in L
 constexpr int kTraceBlock = 256;
 constexpr int kShadeBlock = 256;
 constexpr int kUpdateBlock = 320;  // 4 waves visibility (16x16 texels) + 1 wave irradiance (8x8)
+constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in-block compaction)
+constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
@@ -76,6 +78,8 @@ struct FrameArgs {
     GpuHit* hits;
     uint16_t* surfels;
     int32_t* spill;
+    float4* shade_scratch;   // per shading block: [chunk] partial colours + [chunk][lights] light records
+    uint32_t light_count;    // has_sun + spot lights
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };
@@ -83,6 +87,8 @@ struct FrameArgs {
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
+size_t shade_lds_bytes(uint32_t lights);
+size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
 const void* kernel_trace_primary_ptr(bool count);

@@ -304,8 +304,15 @@ __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tm
 }
 
 // ---------------------------------------------------------------------------
-// 2. primary traversal (persistent, wave64 ballot refill)
+// 2. primary traversal (persistent, per-lane wave64 ballot refill)
 // ---------------------------------------------------------------------------
+// Every lane owns one probe ray at a time. One outer iteration advances every
+// active lane to its next leaf and tests it (Aila–Laine while-while); lanes whose
+// ray finished are refilled at the top of the next iteration from a wave-private
+// pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays),
+// so the SIMD stays full until the global ray counter runs out.
+constexpr int32_t kNodeDone = static_cast<int32_t>(0x80000000u);
+
 template<bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
@@ -315,50 +322,167 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t total = f.window_rays;
     const uint32_t lane = threadIdx.x & 63u;
+    const float tmin = 0.0001f; // raygen.rgen:116
     uint32_t cNodes = 0, cTris = 0, cHits = 0;
+
+    uint32_t poolNext = 0, poolEnd = 0;
+    bool exhausted = false;
+    bool active = false;
+    uint32_t ray = 0;
+    int pass = 0;
+    int32_t node = kNodeDone;
+    V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 }, ooeo = { 0, 0, 0 };
+    RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+    float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
+
     for (;;) {
-        // wave64 refill: one atomic per wave hands out 64 consecutive rays; rays of
-        // one probe share an origin, so a wave starts its descent coherently.
-        uint32_t rayBase = 0;
-        if (lane == 0) rayBase = atomicAdd(f.ray_counter, 64u);
-        rayBase = __shfl(rayBase, 0);
-        if (rayBase >= total) break;
-        const uint32_t ray = rayBase + lane;
-        if (ray < total) {
-            const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
-            const GpuProbeSlot ps = f.slots[slot];
-            const float4 fb = f.fib[sample];
-            const V3 o = { ps.pos[0], ps.pos[1], ps.pos[2] };
-            const V3 d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
-            const float tmin = 0.0001f; // raygen.rgen:116
-            RayHit h { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-            // opaque pass: RayFlags_Opaque, cullMask 0x01, tmax = zFar (raygen.rgen:122-134)
-            traverse<false, false, COUNT>(sc, sc.root_opaque, o, d, tmin, h, st, cNodes, cTris);
-            if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
-            float tmaxSigned = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
-            // masked pass: RayFlags_NoOpaque, cullMask 0x02, tmax = previous hit T
-            // (raygen.rgen:136-147); a negative tmax (backface) is an empty interval.
-            if (sc.root_masked >= 0 && tmaxSigned >= tmin) {
-                RayHit m { tmaxSigned, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-                traverse<false, true, COUNT>(sc, sc.root_masked, o, d, tmin, m, st, cNodes, cTris);
-                if (m.tri != kNoHit) {
-                    m.backface = m.backface != (sc.instances[m.inst].flip_facing != 0);
-                    h = m;
+        // ---- refill finished lanes --------------------------------------------
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && !exhausted) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(need));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
+            const uint32_t avail = poolEnd - poolNext;
+            uint32_t fresh = 0;
+            if (avail < n) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(f.ray_counter, 64u);
+                fresh = __shfl(b, 0);
+            }
+            if (!active) {
+                uint32_t r = kNoHit;
+                if (rank < avail) r = poolNext + rank;
+                else if (fresh < total) r = fresh + (rank - avail);
+                if (r < total && (rank < avail || r < min(fresh + 64u, total))) {
+                    ray = r;
+                    active = true;
+                    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+                    const GpuProbeSlot ps = f.slots[slot];
+                    const float4 fb = f.fib[sample];
+                    o = { ps.pos[0], ps.pos[1], ps.pos[2] };
+                    d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+                    idir = safeInv(d);
+                    ooeo = o * idir;
+                    h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                    pass = 0;
+                    node = sc.root_opaque;
+                    st.depth = 0;
+                    if (node < 0) node = kNodeDone;
                 }
             }
-            GpuHit out;
-            if (h.tri == kNoHit) {
-                out.t = __builtin_bit_cast(float, 0x7f800000u);
-                out.u = out.v = 0.0f;
-                out.tri = kNoHit;
+            if (avail < n) {
+                if (fresh >= total) {
+                    exhausted = true;
+                    poolNext = poolEnd = 0;
+                } else {
+                    poolNext = fresh + (n - avail);
+                    poolEnd = min(fresh + 64u, total);
+                    if (poolNext > poolEnd) poolNext = poolEnd;
+                }
             } else {
-                out.t = h.backface ? -h.t : h.t;
-                out.u = h.u;
-                out.v = h.v;
-                out.tri = h.tri;
-                if (COUNT) cHits++;
+                poolNext += n;
             }
-            f.hits[ray] = out;
+        }
+        if (__ballot(active) == 0) break;
+        if (active) {
+            // ---- descend to the next leaf --------------------------------------
+            while (node >= 0) {
+                const float4* np = reinterpret_cast<const float4*>(sc.nodes + node);
+                const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+                const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+                if (COUNT) cNodes++;
+                const float tmax = h.t;
+                float c0lox = fmaf_(n0.x, idir.x, -ooeo.x), c0hix = fmaf_(n0.y, idir.x, -ooeo.x);
+                float c0loy = fmaf_(n0.z, idir.y, -ooeo.y), c0hiy = fmaf_(n0.w, idir.y, -ooeo.y);
+                float c0loz = fmaf_(n2.x, idir.z, -ooeo.z), c0hiz = fmaf_(n2.y, idir.z, -ooeo.z);
+                float c1lox = fmaf_(n1.x, idir.x, -ooeo.x), c1hix = fmaf_(n1.y, idir.x, -ooeo.x);
+                float c1loy = fmaf_(n1.z, idir.y, -ooeo.y), c1hiy = fmaf_(n1.w, idir.y, -ooeo.y);
+                float c1loz = fmaf_(n2.z, idir.z, -ooeo.z), c1hiz = fmaf_(n2.w, idir.z, -ooeo.z);
+                float t0n = fmaxf(fmaxf(fminf(c0lox, c0hix), fminf(c0loy, c0hiy)), fmaxf(fminf(c0loz, c0hiz), tmin));
+                float t0f = fminf(fminf(fmaxf(c0lox, c0hix), fmaxf(c0loy, c0hiy)), fminf(fmaxf(c0loz, c0hiz), tmax));
+                float t1n = fmaxf(fmaxf(fminf(c1lox, c1hix), fminf(c1loy, c1hiy)), fmaxf(fminf(c1loz, c1hiz), tmin));
+                float t1f = fminf(fminf(fmaxf(c1lox, c1hix), fmaxf(c1loy, c1hiy)), fminf(fmaxf(c1loz, c1hiz), tmax));
+                const bool hit0 = t0n <= fmaf_(t0f, 1.00001f, 1e-7f);
+                const bool hit1 = t1n <= fmaf_(t1f, 1.00001f, 1e-7f);
+                if (hit0 && hit1) {
+                    int32_t nearC = n3.x, farC = n3.y;
+                    if (t1n < t0n) { nearC = n3.y; farC = n3.x; }
+                    st.push(farC);
+                    node = nearC;
+                } else if (hit0) {
+                    node = n3.x;
+                } else if (hit1) {
+                    node = n3.y;
+                } else {
+                    node = st.depth == 0 ? kNodeDone : st.pop();
+                }
+            }
+            // ---- test the leaf ----------------------------------------------------
+            if (node != kNodeDone) {
+                const uint32_t code = static_cast<uint32_t>(~node);
+                const uint32_t first = code >> kLeafCountBits;
+                const uint32_t count = (code & (kMaxLeafSize - 1)) + 1u;
+                for (uint32_t i = first; i < first + count; ++i) {
+                    const GpuTriangle tr = loadTri(sc.tris, i);
+                    if (COUNT) cTris++;
+                    float tt, uu, vv;
+                    bool bf;
+                    if (!intersectTri(o, d, tmin, h.t, tr, &tt, &uu, &vv, &bf)) continue;
+                    const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
+                    const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
+                    if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
+                    if (pass == 1 && !alphaAccept(sc, inst, prim, uu, vv)) continue;
+                    h.t = tt;
+                    h.u = uu;
+                    h.v = vv;
+                    h.tri = i;
+                    h.inst = inst;
+                    h.prim = prim;
+                    h.backface = bf;
+                }
+                node = st.depth == 0 ? kNodeDone : st.pop();
+            }
+            // ---- pass finished -----------------------------------------------------
+            if (node == kNodeDone) {
+                if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
+                bool finished = true;
+                if (pass == 0) {
+                    // opaque pass done (raygen.rgen:122-134); masked pass: RayFlags_NoOpaque,
+                    // cullMask 0x02, tmax = previous hit T (:136-147); a negative tmax
+                    // (backface) is an empty interval.
+                    opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
+                    if (sc.root_masked >= 0 && opaqueT >= tmin) {
+                        pass = 1;
+                        finished = false;
+                        // keep the opaque hit in the stack-free registers: restart with tmax = opaqueT
+                        node = sc.root_masked;
+                        st.depth = 0;
+                        // stash the opaque hit; the masked pass searches [tmin, opaqueT]
+                        f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
+                        h = RayHit { opaqueT, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                    }
+                }
+                if (finished) {
+                    if (pass == 1 && h.tri == kNoHit) {
+                        // masked pass found nothing: the opaque result (already stored) stands
+                        if (COUNT && f.hits[ray].tri != kNoHit) cHits++;
+                    } else {
+                        GpuHit out;
+                        if (h.tri == kNoHit) {
+                            out.t = __builtin_bit_cast(float, 0x7f800000u);
+                            out.u = out.v = 0.0f;
+                            out.tri = kNoHit;
+                        } else {
+                            out.t = h.backface ? -h.t : h.t;
+                            out.u = h.u;
+                            out.v = h.v;
+                            out.tri = h.tri;
+                            if (COUNT) cHits++;
+                        }
+                        f.hits[ray] = out;
+                    }
+                    active = false;
+                }
+            }
         }
     }
     if (COUNT) {
@@ -369,22 +493,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
 }
 
 // ---------------------------------------------------------------------------
-// 3. shading
+// 3. shading helpers
 // ---------------------------------------------------------------------------
-template<bool COUNT>
-__device__ float traceShadowRay(const SceneArgs& sc, V3 X, V3 L, float maxDistance, Stack<kShadeBlock>& st, uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow)
-{
-    // opaque.rchit:35-54: TerminateOnFirstHit|SkipClosestHit|Opaque, cullMask 0xff, tmin 0.025
-    const float tmin = 0.025f;
-    if (!(maxDistance >= tmin)) return 1.0f;
-    if (COUNT) cShadow++;
-    RayHit h { maxDistance, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-    if (traverse<true, false, COUNT>(sc, sc.root_opaque, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
-    if (traverse<true, false, COUNT>(sc, sc.root_masked, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
-    if (traverse<true, false, COUNT>(sc, sc.root_blend, X, L, tmin, h, st, cNodes, cTris)) return 0.0f;
-    return 1.0f;
-}
-
 // probeSampling.glsl:9-27
 __device__ __forceinline__ void atlasSampleUV(const FrameArgs& f, int px, int py, int pz, V3 dir, int res, float invW, float invH, float* u, float* v)
 {
@@ -508,38 +618,113 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
     return irradiance;
 }
 
+
+// ---------------------------------------------------------------------------
+// 3. shading (in-block compaction: classify -> dense surface -> dense shadow -> finish)
+// ---------------------------------------------------------------------------
+// Each block takes chunks of kShadeChunk consecutive probe rays. Misses and
+// backface hits are finished in the classify phase; front hits are compacted
+// into an LDS list and shaded densely; their shadow rays (one per lit light) are
+// compacted again and traced densely; a last pass adds the light terms in the
+// reference's order. Per light the closest hit's term is precomputed for both
+// shadowFactor = 1 (T) and 0 (Z) (opaque.rchit:56-103), so the final sum is the
+// same IEEE sequence as the single-pass shader: base (+ T or Z per lit light) + indirect.
+template<bool COUNT>
+__device__ __forceinline__ bool shadowOccluded(const SceneArgs& sc, V3 X, V3 L, float maxDistance, Stack<kShadeBlock>& st, uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow)
+{
+    // opaque.rchit:35-54: TerminateOnFirstHit|SkipClosestHit|Opaque, cullMask 0xff, tmin 0.025
+    const float tmin = 0.025f;
+    if (!(maxDistance >= tmin)) return false;
+    if (COUNT) cShadow++;
+    RayHit h { maxDistance, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+    if (traverse<true, false, COUNT>(sc, sc.root_opaque, X, L, tmin, h, st, cNodes, cTris)) return true;
+    if (traverse<true, false, COUNT>(sc, sc.root_masked, X, L, tmin, h, st, cNodes, cTris)) return true;
+    if (traverse<true, false, COUNT>(sc, sc.root_blend, X, L, tmin, h, st, cNodes, cTris)) return true;
+    return false;
+}
+
+__device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3 color, float dist)
+{
+    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+    uint2 packed;
+    packed.x = static_cast<uint32_t>(f32_to_f16(color.x)) | (static_cast<uint32_t>(f32_to_f16(color.y)) << 16);
+    packed.y = static_cast<uint32_t>(f32_to_f16(color.z)) | (static_cast<uint32_t>(f32_to_f16(dist)) << 16);
+    reinterpret_cast<uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + sample] = packed;
+}
+
+__device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* origin, V3* dir)
+{
+    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+    const GpuProbeSlot ps = f.slots[slot];
+    const float4 fb = f.fib[sample];
+    *origin = { ps.pos[0], ps.pos[1], ps.pos[2] };
+    *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+}
+
+// Light record (64 B): shadow ray + both candidate terms.
+struct alignas(16) LightRec {
+    float4 origin_tmax;
+    float4 dir;
+    float4 T; // term with shadowFactor = 1
+    float4 Z; // term with shadowFactor = 0
+};
+
+
 template<bool COUNT>
 __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f)
 {
-    __shared__ int32_t ldsStack[kStackLds * kShadeBlock];
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    int32_t* ldsStack = reinterpret_cast<int32_t*>(lds);
+    uint32_t* listA = lds + kStackLds * kShadeBlock;   // compacted front hits (ray index)
+    uint32_t* needMask = listA + kShadeChunk;          // per front hit: lit lights (shadow ray issued)
+    uint32_t* occMask = needMask + kShadeChunk;        // per front hit: occluded lights
+    uint32_t* listB = occMask + kShadeChunk;           // compacted shadow rays: (front << 4) | light
+    uint32_t* counts = listB + kShadeChunk * f.light_count + (f.light_count == 0 ? 1 : 0);
     const uint32_t gtid = blockIdx.x * kShadeBlock + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * kShadeBlock;
-    Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
+    Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kShadeBlock, 0 };
+    const uint32_t L = f.light_count;
+    float4* partial = f.shade_scratch + static_cast<size_t>(blockIdx.x) * kShadeChunk * (2 + 4 * L);
+    LightRec* lrec = reinterpret_cast<LightRec*>(partial + 2 * kShadeChunk);
     uint32_t cNodes = 0, cTris = 0, cShadow = 0, cFront = 0;
-    for (uint32_t ray = gtid; ray < f.window_rays; ray += nthreads) {
-        const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
-        const GpuHit hit = f.hits[ray];
-        const GpuProbeSlot ps = f.slots[slot];
-        const float4 fb = f.fib[sample];
-        const V3 origin = { ps.pos[0], ps.pos[1], ps.pos[2] };
-        const V3 dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
-        V3 color;
-        float dist;
-        if (hit.tri == kNoHit) {
-            // miss (raygen.rgen:149-158)
-            dist = f.z_far;
-            float u, v;
-            sphericalUvFromDirection(dir, &u, &v);
-            float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.env_texture, u, v);
-            color = f.environment_multiplier * v3(c.x, c.y, c.z);
-        } else if (hit.t < 0.0f) {
-            // backface: colour 0, depth x 0.2 (raygen.rgen:208-213); the closest-hit
-            // colour and the indirect term are overwritten, so they are not evaluated.
-            color = splat(0.0f);
-            dist = hit.t * 0.2f;
-        } else {
-            const float T = hit.t;
+
+    for (uint32_t chunk = blockIdx.x * kShadeChunk; chunk < f.window_rays; chunk += gridDim.x * kShadeChunk) {
+        if (threadIdx.x == 0) {
+            counts[0] = 0;
+            counts[1] = 0;
+        }
+        __syncthreads();
+        // ---- A. classify: misses and backfaces finish here ----------------------
+        for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
+            const uint32_t ray = chunk + r;
+            if (ray >= f.window_rays) break;
+            const GpuHit hit = f.hits[ray];
+            if (hit.tri == kNoHit) {
+                // miss (raygen.rgen:149-158)
+                V3 origin, dir;
+                rayOf(f, ray, &origin, &dir);
+                float u, v;
+                sphericalUvFromDirection(dir, &u, &v);
+                float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.env_texture, u, v);
+                storeSurfel(f, ray, f.environment_multiplier * v3(c.x, c.y, c.z), f.z_far);
+            } else if (hit.t < 0.0f) {
+                // backface: colour 0, depth x 0.2 (raygen.rgen:208-213); the closest-hit
+                // colour and the indirect term are overwritten, so they are not evaluated.
+                storeSurfel(f, ray, splat(0.0f), hit.t * 0.2f);
+            } else {
+                const uint32_t k = atomicAdd(&counts[0], 1u);
+                listA[k] = ray;
+            }
+        }
+        __syncthreads();
+        const uint32_t nA = counts[0];
+        // ---- B. dense surface shading of front hits -----------------------------
+        for (uint32_t k = threadIdx.x; k < nA; k += kShadeBlock) {
+            const uint32_t ray = listA[k];
             if (COUNT) cFront++;
+            const GpuHit hit = f.hits[ray];
+            V3 origin, dir;
+            rayOf(f, ray, &origin, &dir);
+            const float T = hit.t;
             const GpuTriangle tr = loadTri(sc.tris, hit.tri);
             const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
             const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
@@ -548,9 +733,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
             const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
             float bx = 1.0f - hit.u - hit.v, by = hit.u, bz = hit.v;
             const float* vx[3];
-            for (int k = 0; k < 3; ++k) {
-                uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + k];
-                vx[k] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+            for (int q = 0; q < 3; ++q) {
+                uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
+                vx[q] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
             }
             // opaque.rchit:118-131 (front face: no flip)
             V3 N = normalize(v3(vx[0][2], vx[0][3], vx[0][4]) * bx + v3(vx[1][2], vx[1][3], vx[1][4]) * by + v3(vx[2][2], vx[2][3], vx[2][4]) * bz);
@@ -569,28 +754,37 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
             const float clearcoat = mat.clearcoat, ccRough = mat.clearcoat_roughness;
             const V3 V = -dir;
             V3 ambient = f.ambient_amount * baseColor;
-            color = emissive + ambient;
+            const V3 base = emissive + ambient;
             const V3 hitPoint = origin + T * dir;
+            uint32_t need = 0;
+            uint32_t l = 0;
             if (sc.has_sun) { // opaque.rchit:56-73
-                V3 L = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
-                float LdotN = dot(L, N);
+                V3 Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+                float LdotN = dot(Ld, N);
                 if (LdotN > 0.0f) {
-                    float shadowFactor = traceShadowRay<COUNT>(sc, hitPoint, L, 2.0f * f.z_far, st, cNodes, cTris, cShadow);
-                    V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
-                    V3 directLight = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]) * shadowFactor;
-                    color = color + brdf * LdotN * directLight;
+                    V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                    V3 lc = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]);
+                    V3 tT = brdf * LdotN * (lc * 1.0f);
+                    V3 tZ = brdf * LdotN * (lc * 0.0f);
+                    LightRec rec;
+                    rec.origin_tmax = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far);
+                    rec.dir = make_float4(Ld.x, Ld.y, Ld.z, 0.0f);
+                    rec.T = make_float4(tT.x, tT.y, tT.z, 0.0f);
+                    rec.Z = make_float4(tZ.x, tZ.y, tZ.z, 0.0f);
+                    lrec[static_cast<size_t>(k) * L + l] = rec;
+                    need |= 1u << l;
                 }
+                l++;
             }
-            for (int li = 0; li < sc.spot_count; ++li) { // opaque.rchit:75-103
+            for (int li = 0; li < sc.spot_count; ++li, ++l) { // opaque.rchit:75-103
                 const GpuSpotLight sl = sc.spots[li];
                 V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
-                V3 L = -normalize(sdir);
-                float LdotN = dot(L, N);
+                V3 Ld = -normalize(sdir);
+                float LdotN = dot(Ld, N);
                 if (LdotN > 0.0f) {
                     V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
                     float distanceToLight = length(toLight);
                     V3 normalizedToLight = toLight / distanceToLight;
-                    float shadowFactor = traceShadowRay<COUNT>(sc, hitPoint, normalizedToLight, distanceToLight - 0.001f, st, cNodes, cTris, cShadow);
                     float distanceAttenuation = 1.0f / square(distanceToLight);
                     // evaluateIESLookupTable (lighting.glsl:20-39)
                     V3 lrd = -normalizedToLight;
@@ -604,26 +798,69 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
                         float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
                         iesValue = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(sl.ies_texture), lx, ly).x;
                     }
-                    V3 brdf = evaluateDefaultBRDF(L, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
-                    V3 directLight = v3(sl.color[0], sl.color[1], sl.color[2]) * shadowFactor * distanceAttenuation * iesValue;
-                    color = color + brdf * LdotN * directLight;
+                    V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                    V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
+                    V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
+                    V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
+                    LightRec rec;
+                    rec.origin_tmax = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f);
+                    rec.dir = make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, 0.0f);
+                    rec.T = make_float4(tT.x, tT.y, tT.z, 0.0f);
+                    rec.Z = make_float4(tZ.x, tZ.y, tZ.z, 0.0f);
+                    lrec[static_cast<size_t>(k) * L + l] = rec;
+                    need |= 1u << l;
                 }
             }
             // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
-            dist = T;
-            const V3 hitPos = origin + dist * dir;
+            const V3 hitPos = origin + T * dir;
             const V3 Vi = -dir;
             V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
             V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
             V3 irradiance = sampleDDGI(f, hitPos, N, Vi);
             V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
-            color = color + baseColor * indirect;
+            const V3 bi = baseColor * indirect;
+            needMask[k] = need;
+            occMask[k] = 0;
+            if (need == 0) {
+                storeSurfel(f, ray, base + bi, T);
+            } else {
+                partial[2 * k] = make_float4(base.x, base.y, base.z, T);
+                partial[2 * k + 1] = make_float4(bi.x, bi.y, bi.z, 0.0f);
+                for (uint32_t b = need; b; b &= b - 1) {
+                    const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
+                    const uint32_t j = atomicAdd(&counts[1], 1u);
+                    listB[j] = (k << 4) | ll;
+                }
+            }
         }
-        // imageStore(surfelImage, (slot, sample), vec4(color, dist)) -> fp16
-        uint2 packed;
-        packed.x = static_cast<uint32_t>(f32_to_f16(color.x)) | (static_cast<uint32_t>(f32_to_f16(color.y)) << 16);
-        packed.y = static_cast<uint32_t>(f32_to_f16(color.z)) | (static_cast<uint32_t>(f32_to_f16(dist)) << 16);
-        reinterpret_cast<uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + sample] = packed;
+        __syncthreads();
+        // ---- C. dense shadow rays ------------------------------------------------
+        const uint32_t nB = counts[1];
+        for (uint32_t j = threadIdx.x; j < nB; j += kShadeBlock) {
+            const uint32_t e = listB[j];
+            const uint32_t k = e >> 4, ll = e & 15u;
+            const LightRec rec = lrec[static_cast<size_t>(k) * L + ll];
+            const V3 X = v3(rec.origin_tmax.x, rec.origin_tmax.y, rec.origin_tmax.z);
+            const V3 Ld = v3(rec.dir.x, rec.dir.y, rec.dir.z);
+            if (shadowOccluded<COUNT>(sc, X, Ld, rec.origin_tmax.w, st, cNodes, cTris, cShadow)) atomicOr(&occMask[k], 1u << ll);
+        }
+        __syncthreads();
+        // ---- D. finish lit front hits in the reference's light order -------------
+        for (uint32_t k = threadIdx.x; k < nA; k += kShadeBlock) {
+            const uint32_t need = needMask[k];
+            if (need == 0) continue;
+            const uint32_t occ = occMask[k];
+            const float4 p0 = partial[2 * k], p1 = partial[2 * k + 1];
+            V3 color = v3(p0.x, p0.y, p0.z);
+            for (uint32_t b = need; b; b &= b - 1) {
+                const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
+                const float4 t = (occ >> ll) & 1u ? lrec[static_cast<size_t>(k) * L + ll].Z : lrec[static_cast<size_t>(k) * L + ll].T;
+                color = color + v3(t.x, t.y, t.z);
+            }
+            color = color + v3(p1.x, p1.y, p1.z);
+            storeSurfel(f, listA[k], color, p0.w);
+        }
+        __syncthreads();
     }
     if (COUNT) {
         atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
@@ -632,7 +869,6 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
         atomicAdd(&f.counters[6], static_cast<unsigned long long>(cFront));
     }
 }
-
 // ---------------------------------------------------------------------------
 // 4. probe update: irradiance + visibility + borders + offsets, one WG per probe
 // ---------------------------------------------------------------------------
@@ -668,6 +904,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
     constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
     __shared__ float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
     __shared__ uint2 sSurf[ARK_DDGI_MAX_RAYS_PER_PROBE];
+    __shared__ float2 sDist[ARK_DDGI_MAX_RAYS_PER_PROBE]; // (d, d^2), d = min(|surfel.a|, 1.5 * gridMaxSpacing)
     __shared__ uint2 sIrrTile[(IR + 2) * (IR + 2)];
     __shared__ uint32_t sVisTile[(VR + 2) * (VR + 2)];
     const uint32_t slot = blockIdx.x;
@@ -683,7 +920,14 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         sDir[0][s] = d.x;
         sDir[1][s] = d.y;
         sDir[2][s] = d.z;
-        sSurf[s] = reinterpret_cast<const uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + s];
+        const uint2 sv = reinterpret_cast<const uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + s];
+        sSurf[s] = sv;
+        // probeUpdateVisibility.comp:45-48 (per ray; identical for every texel)
+        const float gridMaxSpacing = fmaxf_(f.spacing[0], fmaxf_(f.spacing[1], f.spacing[2]));
+        const float maxDistance = 1.5f * gridMaxSpacing;
+        float dd = f16_to_f32(static_cast<uint16_t>(sv.y >> 16));
+        dd = fminf_(fabsf_(dd), maxDistance);
+        sDist[s] = make_float2(dd, square(dd));
     }
     __syncthreads();
     // tile origin (ddgi/common.glsl:53-67)
@@ -696,21 +940,26 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
     const float epsilon = 1e-9f * static_cast<float>(R);
     if (tid < VR * VR) {
         // probeUpdateVisibility.comp:24-63
-        const int tx = tid % VR, ty = tid / VR;
+        // each wave owns an 8x8 block of the octahedral tile (a compact cone of
+        // directions), so a ray that is behind all 64 texels skips the pow for the wave
+        const int wv = tid >> 6, ln = tid & 63;
+        const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
         float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(VR);
         float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(VR);
         const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
-        const float gridMaxSpacing = fmaxf_(f.spacing[0], fmaxf_(f.spacing[1], f.spacing[2]));
-        const float maxDistance = 1.5f * gridMaxSpacing;
+        const float sharp = f.visibility_sharpness;
+        const bool skipZero = sharp > 0.0f; // pow(0, s > 0) == 0 adds exactly +0 to finite sums
         float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
         for (uint32_t s = 0; s < R; ++s) {
             V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-            float weight = powf_(fmaxf_(0.0f, dot(texelDirection, rd)), f.visibility_sharpness);
-            float d = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
-            d = fminf_(fabsf_(d), maxDistance);
-            nv0 += weight * d;
-            nv1 += weight * square(d);
-            totalWeight += weight;
+            const float x = fmaxf_(0.0f, dot(texelDirection, rd));
+            if (x > 0.0f || !skipZero) {
+                float weight = powf_(x, sharp);
+                const float2 dd = sDist[s];
+                nv0 += weight * dd.x;
+                nv1 += weight * dd.y;
+                totalWeight += weight;
+            }
         }
         float den = fmaxf_(totalWeight, epsilon);
         nv0 = nv0 / den;
@@ -834,10 +1083,21 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
     return hipGetLastError();
 }
 
+size_t shade_lds_bytes(uint32_t lights)
+{
+    return static_cast<size_t>(kStackLds) * kShadeBlock * 4 + static_cast<size_t>(kShadeChunk) * (3 + lights) * 4 + 16;
+}
+
+size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights)
+{
+    return static_cast<size_t>(blocks) * kShadeChunk * (2 + 4 * static_cast<size_t>(lights)) * 16;
+}
+
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    if (count) hipLaunchKernelGGL(dev::k_shade<true>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL(dev::k_shade<false>, dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    const size_t lds = shade_lds_bytes(f.light_count);
+    if (count) hipLaunchKernelGGL(dev::k_shade<true>, dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    else hipLaunchKernelGGL(dev::k_shade<false>, dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
     return hipGetLastError();
 }
 

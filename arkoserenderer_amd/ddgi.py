@@ -135,7 +135,7 @@ class DDGIContext:
 
     def read(self, which: int) -> np.ndarray:
         n = self.size(which)
-        dt = np.float32 if which == abi.ARK_DDGI_PROBE_OFFSETS else np.uint16
+        dt = np.float32 if which in (abi.ARK_DDGI_PROBE_OFFSETS, abi.ARK_DDGI_DEBUG_HITS) else np.uint16
         out = np.empty(n // np.dtype(dt).itemsize, dtype=dt)
         self.check(self.lib.ark_ddgi_read(self.h, which, out.ctypes.data, n), "ark_ddgi_read")
         return out

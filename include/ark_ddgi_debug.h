@@ -12,6 +12,11 @@
 extern "C" {
 #endif
 
+/* Extra resource id for ark_ddgi_read: the primary-pass hit records of the last
+ * update, 16 B each ({float t (negative = backface, +inf = miss), u, v, uint32
+ * leaf-order triangle}) in [slot][max_rays_per_probe] order. */
+#define ARK_DDGI_DEBUG_HITS 100
+
 /* Evaluates op (0 sin, 1 cos, 2 acos, 3 atan2(x,y), 4 log2, 5 exp2, 6 pow(x,y),
  * 7 fp32->fp16->fp32 round trip) on `device` for n inputs (host arrays). */
 int ark_ddgi_debug_fmath(int device, int op, const float* x, const float* y, float* out, uint64_t n);
