@@ -208,4 +208,54 @@ ARK_HD float powf_(float x, float y)
     return exp2f_(y * log2f_(x));
 }
 
+// powf_ restricted to x > 0 finite, y finite with y*log2(x) <= 128, written
+// without branches (selects only) so it vectorises in the hot visibility loop.
+// Bitwise identical to powf_ on that domain: the same IEEE operations in the
+// same order (tests/test_fmath.py and tests/test_gpu_fmath.py pin this).
+ARK_HD float powf_pos_(float x, float y)
+{
+    // log2f_ main path
+    const bool den = x < 0x1p-126f;
+    const float xs = den ? x * 0x1p+23f : x;
+    const uint32_t u = f2u(xs);
+    int e = (den ? -23 : 0) + static_cast<int>((u >> 23) & 0xffu) - 126;
+    const float m0 = u2f((u & 0x007fffffu) | 0x3f000000u);
+    const bool lo = m0 < 0.70710678118654752440f;
+    e -= lo ? 1 : 0;
+    const float m = lo ? (m0 + m0 - 1.0f) : (m0 - 1.0f);
+    const float z2 = m * m;
+    float p = fmaf_(m, 7.0376836292e-2f, -1.1514610310e-1f);
+    p = fmaf_(m, p, 1.1676998740e-1f);
+    p = fmaf_(m, p, -1.2420140846e-1f);
+    p = fmaf_(m, p, 1.4249322787e-1f);
+    p = fmaf_(m, p, -1.6668057665e-1f);
+    p = fmaf_(m, p, 2.0000714765e-1f);
+    p = fmaf_(m, p, -2.4999993993e-1f);
+    p = fmaf_(m, p, 3.3333331174e-1f);
+    float yy = m * (z2 * p);
+    yy = fmaf_(-0.5f, z2, yy);
+    const float LOG2EA = 0.44269504088896340736f;
+    float r = yy * LOG2EA;
+    r = fmaf_(m, LOG2EA, r);
+    r = r + yy;
+    r = r + m;
+    const float l2 = r + static_cast<float>(e);
+    // exp2f_ main path
+    const float z = y * l2;
+    const float i = floorf_(z + 0.5f);
+    const float f = z - i;
+    float q = fmaf_(f, 1.535336188319500e-4f, 1.339887440266574e-3f);
+    q = fmaf_(f, q, 9.618437357674640e-3f);
+    q = fmaf_(f, q, 5.550332471162809e-2f);
+    q = fmaf_(f, q, 2.402264791363012e-1f);
+    q = fmaf_(f, q, 6.931472028550421e-1f);
+    float t = fmaf_(f, q, 1.0f);
+    int n = static_cast<int>(i);
+    const bool sub = n < -126;
+    t = sub ? t * 0x1p-126f : t;
+    n = sub ? n + 126 : n;
+    const float res = t * u2f(static_cast<uint32_t>(n + 127) << 23);
+    return (z < -151.0f || n < -126) ? 0.0f : res;
+}
+
 } // namespace ark

@@ -948,13 +948,23 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(VR);
         const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
         const float sharp = f.visibility_sharpness;
-        const bool skipZero = sharp > 0.0f; // pow(0, s > 0) == 0 adds exactly +0 to finite sums
         float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
-        for (uint32_t s = 0; s < R; ++s) {
-            V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-            const float x = fmaxf_(0.0f, dot(texelDirection, rd));
-            if (x > 0.0f || !skipZero) {
-                float weight = powf_(x, sharp);
+        if (sharp > 0.0f && sharp <= 64.0f) {
+            // weight = pow(max(0, d), sharp): pow(0, s > 0) = 0 exactly, and for x in
+            // (0, 1+eps] powf_pos_ == powf_ bit for bit, so a select replaces the branches
+            for (uint32_t s = 0; s < R; ++s) {
+                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+                const float x = fmaxf_(0.0f, dot(texelDirection, rd));
+                const float weight = x > 0.0f ? powf_pos_(x, sharp) : 0.0f;
+                const float2 dd = sDist[s];
+                nv0 += weight * dd.x;
+                nv1 += weight * dd.y;
+                totalWeight += weight;
+            }
+        } else {
+            for (uint32_t s = 0; s < R; ++s) {
+                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+                const float weight = powf_(fmaxf_(0.0f, dot(texelDirection, rd)), sharp);
                 const float2 dd = sDist[s];
                 nv0 += weight * dd.x;
                 nv1 += weight * dd.y;
@@ -1005,6 +1015,39 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             *t = nw;
             sIrrTile[(ty + 1) * (IR + 2) + tx + 1] = nw;
         }
+        // probe offsets (probeUpdateOffset.comp:27-96; full-barrier semantics): one lane of
+        // the irradiance wave, overlapped with the (longer) visibility waves
+        if (f.update_offsets && tid == kUpdateBlock - 1) {
+            const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
+            const float maxOffset = minAxialSpacing / 2.0f;
+            float4 cur = f.offsets[probeIdx];
+            V3 currentOffset = v3(cur.x, cur.y, cur.z);
+            V3 offset = splat(0.0f);
+            uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
+            V3 accumBackfaceDir = splat(0.0f), accumNearFrontfaceDir = splat(0.0f);
+            for (uint32_t s = 0; s < R; ++s) {
+                V3 d = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+                float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
+                if (a > 0.0f && a < maxOffset) {
+                    accumNearFrontfaceDir = accumNearFrontfaceDir + d;
+                    nearFrontfaceCount += 1;
+                } else if (a < 0.0f) {
+                    backfaceCount += 1;
+                    accumBackfaceDir = accumBackfaceDir + d;
+                }
+            }
+            const float stepSize = 0.125f, lerpSpeed = 10.0f;
+            if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
+                offset = offset + normalize(accumBackfaceDir) * stepSize;
+            else if (nearFrontfaceCount >= 1)
+                offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
+            else
+                offset = offset - currentOffset * stepSize;
+            V3 newOffset = currentOffset + offset;
+            if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
+            newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
+            f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
+        }
     }
     __syncthreads();
     // Border texels of this (updated) tile. Tiles not updated this frame already
@@ -1020,38 +1063,6 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         borderSource(IR, tid - (4 * VR + 4), &dx, &dy, &sx, &sy);
         uint2 val = sIrrTile[sy * (IR + 2) + sx];
         reinterpret_cast<uint2*>(f.irr)[static_cast<size_t>(tileY * (IR + 2) + dy) * f.Wi + tileX * (IR + 2) + dx] = val;
-    }
-    // probe offsets (probeUpdateOffset.comp:27-96), one lane, full barrier semantics
-    if (f.update_offsets && tid == kUpdateBlock - 1) {
-        const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
-        const float maxOffset = minAxialSpacing / 2.0f;
-        float4 cur = f.offsets[probeIdx];
-        V3 currentOffset = v3(cur.x, cur.y, cur.z);
-        V3 offset = splat(0.0f);
-        uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
-        V3 accumBackfaceDir = splat(0.0f), accumNearFrontfaceDir = splat(0.0f);
-        for (uint32_t s = 0; s < R; ++s) {
-            V3 d = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-            float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
-            if (a > 0.0f && a < maxOffset) {
-                accumNearFrontfaceDir = accumNearFrontfaceDir + d;
-                nearFrontfaceCount += 1;
-            } else if (a < 0.0f) {
-                backfaceCount += 1;
-                accumBackfaceDir = accumBackfaceDir + d;
-            }
-        }
-        const float stepSize = 0.125f, lerpSpeed = 10.0f;
-        if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
-            offset = offset + normalize(accumBackfaceDir) * stepSize;
-        else if (nearFrontfaceCount >= 1)
-            offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
-        else
-            offset = offset - currentOffset * stepSize;
-        V3 newOffset = currentOffset + offset;
-        if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-        newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
-        f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
     }
 }
 

@@ -19,6 +19,7 @@ __host__ __device__ inline float evalOp(int op, float x, float y)
     case 4: return ark::log2f_(x);
     case 5: return ark::exp2f_(x);
     case 6: return ark::powf_(x, y);
+    case 8: return ark::powf_pos_(x, y);
     default: return x;
     }
 }

@@ -18,7 +18,7 @@ extern "C" {
 #define ARK_DDGI_DEBUG_HITS 100
 
 /* Evaluates op (0 sin, 1 cos, 2 acos, 3 atan2(x,y), 4 log2, 5 exp2, 6 pow(x,y),
- * 7 fp32->fp16->fp32 round trip) on `device` for n inputs (host arrays). */
+ * 7 fp32->fp16->fp32 round trip, 8 powf_pos_(x,y)) on `device` for n inputs (host arrays). */
 int ark_ddgi_debug_fmath(int device, int op, const float* x, const float* y, float* out, uint64_t n);
 
 /* Host-side evaluation of the same functions (for comparison with the device). */

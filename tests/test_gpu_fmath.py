@@ -42,6 +42,20 @@ def test_device_fmath_matches_host(op):
     assert same.all(), f"op {op}: {np.count_nonzero(~same)} differ, e.g. x={x[~same][:3]} dev={dev[~same][:3]} host={host[~same][:3]}"
 
 
+def test_device_powf_pos_matches_powf():
+    """The branch-free pow of the visibility loop == powf_ (host) on its domain."""
+    lib = abi.load_library()
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(0, 1, 300_000), np.exp(rng.uniform(-100, 0, 100_000)),
+                        rng.uniform(0.9999, 1.0000002, 50_000)]).astype(np.float32)
+    x = x[x > 0]
+    y = rng.uniform(0.01, 64, x.size).astype(np.float32)
+    dev = np.empty_like(x)
+    assert lib.ark_ddgi_debug_fmath(0, 8, x.ctypes.data, y.ctypes.data, dev.ctypes.data, x.size) == 0
+    host = O.fmath(6, x, y)
+    assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
+
+
 def test_device_fp16_rne_ties():
     """fp32 -> fp16 on the device vs the oracle's RNE (incl. exact ties, subnormals, overflow)."""
     lib = abi.load_library()
