@@ -197,7 +197,26 @@ ARK_HD float exp2f_(float x)
     return r * u2f(static_cast<uint32_t>(n + 127) << 23);
 }
 
-// GLSL pow(x, y) for x >= 0 (x < 0 is undefined in GLSL; NaN here).
+// x^n for an integer n >= 1 by right-to-left binary exponentiation (exact
+// multiply order fixed here; <= ~log2(n)+popcount(n) roundings).
+ARK_HD float powi_(float x, int n)
+{
+    float result = 1.0f, base = x;
+    for (;;) {
+        if (n & 1) result = result * base;
+        n >>= 1;
+        if (n == 0) break;
+        base = base * base;
+    }
+    return result;
+}
+
+ARK_HD bool is_small_int_(float y) { return y >= 1.0f && y <= 64.0f && floorf_(y) == y; }
+
+// GLSL pow(x, y) for x >= 0 (x < 0 is undefined in GLSL; NaN here). Integral
+// exponents 1..64 (Schlick's ^5, the visibility sharpness 50) use powi_: about as
+// accurate as exp2(y*log2(x)) (tests/test_fmath.py bounds both) at a fraction of
+// the instructions; other exponents use exp2f_/log2f_.
 ARK_HD float powf_(float x, float y)
 {
     if (y == 0.0f || x == 1.0f) return 1.0f;
@@ -205,10 +224,12 @@ ARK_HD float powf_(float x, float y)
     if (x < 0.0f) return nan_();
     if (x == 0.0f) return y > 0.0f ? 0.0f : inf_();
     if (x == inf_()) return y > 0.0f ? inf_() : 0.0f;
+    if (is_small_int_(y)) return powi_(x, static_cast<int>(y));
     return exp2f_(y * log2f_(x));
 }
 
-// powf_ restricted to x > 0 finite, y finite with y*log2(x) <= 128, written
+// powf_ restricted to x > 0 finite, y finite and not a small integer (see powf_),
+// with y*log2(x) < 127.5, written
 // without branches (selects only) so it vectorises in the hot visibility loop.
 // Bitwise identical to powf_ on that domain: the same IEEE operations in the
 // same order (tests/test_fmath.py and tests/test_gpu_fmath.py pin this).

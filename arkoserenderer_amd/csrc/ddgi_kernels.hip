@@ -949,9 +949,21 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
         const float sharp = f.visibility_sharpness;
         float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
-        if (sharp > 0.0f && sharp <= 64.0f) {
-            // weight = pow(max(0, d), sharp): pow(0, s > 0) = 0 exactly, and for x in
-            // (0, 1+eps] powf_pos_ == powf_ bit for bit, so a select replaces the branches
+        if (is_small_int_(sharp)) {
+            // weight = pow(max(0, d), sharp) with an integral sharpness (default 50):
+            // powf_ == powi_ for x > 0 and pow(0, s) = +0, so a select replaces the branches
+            const int ns = static_cast<int>(sharp);
+            for (uint32_t s = 0; s < R; ++s) {
+                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
+                const float x = fmaxf_(0.0f, dot(texelDirection, rd));
+                const float weight = x > 0.0f ? powi_(x, ns) : 0.0f;
+                const float2 dd = sDist[s];
+                nv0 += weight * dd.x;
+                nv1 += weight * dd.y;
+                totalWeight += weight;
+            }
+        } else if (sharp > 0.0f && sharp <= 64.0f) {
+            // non-integral sharpness: powf_pos_ == powf_ bit for bit on (0, 1+eps]
             for (uint32_t s = 0; s < R; ++s) {
                 V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
                 const float x = fmaxf_(0.0f, dot(texelDirection, rd));

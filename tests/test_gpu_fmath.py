@@ -25,9 +25,12 @@ def _inputs(op, n=200_000, seed=1):
         x = rng.uniform(-160, 130, n)
     elif op == 6:
         x = rng.uniform(0, 1, n)
+        x[: n // 4] = rng.uniform(0, 2, n // 4)
     else:
         x = rng.normal(scale=100, size=n)
     y = rng.normal(size=n) if op == 3 else (rng.uniform(0.1, 60, n) if op == 6 else np.zeros(n))
+    if op == 6:
+        y[: n // 3] = rng.integers(1, 65, n // 3)  # integral exponents (powi_ path)
     return x.astype(np.float32), y.astype(np.float32)
 
 
@@ -50,6 +53,7 @@ def test_device_powf_pos_matches_powf():
                         rng.uniform(0.9999, 1.0000002, 50_000)]).astype(np.float32)
     x = x[x > 0]
     y = rng.uniform(0.01, 64, x.size).astype(np.float32)
+    y[np.floor(y) == y] += 0.25  # integral exponents take powi_, not powf_pos_
     dev = np.empty_like(x)
     assert lib.ark_ddgi_debug_fmath(0, 8, x.ctypes.data, y.ctypes.data, dev.ctypes.data, x.size) == 0
     host = O.fmath(6, x, y)
