@@ -33,18 +33,26 @@ def device_bytes(ptr: int, nbytes: int, device):
 class SlabExchange:
     """In-place all-gather of the irradiance and visibility atlases of one
     DDGIContext (one Z-slab per rank). Works with any torch.distributed backend
-    whose tensors live where the atlases live (nccl on GPU; gloo for CPU tests)."""
+    whose tensors live where the atlases live (nccl = RCCL on GPU; gloo on CPU
+    for the multi-process tests)."""
 
-    def __init__(self, views, rank: int, world: int, device, group=None):
+    def __init__(self, buffers, rank: int, world: int, group=None):
+        """buffers: [(full_atlas_bytes_tensor, slab_offset, slab_bytes), ...]"""
         self.rank, self.world, self.group = rank, world, group
         self.bufs = []
+        for full, off, slab in buffers:
+            assert slab * world == full.numel() and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
+            self.bufs.append((full, full[off:off + slab]))
+
+    @classmethod
+    def from_views(cls, views, rank: int, world: int, device, group=None):
+        bufs = []
         for ptr, total, off, slab in (
             (views.irradiance_atlas, views.irradiance_bytes, views.irradiance_slab_offset, views.irradiance_slab_bytes),
             (views.visibility_atlas, views.visibility_bytes, views.visibility_slab_offset, views.visibility_slab_bytes),
         ):
-            full = device_bytes(ptr, total, device)
-            assert slab * world == total and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
-            self.bufs.append((full, full[off:off + slab]))
+            bufs.append((device_bytes(ptr, total, device), int(off), int(slab)))
+        return cls(bufs, rank, world, group)
 
     def exchange(self):
         import torch.distributed as dist

@@ -217,14 +217,19 @@ ARK_HD bool is_small_int_(float y) { return y >= 1.0f && y <= 64.0f && floorf_(y
 // exponents 1..64 (Schlick's ^5, the visibility sharpness 50) use powi_: about as
 // accurate as exp2(y*log2(x)) (tests/test_fmath.py bounds both) at a fraction of
 // the instructions; other exponents use exp2f_/log2f_.
+//
+// Negative bases (GLSL: undefined) with an integral exponent are evaluated as the
+// product, like a driver's expansion of pow(x, 5.0) into multiplies: Schlick's
+// pow(1 - VdotH, 5) sees 1 - VdotH = -1.2e-7 on head-on hits (VdotH rounds to
+// 1.0000001), and a NaN there would poison the atlases.
 ARK_HD float powf_(float x, float y)
 {
     if (y == 0.0f || x == 1.0f) return 1.0f;
     if (isnan_(x) || isnan_(y)) return nan_();
+    if (is_small_int_(y)) return powi_(x, static_cast<int>(y));
     if (x < 0.0f) return nan_();
     if (x == 0.0f) return y > 0.0f ? 0.0f : inf_();
     if (x == inf_()) return y > 0.0f ? inf_() : 0.0f;
-    if (is_small_int_(y)) return powi_(x, static_cast<int>(y));
     return exp2f_(y * log2f_(x));
 }
 

@@ -91,7 +91,7 @@ def main():
     bvh = ctx.bvh_stats()
     stream = torch.cuda.current_stream(device)
     sptr = stream.cuda_stream
-    exch = SlabExchange(ctx.device_views(), rank, world, device) if world > 1 else None
+    exch = SlabExchange.from_views(ctx.device_views(), rank, world, device) if world > 1 else None
     setup_s = time.time() - t_setup
 
     frame = 0

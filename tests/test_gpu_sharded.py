@@ -1,0 +1,120 @@
+"""Z-slab sharding on the GPU (one box, one GPU): two contexts each own half the
+grid; after every update the slab bands are exchanged; both must equal the
+unsharded oracle bit for bit. Plus: the RCCL-facing torch view of the atlases
+and a 1-rank RCCL all-gather through SlabExchange."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from arkoserenderer_amd import abi
+from arkoserenderer_amd import ddgi as D
+from arkoserenderer_amd import scene as S
+import oracle_lib as O
+from parity import diff_report, make_desc
+
+pytestmark = pytest.mark.gpu
+
+
+def _exchange_host(ctxs):
+    """Emulates the in-place all-gather with host copies of each owner's band."""
+    world = len(ctxs)
+    for which in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY):
+        atl = [c.read(which).view(np.uint8) for c in ctxs]
+        slab = atl[0].size // world
+        full = np.concatenate([atl[r][r * slab:(r + 1) * slab] for r in range(world)])
+        for c in ctxs:
+            c.write(which, full)
+
+
+@pytest.mark.parametrize("window", [512, 150])
+def test_two_slabs_equal_unsharded(window):
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=window, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=512)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    ctxs = [D.DDGIContext(grid, ex["z_far"], cfg, 0, r, 2) for r in range(2)]
+    for c in ctxs:
+        c.set_scene(sc)
+    orc = O.Oracle(make_desc(grid, ex["z_far"], cfg))
+    orc.set_scene(sc)
+    idx = 0
+    N = grid.probe_count()
+    for f in range(4):
+        p = D.frame_params(cfg, grid, D.AppState(f), idx, **exposure)
+        for c in ctxs:
+            c.update(p)
+        for c in ctxs:
+            c.synchronize()
+        _exchange_host(ctxs)
+        orc.update(p)
+        idx = (idx + p.probe_updates) % N
+        for which in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY):
+            o = orc.read(which)
+            for c in ctxs:
+                r = diff_report("atlas", c.read(which), o)
+                assert r["mismatch"] == 0, (f, which, r)
+        # offsets: each probe's offset lives on the rank owning its z (owner-only)
+        o_off = orc.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)
+        z = (np.arange(N) % (8 * 8)) // 8
+        for r, c in enumerate(ctxs):
+            mine = (z >= 4 * r) & (z < 4 * (r + 1))
+            assert np.array_equal(c.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[mine], o_off[mine])
+
+
+def test_device_bytes_view_and_one_rank_rccl_allgather():
+    import torch
+    import torch.distributed as dist
+
+    from arkoserenderer_amd.collective import SlabExchange, device_bytes
+
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((4, 4, 4), (0.5, 0.5, 0.5), (-0.75, 0.25, -0.75))
+    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=64, max_rays_per_probe=32, max_probe_updates=64)
+    ctx = D.DDGIContext(grid, ex["z_far"], cfg)
+    ctx.set_scene(sc)
+    ctx.update(D.frame_params(cfg, grid, D.AppState(0), 0, light_pre_exposure=ex["light_pre_exposure"],
+                              environment_brightness=ex["environment_brightness"]))
+    ctx.synchronize()
+    v = ctx.device_views()
+    dev = torch.device("cuda", 0)
+    t = device_bytes(v.irradiance_atlas, v.irradiance_bytes, dev)
+    assert np.array_equal(t.cpu().numpy(), ctx.read(abi.ARK_DDGI_ATLAS_IRRADIANCE).view(np.uint8))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        before = ctx.read(abi.ARK_DDGI_ATLAS_VISIBILITY).copy()
+        SlabExchange.from_views(v, 0, 1, dev).exchange()
+        torch.cuda.synchronize()
+        assert np.array_equal(ctx.read(abi.ARK_DDGI_ATLAS_VISIBILITY), before)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_golden_fixtures_on_gpu():
+    """The HIP path reproduces the committed oracle fixtures (no oracle at run time)."""
+    import hashlib
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden as G
+    from parity import RESOURCES
+
+    for name in G.GOLDEN_SCENES:
+        f = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name}.npz"))
+        want = dict(zip(f["keys"].tolist(), f["values"].tolist()))
+        sc, grid, cfg, frames, zfar, exposure = G.scene_spec(name)
+        ctx = D.DDGIContext(grid, zfar, cfg)
+        ctx.set_scene(sc)
+        idx = 0
+        for fr in range(frames):
+            p = D.frame_params(cfg, grid, D.AppState(fr), idx, **exposure)
+            ctx.update(p)
+            ctx.synchronize()
+            idx = (idx + p.probe_updates) % grid.probe_count()
+            for k, w in RESOURCES.items():
+                assert hashlib.sha256(ctx.read(w).tobytes()).hexdigest() == want[f"{k}_{fr}"], (name, fr, k)
+        ctx.close()
