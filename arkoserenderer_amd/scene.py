@@ -144,6 +144,32 @@ class SceneData:
         self._keepalive = keep
         return s
 
+    def save_binary(self, path: str):
+        """Writes the ARKSCN1 container read by the C++ headless driver
+        (arkoserenderer_amd/host/apps/ddgi_headless.cpp)."""
+        import struct
+
+        with open(path, "wb") as fh:
+            fh.write(b"ARKSCN1\0")
+            fh.write(struct.pack("<7Q", self.indices.size, self.positions.shape[0], self.meshes.size, self.materials.size,
+                                 self.instances.size, len(self.textures), len(self.spots)))
+            sun = self.sun if self.sun is not None else ((0, 0, 0), (0, 0, 0))
+            fh.write(struct.pack("<i6fi", 1 if self.sun is not None else 0, *sun[0], *sun[1], self.environment_texture))
+            fh.write(np.ascontiguousarray(self.indices, np.uint32).tobytes())
+            fh.write(np.ascontiguousarray(self.positions, np.float32).tobytes())
+            for a in (self.vertices, self.meshes, self.materials, self.instances):
+                fh.write(np.ascontiguousarray(a).tobytes())
+            for sl in self.spots:
+                sp = abi.ArkSpotLight()
+                for k in range(3):
+                    sp.color[k], sp.world_space_direction[k] = sl.color[k], sl.direction[k]
+                    sp.world_space_right[k], sp.world_space_up[k], sp.world_space_position[k] = sl.right[k], sl.up[k], sl.position[k]
+                sp.outer_cone_half_angle, sp.ies_profile_index = sl.outer_cone_half_angle, sl.ies_profile_index
+                fh.write(bytes(sp))
+            for t in self.textures:
+                fh.write(struct.pack("<4i", t.width, t.height, t.format, t.wrap))
+                fh.write(np.ascontiguousarray(t.data).tobytes())
+
     def bounds(self):
         lo = np.full(3, np.inf, np.float32)
         hi = np.full(3, -np.inf, np.float32)
