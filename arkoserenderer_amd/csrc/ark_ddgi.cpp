@@ -55,6 +55,45 @@ uint16_t f32_to_f16_host(float f)
     return u;
 }
 
+// Traversal order of a probe's R samples: groups of 64 (one wave's refill pool)
+// with nearby directions, so the lanes of a wave descend similar BVH paths.
+// Balanced greedy clustering around ceil(R/64) spherical-Fibonacci centres.
+// Only the lane -> sample assignment changes; every sample is traced exactly
+// once and its hit record is stored at its own index, so results do not depend
+// on the order. ARK_RAY_ORDER=0 selects the identity (sample order).
+void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
+{
+    order.resize(R);
+    for (uint32_t i = 0; i < R; ++i) order[i] = i;
+    const char* env = std::getenv("ARK_RAY_ORDER");
+    const uint32_t G = (R + 63) / 64;
+    if (G <= 1 || (env && std::atoi(env) == 0)) return;
+    auto fib = [](uint32_t i, uint32_t n, double* d) { // same point set as sphericalFibonacci (math accuracy irrelevant here)
+        const double phi = 2.0 * M_PI * std::fmod(i * 0.6180339887498949, 1.0);
+        const double z = 1.0 - (2.0 * i + 1.0) / n, r = std::sqrt(std::max(0.0, 1.0 - z * z));
+        d[0] = std::cos(phi) * r; d[1] = std::sin(phi) * r; d[2] = z;
+    };
+    std::vector<double> pts(3 * R), ctr(3 * G);
+    for (uint32_t i = 0; i < R; ++i) fib(i, R, &pts[3 * i]);
+    for (uint32_t g = 0; g < G; ++g) fib(g, G, &ctr[3 * g]);
+    struct Pair { double d; uint32_t i, g; };
+    std::vector<Pair> pairs;
+    pairs.reserve(static_cast<size_t>(R) * G);
+    for (uint32_t i = 0; i < R; ++i)
+        for (uint32_t g = 0; g < G; ++g)
+            pairs.push_back({ pts[3 * i] * ctr[3 * g] + pts[3 * i + 1] * ctr[3 * g + 1] + pts[3 * i + 2] * ctr[3 * g + 2], i, g });
+    std::stable_sort(pairs.begin(), pairs.end(), [](const Pair& a, const Pair& b) { return a.d > b.d; });
+    std::vector<int> groupOf(R, -1);
+    std::vector<uint32_t> room(G, 64u);
+    room[G - 1] = R - 64u * (G - 1);
+    for (const Pair& q : pairs)
+        if (groupOf[q.i] < 0 && room[q.g] > 0) { groupOf[q.i] = static_cast<int>(q.g); room[q.g]--; }
+    uint32_t k = 0;
+    for (uint32_t g = 0; g < G; ++g)
+        for (uint32_t i = 0; i < R; ++i)
+            if (groupOf[i] == static_cast<int>(g)) order[k++] = i;
+}
+
 } // namespace
 
 struct ArkDdgiCtx {
@@ -70,7 +109,9 @@ struct ArkDdgiCtx {
     // persistent resources
     DeviceBuffer irr, vis, offsets;
     // working set
-    DeviceBuffer slots, fib, hits, surfels, spill, rayCounter, counters, shadeScratch;
+    DeviceBuffer slots, fib, order, hits, surfels, spill, rayCounter, counters, shadeScratch;
+    std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
+    uint32_t orderR = 0;
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0;
@@ -212,9 +253,10 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->offsets.alloc(static_cast<size_t>(ctx->N) * 16)) != hipSuccess) return bad(e, "alloc offsets");
     if ((e = ctx->slots.alloc(K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
     if ((e = ctx->fib.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib");
+    if ((e = ctx->order.alloc(R * 4)) != hipSuccess) return bad(e, "alloc order");
     if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
-    if ((e = ctx->rayCounter.alloc(256)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->rayCounter.alloc(2 * kRayParts * kRayCounterStride * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0;
@@ -236,7 +278,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeScratch,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeScratch,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
@@ -517,6 +559,12 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     f.offsets = ctx->offsets.as<float4>();
     f.slots = ctx->slots.as<GpuProbeSlot>();
     f.fib = ctx->fib.as<float4>();
+    if (ctx->orderR != R) {
+        sampleTraversalOrder(R, ctx->orderHost);
+        ARK_HIP(hipMemcpyAsync(ctx->order.ptr, ctx->orderHost.data(), R * 4, hipMemcpyHostToDevice, s));
+        ctx->orderR = R;
+    }
+    f.order = ctx->order.as<uint32_t>();
     f.hits = ctx->hits.as<GpuHit>();
     f.surfels = ctx->surfels.as<uint16_t>();
     f.spill = ctx->spill.as<int32_t>();
@@ -527,7 +575,7 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     const bool timing = ctx->timing;
     const bool count = ctx->counting;
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
-    ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, 4, s));
+    ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, ctx->rayCounter.bytes, s));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
     ARK_HIP(launch_probe_slots(f, s));
     if (f.window_probes > 0) {

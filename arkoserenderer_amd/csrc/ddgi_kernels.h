@@ -14,6 +14,8 @@ constexpr int kStackLds = 16;      // traversal stack entries per lane kept in L
 constexpr int kTraceBlock = 256;
 constexpr int kShadeBlock = 256;
 constexpr int kUpdateBlock = 320;  // 4 waves visibility (16x16 texels) + 1 wave irradiance (8x8)
+constexpr int kRayParts = 8;          // per-XCD ray partitions (one head counter each)
+constexpr int kRayCounterStride = 32; // u32 words between partition heads (128 B: one line each)
 constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in-block compaction)
 constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
@@ -75,6 +77,7 @@ struct FrameArgs {
     float4* offsets;
     GpuProbeSlot* slots;
     float4* fib;
+    const uint32_t* order;   // traversal order of the R samples (lane -> sample), see sampleTraversalOrder
     GpuHit* hits;
     uint16_t* surfels;
     int32_t* spill;

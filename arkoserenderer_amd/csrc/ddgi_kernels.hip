@@ -313,6 +313,45 @@ __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tm
 // so the SIMD stays full until the global ray counter runs out.
 constexpr int32_t kNodeDone = static_cast<int32_t>(0x80000000u);
 
+// XCD-aware work split: the window's probes are cut into kRayParts contiguous
+// partitions with one head counter each (ray_counter[p * kRayCounterStride]).
+// A wave drains the partition of the XCD it runs on first (read from
+// HW_REG_XCC_ID), then steals from the others in order. Rays of neighbouring
+// probes touch the same BVH neighbourhood, so each XCD's L2 sees ~1/8 of the
+// in-flight working set. Placement only affects speed: every ray is taken
+// exactly once whichever wave takes it.
+__device__ __forceinline__ uint32_t xccId()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & (kRayParts - 1);
+}
+
+__device__ __forceinline__ uint32_t partRayBegin(const FrameArgs& f, uint32_t p)
+{
+    return static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * p / kRayParts) * f.R;
+}
+
+// One lane only: next chunk of at most CHUNK consecutive rays from the head
+// counters at `heads`, or b >= e when every partition is drained.
+// `tried` = partitions already found empty (uniform over the caller's group).
+template<uint32_t CHUNK>
+__device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+{
+    b = e = 0;
+    for (; tried < kRayParts; ++tried) {
+        const uint32_t p = (home + tried) & (kRayParts - 1);
+        const uint32_t pb = partRayBegin(f, p), pe = partRayBegin(f, p + 1);
+        if (pb >= pe) continue;
+        const uint32_t off = atomicAdd(heads + p * kRayCounterStride, CHUNK);
+        if (off < pe - pb) {
+            b = pb + off;
+            e = min(b + CHUNK, pe);
+            return;
+        }
+    }
+}
+
 template<bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
@@ -320,12 +359,13 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
-    const uint32_t total = f.window_rays;
     const uint32_t lane = threadIdx.x & 63u;
     const float tmin = 0.0001f; // raygen.rgen:116
     uint32_t cNodes = 0, cTris = 0, cHits = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
+    const uint32_t home = xccId();
+    uint32_t tried = 0; // partitions found drained (wave-uniform)
     bool exhausted = false;
     bool active = false;
     uint32_t ray = 0;
@@ -342,24 +382,26 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
             const uint32_t n = static_cast<uint32_t>(__popcll(need));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
             const uint32_t avail = poolEnd - poolNext;
-            uint32_t fresh = 0;
+            uint32_t fb = 0, fe = 0; // fresh chunk [fb, fe)
             if (avail < n) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(f.ray_counter, 64u);
-                fresh = __shfl(b, 0);
+                uint32_t b = 0, e = 0, t = tried;
+                if (lane == 0) grabRays<64u>(f, f.ray_counter, home, t, b, e);
+                fb = __shfl(b, 0);
+                fe = __shfl(e, 0);
+                tried = __shfl(t, 0);
             }
             if (!active) {
                 uint32_t r = kNoHit;
                 if (rank < avail) r = poolNext + rank;
-                else if (fresh < total) r = fresh + (rank - avail);
-                if (r < total && (rank < avail || r < min(fresh + 64u, total))) {
-                    ray = r;
+                else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
+                if (r != kNoHit) {
+                    const uint32_t slot = r / f.R, sample = f.order[r - slot * f.R];
+                    ray = slot * f.R + sample; // hit record index
                     active = true;
-                    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
                     const GpuProbeSlot ps = f.slots[slot];
-                    const float4 fb = f.fib[sample];
+                    const float4 fv = f.fib[sample];
                     o = { ps.pos[0], ps.pos[1], ps.pos[2] };
-                    d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+                    d = rotate(v3(fv.x, fv.y, fv.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
                     idir = safeInv(d);
                     ooeo = o * idir;
                     h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
@@ -370,13 +412,12 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                 }
             }
             if (avail < n) {
-                if (fresh >= total) {
+                if (fb >= fe) {
                     exhausted = true;
                     poolNext = poolEnd = 0;
                 } else {
-                    poolNext = fresh + (n - avail);
-                    poolEnd = min(fresh + 64u, total);
-                    if (poolNext > poolEnd) poolNext = poolEnd;
+                    poolNext = min(fb + (n - avail), fe);
+                    poolEnd = fe;
                 }
             } else {
                 poolNext += n;
@@ -679,7 +720,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
     uint32_t* needMask = listA + kShadeChunk;          // per front hit: lit lights (shadow ray issued)
     uint32_t* occMask = needMask + kShadeChunk;        // per front hit: occluded lights
     uint32_t* listB = occMask + kShadeChunk;           // compacted shadow rays: (front << 4) | light
-    uint32_t* counts = listB + kShadeChunk * f.light_count + (f.light_count == 0 ? 1 : 0);
+    uint32_t* counts = listB + kShadeChunk * f.light_count;             // [0] nA [1] nB [2,3] chunk
     const uint32_t gtid = blockIdx.x * kShadeBlock + threadIdx.x;
     Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kShadeBlock, 0 };
     const uint32_t L = f.light_count;
@@ -687,16 +728,26 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
     LightRec* lrec = reinterpret_cast<LightRec*>(partial + 2 * kShadeChunk);
     uint32_t cNodes = 0, cTris = 0, cShadow = 0, cFront = 0;
 
-    for (uint32_t chunk = blockIdx.x * kShadeChunk; chunk < f.window_rays; chunk += gridDim.x * kShadeChunk) {
+    // chunks come from the second set of per-XCD partition heads (see grabRays)
+    uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
+    const uint32_t home = xccId();
+    uint32_t tried = 0;
+    for (;;) {
         if (threadIdx.x == 0) {
+            uint32_t b, e;
+            grabRays<static_cast<uint32_t>(kShadeChunk)>(f, heads, home, tried, b, e);
             counts[0] = 0;
             counts[1] = 0;
+            counts[2] = b;
+            counts[3] = e;
         }
         __syncthreads();
+        const uint32_t chunk = counts[2], chunkEnd = counts[3];
+        if (chunk >= chunkEnd) break;
         // ---- A. classify: misses and backfaces finish here ----------------------
         for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
             const uint32_t ray = chunk + r;
-            if (ray >= f.window_rays) break;
+            if (ray >= chunkEnd) break;
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
                 // miss (raygen.rgen:149-158)
