@@ -175,9 +175,10 @@ int clearHistory(ArkDdgiCtx* ctx)
 
 int ensureSpill(ArkDdgiCtx* ctx)
 {
+    // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
     uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
     uint32_t threads = std::max(ctx->traceBlocks * kTraceBlock, ctx->shadeBlocks * kShadeBlock);
-    size_t bytes = static_cast<size_t>(need) * threads * sizeof(int32_t);
+    size_t bytes = static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
     if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
     ctx->spillEntries = need;
@@ -342,56 +343,62 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         }
     }
     BvhBuildOptions opt;
+    opt.max_leaf_size = kBvh8MaxLeafSize;
     // host threads for the build: the box's CPU share per GPU is 16 cores
     opt.threads = 16;
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
-    std::vector<GpuBvhNode> allNodes;
+    std::vector<GpuBvh8Node> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
     uint32_t maxDepth = 0, maxLeaf = 0;
     float sah = 0.0f;
     for (int c = 0; c < 3; ++c) {
         if (cls[c].empty()) continue;
-        BvhBuildResult r = build_bvh(cls[c], opt, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()));
+        BvhBuildResult r2 = build_bvh(cls[c], opt, 0u, 0u);
+        std::vector<BuildTriangle>().swap(cls[c]);
+        if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH2 leaf of %u triangles", r2.max_leaf);
+        if (c == 0) sah = r2.sah_cost;
+        maxLeaf = std::max(maxLeaf, r2.max_leaf);
+        Bvh8BuildResult r = collapse_bvh8(r2, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()));
         roots[c] = static_cast<int32_t>(allNodes.size());
-        if (c == 0) sah = r.sah_cost;
         maxDepth = std::max(maxDepth, r.max_depth);
-        maxLeaf = std::max(maxLeaf, r.max_leaf);
         allNodes.insert(allNodes.end(), r.nodes.begin(), r.nodes.end());
         allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
-        std::vector<BuildTriangle>().swap(cls[c]);
     }
-    if (allTris.size() >= (1ull << (31 - kLeafCountBits))) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "too many triangles for the leaf encoding");
+    if (allNodes.size() >= (1ull << 31) || allTris.size() >= (1ull << 31)) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "scene too large for 31-bit BVH indices");
     // Structural check before anything reaches the GPU: every node is referenced
-    // at most once from a root-reachable parent (no cycles, no sharing), every
-    // leaf range lies inside the triangle array and every triangle is covered once.
+    // once from a root-reachable parent (no cycles, no sharing), every leaf's
+    // triangles lie inside the triangle array and every triangle is covered once.
     {
         std::vector<uint8_t> seenNode(allNodes.size(), 0);
         std::vector<uint8_t> seenTri(allTris.size(), 0);
-        std::vector<int32_t> work;
+        std::vector<uint32_t> work;
         for (int c = 0; c < 3; ++c)
-            if (roots[c] >= 0) work.push_back(roots[c]);
+            if (roots[c] >= 0) work.push_back(static_cast<uint32_t>(roots[c]));
         while (!work.empty()) {
-            int32_t n = work.back();
+            const uint32_t n = work.back();
             work.pop_back();
-            if (n < 0 || static_cast<size_t>(n) >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %d", n);
+            if (n >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u", n);
             seenNode[n] = 1;
-            for (int k = 0; k < 2; ++k) {
-                int32_t ch = allNodes[n].child[k];
-                if (ch >= 0) {
-                    work.push_back(ch);
-                } else {
-                    const float lo = allNodes[n].n0[0];
-                    uint32_t code = static_cast<uint32_t>(~ch);
-                    uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
-                    const bool farSentinel = (k == 0 ? lo : allNodes[n].n1[0]) > 1e29f;
-                    if (farSentinel) continue;
-                    if (static_cast<uint64_t>(first) + cnt > allTris.size()) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
-                    for (uint32_t t = first; t < first + cnt; ++t) {
+            const GpuBvh8Node& nd = allNodes[n];
+            uint32_t internal = 0;
+            for (int sl = 0; sl < 8; ++sl) {
+                const bool isInternal = (nd.imask >> sl) & 1u;
+                if (isInternal) {
+                    if (nd.meta[sl] != 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
+                    work.push_back(nd.child_base + internal++);
+                } else if (nd.meta[sl] != 0) {
+                    const uint32_t unary = nd.meta[sl] >> 5, off = nd.meta[sl] & 31u;
+                    if (unary != 1u && unary != 3u && unary != 7u) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf code");
+                    const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : 3u);
+                    if (off + cnt > 24u || static_cast<uint64_t>(nd.tri_base) + off + cnt > allTris.size()) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
+                    for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
                         if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
                         seenTri[t] = 1;
                     }
                 }
+                for (int a = 0; a < 3; ++a)
+                    if ((isInternal || nd.meta[sl] != 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
             }
         }
         for (size_t t = 0; t < seenTri.size(); ++t)
@@ -459,7 +466,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, ctx->texels, texels.data(), texels.size())) != 0) return rc;
     if ((rc = upload(ctx, ctx->spots, gspots.data(), gspots.size())) != 0) return rc;
     SceneArgs& sc = ctx->scene;
-    sc.nodes = ctx->nodes.as<GpuBvhNode>();
+    sc.nodes = ctx->nodes.as<GpuBvh8Node>();
     sc.tris = ctx->tris.as<GpuTriangle>();
     sc.root_opaque = roots[0];
     sc.root_masked = roots[1];
@@ -499,7 +506,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     ctx->bvhStats.max_leaf_size = maxLeaf;
     ctx->bvhStats.sah_cost = sah;
     ctx->bvhStats.build_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    ctx->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvhNode);
+    ctx->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvh8Node);
     ctx->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
     return ARK_DDGI_OK;
 }
@@ -567,7 +574,7 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     f.order = ctx->order.as<uint32_t>();
     f.hits = ctx->hits.as<GpuHit>();
     f.surfels = ctx->surfels.as<uint16_t>();
-    f.spill = ctx->spill.as<int32_t>();
+    f.spill = ctx->spill.as<uint32_t>();
     f.shade_scratch = ctx->shadeScratch.as<float4>();
     f.light_count = ctx->lightCount;
     f.ray_counter = ctx->rayCounter.as<uint32_t>();

@@ -293,7 +293,169 @@ private:
     std::atomic<int> m_threadsAvail { 0 };
 };
 
+// --- 8-wide collapse -------------------------------------------------------------
+
+struct Child8 {
+    int32_t code; // BVH2 child code: >= 0 internal node, < 0 leaf
+    Aabb box;
+};
+
+void childrenOf(const GpuBvhNode& nd, Child8 out[2], int& n)
+{
+    n = 0;
+    const float lo[2][3] = { { nd.n0[0], nd.n0[2], nd.n2[0] }, { nd.n1[0], nd.n1[2], nd.n2[2] } };
+    const float hi[2][3] = { { nd.n0[1], nd.n0[3], nd.n2[1] }, { nd.n1[1], nd.n1[3], nd.n2[3] } };
+    for (int c = 0; c < 2; ++c) {
+        if (lo[c][0] > 1e29f) continue; // far sentinel of a single-leaf root
+        Child8& ch = out[n++];
+        ch.code = nd.child[c];
+        for (int a = 0; a < 3; ++a) {
+            ch.box.lo[a] = lo[c][a];
+            ch.box.hi[a] = hi[c][a];
+        }
+    }
+}
+
+// Grid for one axis of a node box [L, H]: step 2^e, anchor p = k * 2^e <= L with
+// p + 255 * 2^e >= H and |k| + 256 < 2^24 (every plane p + q * 2^e exact in fp32).
+void quantGrid(float L, float H, int& e, double& p)
+{
+    const double ext = static_cast<double>(H) - static_cast<double>(L);
+    e = ext > 0.0 ? static_cast<int>(std::ceil(std::log2(ext / 255.0))) : -100;
+    e = std::max(-100, e);
+    for (;; ++e) {
+        const double step = std::ldexp(1.0, e);
+        const double k = std::floor(static_cast<double>(L) / step);
+        if (std::fabs(k) + 256.0 >= 16777216.0) continue;
+        p = k * step;
+        if (p + 255.0 * step < static_cast<double>(H)) continue;
+        return;
+    }
+}
+
 } // namespace
+
+Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base)
+{
+    Bvh8BuildResult res;
+    if (bvh2.nodes.empty()) return res;
+    struct Item {
+        uint32_t src;
+        uint32_t dst;
+        uint32_t depth;
+    };
+    std::vector<Item> queue;
+    queue.push_back({ 0u, 0u, 1u });
+    res.nodes.resize(1);
+    res.tris.reserve(bvh2.tris.size());
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const Item it = queue[qi];
+        res.max_depth = std::max(res.max_depth, it.depth);
+        // gather up to 8 children: open the largest-area internal child first
+        Child8 ch[8];
+        int n = 0;
+        {
+            Child8 two[2];
+            int m = 0;
+            childrenOf(bvh2.nodes[it.src], two, m);
+            for (int c = 0; c < m; ++c) ch[n++] = two[c];
+        }
+        for (;;) {
+            int best = -1;
+            float bestArea = -1.0f;
+            for (int c = 0; c < n; ++c)
+                if (ch[c].code >= 0 && ch[c].box.area() > bestArea) {
+                    bestArea = ch[c].box.area();
+                    best = c;
+                }
+            if (best < 0) break;
+            Child8 two[2];
+            int m = 0;
+            childrenOf(bvh2.nodes[ch[best].code], two, m);
+            if (n - 1 + m > 8) break;
+            ch[best] = two[0];
+            for (int c = 1; c < m; ++c) ch[n++] = two[c];
+            if (m == 0) ch[best] = ch[--n];
+        }
+        // octant slots: greedy on the alignment of child centre offsets with slot signs
+        Aabb box;
+        for (int c = 0; c < n; ++c) box.grow(ch[c].box);
+        float pc[3];
+        for (int a = 0; a < 3; ++a) pc[a] = 0.5f * (box.lo[a] + box.hi[a]);
+        struct Cand {
+            float score;
+            int c, s;
+        };
+        Cand cand[64];
+        int nc = 0;
+        for (int c = 0; c < n; ++c)
+            for (int s = 0; s < 8; ++s) {
+                float sc = 0.0f;
+                for (int a = 0; a < 3; ++a) {
+                    const float off = 0.5f * (ch[c].box.lo[a] + ch[c].box.hi[a]) - pc[a];
+                    sc += ((s >> a) & 1) ? off : -off;
+                }
+                cand[nc++] = { sc, c, s };
+            }
+        std::stable_sort(cand, cand + nc, [](const Cand& x, const Cand& y) { return x.score > y.score; });
+        int slotOf[8], childIn[8];
+        for (int k = 0; k < 8; ++k) slotOf[k] = childIn[k] = -1;
+        for (int k = 0; k < nc; ++k)
+            if (slotOf[cand[k].c] < 0 && childIn[cand[k].s] < 0) {
+                slotOf[cand[k].c] = cand[k].s;
+                childIn[cand[k].s] = cand[k].c;
+            }
+        // quantization grid of this node
+        GpuBvh8Node nd;
+        std::memset(&nd, 0, sizeof(nd));
+        double step[3], p[3];
+        for (int a = 0; a < 3; ++a) {
+            int e;
+            quantGrid(box.lo[a], box.hi[a], e, p[a]);
+            step[a] = std::ldexp(1.0, e);
+            nd.p[a] = static_cast<float>(p[a]);
+            nd.e[a] = static_cast<uint8_t>(e + 127);
+        }
+        // children in slot order: internal ones get consecutive node indices, leaf
+        // triangles are appended contiguously
+        const uint32_t childBase = static_cast<uint32_t>(res.nodes.size());
+        const uint32_t triStart = static_cast<uint32_t>(res.tris.size());
+        nd.child_base = node_base + childBase;
+        nd.tri_base = tri_base + triStart;
+        uint32_t nInternal = 0;
+        for (int s = 0; s < 8; ++s) {
+            const int c = childIn[s];
+            if (c < 0) continue;
+            const Child8& k = ch[c];
+            for (int a = 0; a < 3; ++a) {
+                double ql = std::floor((static_cast<double>(k.box.lo[a]) - p[a]) / step[a]);
+                double qh = std::ceil((static_cast<double>(k.box.hi[a]) - p[a]) / step[a]);
+                ql = std::min(255.0, std::max(0.0, ql));
+                qh = std::min(255.0, std::max(0.0, qh));
+                // outward rounding, checked on the exact fp32 decode
+                while (ql > 0.0 && static_cast<double>(static_cast<float>(p[a] + ql * step[a])) > k.box.lo[a]) ql -= 1.0;
+                while (qh < 255.0 && static_cast<double>(static_cast<float>(p[a] + qh * step[a])) < k.box.hi[a]) qh += 1.0;
+                nd.qlo[a][s] = static_cast<uint8_t>(ql);
+                nd.qhi[a][s] = static_cast<uint8_t>(qh);
+            }
+            if (k.code >= 0) {
+                nd.imask |= static_cast<uint8_t>(1u << s);
+                queue.push_back({ static_cast<uint32_t>(k.code), childBase + nInternal, it.depth + 1 });
+                nInternal++;
+            } else {
+                const uint32_t code = static_cast<uint32_t>(~k.code);
+                const uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
+                const uint32_t off = static_cast<uint32_t>(res.tris.size()) - triStart;
+                for (uint32_t t = first; t < first + cnt; ++t) res.tris.push_back(bvh2.tris[t]);
+                nd.meta[s] = static_cast<uint8_t>((((1u << cnt) - 1u) << 5) | off);
+                res.leaf_children++;
+            }
+        }
+        res.nodes.resize(res.nodes.size() + nInternal);
+        res.nodes[it.dst] = nd;
+    }
+    return res;
+}
 
 BvhBuildResult build_bvh(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t node_base, uint32_t tri_base)
 {

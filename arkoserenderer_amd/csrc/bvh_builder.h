@@ -39,4 +39,18 @@ struct BvhBuildResult {
 // one node array and one triangle array.
 BvhBuildResult build_bvh(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t node_base, uint32_t tri_base);
 
+struct Bvh8BuildResult {
+    std::vector<GpuBvh8Node> nodes; // node 0 (+ node_base) is the root
+    std::vector<GpuTriangle> tris;  // in BVH8 leaf order
+    uint32_t max_depth = 0;
+    uint32_t leaf_children = 0;
+};
+
+// Collapses a BVH2 (built with max_leaf_size <= kBvh8MaxLeafSize, node_base 0,
+// tri_base 0) into the 8-wide quantized layout: every node adopts the largest-area
+// internal descendants of its BVH2 node until it has 8 children, children are
+// placed in octant slots, and the triangles of each node's leaf children are
+// stored contiguously. Node/triangle indices are offset by node_base/tri_base.
+Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base);
+
 } // namespace ark

@@ -10,7 +10,7 @@
 
 namespace ark {
 
-constexpr int kStackLds = 16;      // traversal stack entries per lane kept in LDS (power of 2)
+constexpr int kStackLds = 8;       // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
 constexpr int kTraceBlock = 256;
 constexpr int kShadeBlock = 256;
 constexpr int kUpdateBlock = 320;  // 4 waves visibility (16x16 texels) + 1 wave irradiance (8x8)
@@ -22,7 +22,7 @@ constexpr uint32_t kNoHit = 0xffffffffu;
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {
-    const GpuBvhNode* nodes;
+    const GpuBvh8Node* nodes;
     const GpuTriangle* tris;
     int32_t root_opaque; // -1 = no geometry of that hit-mask class
     int32_t root_masked;
@@ -80,7 +80,7 @@ struct FrameArgs {
     const uint32_t* order;   // traversal order of the R samples (lane -> sample), see sampleTraversalOrder
     GpuHit* hits;
     uint16_t* surfels;
-    int32_t* spill;
+    uint32_t* spill;
     float4* shade_scratch;   // per shading block: [chunk] partial colours + [chunk][lights] light records
     uint32_t light_count;    // has_sun + spot lights
     uint32_t* ray_counter;

@@ -5,8 +5,9 @@
 //                       ray rotation) and the spherical-Fibonacci table.
 //   2. k_trace_primary  persistent traversal of all K*R probe rays: opaque pass
 //                       (closest hit) then masked pass (alpha-tested any-hit),
-//                       software BVH2 with a per-lane LDS ring stack (spilling to
-//                       HBM only beyond kStackLds entries) and wave64 ballot
+//                       software 8-wide quantized BVH (80 B nodes) with a per-lane
+//                       LDS ring stack of node groups (spilling to HBM only beyond
+//                       kStackLds entries) and wave64 ballot
 //                       refill of finished lanes (raygen.rgen:114-171).
 //   3. k_shade          closest-hit shading (opaque.rchit:105-176) with shadow
 //                       rays (any-hit traversal), environment on miss
@@ -132,29 +133,41 @@ __global__ void __launch_bounds__(1024) k_probe_slots_sharded(FrameArgs f)
 // ---------------------------------------------------------------------------
 // BVH traversal
 // ---------------------------------------------------------------------------
-// Per-lane traversal stack: the top kStackLds entries live in an LDS ring
-// (slot-major, so the 64 lanes of a wave hit distinct banks), deeper entries
-// spill to a per-lane HBM area [entry][lane] that only deep descents touch.
+// Per-lane traversal stack of node groups {child_base, hits | imask << 8}: the top
+// kStackLds entries live in an LDS ring (slot-major, so the 64 lanes of a wave hit
+// distinct banks), deeper entries spill to a per-lane HBM area
+// [entry][word][lane] that only deep descents touch.
 template<int BLOCK>
 struct Stack {
-    int32_t* lds;
-    int32_t* spill;
+    uint32_t* lds;
+    uint32_t* spill;
     uint32_t spillStride;
     int depth;
-    __device__ __forceinline__ void push(int32_t v)
+    __device__ __forceinline__ void push(uint32_t a, uint32_t b)
     {
-        int slot = depth & (kStackLds - 1);
-        if (depth >= kStackLds) spill[static_cast<size_t>(depth - kStackLds) * spillStride] = lds[slot * BLOCK];
-        lds[slot * BLOCK] = v;
+        const int slot = depth & (kStackLds - 1);
+        uint32_t* l = lds + slot * 2 * BLOCK;
+        if (depth >= kStackLds) {
+            uint32_t* sp = spill + static_cast<size_t>(depth - kStackLds) * 2 * spillStride;
+            sp[0] = l[0];
+            sp[spillStride] = l[BLOCK];
+        }
+        l[0] = a;
+        l[BLOCK] = b;
         depth++;
     }
-    __device__ __forceinline__ int32_t pop()
+    __device__ __forceinline__ void pop(uint32_t& a, uint32_t& b)
     {
         depth--;
-        int slot = depth & (kStackLds - 1);
-        int32_t v = lds[slot * BLOCK];
-        if (depth >= kStackLds) lds[slot * BLOCK] = spill[static_cast<size_t>(depth - kStackLds) * spillStride];
-        return v;
+        const int slot = depth & (kStackLds - 1);
+        uint32_t* l = lds + slot * 2 * BLOCK;
+        a = l[0];
+        b = l[BLOCK];
+        if (depth >= kStackLds) {
+            const uint32_t* sp = spill + static_cast<size_t>(depth - kStackLds) * 2 * spillStride;
+            l[0] = sp[0];
+            l[BLOCK] = sp[spillStride];
+        }
     }
 };
 
@@ -228,55 +241,101 @@ __device__ bool alphaAccept(const SceneArgs& sc, uint32_t inst, uint32_t prim, f
     return !(c.w < mat.mask_cutoff);
 }
 
-// Closest-hit (ANY=false) or first-hit (ANY=true) traversal of one BVH root.
-// Box tests use the fma slab form; boxes are inflated at build time and the
-// comparison keeps a relative margin, so an exact triangle hit is never culled.
+// Ray octant (bit a: idir[a] < 0); slots are visited in increasing (slot ^ oct).
+__device__ __forceinline__ uint32_t rayOctant(V3 idir)
+{
+    return (idir.x < 0.0f ? 1u : 0u) | (idir.y < 0.0f ? 2u : 0u) | (idir.z < 0.0f ? 4u : 0u);
+}
+
+// Node group holding only the root: slot 0 of a virtual parent at `root`.
+__device__ __forceinline__ uint32_t rootGroupBits(uint32_t oct) { return (1u << oct) | (1u << 8); }
+
+// Next child of a non-empty node group; removes it from the group.
+__device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uint32_t oct)
+{
+    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(bits & 0xffu));
+    const uint32_t slot = k ^ oct;
+    bits &= ~(1u << k);
+    return base + static_cast<uint32_t>(__builtin_popcount((bits >> 8) & ((1u << slot) - 1u)));
+}
+
+// Tests the 8 children of one BVH8 node against [tmin, tmax]. Quantized planes
+// decode exactly (fma of an 8-bit integer, a power of two and the anchor); the
+// near/far plane of each axis is chosen by the ray octant, which equals the
+// min/max of the two slab distances (fma is monotone in its first argument).
+// Returns the hit internal children as a node group and the hit leaf children's
+// triangles as a bit mask over [tBase, tBase + 24).
+__device__ __forceinline__ void visitNode8(const GpuBvh8Node* __restrict__ nodes, uint32_t idx, V3 idir, V3 ooeo, uint32_t oct, float tmin,
+                                           float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
+{
+    const uint4* np = reinterpret_cast<const uint4*>(nodes + idx);
+    const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+    const float px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
+    const float sx = __uint_as_float((w0.w & 0xffu) << 23);
+    const float sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
+    const float sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
+    const uint32_t imask = w0.w >> 24;
+    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
+    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
+    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
+    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
+    uint32_t hits = 0, tb = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
+        const bool hiWord = s >= 4;
+        const float qnx = static_cast<float>(((hiWord ? nX1 : nX0) >> sh) & 0xffu);
+        const float qny = static_cast<float>(((hiWord ? nY1 : nY0) >> sh) & 0xffu);
+        const float qnz = static_cast<float>(((hiWord ? nZ1 : nZ0) >> sh) & 0xffu);
+        const float qfx = static_cast<float>(((hiWord ? fX1 : fX0) >> sh) & 0xffu);
+        const float qfy = static_cast<float>(((hiWord ? fY1 : fY0) >> sh) & 0xffu);
+        const float qfz = static_cast<float>(((hiWord ? fZ1 : fZ0) >> sh) & 0xffu);
+        const float tnx = fmaf_(fmaf_(qnx, sx, px), idir.x, -ooeo.x);
+        const float tny = fmaf_(fmaf_(qny, sy, py), idir.y, -ooeo.y);
+        const float tnz = fmaf_(fmaf_(qnz, sz, pz), idir.z, -ooeo.z);
+        const float tfx = fmaf_(fmaf_(qfx, sx, px), idir.x, -ooeo.x);
+        const float tfy = fmaf_(fmaf_(qfy, sy, py), idir.y, -ooeo.y);
+        const float tfz = fmaf_(fmaf_(qfz, sz, pz), idir.z, -ooeo.z);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+        if (tn <= fmaf_(tf, 1.00001f, 1e-7f)) {
+            const uint32_t meta = ((hiWord ? w1.w : w1.z) >> sh) & 0xffu;
+            if ((imask >> s) & 1u) hits |= 1u << (static_cast<uint32_t>(s) ^ oct);
+            else tb |= (meta >> 5) << (meta & 31u); // empty slot: meta 0 adds nothing
+        }
+    }
+    gBase = w1.x;
+    gBits = hits | (imask << 8);
+    tBase = w1.y;
+    tBits = tb;
+}
+
+// Closest-hit (ANY=false) or first-hit (ANY=true) traversal of one BVH8 root.
+// Box tests keep a relative margin on top of the build-time inflation, so an
+// exact triangle hit is never culled; the closest hit is order-independent
+// (ties broken on instance, primitive).
 template<bool ANY, bool ALPHA, bool COUNT, int BLOCK>
 __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tmin, RayHit& h, Stack<BLOCK>& st, uint32_t& cNodes, uint32_t& cTris)
 {
     if (root < 0) return false;
     const V3 idir = safeInv(d);
     const V3 ooeo = o * idir;
-    int32_t node = root;
+    const uint32_t oct = rayOctant(idir);
+    uint32_t gBase = static_cast<uint32_t>(root), gBits = rootGroupBits(oct);
     st.depth = 0;
     for (;;) {
-        while (node >= 0) {
-            const float4* np = reinterpret_cast<const float4*>(sc.nodes + node);
-            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-            const int4 n3 = reinterpret_cast<const int4*>(np)[3];
-            if (COUNT) cNodes++;
-            const float tmax = h.t;
-            float c0lox = fmaf_(n0.x, idir.x, -ooeo.x), c0hix = fmaf_(n0.y, idir.x, -ooeo.x);
-            float c0loy = fmaf_(n0.z, idir.y, -ooeo.y), c0hiy = fmaf_(n0.w, idir.y, -ooeo.y);
-            float c0loz = fmaf_(n2.x, idir.z, -ooeo.z), c0hiz = fmaf_(n2.y, idir.z, -ooeo.z);
-            float c1lox = fmaf_(n1.x, idir.x, -ooeo.x), c1hix = fmaf_(n1.y, idir.x, -ooeo.x);
-            float c1loy = fmaf_(n1.z, idir.y, -ooeo.y), c1hiy = fmaf_(n1.w, idir.y, -ooeo.y);
-            float c1loz = fmaf_(n2.z, idir.z, -ooeo.z), c1hiz = fmaf_(n2.w, idir.z, -ooeo.z);
-            float t0n = fmaxf(fmaxf(fminf(c0lox, c0hix), fminf(c0loy, c0hiy)), fmaxf(fminf(c0loz, c0hiz), tmin));
-            float t0f = fminf(fminf(fmaxf(c0lox, c0hix), fmaxf(c0loy, c0hiy)), fminf(fmaxf(c0loz, c0hiz), tmax));
-            float t1n = fmaxf(fmaxf(fminf(c1lox, c1hix), fminf(c1loy, c1hiy)), fmaxf(fminf(c1loz, c1hiz), tmin));
-            float t1f = fminf(fminf(fmaxf(c1lox, c1hix), fmaxf(c1loy, c1hiy)), fminf(fmaxf(c1loz, c1hiz), tmax));
-            const bool hit0 = t0n <= fmaf_(t0f, 1.00001f, 1e-7f);
-            const bool hit1 = t1n <= fmaf_(t1f, 1.00001f, 1e-7f);
-            if (hit0 && hit1) {
-                int32_t nearC = n3.x, farC = n3.y;
-                if (t1n < t0n) { nearC = n3.y; farC = n3.x; }
-                st.push(farC);
-                node = nearC;
-            } else if (hit0) {
-                node = n3.x;
-            } else if (hit1) {
-                node = n3.y;
-            } else {
-                if (st.depth == 0) return h.tri != kNoHit;
-                node = st.pop();
-            }
+        if ((gBits & 0xffu) == 0) {
+            if (st.depth == 0) break;
+            st.pop(gBase, gBits);
         }
-        // leaf
-        const int32_t code = ~node;
-        const uint32_t first = static_cast<uint32_t>(code) >> kLeafCountBits;
-        const uint32_t count = (static_cast<uint32_t>(code) & (kMaxLeafSize - 1)) + 1u;
-        for (uint32_t i = first; i < first + count; ++i) {
+        const uint32_t child = nextChild(gBase, gBits, oct);
+        if (gBits & 0xffu) st.push(gBase, gBits);
+        uint32_t tBase, tBits;
+        visitNode8(sc.nodes, child, idir, ooeo, oct, tmin, h.t, gBase, gBits, tBase, tBits);
+        if (COUNT) cNodes++;
+        while (tBits) {
+            const uint32_t i = tBase + static_cast<uint32_t>(__builtin_ctz(tBits));
+            tBits &= tBits - 1u;
             const GpuTriangle tr = loadTri(sc.tris, i);
             if (COUNT) cTris++;
             float tt, uu, vv;
@@ -298,20 +357,18 @@ __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tm
             h.prim = prim;
             h.backface = bf;
         }
-        if (st.depth == 0) return h.tri != kNoHit;
-        node = st.pop();
     }
+    return h.tri != kNoHit;
 }
 
 // ---------------------------------------------------------------------------
 // 2. primary traversal (persistent, per-lane wave64 ballot refill)
 // ---------------------------------------------------------------------------
-// Every lane owns one probe ray at a time. One outer iteration advances every
-// active lane to its next leaf and tests it (Aila–Laine while-while); lanes whose
-// ray finished are refilled at the top of the next iteration from a wave-private
+// Every lane owns one probe ray at a time. One outer iteration visits one BVH8
+// node per active lane and tests the triangles of its hit leaf children; lanes
+// whose ray finished are refilled at the top of the next iteration from a wave-private
 // pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays),
 // so the SIMD stays full until the global ray counter runs out.
-constexpr int32_t kNodeDone = static_cast<int32_t>(0x80000000u);
 
 // XCD-aware work split: the window's probes are cut into kRayParts contiguous
 // partitions with one head counter each (ray_counter[p * kRayCounterStride]).
@@ -355,7 +412,7 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 template<bool COUNT>
 __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
-    __shared__ int32_t ldsStack[kStackLds * kTraceBlock];
+    __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
@@ -370,7 +427,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
     bool active = false;
     uint32_t ray = 0;
     int pass = 0;
-    int32_t node = kNodeDone;
+    uint32_t gBase = 0, gBits = 0; // current node group
+    uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 }, ooeo = { 0, 0, 0 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
@@ -405,10 +463,11 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                     idir = safeInv(d);
                     ooeo = o * idir;
                     h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                    oct = rayOctant(idir);
                     pass = 0;
-                    node = sc.root_opaque;
                     st.depth = 0;
-                    if (node < 0) node = kNodeDone;
+                    gBase = static_cast<uint32_t>(sc.root_opaque);
+                    gBits = sc.root_opaque >= 0 ? rootGroupBits(oct) : 0u;
                 }
             }
             if (avail < n) {
@@ -425,44 +484,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
         }
         if (__ballot(active) == 0) break;
         if (active) {
-            // ---- descend to the next leaf --------------------------------------
-            while (node >= 0) {
-                const float4* np = reinterpret_cast<const float4*>(sc.nodes + node);
-                const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-                const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+            // ---- one node: test its 8 children, then its hit leaf triangles -------
+            if ((gBits & 0xffu) == 0 && st.depth > 0) st.pop(gBase, gBits);
+            if (gBits & 0xffu) {
+                const uint32_t child = nextChild(gBase, gBits, oct);
+                if (gBits & 0xffu) st.push(gBase, gBits);
+                uint32_t tBase, tBits;
+                visitNode8(sc.nodes, child, idir, ooeo, oct, tmin, h.t, gBase, gBits, tBase, tBits);
                 if (COUNT) cNodes++;
-                const float tmax = h.t;
-                float c0lox = fmaf_(n0.x, idir.x, -ooeo.x), c0hix = fmaf_(n0.y, idir.x, -ooeo.x);
-                float c0loy = fmaf_(n0.z, idir.y, -ooeo.y), c0hiy = fmaf_(n0.w, idir.y, -ooeo.y);
-                float c0loz = fmaf_(n2.x, idir.z, -ooeo.z), c0hiz = fmaf_(n2.y, idir.z, -ooeo.z);
-                float c1lox = fmaf_(n1.x, idir.x, -ooeo.x), c1hix = fmaf_(n1.y, idir.x, -ooeo.x);
-                float c1loy = fmaf_(n1.z, idir.y, -ooeo.y), c1hiy = fmaf_(n1.w, idir.y, -ooeo.y);
-                float c1loz = fmaf_(n2.z, idir.z, -ooeo.z), c1hiz = fmaf_(n2.w, idir.z, -ooeo.z);
-                float t0n = fmaxf(fmaxf(fminf(c0lox, c0hix), fminf(c0loy, c0hiy)), fmaxf(fminf(c0loz, c0hiz), tmin));
-                float t0f = fminf(fminf(fmaxf(c0lox, c0hix), fmaxf(c0loy, c0hiy)), fminf(fmaxf(c0loz, c0hiz), tmax));
-                float t1n = fmaxf(fmaxf(fminf(c1lox, c1hix), fminf(c1loy, c1hiy)), fmaxf(fminf(c1loz, c1hiz), tmin));
-                float t1f = fminf(fminf(fmaxf(c1lox, c1hix), fmaxf(c1loy, c1hiy)), fminf(fmaxf(c1loz, c1hiz), tmax));
-                const bool hit0 = t0n <= fmaf_(t0f, 1.00001f, 1e-7f);
-                const bool hit1 = t1n <= fmaf_(t1f, 1.00001f, 1e-7f);
-                if (hit0 && hit1) {
-                    int32_t nearC = n3.x, farC = n3.y;
-                    if (t1n < t0n) { nearC = n3.y; farC = n3.x; }
-                    st.push(farC);
-                    node = nearC;
-                } else if (hit0) {
-                    node = n3.x;
-                } else if (hit1) {
-                    node = n3.y;
-                } else {
-                    node = st.depth == 0 ? kNodeDone : st.pop();
-                }
-            }
-            // ---- test the leaf ----------------------------------------------------
-            if (node != kNodeDone) {
-                const uint32_t code = static_cast<uint32_t>(~node);
-                const uint32_t first = code >> kLeafCountBits;
-                const uint32_t count = (code & (kMaxLeafSize - 1)) + 1u;
-                for (uint32_t i = first; i < first + count; ++i) {
+                while (tBits) {
+                    const uint32_t i = tBase + static_cast<uint32_t>(__builtin_ctz(tBits));
+                    tBits &= tBits - 1u;
                     const GpuTriangle tr = loadTri(sc.tris, i);
                     if (COUNT) cTris++;
                     float tt, uu, vv;
@@ -480,10 +512,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                     h.prim = prim;
                     h.backface = bf;
                 }
-                node = st.depth == 0 ? kNodeDone : st.pop();
             }
             // ---- pass finished -----------------------------------------------------
-            if (node == kNodeDone) {
+            if ((gBits & 0xffu) == 0 && st.depth == 0) {
                 if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
                 bool finished = true;
                 if (pass == 0) {
@@ -495,7 +526,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                         pass = 1;
                         finished = false;
                         // keep the opaque hit in the stack-free registers: restart with tmax = opaqueT
-                        node = sc.root_masked;
+                        gBase = static_cast<uint32_t>(sc.root_masked);
+                        gBits = rootGroupBits(oct);
                         st.depth = 0;
                         // stash the opaque hit; the masked pass searches [tmin, opaqueT]
                         f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
@@ -715,8 +747,8 @@ template<bool COUNT>
 __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    int32_t* ldsStack = reinterpret_cast<int32_t*>(lds);
-    uint32_t* listA = lds + kStackLds * kShadeBlock;   // compacted front hits (ray index)
+    uint32_t* ldsStack = lds;
+    uint32_t* listA = lds + kStackLds * 2 * kShadeBlock;   // compacted front hits (ray index)
     uint32_t* needMask = listA + kShadeChunk;          // per front hit: lit lights (shadow ray issued)
     uint32_t* occMask = needMask + kShadeChunk;        // per front hit: occluded lights
     uint32_t* listB = occMask + kShadeChunk;           // compacted shadow rays: (front << 4) | light
@@ -1159,7 +1191,7 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
 
 size_t shade_lds_bytes(uint32_t lights)
 {
-    return static_cast<size_t>(kStackLds) * kShadeBlock * 4 + static_cast<size_t>(kShadeChunk) * (3 + lights) * 4 + 16;
+    return static_cast<size_t>(kStackLds) * 2 * kShadeBlock * 4 + static_cast<size_t>(kShadeChunk) * (3 + lights) * 4 + 16;
 }
 
 size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights)

@@ -24,6 +24,36 @@ static_assert(sizeof(GpuBvhNode) == 64, "node is 64 B");
 constexpr int kLeafCountBits = 3;           // up to 8 triangles per leaf
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;
 
+// 8-wide BVH node with quantized child boxes, 80 B = 5 x 16 B (compressed wide
+// BVH: one fetch tests 8 children). Child boxes are stored as 8-bit offsets on a
+// per-axis power-of-two grid anchored at p:
+//     plane = p + q * 2^(e - 127),  q in [0, 255]
+// p is an exact multiple of the grid step and |p / step| + 255 < 2^24, so every
+// plane decodes EXACTLY in fp32 (one fma), and q is rounded outward, so a decoded
+// child box contains the (already inflated) BVH2 child box it replaces.
+//   w0..2  p.xyz            w3  e.x | e.y << 8 | e.z << 16 | imask << 24
+//   w4     child_base       w5  tri_base          w6,7  meta[8]
+//   w8,9   qlo.x[8]         w10,11 qlo.y[8]       w12,13 qlo.z[8]
+//   w14,15 qhi.x[8]         w16,17 qhi.y[8]       w18,19 qhi.z[8]
+// Slot s of a node holds its child whose centre lies on the (s & 1 ? + : -) x,
+// (s & 2 ? + : -) y, (s & 4 ? + : -) z side of the node centre, as far as the
+// children allow, so visiting hit slots in increasing (s ^ rayOctant) order is
+// roughly front to back. imask bit s: internal child, stored at
+// child_base + popcount(imask & ((1 << s) - 1)). meta[s] != 0: leaf child whose
+// (meta >> 5) unary-coded 1..3 triangles start at tri_base + (meta & 31).
+struct alignas(16) GpuBvh8Node {
+    float p[3];
+    uint8_t e[3];
+    uint8_t imask;
+    uint32_t child_base;
+    uint32_t tri_base;
+    uint8_t meta[8];
+    uint8_t qlo[3][8];
+    uint8_t qhi[3][8];
+};
+static_assert(sizeof(GpuBvh8Node) == 80, "BVH8 node is 80 B");
+constexpr int kBvh8MaxLeafSize = 3;
+
 // World-space triangle record, 48 B = 3 x 16 B, in leaf order:
 //   t0 = (v0.x, v0.y, v0.z, e1.x)   t1 = (e1.y, e1.z, e2.x, e2.y)
 //   t2 = (e2.z, instance, primitive, 0)     (e1 = v1 - v0, e2 = v2 - v0)

@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 # Algorithmic bytes (SURVEY.md §8d model, adapted to this build's layouts)
-NODE_BYTES = 64        # GpuBvhNode (two child boxes + child codes)
+NODE_BYTES = 80        # GpuBvh8Node (8 quantized child boxes + bases + leaf codes)
 TRI_BYTES = 48         # GpuTriangle (v0, e1, e2, instance, primitive)
 HIT_RECORD_BYTES = 16  # GpuHit
 SURFEL_BYTES = 8       # RGBA16F surfel
