@@ -265,11 +265,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // min/max of the two slab distances (fma is monotone in its first argument).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
-__device__ __forceinline__ void visitNode8(const GpuBvh8Node* __restrict__ nodes, uint32_t idx, V3 idir, V3 ooeo, uint32_t oct, float tmin,
+__device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 idir, V3 ooeo, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
-    const uint4* np = reinterpret_cast<const uint4*>(nodes + idx);
-    const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
     const float px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
     const float sx = __uint_as_float((w0.w & 0xffu) << 23);
     const float sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
@@ -310,6 +308,69 @@ __device__ __forceinline__ void visitNode8(const GpuBvh8Node* __restrict__ nodes
     tBits = tb;
 }
 
+__device__ __forceinline__ GpuTriangle triFromWords(uint4 a, uint4 b, uint4 c)
+{
+    GpuTriangle t;
+    t.t0[0] = __uint_as_float(a.x); t.t0[1] = __uint_as_float(a.y); t.t0[2] = __uint_as_float(a.z); t.t0[3] = __uint_as_float(a.w);
+    t.t1[0] = __uint_as_float(b.x); t.t1[1] = __uint_as_float(b.y); t.t1[2] = __uint_as_float(b.z); t.t1[3] = __uint_as_float(b.w);
+    t.t2[0] = __uint_as_float(c.x); t.t2[1] = __uint_as_float(c.y); t.t2[2] = __uint_as_float(c.z); t.t2[3] = __uint_as_float(c.w);
+    return t;
+}
+
+// One traversal step of one lane: a pending triangle of the current leaf group is
+// tested, otherwise the next child of the current node group is visited (popping
+// a group when it is empty). Triangles and nodes are fetched by the same five
+// 16-B loads, so a wave whose lanes mix both kinds of step waits for memory
+// once per step instead of once per node plus once per triangle.
+struct TravState {
+    uint32_t gBase, gBits; // node group: hits (k-space) | imask << 8
+    uint32_t tBase, tBits; // triangle group
+};
+
+template<int BLOCK>
+__device__ __forceinline__ bool travDone(const TravState& ts, const Stack<BLOCK>& st)
+{
+    return ts.tBits == 0 && (ts.gBits & 0xffu) == 0 && st.depth == 0;
+}
+
+// Returns true when a triangle was tested and produced a candidate (tt, uu, vv, bf,
+// index i, inst, prim) in [tmin, tmax]; node steps always return false.
+template<int BLOCK>
+__device__ __forceinline__ bool travStep(const SceneArgs& sc, TravState& ts, Stack<BLOCK>& st, V3 o, V3 d, V3 idir, V3 ooeo, uint32_t oct, float tmin,
+                                         float tmax, uint32_t& i, float& tt, float& uu, float& vv, bool& bf, uint32_t& inst, uint32_t& prim,
+                                         uint32_t& cNodes, uint32_t& cTris)
+{
+    const bool isTri = ts.tBits != 0;
+    const uint4* src;
+    if (isTri) {
+        i = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
+        ts.tBits &= ts.tBits - 1u;
+        src = reinterpret_cast<const uint4*>(sc.tris + i);
+    } else {
+        if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
+        const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
+        if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
+        src = reinterpret_cast<const uint4*>(sc.nodes + child);
+    }
+    const uint4 w0 = src[0], w1 = src[1], w2 = src[2];
+    uint4 w3 = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0);
+    if (!isTri) {
+        w3 = src[3];
+        w4 = src[4];
+    }
+    if (isTri) {
+        cTris++;
+        const GpuTriangle tr = triFromWords(w0, w1, w2);
+        if (!intersectTri(o, d, tmin, tmax, tr, &tt, &uu, &vv, &bf)) return false;
+        inst = w2.y;
+        prim = w2.z;
+        return true;
+    }
+    cNodes++;
+    visitNode8(w0, w1, w2, w3, w4, idir, ooeo, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
+    return false;
+}
+
 // Closest-hit (ANY=false) or first-hit (ANY=true) traversal of one BVH8 root.
 // Box tests keep a relative margin on top of the build-time inflation, so an
 // exact triangle hit is never culled; the closest hit is order-independent
@@ -321,42 +382,31 @@ __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tm
     const V3 idir = safeInv(d);
     const V3 ooeo = o * idir;
     const uint32_t oct = rayOctant(idir);
-    uint32_t gBase = static_cast<uint32_t>(root), gBits = rootGroupBits(oct);
+    TravState ts { static_cast<uint32_t>(root), rootGroupBits(oct), 0u, 0u };
     st.depth = 0;
-    for (;;) {
-        if ((gBits & 0xffu) == 0) {
-            if (st.depth == 0) break;
-            st.pop(gBase, gBits);
-        }
-        const uint32_t child = nextChild(gBase, gBits, oct);
-        if (gBits & 0xffu) st.push(gBase, gBits);
-        uint32_t tBase, tBits;
-        visitNode8(sc.nodes, child, idir, ooeo, oct, tmin, h.t, gBase, gBits, tBase, tBits);
-        if (COUNT) cNodes++;
-        while (tBits) {
-            const uint32_t i = tBase + static_cast<uint32_t>(__builtin_ctz(tBits));
-            tBits &= tBits - 1u;
-            const GpuTriangle tr = loadTri(sc.tris, i);
-            if (COUNT) cTris++;
-            float tt, uu, vv;
-            bool bf;
-            if (!intersectTri(o, d, tmin, h.t, tr, &tt, &uu, &vv, &bf)) continue;
-            const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
-            const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
-            if (ANY) {
-                h.tri = i;
-                return true;
-            }
-            if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
-            if (ALPHA && !alphaAccept(sc, inst, prim, uu, vv)) continue;
-            h.t = tt;
-            h.u = uu;
-            h.v = vv;
+    uint32_t n = 0, t = 0;
+    while (!travDone(ts, st)) {
+        uint32_t i, inst, prim;
+        float tt, uu, vv;
+        bool bf;
+        if (!travStep(sc, ts, st, o, d, idir, ooeo, oct, tmin, h.t, i, tt, uu, vv, bf, inst, prim, n, t)) continue;
+        if (ANY) {
             h.tri = i;
-            h.inst = inst;
-            h.prim = prim;
-            h.backface = bf;
+            break;
         }
+        if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
+        if (ALPHA && !alphaAccept(sc, inst, prim, uu, vv)) continue;
+        h.t = tt;
+        h.u = uu;
+        h.v = vv;
+        h.tri = i;
+        h.inst = inst;
+        h.prim = prim;
+        h.backface = bf;
+    }
+    if (COUNT) {
+        cNodes += n;
+        cTris += t;
     }
     return h.tri != kNoHit;
 }
@@ -427,7 +477,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
     bool active = false;
     uint32_t ray = 0;
     int pass = 0;
-    uint32_t gBase = 0, gBits = 0; // current node group
+    TravState ts { 0u, 0u, 0u, 0u };
     uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 }, ooeo = { 0, 0, 0 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
@@ -466,8 +516,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                     oct = rayOctant(idir);
                     pass = 0;
                     st.depth = 0;
-                    gBase = static_cast<uint32_t>(sc.root_opaque);
-                    gBits = sc.root_opaque >= 0 ? rootGroupBits(oct) : 0u;
+                    ts = TravState { static_cast<uint32_t>(sc.root_opaque), sc.root_opaque >= 0 ? rootGroupBits(oct) : 0u, 0u, 0u };
                 }
             }
             if (avail < n) {
@@ -484,26 +533,14 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
         }
         if (__ballot(active) == 0) break;
         if (active) {
-            // ---- one node: test its 8 children, then its hit leaf triangles -------
-            if ((gBits & 0xffu) == 0 && st.depth > 0) st.pop(gBase, gBits);
-            if (gBits & 0xffu) {
-                const uint32_t child = nextChild(gBase, gBits, oct);
-                if (gBits & 0xffu) st.push(gBase, gBits);
-                uint32_t tBase, tBits;
-                visitNode8(sc.nodes, child, idir, ooeo, oct, tmin, h.t, gBase, gBits, tBase, tBits);
-                if (COUNT) cNodes++;
-                while (tBits) {
-                    const uint32_t i = tBase + static_cast<uint32_t>(__builtin_ctz(tBits));
-                    tBits &= tBits - 1u;
-                    const GpuTriangle tr = loadTri(sc.tris, i);
-                    if (COUNT) cTris++;
-                    float tt, uu, vv;
-                    bool bf;
-                    if (!intersectTri(o, d, tmin, h.t, tr, &tt, &uu, &vv, &bf)) continue;
-                    const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
-                    const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
-                    if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
-                    if (pass == 1 && !alphaAccept(sc, inst, prim, uu, vv)) continue;
+            // ---- one step: a pending leaf triangle, or the next node --------------
+            if (!travDone(ts, st)) {
+                uint32_t i, inst, prim;
+                float tt, uu, vv;
+                bool bf;
+                if (travStep(sc, ts, st, o, d, idir, ooeo, oct, tmin, h.t, i, tt, uu, vv, bf, inst, prim, cNodes, cTris) &&
+                    !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
+                    !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
                     h.t = tt;
                     h.u = uu;
                     h.v = vv;
@@ -514,7 +551,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                 }
             }
             // ---- pass finished -----------------------------------------------------
-            if ((gBits & 0xffu) == 0 && st.depth == 0) {
+            if (travDone(ts, st)) {
                 if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
                 bool finished = true;
                 if (pass == 0) {
@@ -526,8 +563,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, Fra
                         pass = 1;
                         finished = false;
                         // keep the opaque hit in the stack-free registers: restart with tmax = opaqueT
-                        gBase = static_cast<uint32_t>(sc.root_masked);
-                        gBits = rootGroupBits(oct);
+                        ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(oct), 0u, 0u };
                         st.depth = 0;
                         // stash the opaque hit; the masked pass searches [tmin, opaqueT]
                         f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
