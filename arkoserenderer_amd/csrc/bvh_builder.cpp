@@ -1,6 +1,8 @@
 // bvh_builder.cpp — binned SAH BVH2 over world-space triangles (host, C++ threads).
 #include "bvh_builder.h"
 
+#include "../../include/ark_ddgi_debug.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -465,3 +467,98 @@ BvhBuildResult build_bvh(const std::vector<BuildTriangle>& tris, const BvhBuildO
 }
 
 } // namespace ark
+
+// ark_ddgi_debug.h: host-side structural check of the BVH8 (see the header).
+extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out)
+{
+    using namespace ark;
+    std::vector<BuildTriangle> tris(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            tris[i].v0[a] = triangles[9 * i + a];
+            tris[i].v1[a] = triangles[9 * i + 3 + a];
+            tris[i].v2[a] = triangles[9 * i + 6 + a];
+        }
+        tris[i].instance = 0;
+        tris[i].primitive = static_cast<uint32_t>(i);
+    }
+    BvhBuildOptions opt;
+    opt.max_leaf_size = kBvh8MaxLeafSize;
+    const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
+    const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u);
+    uint64_t violations = 0, internalChildren = 0;
+    std::vector<uint32_t> seen(n, 0);
+    struct Box {
+        float lo[3], hi[3];
+    };
+    struct Item {
+        uint32_t node;
+        std::vector<Box> anc;
+    };
+    std::vector<Item> work;
+    if (!r8.nodes.empty()) work.push_back({ 0u, {} });
+    while (!work.empty()) {
+        Item it = std::move(work.back());
+        work.pop_back();
+        if (it.node >= r8.nodes.size()) {
+            violations++;
+            continue;
+        }
+        const GpuBvh8Node& nd = r8.nodes[it.node];
+        uint32_t internal = 0;
+        for (int s = 0; s < 8; ++s) {
+            const bool in = (nd.imask >> s) & 1u;
+            if (!in && nd.meta[s] == 0) continue;
+            Box b;
+            for (int a = 0; a < 3; ++a) {
+                const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
+                b.lo[a] = std::fma(static_cast<float>(nd.qlo[a][s]), step, nd.p[a]);
+                b.hi[a] = std::fma(static_cast<float>(nd.qhi[a][s]), step, nd.p[a]);
+                if (static_cast<double>(b.lo[a]) != static_cast<double>(nd.p[a]) + nd.qlo[a][s] * static_cast<double>(step)) violations++;
+                if (static_cast<double>(b.hi[a]) != static_cast<double>(nd.p[a]) + nd.qhi[a][s] * static_cast<double>(step)) violations++;
+            }
+            std::vector<Box> anc = it.anc;
+            anc.push_back(b);
+            if (in) {
+                internalChildren++;
+                work.push_back({ nd.child_base + internal++, std::move(anc) });
+                continue;
+            }
+            const uint32_t unary = nd.meta[s] >> 5, off = nd.meta[s] & 31u;
+            const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : (unary == 7u ? 3u : 0u));
+            if (cnt == 0 || off + cnt > 24u) {
+                violations++;
+                continue;
+            }
+            for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
+                if (t >= r8.tris.size()) {
+                    violations++;
+                    continue;
+                }
+                const GpuTriangle& g = r8.tris[t];
+                uint32_t prim;
+                std::memcpy(&prim, &g.t2[2], 4);
+                if (prim < n) seen[prim]++;
+                if (prim >= n) continue;
+                const float* verts[3] = { tris[prim].v0, tris[prim].v1, tris[prim].v2 };
+                for (int k = 0; k < 3; ++k)
+                    for (int a = 0; a < 3; ++a)
+                        for (const Box& bx : anc)
+                            if (verts[k][a] < bx.lo[a] || verts[k][a] > bx.hi[a]) violations++;
+            }
+        }
+    }
+    for (uint64_t i = 0; i < n; ++i)
+        if (seen[i] != 1) violations++;
+    if (out) {
+        out[0] = r8.nodes.size();
+        out[1] = r8.leaf_children;
+        out[2] = r8.max_depth;
+        out[3] = violations;
+        out[4] = r8.tris.size();
+        out[5] = r2.nodes.size();
+        out[6] = internalChildren;
+        out[7] = 0;
+    }
+    return violations == 0 ? 0 : 1;
+}

@@ -993,6 +993,25 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
 // ---------------------------------------------------------------------------
 // probeBorderCopyCorners.comp / probeBorderCopyEdges.comp for one tile of side
 // res+2, as a (dst <- src) map over the 4*res+4 border texels (tile-local).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// powi_(x, N) on two lanes of a packed pair: the same binary-exponentiation
+// sequence of IEEE multiplies (ark_fmath.h), unrolled for a constant N.
+template<int N>
+__device__ __forceinline__ f2 powi2(f2 x)
+{
+    f2 result = { 1.0f, 1.0f }, base = x;
+    int n = N;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (n & 1) result = result * base;
+        n >>= 1;
+        if (n == 0) break;
+        base = base * base;
+    }
+    return result;
+}
+
 __device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, int* sx, int* sy)
 {
     const int side = res + 2;
@@ -1021,11 +1040,12 @@ __device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, i
 __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
 {
     constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
-    __shared__ float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
+    __shared__ __attribute__((aligned(16))) float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
     __shared__ uint2 sSurf[ARK_DDGI_MAX_RAYS_PER_PROBE];
-    __shared__ float2 sDist[ARK_DDGI_MAX_RAYS_PER_PROBE]; // (d, d^2), d = min(|surfel.a|, 1.5 * gridMaxSpacing)
+    __shared__ __attribute__((aligned(16))) float2 sDist[ARK_DDGI_MAX_RAYS_PER_PROBE]; // (d, d^2), d = min(|surfel.a|, 1.5 * gridMaxSpacing)
     __shared__ uint2 sIrrTile[(IR + 2) * (IR + 2)];
     __shared__ uint32_t sVisTile[(VR + 2) * (VR + 2)];
+    __shared__ uint8_t sClass[ARK_DDGI_MAX_RAYS_PER_PROBE]; // offsets: 1 near front face, 2 back face, 0 other
     const uint32_t slot = blockIdx.x;
     if (slot >= f.window_probes) return;
     const GpuProbeSlot ps = f.slots[slot];
@@ -1068,8 +1088,31 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
         const float sharp = f.visibility_sharpness;
         float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
-        if (is_small_int_(sharp)) {
-            // weight = pow(max(0, d), sharp) with an integral sharpness (default 50):
+        if (sharp == 50.0f && (R & 1u) == 0) {
+            // default sharpness, two rays per iteration in packed fp32 (v_pk_mul/add):
+            // every product and sum is the same IEEE operation as the scalar loop
+            // below, and the three sums still run over the rays in order
+            nv0 = nv1 = totalWeight = 0.0f;
+            for (uint32_t s = 0; s < R; s += 2) {
+                const f2 rx = *reinterpret_cast<const f2*>(&sDir[0][s]);
+                const f2 ry = *reinterpret_cast<const f2*>(&sDir[1][s]);
+                const f2 rz = *reinterpret_cast<const f2*>(&sDir[2][s]);
+                const f2 dp = (texelDirection.x * rx + texelDirection.y * ry) + texelDirection.z * rz;
+                const f2 x = { fmaxf_(0.0f, dp.x), fmaxf_(0.0f, dp.y) };
+                const f2 p = powi2<50>(x);
+                const f2 weight = { x.x > 0.0f ? p.x : 0.0f, x.y > 0.0f ? p.y : 0.0f };
+                const float4 dd = *reinterpret_cast<const float4*>(&sDist[s]);
+                const f2 m0 = weight * f2 { dd.x, dd.z };
+                const f2 m1 = weight * f2 { dd.y, dd.w };
+                nv0 += m0.x;
+                nv0 += m0.y;
+                nv1 += m1.x;
+                nv1 += m1.y;
+                totalWeight += weight.x;
+                totalWeight += weight.y;
+            }
+        } else if (is_small_int_(sharp)) {
+            // weight = pow(max(0, d), sharp) with an integral sharpness:
             // powf_ == powi_ for x > 0 and pow(0, s) = +0, so a select replaces the branches
             const int ns = static_cast<int>(sharp);
             for (uint32_t s = 0; s < R; ++s) {
@@ -1146,38 +1189,53 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             *t = nw;
             sIrrTile[(ty + 1) * (IR + 2) + tx + 1] = nw;
         }
-        // probe offsets (probeUpdateOffset.comp:27-96; full-barrier semantics): one lane of
-        // the irradiance wave, overlapped with the (longer) visibility waves
-        if (f.update_offsets && tid == kUpdateBlock - 1) {
+        // probe offsets (probeUpdateOffset.comp:27-96; full-barrier semantics) in the
+        // irradiance wave, overlapped with the (longer) visibility waves: the rays are
+        // classified in parallel (counts by ballot), then six lanes each run one of
+        // the two direction sums' components over the rays in order (adding +0 for
+        // rays of the other classes leaves a sum unchanged), and one lane finishes.
+        if (f.update_offsets) {
             const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
             const float maxOffset = minAxialSpacing / 2.0f;
-            float4 cur = f.offsets[probeIdx];
-            V3 currentOffset = v3(cur.x, cur.y, cur.z);
-            V3 offset = splat(0.0f);
             uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
-            V3 accumBackfaceDir = splat(0.0f), accumNearFrontfaceDir = splat(0.0f);
-            for (uint32_t s = 0; s < R; ++s) {
-                V3 d = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-                float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
-                if (a > 0.0f && a < maxOffset) {
-                    accumNearFrontfaceDir = accumNearFrontfaceDir + d;
-                    nearFrontfaceCount += 1;
-                } else if (a < 0.0f) {
-                    backfaceCount += 1;
-                    accumBackfaceDir = accumBackfaceDir + d;
+            for (uint32_t s0 = 0; s0 < R; s0 += 64) {
+                const uint32_t s = s0 + static_cast<uint32_t>(i);
+                uint32_t cls = 0;
+                if (s < R) {
+                    const float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
+                    cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
+                    sClass[s] = static_cast<uint8_t>(cls);
                 }
+                nearFrontfaceCount += static_cast<uint32_t>(__popcll(__ballot(cls == 1u)));
+                backfaceCount += static_cast<uint32_t>(__popcll(__ballot(cls == 2u)));
             }
-            const float stepSize = 0.125f, lerpSpeed = 10.0f;
-            if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
-                offset = offset + normalize(accumBackfaceDir) * stepSize;
-            else if (nearFrontfaceCount >= 1)
-                offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
-            else
-                offset = offset - currentOffset * stepSize;
-            V3 newOffset = currentOffset + offset;
-            if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-            newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
-            f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float acc = 0.0f;
+            if (i < 6) {
+                const float* dirc = sDir[i % 3];
+                const uint32_t want = i < 3 ? 1u : 2u;
+                for (uint32_t s = 0; s < R; ++s) acc += sClass[s] == want ? dirc[s] : 0.0f;
+            }
+            const V3 accumNearFrontfaceDir = v3(__shfl(acc, 0), __shfl(acc, 1), __shfl(acc, 2));
+            const V3 accumBackfaceDir = v3(__shfl(acc, 3), __shfl(acc, 4), __shfl(acc, 5));
+            if (i == 0) {
+                float4 cur = f.offsets[probeIdx];
+                V3 currentOffset = v3(cur.x, cur.y, cur.z);
+                V3 offset = splat(0.0f);
+                const float stepSize = 0.125f, lerpSpeed = 10.0f;
+                if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
+                    offset = offset + normalize(accumBackfaceDir) * stepSize;
+                else if (nearFrontfaceCount >= 1)
+                    offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
+                else
+                    offset = offset - currentOffset * stepSize;
+                V3 newOffset = currentOffset + offset;
+                if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
+                newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
+                f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
+            }
         }
     }
     __syncthreads();

@@ -30,6 +30,15 @@ int ark_ddgi_debug_fmath_host(int op, const float* x, const float* y, float* out
  * ArkDdgiCounters, ArkDdgiDeviceViews, ArkDdgiBvhStats. Returns the count written. */
 int ark_ddgi_debug_struct_sizes(uint32_t* out, int n);
 
+/* Builds the BVH used by ark_ddgi_set_scene (binned-SAH BVH2 with leaves of at most
+ * 3 triangles, collapsed into 8-wide quantized nodes) over n world-space triangles
+ * (9 floats each) on the host and checks it: every triangle in exactly one leaf,
+ * every quantized plane exactly representable, every triangle vertex inside the
+ * decoded boxes of its leaf and of all its ancestors. out[8] = {nodes, leaf
+ * children, max depth, violations, triangles, bvh2 nodes, internal children, 0}.
+ * Returns 0 when the check passes, 1 when it found violations. No GPU. */
+int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif
