@@ -344,6 +344,17 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     }
     BvhBuildOptions opt;
     opt.max_leaf_size = kBvh8MaxLeafSize;
+    {
+        float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+        for (int c = 0; c < 3; ++c)
+            for (const BuildTriangle& t : cls[c])
+                for (const float* v : { t.v0, t.v1, t.v2 })
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = std::min(lo[a], v[a]);
+                        hi[a] = std::max(hi[a], v[a]);
+                    }
+        opt.inflate_abs = bvh8_inflation_box(lo, hi); // one inflation for all classes (shadow rays test all)
+    }
     // host threads for the build: the box's CPU share per GPU is 16 cores
     opt.threads = 16;
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));

@@ -213,10 +213,18 @@ ARK_HD float powi_(float x, int n)
 
 ARK_HD bool is_small_int_(float y) { return y >= 1.0f && y <= 64.0f && floorf_(y) == y; }
 
+// Exponents with a square-root form: 1/4, 1/2 and n + 1/2 for n in 1..16.
+ARK_HD bool is_root_exp_(float y) { return y == 0.25f || y == 0.5f || (y > 1.0f && y <= 16.5f && floorf_(y) + 0.5f == y); }
+
 // GLSL pow(x, y) for x >= 0 (x < 0 is undefined in GLSL; NaN here). Integral
 // exponents 1..64 (Schlick's ^5, the visibility sharpness 50) use powi_: about as
 // accurate as exp2(y*log2(x)) (tests/test_fmath.py bounds both) at a fraction of
 // the instructions; other exponents use exp2f_/log2f_.
+//
+// Exponents 1/4, 1/2 and n + 1/2 (the DDGI smoothing pow(x, 0.25) and the
+// irradiance decode pow(x, 2.5)) use correctly rounded square roots: sqrt(sqrt(x)),
+// sqrt(x), powi_(x, n) * sqrt(x) (<= 2 ulp; GLSL leaves pow's precision to the
+// implementation, this fixes one on both sides).
 //
 // Negative bases (GLSL: undefined) with an integral exponent are evaluated as the
 // product, like a driver's expansion of pow(x, 5.0) into multiplies: Schlick's
@@ -228,12 +236,18 @@ ARK_HD float powf_(float x, float y)
     if (isnan_(x) || isnan_(y)) return nan_();
     if (is_small_int_(y)) return powi_(x, static_cast<int>(y));
     if (x < 0.0f) return nan_();
+    if (is_root_exp_(y)) {
+        if (y == 0.25f) return sqrtf_(sqrtf_(x));
+        if (y == 0.5f) return sqrtf_(x);
+        return powi_(x, static_cast<int>(y)) * sqrtf_(x);
+    }
     if (x == 0.0f) return y > 0.0f ? 0.0f : inf_();
     if (x == inf_()) return y > 0.0f ? inf_() : 0.0f;
     return exp2f_(y * log2f_(x));
 }
 
-// powf_ restricted to x > 0 finite, y finite and not a small integer (see powf_),
+// powf_ restricted to x > 0 finite, y finite, not a small integer and not a
+// square-root exponent (see powf_),
 // with y*log2(x) < 127.5, written
 // without branches (selects only) so it vectorises in the hot visibility loop.
 // Bitwise identical to powf_ on that domain: the same IEEE operations in the

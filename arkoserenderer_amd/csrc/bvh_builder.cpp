@@ -138,7 +138,7 @@ private:
                 m = std::max(m, std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])));
                 e = std::max(e, b.hi[a] - b.lo[a]);
             }
-            const float eps = m * 2e-6f + e * 1e-5f + 1e-7f;
+            const float eps = m * 2e-6f + e * 1e-5f + 1e-7f + m_opt.inflate_abs;
             for (int a = 0; a < 3; ++a) {
                 b.lo[a] -= eps;
                 b.hi[a] += eps;
@@ -337,6 +337,25 @@ void quantGrid(float L, float H, int& e, double& p)
 
 } // namespace
 
+float bvh8_inflation(const float* xyz, uint64_t nTriangles)
+{
+    float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    for (uint64_t i = 0; i < nTriangles * 3; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], xyz[3 * i + a]);
+            hi[a] = std::max(hi[a], xyz[3 * i + a]);
+        }
+    return bvh8_inflation_box(lo, hi);
+}
+
+float bvh8_inflation_box(const float lo[3], const float hi[3])
+{
+    double d2 = 0.0;
+    for (int a = 0; a < 3; ++a)
+        if (hi[a] >= lo[a]) d2 += (static_cast<double>(hi[a]) - lo[a]) * (static_cast<double>(hi[a]) - lo[a]);
+    return static_cast<float>(1e-6 * std::sqrt(d2));
+}
+
 Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base)
 {
     Bvh8BuildResult res;
@@ -484,6 +503,7 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
     }
     BvhBuildOptions opt;
     opt.max_leaf_size = kBvh8MaxLeafSize;
+    opt.inflate_abs = bvh8_inflation(triangles, n);
     const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
     const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u);
     uint64_t violations = 0, internalChildren = 0;

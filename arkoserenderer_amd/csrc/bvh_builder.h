@@ -22,6 +22,7 @@ struct BvhBuildOptions {
     int bins = 32;
     int max_depth = 60;      // hard cap: splits fall back to object median near it
     int threads = 0;         // 0 = hardware concurrency
+    float inflate_abs = 0.0f; // absolute box inflation on top of the relative one (see collapse_bvh8 / visitNode8)
     float traversal_cost = 1.0f;
     float intersection_cost = 1.0f;
 };
@@ -52,5 +53,12 @@ struct Bvh8BuildResult {
 // placed in octant slots, and the triangles of each node's leaf children are
 // stored contiguously. Node/triangle indices are offset by node_base/tri_base.
 Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base);
+
+// Absolute box inflation for the BVH8 slab test: 1e-6 of the diagonal of the
+// bounding box of nTriangles world-space triangles (9 floats each). It bounds
+// the rounding of (p - o) * idir for anchors p and ray origins o in the scene
+// (about 2 ulp of the diagonal, i.e. 2.4e-7 of it) with a 4x margin.
+float bvh8_inflation(const float* xyz, uint64_t nTriangles);
+float bvh8_inflation_box(const float lo[3], const float hi[3]);
 
 } // namespace ark

@@ -21,12 +21,16 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/ark_ddgi.h"
 #include "ddgi_device.h"
 #include "ddgi_kernels.h"
 
 namespace ark {
 namespace dev {
+
+typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
 
 // ---------------------------------------------------------------------------
 // 1. window -> slots
@@ -259,51 +263,71 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
     return base + static_cast<uint32_t>(__builtin_popcount((bits >> 8) & ((1u << slot) - 1u)));
 }
 
-// Tests the 8 children of one BVH8 node against [tmin, tmax]. Quantized planes
-// decode exactly (fma of an 8-bit integer, a power of two and the anchor); the
-// near/far plane of each axis is chosen by the ray octant, which equals the
-// min/max of the two slab distances (fma is monotone in its first argument).
+// Tests the 8 children of one BVH8 node against [tmin, tmax]. A slab distance is
+// one fma of the 8-bit plane index q:  t = q * (step * idir) + (p - o) * idir,
+// where step * idir is exact (a power of two) and (p - o) * idir carries at most
+// about 2 ulp of |p - o| * |idir|; the build inflates every box by 1e-6 of the
+// scene diagonal on top of its own relative margin (bvh_builder.cpp), which
+// covers that error, and the comparison keeps a relative margin for far boxes,
+// so a box holding an exact triangle hit is never culled. The near/far plane of
+// each axis is chosen by the ray octant. Two slots per packed fp32 operation.
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
-__device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 idir, V3 ooeo, uint32_t oct, float tmin,
+__device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
-    const float px = __uint_as_float(w0.x), py = __uint_as_float(w0.y), pz = __uint_as_float(w0.z);
-    const float sx = __uint_as_float((w0.w & 0xffu) << 23);
-    const float sy = __uint_as_float(((w0.w >> 8) & 0xffu) << 23);
-    const float sz = __uint_as_float(((w0.w >> 16) & 0xffu) << 23);
+    const float ax = __uint_as_float((w0.w & 0xffu) << 23) * idir.x;
+    const float ay = __uint_as_float(((w0.w >> 8) & 0xffu) << 23) * idir.y;
+    const float az = __uint_as_float(((w0.w >> 16) & 0xffu) << 23) * idir.z;
+    const float bx = (__uint_as_float(w0.x) - o.x) * idir.x;
+    const float by = (__uint_as_float(w0.y) - o.y) * idir.y;
+    const float bz = (__uint_as_float(w0.z) - o.z) * idir.z;
+    const f2 Ax = { ax, ax }, Ay = { ay, ay }, Az = { az, az }, Bx = { bx, bx }, By = { by, by }, Bz = { bz, bz };
+    const f2 Tmin = { tmin, tmin }, Tmax = { tmax, tmax };
     const uint32_t imask = w0.w >> 24;
     const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
     const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-    uint32_t hits = 0, tb = 0;
+    uint32_t hitSlots = 0;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < 8; s += 2) {
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
         const bool hiWord = s >= 4;
-        const float qnx = static_cast<float>(((hiWord ? nX1 : nX0) >> sh) & 0xffu);
-        const float qny = static_cast<float>(((hiWord ? nY1 : nY0) >> sh) & 0xffu);
-        const float qnz = static_cast<float>(((hiWord ? nZ1 : nZ0) >> sh) & 0xffu);
-        const float qfx = static_cast<float>(((hiWord ? fX1 : fX0) >> sh) & 0xffu);
-        const float qfy = static_cast<float>(((hiWord ? fY1 : fY0) >> sh) & 0xffu);
-        const float qfz = static_cast<float>(((hiWord ? fZ1 : fZ0) >> sh) & 0xffu);
-        const float tnx = fmaf_(fmaf_(qnx, sx, px), idir.x, -ooeo.x);
-        const float tny = fmaf_(fmaf_(qny, sy, py), idir.y, -ooeo.y);
-        const float tnz = fmaf_(fmaf_(qnz, sz, pz), idir.z, -ooeo.z);
-        const float tfx = fmaf_(fmaf_(qfx, sx, px), idir.x, -ooeo.x);
-        const float tfy = fmaf_(fmaf_(qfy, sy, py), idir.y, -ooeo.y);
-        const float tfz = fmaf_(fmaf_(qfz, sz, pz), idir.z, -ooeo.z);
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-        if (tn <= fmaf_(tf, 1.00001f, 1e-7f)) {
-            const uint32_t meta = ((hiWord ? w1.w : w1.z) >> sh) & 0xffu;
-            if ((imask >> s) & 1u) hits |= 1u << (static_cast<uint32_t>(s) ^ oct);
-            else tb |= (meta >> 5) << (meta & 31u); // empty slot: meta 0 adds nothing
+        auto q2 = [&](uint32_t w0_, uint32_t w1_) {
+            const uint32_t w = hiWord ? w1_ : w0_;
+            return f2 { static_cast<float>((w >> sh) & 0xffu), static_cast<float>((w >> (sh + 8u)) & 0xffu) };
+        };
+        const f2 tnx = __builtin_elementwise_fma(q2(nX0, nX1), Ax, Bx);
+        const f2 tny = __builtin_elementwise_fma(q2(nY0, nY1), Ay, By);
+        const f2 tnz = __builtin_elementwise_fma(q2(nZ0, nZ1), Az, Bz);
+        const f2 tfx = __builtin_elementwise_fma(q2(fX0, fX1), Ax, Bx);
+        const f2 tfy = __builtin_elementwise_fma(q2(fY0, fY1), Ay, By);
+        const f2 tfz = __builtin_elementwise_fma(q2(fZ0, fZ1), Az, Bz);
+        const f2 tn = __builtin_elementwise_max(__builtin_elementwise_max(tnx, tny), __builtin_elementwise_max(tnz, Tmin));
+        const f2 tf = __builtin_elementwise_min(__builtin_elementwise_min(tfx, tfy), __builtin_elementwise_min(tfz, Tmax));
+        const f2 lim = __builtin_elementwise_fma(tf, f2 { 1.00001f, 1.00001f }, f2 { 1e-7f, 1e-7f });
+        hitSlots |= (tn.x <= lim.x ? 1u : 0u) << s;
+        hitSlots |= (tn.y <= lim.y ? 1u : 0u) << (s + 1);
+    }
+    // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
+    // swapping bit pairs / pairs of pairs / nibbles per octant bit
+    uint32_t m = hitSlots & imask;
+    m = fx ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
+    m = fy ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
+    m = fz ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
+    // leaf children: their triangle ranges (meta: unary count << 5 | offset)
+    uint32_t tb = 0;
+    const uint32_t leafHits = hitSlots & ~imask;
+    if (leafHits) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const uint32_t meta = ((s < 4 ? w1.z : w1.w) >> ((s & 3) * 8)) & 0xffu;
+            tb |= ((leafHits >> s) & 1u) ? ((meta >> 5) << (meta & 31u)) : 0u;
         }
     }
     gBase = w1.x;
-    gBits = hits | (imask << 8);
+    gBits = m | (imask << 8);
     tBase = w1.y;
     tBits = tb;
 }
@@ -367,7 +391,7 @@ __device__ __forceinline__ bool travStep(const SceneArgs& sc, TravState& ts, Sta
         return true;
     }
     cNodes++;
-    visitNode8(w0, w1, w2, w3, w4, idir, ooeo, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
+    visitNode8(w0, w1, w2, w3, w4, o, idir, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
     return false;
 }
 
@@ -459,8 +483,8 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
     }
 }
 
-template<bool COUNT>
-__global__ void __launch_bounds__(kTraceBlock) k_trace_primary(SceneArgs sc, FrameArgs f)
+template<bool COUNT, int WPE>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
@@ -779,8 +803,8 @@ struct alignas(16) LightRec {
 };
 
 
-template<bool COUNT>
-__global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f)
+template<bool COUNT, int WPE>
+__global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* ldsStack = lds;
@@ -993,7 +1017,6 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(SceneArgs sc, FrameArgs f
 // ---------------------------------------------------------------------------
 // probeBorderCopyCorners.comp / probeBorderCopyEdges.comp for one tile of side
 // res+2, as a (dst <- src) map over the 4*res+4 border texels (tile-local).
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // powi_(x, N) on two lanes of a packed pair: the same binary-exponentiation
 // sequence of IEEE multiplies (ark_fmath.h), unrolled for a constant N.
@@ -1124,7 +1147,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 nv1 += weight * dd.y;
                 totalWeight += weight;
             }
-        } else if (sharp > 0.0f && sharp <= 64.0f) {
+        } else if (sharp > 0.0f && sharp <= 64.0f && !is_root_exp_(sharp)) {
             // non-integral sharpness: powf_pos_ == powf_ bit for bit on (0, 1+eps]
             for (uint32_t s = 0; s < R; ++s) {
                 V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
@@ -1276,10 +1299,37 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
     return hipGetLastError();
 }
 
+// Occupancy variant of the trace kernel (minimum waves per SIMD the register
+// allocation must allow): 6 by default (80 VGPRs, no spill; 3.43 vs 3.61 ms at the
+// compiler's 5 on C4; 8 spills and takes 5.4 ms), ARK_TRACE_WPE = 0 or 8 for tuning.
+static int trace_variant()
+{
+    static const int v = [] {
+        const char* e = std::getenv("ARK_TRACE_WPE");
+        return e ? std::atoi(e) : 6;
+    }();
+    return v;
+}
+
+// Occupancy variant of the shading kernel (minimum waves per SIMD): 4 by default
+// (128 VGPRs, 16 B/lane of spill; 2.05 vs 2.38 ms at the compiler's 3 on C4),
+// ARK_SHADE_WPE = 0 (compiler's choice) or 5 for tuning.
+static int shade_variant()
+{
+    static const int v = [] {
+        const char* e = std::getenv("ARK_SHADE_WPE");
+        return e ? std::atoi(e) : 4;
+    }();
+    return v;
+}
+
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    if (count) hipLaunchKernelGGL(dev::k_trace_primary<true>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL(dev::k_trace_primary<false>, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    const int v = trace_variant();
+    if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else if (v == 8) hipLaunchKernelGGL((dev::k_trace_primary<false, 8>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_trace_primary<false, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -1296,8 +1346,11 @@ size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights)
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     const size_t lds = shade_lds_bytes(f.light_count);
-    if (count) hipLaunchKernelGGL(dev::k_shade<true>, dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
-    else hipLaunchKernelGGL(dev::k_shade<false>, dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    const int v = shade_variant();
+    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_shade<false, 1>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
     return hipGetLastError();
 }
 
@@ -1319,11 +1372,19 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
 
 const void* kernel_trace_primary_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace_primary<true>) : reinterpret_cast<const void*>(&dev::k_trace_primary<false>);
+    const int v = trace_variant();
+    if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1>);
+    if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6>);
+    if (v == 8) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 8>);
+    return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1>);
 }
 const void* kernel_shade_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_shade<true>) : reinterpret_cast<const void*>(&dev::k_shade<false>);
+    const int v = shade_variant();
+    if (count) return reinterpret_cast<const void*>(&dev::k_shade<true, 1>);
+    if (v == 4) return reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
+    if (v == 5) return reinterpret_cast<const void*>(&dev::k_shade<false, 5>);
+    return reinterpret_cast<const void*>(&dev::k_shade<false, 1>);
 }
 
 } // namespace ark

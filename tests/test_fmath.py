@@ -53,6 +53,20 @@ def test_log2_exp2_pow():
     assert O.fmath(6, np.array([0.3], np.float32), np.array([0.0], np.float32))[0] == 1.0
 
 
+def test_pow_square_root_exponents():
+    """pow(x, 1/4) = sqrt(sqrt(x)), pow(x, 1/2) = sqrt(x), pow(x, n + 1/2) = powi(x, n) * sqrt(x),
+    each IEEE fp32 operation correctly rounded (numpy float32 arithmetic is)."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(0, 1, 50_000), rng.uniform(0, 50, 50_000), [0.0, 1.0, np.inf]]).astype(np.float32)
+    x2 = x * x
+    cases = [(0.25, np.sqrt(np.sqrt(x))), (0.5, np.sqrt(x)), (1.5, x * np.sqrt(x)), (2.5, x2 * np.sqrt(x)),
+             (5.5, (x * (x2 * x2)) * np.sqrt(x))]  # powi_(x, 5) = x * (x^2)^2 in binary-exponentiation order
+    for y, ref in cases:
+        got = O.fmath(6, x, np.full_like(x, y))
+        assert np.array_equal(got.view(np.uint32), ref.astype(np.float32).view(np.uint32)), y
+    assert np.isnan(O.fmath(6, np.float32([-1.0]), np.float32([2.5]))[0])
+
+
 @pytest.mark.parametrize("op", [0, 1, 2, 3, 4, 5, 6])
 def test_product_host_build_equals_oracle(op):
     """libark_ddgi's host compile of ark_fmath.h == the oracle's, bit for bit."""
@@ -77,7 +91,8 @@ def test_powf_pos_equals_powf_on_domain():
                         rng.uniform(0.9999, 1.0000002, 20_000)]).astype(np.float32)
     x = x[x > 0]
     y = rng.uniform(0.01, 64, x.size).astype(np.float32)
-    y[np.floor(y) == y] += 0.5
+    y[np.floor(y) == y] += 0.25
+    y[(np.floor(y) + 0.5 == y) | (y == 0.25)] += 0.125  # square-root exponents are outside powf_pos_'s domain
     out = np.empty_like(x)
     assert lib.ark_ddgi_debug_fmath_host(8, x.ctypes.data, y.ctypes.data, out.ctypes.data, x.size) == 0
     assert np.array_equal(out.view(np.uint32), O.fmath(6, x, y).view(np.uint32))

@@ -31,6 +31,7 @@ def _inputs(op, n=200_000, seed=1):
     y = rng.normal(size=n) if op == 3 else (rng.uniform(0.1, 60, n) if op == 6 else np.zeros(n))
     if op == 6:
         y[: n // 3] = rng.integers(1, 65, n // 3)  # integral exponents (powi_ path)
+        y[n // 3: n // 2] = rng.choice(np.float32([0.25, 0.5, 1.5, 2.5, 16.5]), n // 2 - n // 3)  # square-root exponents
     return x.astype(np.float32), y.astype(np.float32)
 
 
