@@ -97,7 +97,7 @@ public:
             g.t2[0] = e2[2];
             std::memcpy(&g.t2[1], &t.instance, 4);
             std::memcpy(&g.t2[2], &t.primitive, 4);
-            g.t2[3] = 0.0f;
+            std::memcpy(&g.t2[3], &t.flip_facing, 4);
         }
         res.max_depth = m_maxDepth.load();
         res.max_leaf = m_maxLeaf.load();
@@ -500,6 +500,7 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
         }
         tris[i].instance = 0;
         tris[i].primitive = static_cast<uint32_t>(i);
+        tris[i].flip_facing = 0;
     }
     BvhBuildOptions opt;
     opt.max_leaf_size = kBvh8MaxLeafSize;

@@ -15,6 +15,7 @@ struct BuildTriangle {
     float v0[3], v1[3], v2[3]; // world space
     uint32_t instance;
     uint32_t primitive;
+    uint32_t flip_facing; // the instance's det(ObjectToWorld) < 0, stored in GpuTriangle t2.w
 };
 
 struct BvhBuildOptions {

@@ -78,11 +78,13 @@ struct FrameArgs {
     GpuProbeSlot* slots;
     float4* fib;
     const uint32_t* order;   // traversal order of the R samples (lane -> sample), see sampleTraversalOrder
+    float4* fib_order;       // fib[order[j]] with w = order[j] (bits), j = traversal position
     GpuHit* hits;
     uint16_t* surfels;
     uint32_t* spill;
     float4* shade_scratch;   // per shading block: [chunk] partial colours + [chunk][lights] light records
     uint32_t light_count;    // has_sun + spot lights
+    uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };

@@ -100,6 +100,10 @@ __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
     if (tid < f.R) {
         V3 d = sphericalFibonacciSample(tid, f.R);
         f.fib[tid] = make_float4(d.x, d.y, d.z, 0.0f);
+        // traversal order: position tid traces sample order[tid] (w = sample index)
+        const uint32_t sample = f.order[tid];
+        V3 e = sphericalFibonacciSample(sample, f.R);
+        f.fib_order[tid] = make_float4(e.x, e.y, e.z, __uint_as_float(sample));
     }
     if (f.sharded) return;
     if (tid < f.window) writeSlot(f, tid, (tid + f.first) % N);
@@ -251,15 +255,23 @@ __device__ __forceinline__ uint32_t rayOctant(V3 idir)
     return (idir.x < 0.0f ? 1u : 0u) | (idir.y < 0.0f ? 2u : 0u) | (idir.z < 0.0f ? 4u : 0u);
 }
 
-// Node group holding only the root: slot 0 of a virtual parent at `root`.
-__device__ __forceinline__ uint32_t rootGroupBits(uint32_t oct) { return (1u << oct) | (1u << 8); }
+// Node group holding only the root: one hit child (k = 0) in the "origin inside"
+// set of a virtual parent with no internal-children mask, so nextChild returns the
+// group base (the root) whatever the ray octant - a fresh lane can fetch the root
+// before its ray direction is known.
+__device__ __forceinline__ uint32_t rootGroupBits() { return 1u | (1u << 16); }
 
-// Next child of a non-empty node group; removes it from the group.
+// Next child of a non-empty node group; removes it from the group. Group bits:
+// 0-7 hit internal children in visiting order (k = slot ^ oct), 8-15 imask (slot
+// order), 16-23 the hit children whose box contains the ray origin (k order).
+// Those go first: their entry distance is zero, so they lead any front-to-back
+// order, and rays leaving the same probe then share their first node fetches.
 __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uint32_t oct)
 {
-    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(bits & 0xffu));
+    const uint32_t inside = (bits >> 16) & 0xffu;
+    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(inside ? inside : (bits & 0xffu)));
     const uint32_t slot = k ^ oct;
-    bits &= ~(1u << k);
+    bits &= ~((1u << k) | (1u << (k + 16)));
     return base + static_cast<uint32_t>(__builtin_popcount((bits >> 8) & ((1u << slot) - 1u)));
 }
 
@@ -289,7 +301,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-    uint32_t hitSlots = 0;
+    uint32_t hitSlots = 0, insideSlots = 0;
 #pragma unroll
     for (int s = 0; s < 8; s += 2) {
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
@@ -309,13 +321,17 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         const f2 lim = __builtin_elementwise_fma(tf, f2 { 1.00001f, 1.00001f }, f2 { 1e-7f, 1e-7f });
         hitSlots |= (tn.x <= lim.x ? 1u : 0u) << s;
         hitSlots |= (tn.y <= lim.y ? 1u : 0u) << (s + 1);
+        // origin inside the box: every near-plane distance <= tmin
+        insideSlots |= (tn.x <= tmin ? 1u : 0u) << (s + 16);
+        insideSlots |= (tn.y <= tmin ? 1u : 0u) << (s + 17);
     }
     // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
     // swapping bit pairs / pairs of pairs / nibbles per octant bit
-    uint32_t m = hitSlots & imask;
-    m = fx ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
-    m = fy ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
-    m = fz ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
+    // (hit and inside masks permuted together: bits 0-7 and 16-23)
+    uint32_t m = (hitSlots & imask) | (insideSlots & (hitSlots << 16) & (imask << 16));
+    m = fx ? (((m & 0x00550055u) << 1) | ((m >> 1) & 0x00550055u)) : m;
+    m = fy ? (((m & 0x00330033u) << 2) | ((m >> 2) & 0x00330033u)) : m;
+    m = fz ? (((m & 0x000f000fu) << 4) | ((m >> 4) & 0x000f000fu)) : m;
     // leaf children: their triangle ranges (meta: unary count << 5 | offset)
     uint32_t tb = 0;
     const uint32_t leafHits = hitSlots & ~imask;
@@ -327,7 +343,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         }
     }
     gBase = w1.x;
-    gBits = m | (imask << 8);
+    gBits = (m & 0x00ff00ffu) | (imask << 8);
     tBase = w1.y;
     tBits = tb;
 }
@@ -357,41 +373,59 @@ __device__ __forceinline__ bool travDone(const TravState& ts, const Stack<BLOCK>
     return ts.tBits == 0 && (ts.gBits & 0xffu) == 0 && st.depth == 0;
 }
 
-// Returns true when a triangle was tested and produced a candidate (tt, uu, vv, bf,
-// index i, inst, prim) in [tmin, tmax]; node steps always return false.
+// A traversal step is split in two so that the fetch can be issued before a
+// freshly refilled lane has its ray set up: travFetch picks the work item (a
+// pending leaf triangle, else the next child of the current node group, popping
+// a group when it is empty) and issues its five 16-B loads; travCompute tests it.
+struct Fetch {
+    uint4 w0, w1, w2, w3, w4;
+    uint32_t i; // triangle index (triangle steps)
+    bool isTri;
+};
+
 template<int BLOCK>
-__device__ __forceinline__ bool travStep(const SceneArgs& sc, TravState& ts, Stack<BLOCK>& st, V3 o, V3 d, V3 idir, V3 ooeo, uint32_t oct, float tmin,
-                                         float tmax, uint32_t& i, float& tt, float& uu, float& vv, bool& bf, uint32_t& inst, uint32_t& prim,
-                                         uint32_t& cNodes, uint32_t& cTris)
+__device__ __forceinline__ void travFetch(const SceneArgs& sc, TravState& ts, Stack<BLOCK>& st, uint32_t oct, Fetch& fx)
 {
-    const bool isTri = ts.tBits != 0;
+    fx.isTri = ts.tBits != 0;
     const uint4* src;
-    if (isTri) {
-        i = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
+    if (fx.isTri) {
+        fx.i = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
         ts.tBits &= ts.tBits - 1u;
-        src = reinterpret_cast<const uint4*>(sc.tris + i);
+        src = reinterpret_cast<const uint4*>(sc.tris + fx.i);
     } else {
         if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
         const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
         if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
         src = reinterpret_cast<const uint4*>(sc.nodes + child);
     }
-    const uint4 w0 = src[0], w1 = src[1], w2 = src[2];
-    uint4 w3 = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0);
-    if (!isTri) {
-        w3 = src[3];
-        w4 = src[4];
+    fx.w0 = src[0];
+    fx.w1 = src[1];
+    fx.w2 = src[2];
+    fx.w3 = fx.w4 = make_uint4(0, 0, 0, 0);
+    if (!fx.isTri) {
+        fx.w3 = src[3];
+        fx.w4 = src[4];
     }
-    if (isTri) {
+}
+
+// Returns true when a triangle step produced a candidate (tt, uu, vv, backface
+// with the instance's handedness applied, inst, prim) in [tmin, tmax]; node steps
+// update the group state and return false.
+__device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o, V3 d, V3 idir, uint32_t oct, float tmin, float tmax, float& tt,
+                                            float& uu, float& vv, bool& backface, uint32_t& inst, uint32_t& prim, uint32_t& cNodes, uint32_t& cTris)
+{
+    if (fx.isTri) {
         cTris++;
-        const GpuTriangle tr = triFromWords(w0, w1, w2);
+        const GpuTriangle tr = triFromWords(fx.w0, fx.w1, fx.w2);
+        bool bf;
         if (!intersectTri(o, d, tmin, tmax, tr, &tt, &uu, &vv, &bf)) return false;
-        inst = w2.y;
-        prim = w2.z;
+        inst = fx.w2.y;
+        prim = fx.w2.z;
+        backface = bf != (fx.w2.w != 0u); // GpuTriangle t2.w: instance flips facing
         return true;
     }
     cNodes++;
-    visitNode8(w0, w1, w2, w3, w4, o, idir, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
+    visitNode8(fx.w0, fx.w1, fx.w2, fx.w3, fx.w4, o, idir, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
     return false;
 }
 
@@ -404,16 +438,18 @@ __device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tm
 {
     if (root < 0) return false;
     const V3 idir = safeInv(d);
-    const V3 ooeo = o * idir;
     const uint32_t oct = rayOctant(idir);
-    TravState ts { static_cast<uint32_t>(root), rootGroupBits(oct), 0u, 0u };
+    TravState ts { static_cast<uint32_t>(root), rootGroupBits(), 0u, 0u };
     st.depth = 0;
     uint32_t n = 0, t = 0;
     while (!travDone(ts, st)) {
-        uint32_t i, inst, prim;
+        Fetch fx;
+        travFetch(sc, ts, st, oct, fx);
+        uint32_t inst, prim;
         float tt, uu, vv;
         bool bf;
-        if (!travStep(sc, ts, st, o, d, idir, ooeo, oct, tmin, h.t, i, tt, uu, vv, bf, inst, prim, n, t)) continue;
+        if (!travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, n, t)) continue;
+        const uint32_t i = fx.i;
         if (ANY) {
             h.tri = i;
             break;
@@ -503,14 +539,14 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     int pass = 0;
     TravState ts { 0u, 0u, 0u, 0u };
     uint32_t oct = 0;
-    V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 }, ooeo = { 0, 0, 0 };
+    V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
         const uint64_t need = __ballot(!active);
-        if (need != 0 && !exhausted) {
+        if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
             const uint32_t n = static_cast<uint32_t>(__popcll(need));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
             const uint32_t avail = poolEnd - poolNext;
@@ -527,20 +563,19 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 if (rank < avail) r = poolNext + rank;
                 else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
                 if (r != kNoHit) {
-                    const uint32_t slot = r / f.R, sample = f.order[r - slot * f.R];
-                    ray = slot * f.R + sample; // hit record index
-                    active = true;
+                    const uint32_t slot = r / f.R;
+                    const float4 fv = f.fib_order[r - slot * f.R]; // (direction, sample index)
                     const GpuProbeSlot ps = f.slots[slot];
-                    const float4 fv = f.fib[sample];
+                    ray = slot * f.R + __float_as_uint(fv.w); // hit record index
                     o = { ps.pos[0], ps.pos[1], ps.pos[2] };
                     d = rotate(v3(fv.x, fv.y, fv.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
                     idir = safeInv(d);
-                    ooeo = o * idir;
-                    h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                     oct = rayOctant(idir);
+                    active = true;
+                    h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                     pass = 0;
                     st.depth = 0;
-                    ts = TravState { static_cast<uint32_t>(sc.root_opaque), sc.root_opaque >= 0 ? rootGroupBits(oct) : 0u, 0u, 0u };
+                    ts = TravState { static_cast<uint32_t>(sc.root_opaque), sc.root_opaque >= 0 ? rootGroupBits() : 0u, 0u, 0u };
                 }
             }
             if (avail < n) {
@@ -559,16 +594,18 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         if (active) {
             // ---- one step: a pending leaf triangle, or the next node --------------
             if (!travDone(ts, st)) {
-                uint32_t i, inst, prim;
+                Fetch fx;
+                travFetch(sc, ts, st, oct, fx);
+                uint32_t inst, prim;
                 float tt, uu, vv;
                 bool bf;
-                if (travStep(sc, ts, st, o, d, idir, ooeo, oct, tmin, h.t, i, tt, uu, vv, bf, inst, prim, cNodes, cTris) &&
+                if (travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, cNodes, cTris) &&
                     !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
                     !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
                     h.t = tt;
                     h.u = uu;
                     h.v = vv;
-                    h.tri = i;
+                    h.tri = fx.i;
                     h.inst = inst;
                     h.prim = prim;
                     h.backface = bf;
@@ -576,7 +613,6 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
             // ---- pass finished -----------------------------------------------------
             if (travDone(ts, st)) {
-                if (h.tri != kNoHit) h.backface = h.backface != (sc.instances[h.inst].flip_facing != 0);
                 bool finished = true;
                 if (pass == 0) {
                     // opaque pass done (raygen.rgen:122-134); masked pass: RayFlags_NoOpaque,
@@ -586,8 +622,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     if (sc.root_masked >= 0 && opaqueT >= tmin) {
                         pass = 1;
                         finished = false;
-                        // keep the opaque hit in the stack-free registers: restart with tmax = opaqueT
-                        ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(oct), 0u, 0u };
+                        ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
                         st.depth = 0;
                         // stash the opaque hit; the masked pass searches [tmin, opaqueT]
                         f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
@@ -1327,6 +1362,7 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
 {
     const int v = trace_variant();
     if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 8) hipLaunchKernelGGL((dev::k_trace_primary<false, 8>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else hipLaunchKernelGGL((dev::k_trace_primary<false, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
@@ -1374,6 +1410,7 @@ const void* kernel_trace_primary_ptr(bool count)
 {
     const int v = trace_variant();
     if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1>);
+    if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5>);
     if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6>);
     if (v == 8) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 8>);
     return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1>);

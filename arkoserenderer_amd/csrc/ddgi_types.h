@@ -56,7 +56,8 @@ constexpr int kBvh8MaxLeafSize = 3;
 
 // World-space triangle record, 48 B = 3 x 16 B, in leaf order:
 //   t0 = (v0.x, v0.y, v0.z, e1.x)   t1 = (e1.y, e1.z, e2.x, e2.y)
-//   t2 = (e2.z, instance, primitive, 0)     (e1 = v1 - v0, e2 = v2 - v0)
+//   t2 = (e2.z, instance, primitive, flip)  (e1 = v1 - v0, e2 = v2 - v0; flip = 1
+//        when the instance's det(ObjectToWorld) < 0, i.e. its facing is mirrored)
 // Closest-hit ties are broken on (instance, primitive), i.e. the global triangle
 // id, so the hit does not depend on the BVH shape (same rule in the oracle).
 struct alignas(16) GpuTriangle {
