@@ -109,12 +109,12 @@ struct ArkDdgiCtx {
     // persistent resources
     DeviceBuffer irr, vis, offsets;
     // working set
-    DeviceBuffer slots, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeScratch;
+    DeviceBuffer slots, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork;
     std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
     uint32_t orderR = 0;
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
-    uint32_t traceBlocks = 0, shadeBlocks = 0;
+    uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0;
     // scene
     bool hasScene = false;
     DeviceBuffer nodes, tris, indices, vertices, meshes, materials, instances, texInfos, texels, spots;
@@ -177,7 +177,7 @@ int ensureSpill(ArkDdgiCtx* ctx)
 {
     // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
     uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
-    uint32_t threads = std::max(ctx->traceBlocks * kTraceBlock, ctx->shadeBlocks * kShadeBlock);
+    uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the two traversal kernels
     size_t bytes = static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
     if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
@@ -258,14 +258,16 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->fibOrder.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib order");
     if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
-    if ((e = ctx->rayCounter.alloc(2 * kRayParts * kRayCounterStride * 4)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
     // persistent grids: as many workgroups as are co-resident
-    int occT = 0, occS = 0;
+    int occT = 0, occS = 0, occW = 0;
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_primary_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occS, kernel_shade_ptr(false), kShadeBlock, 0)) != hipSuccess) return bad(e, "occupancy shade");
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occW, kernel_trace_shadow_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy shadow");
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
+    ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
     if (clearHistory(ctx) != ARK_DDGI_OK) {
         std::fprintf(stderr, "ark_ddgi_create: %s\n", ctx->lastError.c_str());
         delete ctx;
@@ -280,7 +282,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeScratch,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
@@ -504,12 +506,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     ctx->bvhMaxDepth = maxDepth;
     if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
     ctx->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
-    {
-        int occ = 0;
-        ARK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_shade_ptr(false), kShadeBlock, shade_lds_bytes(ctx->lightCount)));
-        ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occ) * ctx->cuCount);
-        ARK_HIP(ctx->shadeScratch.alloc(shade_scratch_bytes(ctx->shadeBlocks, ctx->lightCount)));
-    }
+    // shading work lists for the largest window (front records, light terms, shadow rays)
+    ARK_HIP(ctx->shadeWork.alloc(std::max<size_t>(16, shade_work_bytes(static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax, ctx->lightCount))));
     if ((rc = ensureSpill(ctx)) != 0) return rc;
     ctx->hasScene = true;
     const auto t1 = std::chrono::steady_clock::now();
@@ -589,7 +587,14 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     f.hits = ctx->hits.as<GpuHit>();
     f.surfels = ctx->surfels.as<uint16_t>();
     f.spill = ctx->spill.as<uint32_t>();
-    f.shade_scratch = ctx->shadeScratch.as<float4>();
+    {
+        // work lists carved from one buffer sized for the largest window at set_scene
+        const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
+        char* w = static_cast<char*>(ctx->shadeWork.ptr);
+        f.front_recs = reinterpret_cast<FrontRec*>(w);
+        f.front_lights = reinterpret_cast<FrontLight*>(w + rays * sizeof(FrontRec));
+        f.shadow_rays = reinterpret_cast<ShadowRay*>(w + rays * (sizeof(FrontRec) + ctx->lightCount * sizeof(FrontLight)));
+    }
     f.light_count = ctx->lightCount;
     {
         // refill idle trace lanes in batches of >= 8: the refill (pool atomic, slot and
@@ -599,6 +604,9 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
         f.refill_min = e ? static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(e)))) : 8u;
     }
     f.ray_counter = ctx->rayCounter.as<uint32_t>();
+    f.front_count = f.ray_counter + kFrontCountWord;
+    f.shadow_count = f.ray_counter + kShadowCountWord;
+    f.shadow_heads = f.ray_counter + kShadowHeadWord;
     f.counters = ctx->counters.as<unsigned long long>();
     const bool timing = ctx->timing;
     const bool count = ctx->counting;
@@ -611,10 +619,16 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
         ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
+        if (f.light_count > 0) {
+            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
+            ARK_HIP(launch_shade_finish(f, s));
+        }
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
         ARK_HIP(launch_probe_update(f, s));
     } else if (timing) {
         ARK_HIP(hipEventRecord(ctx->ev[1], s));
         ARK_HIP(hipEventRecord(ctx->ev[2], s));
+        ARK_HIP(hipEventRecord(ctx->ev[4], s));
     }
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
     ctx->timingValid = timing;
@@ -756,8 +770,8 @@ int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out, int count)
     ARK_HIP(hipEventElapsedTime(&ms[0], ctx->ev[0], ctx->ev[3]));
     ARK_HIP(hipEventElapsedTime(&ms[1], ctx->ev[0], ctx->ev[1]));
     ARK_HIP(hipEventElapsedTime(&ms[2], ctx->ev[1], ctx->ev[2]));
-    ARK_HIP(hipEventElapsedTime(&ms[3], ctx->ev[2], ctx->ev[3]));
-    ms[4] = 0.0f; // borders + offsets are fused into the probe-update kernel
+    ARK_HIP(hipEventElapsedTime(&ms[3], ctx->ev[4], ctx->ev[3]));
+    ARK_HIP(hipEventElapsedTime(&ms[4], ctx->ev[2], ctx->ev[4]));
     for (int i = 0; i < count && i < 5; ++i) out[i] = ms[i];
     return ARK_DDGI_OK;
 }

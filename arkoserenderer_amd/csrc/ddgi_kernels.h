@@ -20,6 +20,34 @@ constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in
 constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
 
+// Lit front hit awaiting its shadow rays (k_shade -> k_shade_finish), 48 B.
+struct alignas(16) FrontRec {
+    float4 base_T; // emissive + ambient, w = hit distance T
+    float4 bi_ray; // baseColor * indirect, w = probe ray index (bits)
+    uint32_t need; // lit lights (one shadow ray each)
+    uint32_t occ;  // occluded lights (k_trace_shadow atomicOr)
+    uint32_t _pad[2];
+};
+
+// Per lit light of a front record: the light term with shadowFactor 1 and 0.
+struct alignas(16) FrontLight {
+    float4 T;
+    float4 Z;
+};
+
+// One shadow ray: origin + tmax, direction + owner ((front record << 4) | light).
+struct alignas(16) ShadowRay {
+    float4 origin_tmax;
+    float4 dir_owner;
+};
+
+// Word offsets in the ray-counter buffer: 2 x kRayParts partition heads, then the
+// shading work-list counters (each on its own 128-B line).
+constexpr int kFrontCountWord = 2 * kRayParts * kRayCounterStride;
+constexpr int kShadowCountWord = kFrontCountWord + kRayCounterStride;
+constexpr int kShadowHeadWord = kShadowCountWord + kRayCounterStride; // kRayParts partition heads
+constexpr int kRayCounterWords = kShadowHeadWord + kRayParts * kRayCounterStride;
+
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {
     const GpuBvh8Node* nodes;
@@ -82,7 +110,12 @@ struct FrameArgs {
     GpuHit* hits;
     uint16_t* surfels;
     uint32_t* spill;
-    float4* shade_scratch;   // per shading block: [chunk] partial colours + [chunk][lights] light records
+    FrontRec* front_recs;    // [window_rays] worst case
+    FrontLight* front_lights; // [front record][light_count]
+    ShadowRay* shadow_rays;  // [window_rays * light_count] worst case
+    uint32_t* front_count;   // = ray_counter + kFrontCountWord
+    uint32_t* shadow_count;  // = ray_counter + kShadowCountWord
+    uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
     uint32_t light_count;    // has_sun + spot lights
     uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
     uint32_t* ray_counter;
@@ -92,11 +125,13 @@ struct FrameArgs {
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
-size_t shade_lds_bytes(uint32_t lights);
-size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights);
+hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
+hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s);
+size_t shade_work_bytes(uint64_t rays, uint32_t lights);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
 const void* kernel_trace_primary_ptr(bool count);
 const void* kernel_shade_ptr(bool count);
+const void* kernel_trace_shadow_ptr(bool count);
 
 } // namespace ark

@@ -494,6 +494,25 @@ __device__ __forceinline__ uint32_t xccId()
     return x & (kRayParts - 1);
 }
 
+// Same partitioned dequeue over a flat list of `total` items (shadow rays).
+template<uint32_t CHUNK>
+__device__ __forceinline__ void grabItems(uint32_t* heads, uint32_t total, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+{
+    b = e = 0;
+    for (; tried < kRayParts; ++tried) {
+        const uint32_t p = (home + tried) & (kRayParts - 1);
+        const uint32_t pb = static_cast<uint32_t>(static_cast<uint64_t>(total) * p / kRayParts);
+        const uint32_t pe = static_cast<uint32_t>(static_cast<uint64_t>(total) * (p + 1) / kRayParts);
+        if (pb >= pe) continue;
+        const uint32_t off = atomicAdd(heads + p * kRayCounterStride, CHUNK);
+        if (off < pe - pb) {
+            b = pb + off;
+            e = min(b + CHUNK, pe);
+            return;
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t partRayBegin(const FrameArgs& f, uint32_t p)
 {
     return static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * p / kRayParts) * f.R;
@@ -788,29 +807,18 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 
 
 // ---------------------------------------------------------------------------
-// 3. shading (in-block compaction: classify -> dense surface -> dense shadow -> finish)
+// 3. shading: surface kernel -> shadow-ray kernel -> finish kernel
 // ---------------------------------------------------------------------------
-// Each block takes chunks of kShadeChunk consecutive probe rays. Misses and
-// backface hits are finished in the classify phase; front hits are compacted
-// into an LDS list and shaded densely; their shadow rays (one per lit light) are
-// compacted again and traced densely; a last pass adds the light terms in the
-// reference's order. Per light the closest hit's term is precomputed for both
-// shadowFactor = 1 (T) and 0 (Z) (opaque.rchit:56-103), so the final sum is the
-// same IEEE sequence as the single-pass shader: base (+ T or Z per lit light) + indirect.
-template<bool COUNT>
-__device__ __forceinline__ bool shadowOccluded(const SceneArgs& sc, V3 X, V3 L, float maxDistance, Stack<kShadeBlock>& st, uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow)
-{
-    // opaque.rchit:35-54: TerminateOnFirstHit|SkipClosestHit|Opaque, cullMask 0xff, tmin 0.025
-    const float tmin = 0.025f;
-    if (!(maxDistance >= tmin)) return false;
-    if (COUNT) cShadow++;
-    RayHit h { maxDistance, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-    if (traverse<true, false, COUNT>(sc, sc.root_opaque, X, L, tmin, h, st, cNodes, cTris)) return true;
-    if (traverse<true, false, COUNT>(sc, sc.root_masked, X, L, tmin, h, st, cNodes, cTris)) return true;
-    if (traverse<true, false, COUNT>(sc, sc.root_blend, X, L, tmin, h, st, cNodes, cTris)) return true;
-    return false;
-}
-
+// k_shade takes chunks of kShadeChunk consecutive probe rays. Misses and backface
+// hits are finished in a classify pass; front hits are compacted into an LDS list
+// and shaded densely (material, textures, BRDF per lit light, DDGI indirect).
+// A front hit with no lit light stores its surfel at once. One with lit lights
+// (opaque.rchit:56-103: LdotN > 0) gets a front record - base and indirect terms
+// and, per lit light, the light term for shadowFactor = 1 (T) and 0 (Z) - and one
+// shadow ray per lit light in a global list. k_trace_shadow traces that list
+// densely (persistent, refilled lanes, any-hit over all hit-mask classes) and
+// sets occlusion bits; k_shade_finish adds base (+ T or Z per lit light) +
+// indirect: the same IEEE sequence as the single-pass closest-hit shader.
 __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3 color, float dist)
 {
     const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
@@ -829,31 +837,33 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
     *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
 }
 
-// Light record (64 B): shadow ray + both candidate terms.
-struct alignas(16) LightRec {
-    float4 origin_tmax;
-    float4 dir;
-    float4 T; // term with shadowFactor = 1
-    float4 Z; // term with shadowFactor = 0
-};
-
+// Wave-aggregated allocation: every lane of the converged, full wave passes its
+// count; returns this lane's first index in [*ctr, *ctr + sum). One atomic per wave.
+__device__ __forceinline__ uint32_t waveAlloc(uint32_t* ctr, uint32_t n)
+{
+    const uint32_t lane = __lane_id();
+    uint32_t x = n;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= static_cast<uint32_t>(off)) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    uint32_t base = 0;
+    if (total != 0) {
+        if (lane == 63) base = atomicAdd(ctr, total);
+        base = __shfl(base, 63);
+    }
+    return base + x - n;
+}
 
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* ldsStack = lds;
-    uint32_t* listA = lds + kStackLds * 2 * kShadeBlock;   // compacted front hits (ray index)
-    uint32_t* needMask = listA + kShadeChunk;          // per front hit: lit lights (shadow ray issued)
-    uint32_t* occMask = needMask + kShadeChunk;        // per front hit: occluded lights
-    uint32_t* listB = occMask + kShadeChunk;           // compacted shadow rays: (front << 4) | light
-    uint32_t* counts = listB + kShadeChunk * f.light_count;             // [0] nA [1] nB [2,3] chunk
-    const uint32_t gtid = blockIdx.x * kShadeBlock + threadIdx.x;
-    Stack<kShadeBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kShadeBlock, 0 };
+    __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
+    __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
     const uint32_t L = f.light_count;
-    float4* partial = f.shade_scratch + static_cast<size_t>(blockIdx.x) * kShadeChunk * (2 + 4 * L);
-    LightRec* lrec = reinterpret_cast<LightRec*>(partial + 2 * kShadeChunk);
-    uint32_t cNodes = 0, cTris = 0, cShadow = 0, cFront = 0;
+    uint32_t cFront = 0;
 
     // chunks come from the second set of per-XCD partition heads (see grabRays)
     uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
@@ -864,7 +874,6 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             uint32_t b, e;
             grabRays<static_cast<uint32_t>(kShadeChunk)>(f, heads, home, tried, b, e);
             counts[0] = 0;
-            counts[1] = 0;
             counts[2] = b;
             counts[3] = e;
         }
@@ -896,157 +905,262 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
         __syncthreads();
         const uint32_t nA = counts[0];
         // ---- B. dense surface shading of front hits -----------------------------
-        for (uint32_t k = threadIdx.x; k < nA; k += kShadeBlock) {
-            const uint32_t ray = listA[k];
-            if (COUNT) cFront++;
-            const GpuHit hit = f.hits[ray];
-            V3 origin, dir;
-            rayOf(f, ray, &origin, &dir);
-            const float T = hit.t;
-            const GpuTriangle tr = loadTri(sc.tris, hit.tri);
-            const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
-            const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
-            const GpuInstance gi = sc.instances[inst];
-            const ArkRTTriangleMesh mesh = sc.meshes[gi.rt_mesh_index];
-            const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
-            float bx = 1.0f - hit.u - hit.v, by = hit.u, bz = hit.v;
-            const float* vx[3];
-            for (int q = 0; q < 3; ++q) {
-                uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
-                vx[q] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
-            }
-            // opaque.rchit:118-131 (front face: no flip)
-            V3 N = normalize(v3(vx[0][2], vx[0][3], vx[0][4]) * bx + v3(vx[1][2], vx[1][3], vx[1][4]) * by + v3(vx[2][2], vx[2][3], vx[2][4]) * bz);
-            const float* M = gi.normal_matrix;
-            V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
-            N = normalize(Nw);
-            float uvx = vx[0][0] * bx + vx[1][0] * by + vx[2][0] * bz;
-            float uvy = vx[0][1] * bx + vx[1][1] * by + vx[2][1] * bz;
-            float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
-            V3 baseColor = v3(c.x, c.y, c.z) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
-            c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.emissive), uvx, uvy);
-            V3 emissive = v3(c.x, c.y, c.z) * v3(mat.emissive_factor[0], mat.emissive_factor[1], mat.emissive_factor[2]);
-            c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.metallic_roughness), uvx, uvy);
-            float metallic = c.z * mat.metallic_factor;
-            float roughness = c.y * mat.roughness_factor;
-            const float clearcoat = mat.clearcoat, ccRough = mat.clearcoat_roughness;
-            const V3 V = -dir;
-            V3 ambient = f.ambient_amount * baseColor;
-            const V3 base = emissive + ambient;
-            const V3 hitPoint = origin + T * dir;
+        // (every lane runs every iteration so that the record allocation sees full waves)
+        for (uint32_t k0 = 0; k0 < nA; k0 += kShadeBlock) {
+            const uint32_t kk = k0 + threadIdx.x;
+            const bool valid = kk < nA;
+            const uint32_t ray = valid ? listA[kk] : 0u;
+            // surface (opaque.rchit:105-131)
+            V3 origin = splat(0.0f), dir = splat(0.0f), N = splat(0.0f), baseColor = splat(0.0f), base = splat(0.0f);
+            float T = 0.0f, metallic = 0.0f, roughness = 0.0f, clearcoat = 0.0f, ccRough = 0.0f;
             uint32_t need = 0;
+            if (valid) {
+                if (COUNT) cFront++;
+                const GpuHit hit = f.hits[ray];
+                rayOf(f, ray, &origin, &dir);
+                T = hit.t;
+                const GpuTriangle tr = loadTri(sc.tris, hit.tri);
+                const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
+                const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
+                const GpuInstance gi = sc.instances[inst];
+                const ArkRTTriangleMesh mesh = sc.meshes[gi.rt_mesh_index];
+                const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
+                const float bx = 1.0f - hit.u - hit.v, by = hit.u, bz = hit.v;
+                const float* vx[3];
+                for (int q = 0; q < 3; ++q) {
+                    uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
+                    vx[q] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+                }
+                // opaque.rchit:118-131 (front face: no flip)
+                N = normalize(v3(vx[0][2], vx[0][3], vx[0][4]) * bx + v3(vx[1][2], vx[1][3], vx[1][4]) * by + v3(vx[2][2], vx[2][3], vx[2][4]) * bz);
+                const float* M = gi.normal_matrix;
+                V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
+                N = normalize(Nw);
+                const float uvx = vx[0][0] * bx + vx[1][0] * by + vx[2][0] * bz;
+                const float uvy = vx[0][1] * bx + vx[1][1] * by + vx[2][1] * bz;
+                float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
+                baseColor = v3(c.x, c.y, c.z) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
+                c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.emissive), uvx, uvy);
+                const V3 emissive = v3(c.x, c.y, c.z) * v3(mat.emissive_factor[0], mat.emissive_factor[1], mat.emissive_factor[2]);
+                c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.metallic_roughness), uvx, uvy);
+                metallic = c.z * mat.metallic_factor;
+                roughness = c.y * mat.roughness_factor;
+                clearcoat = mat.clearcoat;
+                ccRough = mat.clearcoat_roughness;
+                const V3 ambient = f.ambient_amount * baseColor;
+                base = emissive + ambient;
+                // lit lights (LdotN > 0): one shadow ray each (opaque.rchit:56-103)
+                uint32_t l = 0;
+                if (sc.has_sun) {
+                    const V3 Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+                    if (dot(Ld, N) > 0.0f) need |= 1u;
+                    l++;
+                }
+                for (int li = 0; li < sc.spot_count; ++li, ++l) {
+                    const V3 Ld = -normalize(v3(sc.spots[li].direction[0], sc.spots[li].direction[1], sc.spots[li].direction[2]));
+                    if (dot(Ld, N) > 0.0f) need |= 1u << l;
+                }
+            }
+            const uint32_t fk = waveAlloc(f.front_count, need != 0 ? 1u : 0u);
+            uint32_t sj = waveAlloc(f.shadow_count, static_cast<uint32_t>(__builtin_popcount(need)));
+            if (!valid) continue;
+            const V3 V = -dir;
+            const V3 hitPoint = origin + T * dir;
             uint32_t l = 0;
             if (sc.has_sun) { // opaque.rchit:56-73
-                V3 Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
-                float LdotN = dot(Ld, N);
-                if (LdotN > 0.0f) {
-                    V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
-                    V3 lc = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]);
-                    V3 tT = brdf * LdotN * (lc * 1.0f);
-                    V3 tZ = brdf * LdotN * (lc * 0.0f);
-                    LightRec rec;
-                    rec.origin_tmax = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far);
-                    rec.dir = make_float4(Ld.x, Ld.y, Ld.z, 0.0f);
-                    rec.T = make_float4(tT.x, tT.y, tT.z, 0.0f);
-                    rec.Z = make_float4(tZ.x, tZ.y, tZ.z, 0.0f);
-                    lrec[static_cast<size_t>(k) * L + l] = rec;
-                    need |= 1u << l;
+                if (need & 1u) {
+                    const V3 Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+                    const float LdotN = dot(Ld, N);
+                    const V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                    const V3 lc = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]);
+                    const V3 tT = brdf * LdotN * (lc * 1.0f);
+                    const V3 tZ = brdf * LdotN * (lc * 0.0f);
+                    f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
+                    f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far),
+                                                      make_float4(Ld.x, Ld.y, Ld.z, __uint_as_float((fk << 4) | l)) };
                 }
                 l++;
             }
             for (int li = 0; li < sc.spot_count; ++li, ++l) { // opaque.rchit:75-103
+                if (!((need >> l) & 1u)) continue;
                 const GpuSpotLight sl = sc.spots[li];
                 V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
                 V3 Ld = -normalize(sdir);
                 float LdotN = dot(Ld, N);
-                if (LdotN > 0.0f) {
-                    V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
-                    float distanceToLight = length(toLight);
-                    V3 normalizedToLight = toLight / distanceToLight;
-                    float distanceAttenuation = 1.0f / square(distanceToLight);
-                    // evaluateIESLookupTable (lighting.glsl:20-39)
-                    V3 lrd = -normalizedToLight;
-                    float iesValue = 0.0f;
-                    float angleV = dot(lrd, sdir);
-                    if (!(angleV <= 0.0f)) {
-                        float hx = dot(lrd, v3(sl.right[0], sl.right[1], sl.right[2]));
-                        float hy = dot(lrd, v3(sl.up[0], sl.up[1], sl.up[2]));
-                        float angleH = atan2f_(hy, hx) + kPi;
-                        float lx = acosf_(angleV) / (2.0f * sl.position[3]);
-                        float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
-                        iesValue = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(sl.ies_texture), lx, ly).x;
-                    }
-                    V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
-                    V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
-                    V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
-                    V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
-                    LightRec rec;
-                    rec.origin_tmax = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f);
-                    rec.dir = make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, 0.0f);
-                    rec.T = make_float4(tT.x, tT.y, tT.z, 0.0f);
-                    rec.Z = make_float4(tZ.x, tZ.y, tZ.z, 0.0f);
-                    lrec[static_cast<size_t>(k) * L + l] = rec;
-                    need |= 1u << l;
+                {
+                        V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
+                        float distanceToLight = length(toLight);
+                        V3 normalizedToLight = toLight / distanceToLight;
+                        float distanceAttenuation = 1.0f / square(distanceToLight);
+                        // evaluateIESLookupTable (lighting.glsl:20-39)
+                        V3 lrd = -normalizedToLight;
+                        float iesValue = 0.0f;
+                        float angleV = dot(lrd, sdir);
+                        if (!(angleV <= 0.0f)) {
+                            float hx = dot(lrd, v3(sl.right[0], sl.right[1], sl.right[2]));
+                            float hy = dot(lrd, v3(sl.up[0], sl.up[1], sl.up[2]));
+                            float angleH = atan2f_(hy, hx) + kPi;
+                            float lx = acosf_(angleV) / (2.0f * sl.position[3]);
+                            float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
+                            iesValue = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(sl.ies_texture), lx, ly).x;
+                        }
+                        V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                        V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
+                        V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
+                        V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
+                    f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
+                    f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f),
+                                                      make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, __uint_as_float((fk << 4) | l)) };
                 }
             }
             // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
-            const V3 hitPos = origin + T * dir;
             const V3 Vi = -dir;
-            V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
-            V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
-            V3 irradiance = sampleDDGI(f, hitPos, N, Vi);
-            V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
+            const V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
+            const V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
+            const V3 irradiance = sampleDDGI(f, hitPoint, N, Vi);
+            const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
-            needMask[k] = need;
-            occMask[k] = 0;
             if (need == 0) {
                 storeSurfel(f, ray, base + bi, T);
             } else {
-                partial[2 * k] = make_float4(base.x, base.y, base.z, T);
-                partial[2 * k + 1] = make_float4(bi.x, bi.y, bi.z, 0.0f);
-                for (uint32_t b = need; b; b &= b - 1) {
-                    const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
-                    const uint32_t j = atomicAdd(&counts[1], 1u);
-                    listB[j] = (k << 4) | ll;
+                f.front_recs[fk] = FrontRec { make_float4(base.x, base.y, base.z, T), make_float4(bi.x, bi.y, bi.z, __uint_as_float(ray)), need, 0u };
+            }
+        }
+        __syncthreads();
+    }
+    if (COUNT) atomicAdd(&f.counters[6], static_cast<unsigned long long>(cFront));
+}
+
+// Persistent any-hit traversal of the shadow-ray list (opaque.rchit:35-54:
+// TerminateOnFirstHit | SkipClosestHit | Opaque, cullMask 0xff, tmin 0.025): the
+// three hit-mask classes in turn, no alpha test. Lanes are refilled from a
+// wave-private pool like k_trace_primary; an occluded ray sets its light's bit in
+// its front record.
+template<bool COUNT, int WPE>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
+{
+    __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
+    const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
+    Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
+    const uint32_t lane = threadIdx.x & 63u;
+    const float tmin = 0.025f;
+    const uint32_t total = *f.shadow_count;
+    const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
+    uint32_t cNodes = 0, cTris = 0, cShadow = 0;
+
+    uint32_t poolNext = 0, poolEnd = 0;
+    const uint32_t home = xccId();
+    uint32_t tried = 0;
+    bool exhausted = false, active = false;
+    uint32_t owner = 0;
+    int pass = 0;
+    float tmax = 0.0f;
+    TravState ts { 0u, 0u, 0u, 0u };
+    uint32_t oct = 0;
+    V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
+    for (;;) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(need));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
+            const uint32_t avail = poolEnd - poolNext;
+            uint32_t fb = 0, fe = 0;
+            if (avail < n) {
+                uint32_t b = 0, e = 0, t = tried;
+                if (lane == 0) grabItems<64u>(f.shadow_heads, total, home, t, b, e);
+                fb = __shfl(b, 0);
+                fe = __shfl(e, 0);
+                tried = __shfl(t, 0);
+            }
+            if (!active) {
+                uint32_t r = kNoHit;
+                if (rank < avail) r = poolNext + rank;
+                else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
+                if (r != kNoHit) {
+                    const ShadowRay sr = f.shadow_rays[r];
+                    o = v3(sr.origin_tmax.x, sr.origin_tmax.y, sr.origin_tmax.z);
+                    d = v3(sr.dir_owner.x, sr.dir_owner.y, sr.dir_owner.z);
+                    tmax = sr.origin_tmax.w;
+                    owner = __float_as_uint(sr.dir_owner.w);
+                    idir = safeInv(d);
+                    oct = rayOctant(idir);
+                    st.depth = 0;
+                    pass = 0;
+                    ts = TravState { 0u, 0u, 0u, 0u };
+                    active = true;
+                    if (tmax >= tmin) {
+                        if (COUNT) cShadow++;
+                        while (pass < 3 && roots[pass] < 0) ++pass;
+                        if (pass < 3) ts = TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u };
+                    } else {
+                        pass = 3; // !(maxDistance >= tmin): not traced, not occluded
+                    }
+                }
+            }
+            if (avail < n) {
+                if (fb >= fe) {
+                    exhausted = true;
+                    poolNext = poolEnd = 0;
+                } else {
+                    poolNext = min(fb + (n - avail), fe);
+                    poolEnd = fe;
+                }
+            } else {
+                poolNext += n;
+            }
+        }
+        if (__ballot(active) == 0) break;
+        if (active) {
+            bool occluded = false;
+            if (!travDone(ts, st)) {
+                Fetch fx;
+                travFetch(sc, ts, st, oct, fx);
+                uint32_t inst, prim;
+                float tt, uu, vv;
+                bool bf;
+                occluded = travCompute(fx, ts, o, d, idir, oct, tmin, tmax, tt, uu, vv, bf, inst, prim, cNodes, cTris);
+            }
+            if (occluded) {
+                atomicOr(&f.front_recs[owner >> 4].occ, 1u << (owner & 15u));
+                active = false;
+            } else if (travDone(ts, st)) {
+                ++pass;
+                while (pass < 3 && roots[pass] < 0) ++pass;
+                if (pass < 3) {
+                    st.depth = 0;
+                    ts = TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u };
+                } else {
+                    active = false;
                 }
             }
         }
-        __syncthreads();
-        // ---- C. dense shadow rays ------------------------------------------------
-        const uint32_t nB = counts[1];
-        for (uint32_t j = threadIdx.x; j < nB; j += kShadeBlock) {
-            const uint32_t e = listB[j];
-            const uint32_t k = e >> 4, ll = e & 15u;
-            const LightRec rec = lrec[static_cast<size_t>(k) * L + ll];
-            const V3 X = v3(rec.origin_tmax.x, rec.origin_tmax.y, rec.origin_tmax.z);
-            const V3 Ld = v3(rec.dir.x, rec.dir.y, rec.dir.z);
-            if (shadowOccluded<COUNT>(sc, X, Ld, rec.origin_tmax.w, st, cNodes, cTris, cShadow)) atomicOr(&occMask[k], 1u << ll);
-        }
-        __syncthreads();
-        // ---- D. finish lit front hits in the reference's light order -------------
-        for (uint32_t k = threadIdx.x; k < nA; k += kShadeBlock) {
-            const uint32_t need = needMask[k];
-            if (need == 0) continue;
-            const uint32_t occ = occMask[k];
-            const float4 p0 = partial[2 * k], p1 = partial[2 * k + 1];
-            V3 color = v3(p0.x, p0.y, p0.z);
-            for (uint32_t b = need; b; b &= b - 1) {
-                const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
-                const float4 t = (occ >> ll) & 1u ? lrec[static_cast<size_t>(k) * L + ll].Z : lrec[static_cast<size_t>(k) * L + ll].T;
-                color = color + v3(t.x, t.y, t.z);
-            }
-            color = color + v3(p1.x, p1.y, p1.z);
-            storeSurfel(f, listA[k], color, p0.w);
-        }
-        __syncthreads();
     }
     if (COUNT) {
         atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[5], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
-        atomicAdd(&f.counters[6], static_cast<unsigned long long>(cFront));
     }
 }
+
+// Lit front hits: base (+ T or Z per lit light, in light order) + indirect.
+__global__ void __launch_bounds__(256) k_shade_finish(FrameArgs f)
+{
+    const uint32_t n = *f.front_count;
+    const uint32_t L = f.light_count;
+    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < n; k += gridDim.x * 256u) {
+        const FrontRec fr = f.front_recs[k];
+        V3 color = v3(fr.base_T.x, fr.base_T.y, fr.base_T.z);
+        for (uint32_t b = fr.need; b; b &= b - 1) {
+            const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
+            const FrontLight& fl = f.front_lights[static_cast<size_t>(k) * L + ll];
+            const float4 t = (fr.occ >> ll) & 1u ? fl.Z : fl.T;
+            color = color + v3(t.x, t.y, t.z);
+        }
+        color = color + v3(fr.bi_ray.x, fr.bi_ray.y, fr.bi_ray.z);
+        storeSurfel(f, __float_as_uint(fr.bi_ray.w), color, fr.base_T.w);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 4. probe update: irradiance + visibility + borders + offsets, one WG per probe
 // ---------------------------------------------------------------------------
@@ -1369,24 +1483,31 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
     return hipGetLastError();
 }
 
-size_t shade_lds_bytes(uint32_t lights)
+size_t shade_work_bytes(uint64_t rays, uint32_t lights)
 {
-    return static_cast<size_t>(kStackLds) * 2 * kShadeBlock * 4 + static_cast<size_t>(kShadeChunk) * (3 + lights) * 4 + 16;
-}
-
-size_t shade_scratch_bytes(uint32_t blocks, uint32_t lights)
-{
-    return static_cast<size_t>(blocks) * kShadeChunk * (2 + 4 * static_cast<size_t>(lights)) * 16;
+    return rays * (sizeof(FrontRec) + static_cast<uint64_t>(lights) * (sizeof(FrontLight) + sizeof(ShadowRay)));
 }
 
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    const size_t lds = shade_lds_bytes(f.light_count);
     const int v = shade_variant();
-    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
-    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
-    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_shade<false, 1>), dim3(blocks), dim3(kShadeBlock), lds, s, sc, f);
+    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_shade<false, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
+{
+    if (count) hipLaunchKernelGGL((dev::k_trace_shadow<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_trace_shadow<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_shade_finish, dim3(2048), dim3(256), 0, s, f);
     return hipGetLastError();
 }
 
@@ -1422,6 +1543,11 @@ const void* kernel_shade_ptr(bool count)
     if (v == 4) return reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
     if (v == 5) return reinterpret_cast<const void*>(&dev::k_shade<false, 5>);
     return reinterpret_cast<const void*>(&dev::k_shade<false, 1>);
+}
+
+const void* kernel_trace_shadow_ptr(bool count)
+{
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6>);
 }
 
 } // namespace ark

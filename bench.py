@@ -36,6 +36,7 @@ SURFEL_BYTES = 8       # RGBA16F surfel
 # + 3 RTVertex 108 + 3 texel fetches 48 + 8-probe DDGI gather 8*(4*4 + 4*8) = 384
 SHADE_HIT_BYTES = 48 + 64 + 12 + 96 + 12 + 108 + 48 + 384
 MISS_BYTES = 16        # environment texel
+SHADOW_RAY_BYTES = 32  # ShadowRay record (written by k_shade, read by k_trace_shadow)
 
 
 def parse():
@@ -148,11 +149,12 @@ def main():
     rays_rank = cnt.rays
     kernel_bytes = {
         "k_trace_primary": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays_rank,
-        "k_shade": HIT_RECORD_BYTES * rays_rank + NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests
-                   + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays_rank - cnt.hits) + SURFEL_BYTES * rays_rank,
+        "k_shade": HIT_RECORD_BYTES * rays_rank + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays_rank - cnt.hits)
+                   + SURFEL_BYTES * rays_rank + SHADOW_RAY_BYTES * cnt.shadow_rays,
+        "k_trace_shadow": NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests + SHADOW_RAY_BYTES * cnt.shadow_rays,
         "k_probe_update": cnt.probes * (R * SURFEL_BYTES + 2 * (64 * 8 + 256 * 4) + (36 * 8 + 68 * 4) + 32),
     }
-    kernel_ms = {"k_trace_primary": avg[1], "k_shade": avg[2], "k_probe_update": avg[3]}
+    kernel_ms = {"k_trace_primary": avg[1], "k_shade": avg[2], "k_trace_shadow": avg[4], "k_probe_update": avg[3]}
     dom = max(kernel_ms, key=kernel_ms.get)
     achieved = kernel_bytes[dom] / (kernel_ms[dom] * 1e-3) / 1e9
     traffic = None

@@ -282,8 +282,9 @@ int ark_ddgi_set_counting(ArkDdgiCtx* ctx, int enabled);
 int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out_counters);
 
 /* Device time of the last update's kernels, from HIP events on the update stream:
- * [0] whole update, [1] primary traversal, [2] shading+shadow rays, [3] probe
- * update (irradiance+visibility), [4] borders+offsets. Milliseconds. */
+ * [0] whole update, [1] primary traversal (+ slot table), [2] surface shading,
+ * [3] probe update (irradiance, visibility, borders, offsets), [4] shadow rays
+ * (traversal + light-term finish). Milliseconds. */
 int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out_ms, int count);
 int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled);
 
