@@ -1263,26 +1263,26 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         if (sharp == 50.0f && (R & 1u) == 0) {
             // default sharpness, two rays per iteration in packed fp32 (v_pk_mul/add):
             // every product and sum is the same IEEE operation as the scalar loop
-            // below, and the three sums still run over the rays in order
-            nv0 = nv1 = totalWeight = 0.0f;
+            // below, and each sum still runs over the rays in order. weight =
+            // powi(max(0, d), 50) needs no select: powi(+0, 50) = +0 = pow(0, 50).
+            // (nv0, nv1) accumulate as one packed pair.
+            f2 nv = { 0.0f, 0.0f };
+            totalWeight = 0.0f;
             for (uint32_t s = 0; s < R; s += 2) {
                 const f2 rx = *reinterpret_cast<const f2*>(&sDir[0][s]);
                 const f2 ry = *reinterpret_cast<const f2*>(&sDir[1][s]);
                 const f2 rz = *reinterpret_cast<const f2*>(&sDir[2][s]);
                 const f2 dp = (texelDirection.x * rx + texelDirection.y * ry) + texelDirection.z * rz;
                 const f2 x = { fmaxf_(0.0f, dp.x), fmaxf_(0.0f, dp.y) };
-                const f2 p = powi2<50>(x);
-                const f2 weight = { x.x > 0.0f ? p.x : 0.0f, x.y > 0.0f ? p.y : 0.0f };
-                const float4 dd = *reinterpret_cast<const float4*>(&sDist[s]);
-                const f2 m0 = weight * f2 { dd.x, dd.z };
-                const f2 m1 = weight * f2 { dd.y, dd.w };
-                nv0 += m0.x;
-                nv0 += m0.y;
-                nv1 += m1.x;
-                nv1 += m1.y;
+                const f2 weight = powi2<50>(x);
+                const float4 dd = *reinterpret_cast<const float4*>(&sDist[s]); // (d0, d0^2, d1, d1^2)
+                nv += f2 { weight.x, weight.x } * f2 { dd.x, dd.y };
+                nv += f2 { weight.y, weight.y } * f2 { dd.z, dd.w };
                 totalWeight += weight.x;
                 totalWeight += weight.y;
             }
+            nv0 = nv.x;
+            nv1 = nv.y;
         } else if (is_small_int_(sharp)) {
             // weight = pow(max(0, d), sharp) with an integral sharpness:
             // powf_ == powi_ for x > 0 and pow(0, s) = +0, so a select replaces the branches
