@@ -1213,7 +1213,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
 {
     constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
     __shared__ __attribute__((aligned(16))) float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
-    __shared__ uint2 sSurf[ARK_DDGI_MAX_RAYS_PER_PROBE];
+    __shared__ __attribute__((aligned(16))) float4 sRad[ARK_DDGI_MAX_RAYS_PER_PROBE]; // surfel radiance (fp16 -> fp32) + signed depth
     __shared__ __attribute__((aligned(16))) float2 sDist[ARK_DDGI_MAX_RAYS_PER_PROBE]; // (d, d^2), d = min(|surfel.a|, 1.5 * gridMaxSpacing)
     __shared__ uint2 sIrrTile[(IR + 2) * (IR + 2)];
     __shared__ uint32_t sVisTile[(VR + 2) * (VR + 2)];
@@ -1232,7 +1232,8 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
         sDir[1][s] = d.y;
         sDir[2][s] = d.z;
         const uint2 sv = reinterpret_cast<const uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + s];
-        sSurf[s] = sv;
+        sRad[s] = make_float4(f16_to_f32(static_cast<uint16_t>(sv.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.x >> 16)),
+                              f16_to_f32(static_cast<uint16_t>(sv.y & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.y >> 16)));
         // probeUpdateVisibility.comp:45-48 (per ray; identical for every texel)
         const float gridMaxSpacing = fmaxf_(f.spacing[0], fmaxf_(f.spacing[1], f.spacing[2]));
         const float maxDistance = 1.5f * gridMaxSpacing;
@@ -1338,13 +1339,32 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
             V3 newIrr = splat(0.0f);
             float totalWeight = 0.0f;
-            for (uint32_t s = 0; s < R; ++s) {
+            uint32_t s = 0;
+            if ((R & 1u) == 0) {
+                // two rays per iteration; (r, g) as one packed pair, every sum in ray order
+                f2 rg = { 0.0f, 0.0f };
+                float b = 0.0f;
+                for (; s < R; s += 2) {
+                    const f2 rx = *reinterpret_cast<const f2*>(&sDir[0][s]);
+                    const f2 ry = *reinterpret_cast<const f2*>(&sDir[1][s]);
+                    const f2 rz = *reinterpret_cast<const f2*>(&sDir[2][s]);
+                    const f2 dp = (texelDirection.x * rx + texelDirection.y * ry) + texelDirection.z * rz;
+                    const float w0 = fmaxf_(0.0f, dp.x), w1 = fmaxf_(0.0f, dp.y);
+                    const float4 r0 = sRad[s], r1 = sRad[s + 1];
+                    rg += f2 { w0, w0 } * f2 { r0.x, r0.y };
+                    b += w0 * r0.z;
+                    rg += f2 { w1, w1 } * f2 { r1.x, r1.y };
+                    b += w1 * r1.z;
+                    totalWeight += w0;
+                    totalWeight += w1;
+                }
+                newIrr = v3(rg.x, rg.y, b);
+            }
+            for (; s < R; ++s) {
                 V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
                 float weight = fmaxf_(0.0f, dot(texelDirection, rd));
-                uint2 sv = sSurf[s];
-                V3 rad = v3(f16_to_f32(static_cast<uint16_t>(sv.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.x >> 16)),
-                            f16_to_f32(static_cast<uint16_t>(sv.y & 0xffffu)));
-                newIrr = newIrr + weight * rad;
+                const float4 r = sRad[s];
+                newIrr = newIrr + weight * v3(r.x, r.y, r.z);
                 totalWeight += weight;
             }
             newIrr = newIrr / fmaxf_(totalWeight, epsilon);
@@ -1374,7 +1394,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 const uint32_t s = s0 + static_cast<uint32_t>(i);
                 uint32_t cls = 0;
                 if (s < R) {
-                    const float a = f16_to_f32(static_cast<uint16_t>(sSurf[s].y >> 16));
+                    const float a = sRad[s].w;
                     cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
                     sClass[s] = static_cast<uint8_t>(cls);
                 }
