@@ -365,6 +365,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     std::vector<GpuBvh8Node> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
+    uint32_t opaqueNodes = 0;
     uint32_t maxDepth = 0, maxLeaf = 0;
     float sah = 0.0f;
     for (int c = 0; c < 3; ++c) {
@@ -376,6 +377,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         maxLeaf = std::max(maxLeaf, r2.max_leaf);
         Bvh8BuildResult r = collapse_bvh8(r2, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()));
         roots[c] = static_cast<int32_t>(allNodes.size());
+        if (c == 0) opaqueNodes = static_cast<uint32_t>(r.nodes.size());
         maxDepth = std::max(maxDepth, r.max_depth);
         allNodes.insert(allNodes.end(), r.nodes.begin(), r.nodes.end());
         allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
@@ -486,6 +488,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     sc.root_opaque = roots[0];
     sc.root_masked = roots[1];
     sc.root_blend = roots[2];
+    sc.opaque_nodes = opaqueNodes;
     sc.texture_count = static_cast<int32_t>(s->texture_count);
     sc.indices = ctx->indices.as<uint32_t>();
     sc.vertices = ctx->vertices.as<float>();

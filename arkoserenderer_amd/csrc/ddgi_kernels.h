@@ -12,6 +12,7 @@ namespace ark {
 
 constexpr int kStackLds = 8;       // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
 constexpr int kTraceBlock = 256;
+constexpr int kLdsNodes = 128;    // top BVH8 nodes of the opaque class cached in LDS per traversal workgroup (10 KB)
 constexpr int kShadeBlock = 256;
 constexpr int kUpdateBlock = 320;  // 4 waves visibility (16x16 texels) + 1 wave irradiance (8x8)
 constexpr int kRayParts = 8;          // per-XCD ray partitions (one head counter each)
@@ -55,6 +56,7 @@ struct SceneArgs {
     int32_t root_opaque; // -1 = no geometry of that hit-mask class
     int32_t root_masked;
     int32_t root_blend;
+    uint32_t opaque_nodes; // node count of the opaque class (breadth-first from root_opaque)
     int32_t texture_count;
     const uint32_t* indices;
     const float* vertices; // RTVertex, 9 floats (36 B) each

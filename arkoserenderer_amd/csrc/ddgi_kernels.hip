@@ -383,8 +383,30 @@ struct Fetch {
     bool isTri;
 };
 
+// The first kLdsNodes nodes of the opaque BVH (its top levels: nodes are laid out
+// breadth first) copied into LDS once per workgroup: every ray starts there, so
+// those fetches skip the vector-memory path.
+struct NodeCache {
+    const uint4* lds; // [count][5]
+    uint32_t base;    // node index of lds[0]
+    uint32_t count;
+};
+
 template<int BLOCK>
-__device__ __forceinline__ void travFetch(const SceneArgs& sc, TravState& ts, Stack<BLOCK>& st, uint32_t oct, Fetch& fx)
+__device__ __forceinline__ NodeCache loadNodeCache(const SceneArgs& sc, uint4* lds)
+{
+    NodeCache nc { lds, sc.root_opaque >= 0 ? static_cast<uint32_t>(sc.root_opaque) : 0u, 0u };
+    if (sc.root_opaque >= 0) {
+        nc.count = min(static_cast<uint32_t>(kLdsNodes), sc.opaque_nodes);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.nodes + nc.base);
+        for (uint32_t i = threadIdx.x; i < nc.count * 5u; i += BLOCK) lds[i] = src[i];
+    }
+    __syncthreads();
+    return nc;
+}
+
+template<int BLOCK>
+__device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& nc, TravState& ts, Stack<BLOCK>& st, uint32_t oct, Fetch& fx)
 {
     fx.isTri = ts.tBits != 0;
     const uint4* src;
@@ -397,6 +419,16 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, TravState& ts, St
         const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
         if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
         src = reinterpret_cast<const uint4*>(sc.nodes + child);
+    }
+    const uint32_t rel = static_cast<uint32_t>(reinterpret_cast<const GpuBvh8Node*>(src) - sc.nodes) - nc.base;
+    if (!fx.isTri && rel < nc.count) {
+        const uint4* l = nc.lds + rel * 5u;
+        fx.w0 = l[0];
+        fx.w1 = l[1];
+        fx.w2 = l[2];
+        fx.w3 = l[3];
+        fx.w4 = l[4];
+        return;
     }
     fx.w0 = src[0];
     fx.w1 = src[1];
@@ -427,48 +459,6 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
     cNodes++;
     visitNode8(fx.w0, fx.w1, fx.w2, fx.w3, fx.w4, o, idir, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
     return false;
-}
-
-// Closest-hit (ANY=false) or first-hit (ANY=true) traversal of one BVH8 root.
-// Box tests keep a relative margin on top of the build-time inflation, so an
-// exact triangle hit is never culled; the closest hit is order-independent
-// (ties broken on instance, primitive).
-template<bool ANY, bool ALPHA, bool COUNT, int BLOCK>
-__device__ bool traverse(const SceneArgs& sc, int32_t root, V3 o, V3 d, float tmin, RayHit& h, Stack<BLOCK>& st, uint32_t& cNodes, uint32_t& cTris)
-{
-    if (root < 0) return false;
-    const V3 idir = safeInv(d);
-    const uint32_t oct = rayOctant(idir);
-    TravState ts { static_cast<uint32_t>(root), rootGroupBits(), 0u, 0u };
-    st.depth = 0;
-    uint32_t n = 0, t = 0;
-    while (!travDone(ts, st)) {
-        Fetch fx;
-        travFetch(sc, ts, st, oct, fx);
-        uint32_t inst, prim;
-        float tt, uu, vv;
-        bool bf;
-        if (!travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, n, t)) continue;
-        const uint32_t i = fx.i;
-        if (ANY) {
-            h.tri = i;
-            break;
-        }
-        if (h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) continue;
-        if (ALPHA && !alphaAccept(sc, inst, prim, uu, vv)) continue;
-        h.t = tt;
-        h.u = uu;
-        h.v = vv;
-        h.tri = i;
-        h.inst = inst;
-        h.prim = prim;
-        h.backface = bf;
-    }
-    if (COUNT) {
-        cNodes += n;
-        cTris += t;
-    }
-    return h.tri != kNoHit;
 }
 
 // ---------------------------------------------------------------------------
@@ -542,6 +532,8 @@ template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
+    __shared__ uint4 ldsNodes[kLdsNodes * 5];
+    const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
@@ -614,7 +606,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             // ---- one step: a pending leaf triangle, or the next node --------------
             if (!travDone(ts, st)) {
                 Fetch fx;
-                travFetch(sc, ts, st, oct, fx);
+                travFetch(sc, nc, ts, st, oct, fx);
                 uint32_t inst, prim;
                 float tt, uu, vv;
                 bool bf;
@@ -1040,6 +1032,8 @@ template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
+    __shared__ uint4 ldsNodes[kLdsNodes * 5];
+    const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
     const uint32_t lane = threadIdx.x & 63u;
@@ -1114,7 +1108,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             bool occluded = false;
             if (!travDone(ts, st)) {
                 Fetch fx;
-                travFetch(sc, ts, st, oct, fx);
+                travFetch(sc, nc, ts, st, oct, fx);
                 uint32_t inst, prim;
                 float tt, uu, vv;
                 bool bf;
