@@ -77,6 +77,9 @@ struct SceneArgs {
     {
         return (idx >= 0 && idx < texture_count) ? idx : white_texture;
     }
+    // Bilinear sample of a material/environment/IES texture; the 1x1 white default
+    // filters to exactly (1, 1, 1, 1) for finite coordinates, so it is not fetched.
+    __device__ __forceinline__ float4 sample(int idx, float u, float v) const;
 };
 
 // Per-update arguments (push constants of DDGINode.cpp:193-292 + resources).

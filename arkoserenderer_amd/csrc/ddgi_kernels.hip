@@ -28,6 +28,14 @@
 #include "ddgi_kernels.h"
 
 namespace ark {
+
+__device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) const
+{
+    const int r = resolveTexture(idx);
+    if (r == white_texture && fabsf(u) < INFINITY && fabsf(v) < INFINITY) return make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    return dev::sampleTexture(tex_infos, texels, r, u, v);
+}
+
 namespace dev {
 
 typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
@@ -245,7 +253,7 @@ __device__ bool alphaAccept(const SceneArgs& sc, uint32_t inst, uint32_t prim, f
     }
     float uvx = uv[0][0] * bx + uv[0][1] * by + uv[0][2] * bz;
     float uvy = uv[1][0] * bx + uv[1][1] * by + uv[1][2] * bz;
-    float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
+    float4 c = sc.sample(mat.base_color, uvx, uvy);
     return !(c.w < mat.mask_cutoff);
 }
 
@@ -701,24 +709,49 @@ __device__ __forceinline__ void sampleAtlas(const uint16_t* __restrict__ atlas, 
     int xa = min(max(x0, 0), W - 1), xb = min(max(x0 + 1, 0), W - 1);
     int ya = min(max(y0, 0), H - 1), yb = min(max(y0 + 1, 0), H - 1);
     uint16_t q[4][CH];
-    auto load = [&](int k, int xx, int yy) {
-        const uint16_t* p = atlas + (static_cast<size_t>(yy) * W + xx) * CH;
+    // one load per texel row when the two texels are adjacent (xb = xa + 1, i.e. not
+    // clamped at the atlas edge): 16 B for RGBA16F, 8 B for RG16F, at the texel's
+    // own (8 B / 4 B) alignment - the device handles the misaligned wide load
+    // (tools/probe/unaligned_load.hip)
+    auto loadRow = [&](int k, int yy) {
+        const uint16_t* pa = atlas + (static_cast<size_t>(yy) * W + xa) * CH;
+        const uint16_t* pb = atlas + (static_cast<size_t>(yy) * W + xb) * CH;
         if (CH == 4) {
-            uint2 w = *reinterpret_cast<const uint2*>(p);
-            q[k][0] = static_cast<uint16_t>(w.x & 0xffffu);
-            q[k][1] = static_cast<uint16_t>(w.x >> 16);
-            q[k][2 % CH] = static_cast<uint16_t>(w.y & 0xffffu);
-            q[k][3 % CH] = static_cast<uint16_t>(w.y >> 16);
+            uint2 wa, wb;
+            if (xb == xa + 1) {
+                const uint4 w = *reinterpret_cast<const uint4*>(pa);
+                wa = make_uint2(w.x, w.y);
+                wb = make_uint2(w.z, w.w);
+            } else {
+                wa = *reinterpret_cast<const uint2*>(pa);
+                wb = *reinterpret_cast<const uint2*>(pb);
+            }
+            q[k][0] = static_cast<uint16_t>(wa.x & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(wa.x >> 16);
+            q[k][2 % CH] = static_cast<uint16_t>(wa.y & 0xffffu);
+            q[k][3 % CH] = static_cast<uint16_t>(wa.y >> 16);
+            q[k + 1][0] = static_cast<uint16_t>(wb.x & 0xffffu);
+            q[k + 1][1] = static_cast<uint16_t>(wb.x >> 16);
+            q[k + 1][2 % CH] = static_cast<uint16_t>(wb.y & 0xffffu);
+            q[k + 1][3 % CH] = static_cast<uint16_t>(wb.y >> 16);
         } else {
-            uint32_t w = *reinterpret_cast<const uint32_t*>(p);
-            q[k][0] = static_cast<uint16_t>(w & 0xffffu);
-            q[k][1] = static_cast<uint16_t>(w >> 16);
+            uint32_t wa, wb;
+            if (xb == xa + 1) {
+                const uint2 w = *reinterpret_cast<const uint2*>(pa);
+                wa = w.x;
+                wb = w.y;
+            } else {
+                wa = *reinterpret_cast<const uint32_t*>(pa);
+                wb = *reinterpret_cast<const uint32_t*>(pb);
+            }
+            q[k][0] = static_cast<uint16_t>(wa & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(wa >> 16);
+            q[k + 1][0] = static_cast<uint16_t>(wb & 0xffffu);
+            q[k + 1][1] = static_cast<uint16_t>(wb >> 16);
         }
     };
-    load(0, xa, ya);
-    load(1, xb, ya);
-    load(2, xa, yb);
-    load(3, xb, yb);
+    loadRow(0, ya); // q[0] = (xa, ya), q[1] = (xb, ya)
+    loadRow(2, yb); // q[2] = (xa, yb), q[3] = (xb, yb)
     for (int c = 0; c < NOUT; ++c) {
         float t00 = f16_to_f32(q[0][c]), t10 = f16_to_f32(q[1][c]);
         float t01 = f16_to_f32(q[2][c]), t11 = f16_to_f32(q[3][c]);
@@ -883,7 +916,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                 rayOf(f, ray, &origin, &dir);
                 float u, v;
                 sphericalUvFromDirection(dir, &u, &v);
-                float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.env_texture, u, v);
+                float4 c = sc.sample(sc.env_texture, u, v);
                 storeSurfel(f, ray, f.environment_multiplier * v3(c.x, c.y, c.z), f.z_far);
             } else if (hit.t < 0.0f) {
                 // backface: colour 0, depth x 0.2 (raygen.rgen:208-213); the closest-hit
@@ -930,11 +963,11 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                 N = normalize(Nw);
                 const float uvx = vx[0][0] * bx + vx[1][0] * by + vx[2][0] * bz;
                 const float uvy = vx[0][1] * bx + vx[1][1] * by + vx[2][1] * bz;
-                float4 c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.base_color), uvx, uvy);
+                float4 c = sc.sample(mat.base_color, uvx, uvy);
                 baseColor = v3(c.x, c.y, c.z) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
-                c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.emissive), uvx, uvy);
+                c = sc.sample(mat.emissive, uvx, uvy);
                 const V3 emissive = v3(c.x, c.y, c.z) * v3(mat.emissive_factor[0], mat.emissive_factor[1], mat.emissive_factor[2]);
-                c = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(mat.metallic_roughness), uvx, uvy);
+                c = sc.sample(mat.metallic_roughness, uvx, uvy);
                 metallic = c.z * mat.metallic_factor;
                 roughness = c.y * mat.roughness_factor;
                 clearcoat = mat.clearcoat;
@@ -994,7 +1027,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                             float angleH = atan2f_(hy, hx) + kPi;
                             float lx = acosf_(angleV) / (2.0f * sl.position[3]);
                             float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
-                            iesValue = sampleTexture(sc.tex_infos, sc.texels, sc.resolveTexture(sl.ies_texture), lx, ly).x;
+                            iesValue = sc.sample(sl.ies_texture, lx, ly).x;
                         }
                         V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
                         V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
@@ -1464,7 +1497,7 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
 
 // Occupancy variant of the trace kernel (minimum waves per SIMD the register
 // allocation must allow): 6 by default (80 VGPRs, no spill; 3.43 vs 3.61 ms at the
-// compiler's 5 on C4; 8 spills and takes 5.4 ms), ARK_TRACE_WPE = 0 or 8 for tuning.
+// compiler's 5 on C4; 8 spilled and took 5.4 ms), ARK_TRACE_WPE = 0 or 5 for tuning.
 static int trace_variant()
 {
     static const int v = [] {
@@ -1492,7 +1525,6 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
     if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else if (v == 8) hipLaunchKernelGGL((dev::k_trace_primary<false, 8>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else hipLaunchKernelGGL((dev::k_trace_primary<false, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     return hipGetLastError();
 }
@@ -1547,7 +1579,6 @@ const void* kernel_trace_primary_ptr(bool count)
     if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1>);
     if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5>);
     if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6>);
-    if (v == 8) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 8>);
     return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1>);
 }
 const void* kernel_shade_ptr(bool count)
