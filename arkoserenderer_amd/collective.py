@@ -61,6 +61,39 @@ class SlabExchange:
             dist.all_gather_into_tensor(full, mine, group=self.group)
 
 
+class OverlappedSlabExchange:
+    """One rank's frame loop with the atlas all-gather of frame N on a side stream,
+    overlapped with frame N+1's probe-ray traversal (which reads only the scene,
+    the slot table and this rank's own probe offsets). Frame N+1's shading waits
+    for the all-gather (it samples the previous atlases at any probe); the
+    all-gather waits for frame N's probe update (ark_ddgi_update_overlapped)."""
+
+    def __init__(self, node, exchange, device):
+        import torch
+
+        self.node, self.exchange = node, exchange
+        self.comm = torch.cuda.Stream(device)
+        self.updated = torch.cuda.Event()
+        self.gathered = torch.cuda.Event()
+        # torch creates events lazily: record once so the raw handles exist
+        cur = torch.cuda.current_stream(device)
+        self.updated.record(cur)
+        self.gathered.record(cur)
+        self.pending = False
+
+    def step(self, app, stream_ptr: int):
+        import torch
+
+        wait = self.gathered.cuda_event if self.pending else None
+        p = self.node.execute_overlapped(app, stream_ptr, wait, self.updated.cuda_event)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.updated)
+            self.exchange()
+            self.gathered.record(self.comm)
+        self.pending = True
+        return p
+
+
 def slab_bands(total_bytes: int, world: int):
     """(offset, bytes) of every rank's band; used by the CPU (gloo) tests."""
     slab = total_bytes // world

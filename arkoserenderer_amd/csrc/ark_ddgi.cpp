@@ -538,7 +538,19 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
     return n;
 }
 
+static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
+
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
+{
+    return updateImpl(ctx, p, hipStream, nullptr, nullptr);
+}
+
+int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent)
+{
+    return updateImpl(ctx, p, hipStream, shadeWaitEvent, doneEvent);
+}
+
+static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!p || p->struct_size != sizeof(ArkDdgiFrameParams)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiFrameParams");
@@ -620,6 +632,9 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
     if (f.window_probes > 0) {
         ARK_HIP(launch_trace_primary(ctx->scene, f, ctx->traceBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
+        // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
+        // rank it waits here for the previous exchange (the traversal above did not)
+        if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (f.light_count > 0) {
@@ -628,12 +643,16 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
         ARK_HIP(launch_probe_update(f, s));
-    } else if (timing) {
-        ARK_HIP(hipEventRecord(ctx->ev[1], s));
-        ARK_HIP(hipEventRecord(ctx->ev[2], s));
-        ARK_HIP(hipEventRecord(ctx->ev[4], s));
+    } else {
+        if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+        if (timing) {
+            ARK_HIP(hipEventRecord(ctx->ev[1], s));
+            ARK_HIP(hipEventRecord(ctx->ev[2], s));
+            ARK_HIP(hipEventRecord(ctx->ev[4], s));
+        }
     }
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
+    if (doneEvent) ARK_HIP(hipEventRecord(static_cast<hipEvent_t>(doneEvent), s));
     ctx->timingValid = timing;
     ctx->countersPending = count;
     ctx->lastRays = f.window_rays;

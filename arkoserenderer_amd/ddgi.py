@@ -125,6 +125,13 @@ class DDGIContext:
     def update(self, params: abi.ArkDdgiFrameParams, stream: int | None = None):
         self.check(self.lib.ark_ddgi_update(self.h, C.byref(params), C.c_void_p(stream) if stream else None), "ark_ddgi_update")
 
+    def update_overlapped(self, params: abi.ArkDdgiFrameParams, stream: int | None, shade_wait_event: int | None,
+                          done_event: int | None):
+        """ark_ddgi_update_overlapped: raw hipStream_t / hipEvent_t handles (ints)."""
+        v = lambda x: C.c_void_p(x) if x else None  # noqa: E731
+        self.check(self.lib.ark_ddgi_update_overlapped(self.h, C.byref(params), v(stream), v(shade_wait_event), v(done_event)),
+                   "ark_ddgi_update_overlapped")
+
     def synchronize(self):
         self.check(self.lib.ark_ddgi_synchronize(self.h), "ark_ddgi_synchronize")
 
@@ -222,6 +229,16 @@ class DDGINode:
 
     def next_params(self, app: AppState) -> abi.ArkDdgiFrameParams:
         return frame_params(self.config, self.grid, app, self.probe_update_idx, **self.exposure)
+
+    def execute_overlapped(self, app: AppState, stream: int | None, shade_wait_event: int | None,
+                           done_event: int | None) -> abi.ArkDdgiFrameParams:
+        """execute() through ark_ddgi_update_overlapped (Z-slab ranks, see collective.py)."""
+        if self.ctx is None:
+            return None
+        p = self.next_params(app)
+        self.ctx.update_overlapped(p, stream, shade_wait_event, done_event)
+        self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
+        return p
 
     def execute(self, app: AppState, stream: int | None = None) -> abi.ArkDdgiFrameParams:
         if self.ctx is None:

@@ -92,16 +92,23 @@ def main():
     bvh = ctx.bvh_stats()
     stream = torch.cuda.current_stream(device)
     sptr = stream.cuda_stream
-    exch = SlabExchange.from_views(ctx.device_views(), rank, world, device) if world > 1 else None
+    # Z-slab ranks: the all-gather of frame N runs on a side stream, overlapped with
+    # frame N+1's primary traversal (collective.OverlappedSlabExchange)
+    exch = None
+    if world > 1:
+        from arkoserenderer_amd.collective import OverlappedSlabExchange
+
+        exch = OverlappedSlabExchange(node, SlabExchange.from_views(ctx.device_views(), rank, world, device).exchange, device)
     setup_s = time.time() - t_setup
 
     frame = 0
 
     def step():
         nonlocal frame
-        node.execute(D.AppState(frame), sptr)
         if exch is not None:
-            exch.exchange()
+            exch.step(D.AppState(frame), sptr)
+        else:
+            node.execute(D.AppState(frame), sptr)
         frame += 1
 
     for _ in range(args.warmup):

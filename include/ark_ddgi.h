@@ -268,6 +268,16 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
+/* ark_ddgi_update for a Z-slab rank that overlaps the atlas exchange with the next
+ * frame's primary traversal: the traversal is enqueued at once, the shading work
+ * (which samples the previous frame's atlases, raygen.rgen:173-185) first waits on
+ * hipEvent_t shade_wait_event (e.g. recorded after the previous all-gather; NULL =
+ * no wait), and hipEvent_t done_event (NULL = none) is recorded after the probe
+ * update so the caller's exchange can start from it. Same work and results as
+ * ark_ddgi_update (DDGINode.cpp:171-298). */
+int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream, void* shade_wait_event,
+                               void* done_event);
+
 /* Resource geometry and transfers (blocking, for tests / state save-load). */
 int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* out_bytes);
 int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);

@@ -1,0 +1,64 @@
+"""Per-rank cost of an S-way Z-slab run, measured on ONE GPU: a context that owns
+slab 0 of S (no exchange) runs the C4 workload; prints its ms/step next to the
+unsharded one. A proxy for strong-scaling headroom (the exchange is not included);
+the driver measures real N-GPU runs.
+
+    python tools/shard_proxy.py [--shards 2 4 8] [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--triangles", type=int, default=10_000_000)
+    args = ap.parse_args()
+    import torch
+
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    scene = S.soup(args.triangles)
+    G, R = 32, 256
+    grid = D.ProbeGrid((G, G, G), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    out = {}
+    for s in args.shards:
+        cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=G ** 3, max_rays_per_probe=R, max_probe_updates=G ** 3,
+                           compute_probe_offsets=True)
+        node = D.DDGINode(cfg)
+        assert node.construct(scene, grid, 10000.0, device=0, shard_rank=0, shard_count=s,
+                              light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+        sptr = torch.cuda.current_stream(dev).cuda_stream
+        for f in range(3):
+            node.execute(D.AppState(f), sptr)
+        node.ctx.set_timing(True)
+        node.execute(D.AppState(3), sptr)
+        kt = node.ctx.last_timings()
+        node.ctx.set_timing(False)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for f in range(args.steps):
+            node.execute(D.AppState(4 + f), sptr)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        out[s] = {"ms_per_step_rank0": round(ms, 4), "kernels_ms": [round(x, 4) for x in kt]}
+        print(json.dumps({"shards": s, **out[s]}), flush=True)
+        node.ctx.close()
+        del node
+    base = out.get(1, {}).get("ms_per_step_rank0")
+    if base:
+        print(json.dumps({"ideal_speedup_without_exchange": {s: round(base / v["ms_per_step_rank0"], 2) for s, v in out.items()}}))
+
+
+if __name__ == "__main__":
+    main()
