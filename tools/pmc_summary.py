@@ -10,6 +10,7 @@ raw and the corrected figure are kept). WRITE_SIZE x 1024 as is.
     python tools/pmc_summary.py gpurun_out/<tag> <tag> [--latest]
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -20,11 +21,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    for k in ("k_trace_primary<true>", "k_trace_primary<false>", "k_shade<true>", "k_shade<false>", "k_shadow", "k_probe_update",
-              "k_probe_slots_sharded", "k_probe_slots", "k_fill_u32", "k_shade_finish", "k_shade_surface"):
-        if k.split("<")[0] in name and (("<" not in k) or k in name):
-            return k.replace("<false>", "").replace("<true>", "_counting")
-    return name
+    """ark::dev::k_trace_primary<false, 6>(...) -> k_trace_primary; <true, ...> -> k_trace_primary_counting."""
+    m = re.search(r"\b(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
+    if not m:
+        return name
+    base = m.group(1)
+    return base + "_counting" if m.group(3) == "true" else base
 
 
 def main():
