@@ -14,7 +14,8 @@ constexpr int kStackLds = 8;       // traversal stack entries (node groups, 2 wo
 constexpr int kTraceBlock = 256;
 constexpr int kLdsNodes = 128;    // top BVH8 nodes of the opaque class cached in LDS per traversal workgroup (10 KB)
 constexpr int kShadeBlock = 256;
-constexpr int kUpdateBlock = 320;  // 4 waves visibility (16x16 texels) + 1 wave irradiance (8x8)
+constexpr int kUpdateProbes = 4;   // probes per probe-update workgroup
+constexpr int kUpdateBlock = 320;  // 4 visibility waves (one probe each) + 1 irradiance wave (4 probes)
 constexpr int kRayParts = 8;          // per-XCD ray partitions (one head counter each)
 constexpr int kRayCounterStride = 32; // u32 words between partition heads (128 B: one line each)
 constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in-block compaction)

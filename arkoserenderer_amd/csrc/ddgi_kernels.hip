@@ -13,10 +13,8 @@
 //                       rays (any-hit traversal), environment on miss
 //                       (raygen.rgen:149-158), indirect from the previous frame's
 //                       atlases (probeSampling.glsl:64-163) -> fp16 surfels.
-//   4. k_probe_update   one workgroup per probe: irradiance + visibility blend
-//                       (probeUpdateIrradiance.comp, probeUpdateVisibility.comp),
-//                       tile border copy (probeBorderCopy*.comp), probe offsets
-//                       (probeUpdateOffset.comp).
+//   4. k_probe_update   (ddgi_update.hip) irradiance + visibility blend,
+//                       tile border copy, probe offsets.
 // No MFMA: the path is traversal/gather, HBM/latency bound.
 
 #include <hip/hip_runtime.h>
@@ -1188,292 +1186,6 @@ __global__ void __launch_bounds__(256) k_shade_finish(FrameArgs f)
     }
 }
 
-// ---------------------------------------------------------------------------
-// 4. probe update: irradiance + visibility + borders + offsets, one WG per probe
-// ---------------------------------------------------------------------------
-// probeBorderCopyCorners.comp / probeBorderCopyEdges.comp for one tile of side
-// res+2, as a (dst <- src) map over the 4*res+4 border texels (tile-local).
-
-// powi_(x, N) on two lanes of a packed pair: the same binary-exponentiation
-// sequence of IEEE multiplies (ark_fmath.h), unrolled for a constant N.
-template<int N>
-__device__ __forceinline__ f2 powi2(f2 x)
-{
-    f2 result = { 1.0f, 1.0f }, base = x;
-    int n = N;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        if (n & 1) result = result * base;
-        n >>= 1;
-        if (n == 0) break;
-        base = base * base;
-    }
-    return result;
-}
-
-__device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, int* sx, int* sy)
-{
-    const int side = res + 2;
-    if (b < 4) { // corners (probeBorderCopyCorners.comp:20-51)
-        int cx = b & 1, cy = b >> 1;
-        int scx = (cx + 1) % 2, scy = (cy + 1) % 2;
-        *dx = cx * (side - 1);
-        *dy = cy * (side - 1);
-        *sx = scx * (side - 1) + (scx == 0 ? 1 : -1);
-        *sy = scy * (side - 1) + (scy == 0 ? 1 : -1);
-        return;
-    }
-    // edges (probeBorderCopyEdges.comp:20-56)
-    b -= 4;
-    const int sideIdx = b / res, step = b % res;
-    const int cornerX[4] = { 0, 1, 1, 0 }, cornerY[4] = { 0, 0, 1, 1 };
-    const int stepX[4] = { 1, 0, -1, 0 }, stepY[4] = { 0, 1, 0, -1 };
-    const int inIdx = (sideIdx + 1) % 4;
-    int cX = cornerX[sideIdx] * (side - 1), cY = cornerY[sideIdx] * (side - 1);
-    *dx = cX + (step + 1) * stepX[sideIdx];
-    *dy = cY + (step + 1) * stepY[sideIdx];
-    *sx = (cX + stepX[inIdx]) + (res - step) * stepX[sideIdx];
-    *sy = (cY + stepY[inIdx]) + (res - step) * stepY[sideIdx];
-}
-
-__global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
-{
-    constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
-    __shared__ __attribute__((aligned(16))) float sDir[3][ARK_DDGI_MAX_RAYS_PER_PROBE];
-    __shared__ __attribute__((aligned(16))) float4 sRad[ARK_DDGI_MAX_RAYS_PER_PROBE]; // surfel radiance (fp16 -> fp32) + signed depth
-    __shared__ __attribute__((aligned(16))) float2 sDist[ARK_DDGI_MAX_RAYS_PER_PROBE]; // (d, d^2), d = min(|surfel.a|, 1.5 * gridMaxSpacing)
-    __shared__ uint2 sIrrTile[(IR + 2) * (IR + 2)];
-    __shared__ uint32_t sVisTile[(VR + 2) * (VR + 2)];
-    __shared__ uint8_t sClass[ARK_DDGI_MAX_RAYS_PER_PROBE]; // offsets: 1 near front face, 2 back face, 0 other
-    const uint32_t slot = blockIdx.x;
-    if (slot >= f.window_probes) return;
-    const GpuProbeSlot ps = f.slots[slot];
-    const uint32_t probeIdx = ps.probe_index;
-    const uint32_t R = f.R;
-    const int tid = threadIdx.x;
-    const V3 axis = v3(ps.axis[0], ps.axis[1], ps.axis[2]);
-    for (uint32_t s = tid; s < R; s += kUpdateBlock) {
-        float4 fb = f.fib[s];
-        V3 d = rotate(v3(fb.x, fb.y, fb.z), axis, ps.angle_sin, ps.angle_cos);
-        sDir[0][s] = d.x;
-        sDir[1][s] = d.y;
-        sDir[2][s] = d.z;
-        const uint2 sv = reinterpret_cast<const uint2*>(f.surfels)[static_cast<size_t>(slot) * f.Rmax + s];
-        sRad[s] = make_float4(f16_to_f32(static_cast<uint16_t>(sv.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.x >> 16)),
-                              f16_to_f32(static_cast<uint16_t>(sv.y & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.y >> 16)));
-        // probeUpdateVisibility.comp:45-48 (per ray; identical for every texel)
-        const float gridMaxSpacing = fmaxf_(f.spacing[0], fmaxf_(f.spacing[1], f.spacing[2]));
-        const float maxDistance = 1.5f * gridMaxSpacing;
-        float dd = f16_to_f32(static_cast<uint16_t>(sv.y >> 16));
-        dd = fminf_(fabsf_(dd), maxDistance);
-        sDist[s] = make_float2(dd, square(dd));
-    }
-    __syncthreads();
-    // tile origin (ddgi/common.glsl:53-67)
-    const uint32_t tilesPerSheet = static_cast<uint32_t>(f.X * f.Z);
-    const uint32_t sheetProbeIdx = probeIdx % tilesPerSheet;
-    const int py = static_cast<int>(probeIdx / tilesPerSheet);
-    const int px = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(f.X));
-    const int pz = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X));
-    const int tileX = px + py * f.X, tileY = pz;
-    const float epsilon = 1e-9f * static_cast<float>(R);
-    if (tid < VR * VR) {
-        // probeUpdateVisibility.comp:24-63
-        // each wave owns an 8x8 block of the octahedral tile (a compact cone of
-        // directions), so a ray that is behind all 64 texels skips the pow for the wave
-        const int wv = tid >> 6, ln = tid & 63;
-        const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
-        float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(VR);
-        float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(VR);
-        const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
-        const float sharp = f.visibility_sharpness;
-        float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
-        if (sharp == 50.0f && (R & 1u) == 0) {
-            // default sharpness, two rays per iteration in packed fp32 (v_pk_mul/add):
-            // every product and sum is the same IEEE operation as the scalar loop
-            // below, and each sum still runs over the rays in order. weight =
-            // powi(max(0, d), 50) needs no select: powi(+0, 50) = +0 = pow(0, 50).
-            // (nv0, nv1) accumulate as one packed pair.
-            f2 nv = { 0.0f, 0.0f };
-            totalWeight = 0.0f;
-            for (uint32_t s = 0; s < R; s += 2) {
-                const f2 rx = *reinterpret_cast<const f2*>(&sDir[0][s]);
-                const f2 ry = *reinterpret_cast<const f2*>(&sDir[1][s]);
-                const f2 rz = *reinterpret_cast<const f2*>(&sDir[2][s]);
-                const f2 dp = (texelDirection.x * rx + texelDirection.y * ry) + texelDirection.z * rz;
-                const f2 x = { fmaxf_(0.0f, dp.x), fmaxf_(0.0f, dp.y) };
-                const f2 weight = powi2<50>(x);
-                const float4 dd = *reinterpret_cast<const float4*>(&sDist[s]); // (d0, d0^2, d1, d1^2)
-                nv += f2 { weight.x, weight.x } * f2 { dd.x, dd.y };
-                nv += f2 { weight.y, weight.y } * f2 { dd.z, dd.w };
-                totalWeight += weight.x;
-                totalWeight += weight.y;
-            }
-            nv0 = nv.x;
-            nv1 = nv.y;
-        } else if (is_small_int_(sharp)) {
-            // weight = pow(max(0, d), sharp) with an integral sharpness:
-            // powf_ == powi_ for x > 0 and pow(0, s) = +0, so a select replaces the branches
-            const int ns = static_cast<int>(sharp);
-            for (uint32_t s = 0; s < R; ++s) {
-                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-                const float x = fmaxf_(0.0f, dot(texelDirection, rd));
-                const float weight = x > 0.0f ? powi_(x, ns) : 0.0f;
-                const float2 dd = sDist[s];
-                nv0 += weight * dd.x;
-                nv1 += weight * dd.y;
-                totalWeight += weight;
-            }
-        } else if (sharp > 0.0f && sharp <= 64.0f && !is_root_exp_(sharp)) {
-            // non-integral sharpness: powf_pos_ == powf_ bit for bit on (0, 1+eps]
-            for (uint32_t s = 0; s < R; ++s) {
-                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-                const float x = fmaxf_(0.0f, dot(texelDirection, rd));
-                const float weight = x > 0.0f ? powf_pos_(x, sharp) : 0.0f;
-                const float2 dd = sDist[s];
-                nv0 += weight * dd.x;
-                nv1 += weight * dd.y;
-                totalWeight += weight;
-            }
-        } else {
-            for (uint32_t s = 0; s < R; ++s) {
-                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-                const float weight = powf_(fmaxf_(0.0f, dot(texelDirection, rd)), sharp);
-                const float2 dd = sDist[s];
-                nv0 += weight * dd.x;
-                nv1 += weight * dd.y;
-                totalWeight += weight;
-            }
-        }
-        float den = fmaxf_(totalWeight, epsilon);
-        nv0 = nv0 / den;
-        nv1 = nv1 / den;
-        const int ax = 1 + tileX * (VR + 2) + tx, ay = 1 + tileY * (VR + 2) + ty;
-        uint32_t* t = reinterpret_cast<uint32_t*>(f.vis) + static_cast<size_t>(ay) * f.Wv + ax;
-        uint32_t old = *t;
-        nv0 = mixf(nv0, f16_to_f32(static_cast<uint16_t>(old & 0xffffu)), f.hysteresis_visibility);
-        nv1 = mixf(nv1, f16_to_f32(static_cast<uint16_t>(old >> 16)), f.hysteresis_visibility);
-        uint32_t nw = static_cast<uint32_t>(f32_to_f16(nv0)) | (static_cast<uint32_t>(f32_to_f16(nv1)) << 16);
-        *t = nw;
-        sVisTile[(ty + 1) * (VR + 2) + tx + 1] = nw;
-    } else {
-        const int i = tid - VR * VR;
-        if (i < IR * IR) {
-            // probeUpdateIrradiance.comp:22-79
-            const int tx = i % IR, ty = i / IR;
-            float uvx = (static_cast<float>(tx) + 0.5f) / static_cast<float>(IR);
-            float uvy = (static_cast<float>(ty) + 0.5f) / static_cast<float>(IR);
-            const V3 texelDirection = octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
-            V3 newIrr = splat(0.0f);
-            float totalWeight = 0.0f;
-            uint32_t s = 0;
-            if ((R & 1u) == 0) {
-                // two rays per iteration; (r, g) as one packed pair, every sum in ray order
-                f2 rg = { 0.0f, 0.0f };
-                float b = 0.0f;
-                for (; s < R; s += 2) {
-                    const f2 rx = *reinterpret_cast<const f2*>(&sDir[0][s]);
-                    const f2 ry = *reinterpret_cast<const f2*>(&sDir[1][s]);
-                    const f2 rz = *reinterpret_cast<const f2*>(&sDir[2][s]);
-                    const f2 dp = (texelDirection.x * rx + texelDirection.y * ry) + texelDirection.z * rz;
-                    const float w0 = fmaxf_(0.0f, dp.x), w1 = fmaxf_(0.0f, dp.y);
-                    const float4 r0 = sRad[s], r1 = sRad[s + 1];
-                    rg += f2 { w0, w0 } * f2 { r0.x, r0.y };
-                    b += w0 * r0.z;
-                    rg += f2 { w1, w1 } * f2 { r1.x, r1.y };
-                    b += w1 * r1.z;
-                    totalWeight += w0;
-                    totalWeight += w1;
-                }
-                newIrr = v3(rg.x, rg.y, b);
-            }
-            for (; s < R; ++s) {
-                V3 rd = v3(sDir[0][s], sDir[1][s], sDir[2][s]);
-                float weight = fmaxf_(0.0f, dot(texelDirection, rd));
-                const float4 r = sRad[s];
-                newIrr = newIrr + weight * v3(r.x, r.y, r.z);
-                totalWeight += weight;
-            }
-            newIrr = newIrr / fmaxf_(totalWeight, epsilon);
-            newIrr = pow3(newIrr, 1.0f / 5.0f);
-            const int ax = 1 + tileX * (IR + 2) + tx, ay = 1 + tileY * (IR + 2) + ty;
-            uint2* t = reinterpret_cast<uint2*>(f.irr) + static_cast<size_t>(ay) * f.Wi + ax;
-            uint2 old = *t;
-            V3 o = v3(f16_to_f32(static_cast<uint16_t>(old.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(old.x >> 16)),
-                      f16_to_f32(static_cast<uint16_t>(old.y & 0xffffu)));
-            newIrr = mix3(newIrr, o, f.hysteresis_irradiance);
-            uint2 nw;
-            nw.x = static_cast<uint32_t>(f32_to_f16(newIrr.x)) | (static_cast<uint32_t>(f32_to_f16(newIrr.y)) << 16);
-            nw.y = static_cast<uint32_t>(f32_to_f16(newIrr.z)) | (static_cast<uint32_t>(f32_to_f16(0.0f)) << 16);
-            *t = nw;
-            sIrrTile[(ty + 1) * (IR + 2) + tx + 1] = nw;
-        }
-        // probe offsets (probeUpdateOffset.comp:27-96; full-barrier semantics) in the
-        // irradiance wave, overlapped with the (longer) visibility waves: the rays are
-        // classified in parallel (counts by ballot), then six lanes each run one of
-        // the two direction sums' components over the rays in order (adding +0 for
-        // rays of the other classes leaves a sum unchanged), and one lane finishes.
-        if (f.update_offsets) {
-            const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
-            const float maxOffset = minAxialSpacing / 2.0f;
-            uint32_t backfaceCount = 0, nearFrontfaceCount = 0;
-            for (uint32_t s0 = 0; s0 < R; s0 += 64) {
-                const uint32_t s = s0 + static_cast<uint32_t>(i);
-                uint32_t cls = 0;
-                if (s < R) {
-                    const float a = sRad[s].w;
-                    cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
-                    sClass[s] = static_cast<uint8_t>(cls);
-                }
-                nearFrontfaceCount += static_cast<uint32_t>(__popcll(__ballot(cls == 1u)));
-                backfaceCount += static_cast<uint32_t>(__popcll(__ballot(cls == 2u)));
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            float acc = 0.0f;
-            if (i < 6) {
-                const float* dirc = sDir[i % 3];
-                const uint32_t want = i < 3 ? 1u : 2u;
-                for (uint32_t s = 0; s < R; ++s) acc += sClass[s] == want ? dirc[s] : 0.0f;
-            }
-            const V3 accumNearFrontfaceDir = v3(__shfl(acc, 0), __shfl(acc, 1), __shfl(acc, 2));
-            const V3 accumBackfaceDir = v3(__shfl(acc, 3), __shfl(acc, 4), __shfl(acc, 5));
-            if (i == 0) {
-                float4 cur = f.offsets[probeIdx];
-                V3 currentOffset = v3(cur.x, cur.y, cur.z);
-                V3 offset = splat(0.0f);
-                const float stepSize = 0.125f, lerpSpeed = 10.0f;
-                if (static_cast<float>(backfaceCount) / static_cast<float>(R) >= 0.25f)
-                    offset = offset + normalize(accumBackfaceDir) * stepSize;
-                else if (nearFrontfaceCount >= 1)
-                    offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
-                else
-                    offset = offset - currentOffset * stepSize;
-                V3 newOffset = currentOffset + offset;
-                if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-                newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
-                f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
-            }
-        }
-    }
-    __syncthreads();
-    // Border texels of this (updated) tile. Tiles not updated this frame already
-    // hold border == f(interior) since their last update (or the uniform clear), so
-    // copying borders of updated tiles only equals the reference's all-tile pass.
-    if (tid < 4 * VR + 4) {
-        int dx, dy, sx, sy;
-        borderSource(VR, tid, &dx, &dy, &sx, &sy);
-        uint32_t val = sVisTile[sy * (VR + 2) + sx];
-        reinterpret_cast<uint32_t*>(f.vis)[static_cast<size_t>(tileY * (VR + 2) + dy) * f.Wv + tileX * (VR + 2) + dx] = val;
-    } else if (tid - (4 * VR + 4) < 4 * IR + 4) {
-        int dx, dy, sx, sy;
-        borderSource(IR, tid - (4 * VR + 4), &dx, &dy, &sx, &sy);
-        uint2 val = sIrrTile[sy * (IR + 2) + sx];
-        reinterpret_cast<uint2*>(f.irr)[static_cast<size_t>(tileY * (IR + 2) + dy) * f.Wi + tileX * (IR + 2) + dx] = val;
-    }
-}
-
 // Atlas clears (DDGINode.cpp:89-94) as 32-bit fills.
 __global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t value)
 {
@@ -1554,13 +1266,6 @@ hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t
 hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s)
 {
     hipLaunchKernelGGL(dev::k_shade_finish, dim3(2048), dim3(256), 0, s, f);
-    return hipGetLastError();
-}
-
-hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s)
-{
-    if (f.window_probes == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_probe_update, dim3(f.window_probes), dim3(kUpdateBlock), 0, s, f);
     return hipGetLastError();
 }
 

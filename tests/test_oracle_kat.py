@@ -241,3 +241,33 @@ def test_hysteresis_blend():
     orc.update(D.frame_params(cfg, grid, D.AppState(1), 0, environment_brightness=0.0))
     b = O.f16_to_f32(orc.read(abi.ARK_DDGI_ATLAS_IRRADIANCE)).reshape(10, 10, 4)[5, 5, 0]
     assert a == np.float32(np.float16(1.0)) and abs(b - 0.93 * a) < 1e-3
+
+
+def test_octahedral_texel_orbits_are_exact():
+    """The probe-update kernel (csrc/ddgi_update.hip) evaluates each orbit
+    {t, x-mirror t', antipode -t, -t'} of tile texels from one decoded direction:
+    the quadrant texel (qx, qy) has the orbit (res-1-qx, qy), (qy+h, qx+h),
+    (h-1-qy, qx+h), h = res/2. Pin that the decoded directions are exact sign
+    flips of each other (z = 0 texels: the antipode's z is +0 as well) and that
+    the orbits partition the tile."""
+    lib = O.load()
+
+    def dec(res, tx, ty):
+        d = np.zeros(3, np.float32)
+        lib.oracle_oct_decode(np.float32((tx + 0.5) / res * 2 - 1), np.float32((ty + 0.5) / res * 2 - 1), d.ctypes.data)
+        return d
+
+    for res in (8, 16):
+        h = res // 2
+        seen = set()
+        for qy in range(h):
+            for qx in range(h):
+                orbit = [(qx, qy), (res - 1 - qx, qy), (qy + h, qx + h), (h - 1 - qy, qx + h)]
+                seen.update(orbit)
+                t, tm, ta, tam = (dec(res, *o) for o in orbit)
+                assert np.array_equal(tm.view(np.uint32), np.array([-t[0], t[1], t[2]], np.float32).view(np.uint32))
+                want_a = np.array([-t[0], -t[1], -t[2] if t[2] != 0 else 0.0], np.float32)
+                want_am = np.array([t[0], -t[1], -t[2] if t[2] != 0 else 0.0], np.float32)
+                assert np.array_equal(ta.view(np.uint32), want_a.view(np.uint32))
+                assert np.array_equal(tam.view(np.uint32), want_am.view(np.uint32))
+        assert len(seen) == res * res
