@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libark_ddgi.so")
+LIB_PATH = os.environ.get("ARK_DDGI_LIB") or os.path.join(_HERE, "lib", "libark_ddgi.so")  # override: tuning builds
 
 ARK_DDGI_IRRADIANCE_RES = 8
 ARK_DDGI_VISIBILITY_RES = 16
@@ -193,7 +193,7 @@ class ArkDdgiCounters(C.Structure):
         ("shadow_rays", C.c_uint64),
         ("shadow_node_visits", C.c_uint64),
         ("shadow_tri_tests", C.c_uint64),
-        ("reserved", C.c_uint64),
+        ("primary_wave_steps", C.c_uint64),
     ]
 
 

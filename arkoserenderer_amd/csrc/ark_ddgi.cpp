@@ -109,9 +109,10 @@ struct ArkDdgiCtx {
     // persistent resources
     DeviceBuffer irr, vis, offsets;
     // working set
-    DeviceBuffer slots, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork;
+    DeviceBuffer slots, slotOrder, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork;
     std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
     uint32_t orderR = 0;
+    int64_t slotOrderKey = -1; // (first, K) the slot order table was built for
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0;
@@ -253,6 +254,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->vis.alloc(static_cast<size_t>(ctx->Wv) * ctx->Hv * 4)) != hipSuccess) return bad(e, "alloc visibility");
     if ((e = ctx->offsets.alloc(static_cast<size_t>(ctx->N) * 16)) != hipSuccess) return bad(e, "alloc offsets");
     if ((e = ctx->slots.alloc(K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
+    if ((e = ctx->slotOrder.alloc(K * 4)) != hipSuccess) return bad(e, "alloc slot order");
     if ((e = ctx->fib.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib");
     if ((e = ctx->order.alloc(R * 4)) != hipSuccess) return bad(e, "alloc order");
     if ((e = ctx->fibOrder.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib order");
@@ -282,7 +284,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
@@ -362,6 +364,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     // host threads for the build: the box's CPU share per GPU is 16 cores
     opt.threads = 16;
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
+    // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
+    if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
     std::vector<GpuBvh8Node> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
@@ -629,6 +633,19 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, ctx->rayCounter.bytes, s));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
     ARK_HIP(launch_probe_slots(f, s));
+    {
+        // slot traversal order (k_slot_order): rebuilt when the window moves
+        static const bool useOrder = [] { const char* e = std::getenv("ARK_SLOT_ORDER"); return !(e && e[0] == '0'); }();
+        f.slot_order = nullptr;
+        if (useOrder) {
+            const int64_t key = (static_cast<int64_t>(f.first) << 32) | K;
+            if (key != ctx->slotOrderKey) {
+                ARK_HIP(launch_slot_order(f, ctx->slotOrder.as<uint32_t>(), s));
+                ctx->slotOrderKey = key;
+            }
+            f.slot_order = ctx->slotOrder.as<uint32_t>();
+        }
+    }
     if (f.window_probes > 0) {
         ARK_HIP(launch_trace_primary(ctx->scene, f, ctx->traceBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
@@ -771,6 +788,7 @@ int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out)
         out->shadow_node_visits = c[4];
         out->shadow_tri_tests = c[5];
         out->front_hits = c[6];
+        out->primary_wave_steps = c[7];
     }
     return ARK_DDGI_OK;
 }

@@ -10,9 +10,15 @@
 
 namespace ark {
 
-constexpr int kStackLds = 8;       // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
+#ifndef ARK_STACK_LDS
+#define ARK_STACK_LDS 8
+#endif
+#ifndef ARK_LDS_NODES
+#define ARK_LDS_NODES 128
+#endif
+constexpr int kStackLds = ARK_STACK_LDS; // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
 constexpr int kTraceBlock = 256;
-constexpr int kLdsNodes = 128;    // top BVH8 nodes of the opaque class cached in LDS per traversal workgroup (10 KB)
+constexpr int kLdsNodes = ARK_LDS_NODES; // top BVH8 nodes of the opaque class cached in LDS per traversal workgroup (80 B each)
 constexpr int kShadeBlock = 256;
 constexpr int kUpdateProbes = 4;   // probes per probe-update workgroup
 constexpr int kUpdateBlock = 320;  // 4 visibility waves (one probe each) + 1 irradiance wave (4 probes)
@@ -112,6 +118,7 @@ struct FrameArgs {
     GpuProbeSlot* slots;
     float4* fib;
     const uint32_t* order;   // traversal order of the R samples (lane -> sample), see sampleTraversalOrder
+    const uint32_t* slot_order; // traversal order of the window's slots (queue position -> slot), null = identity
     float4* fib_order;       // fib[order[j]] with w = order[j] (bits), j = traversal position
     GpuHit* hits;
     uint16_t* surfels;
@@ -129,6 +136,7 @@ struct FrameArgs {
 };
 
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
+hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);

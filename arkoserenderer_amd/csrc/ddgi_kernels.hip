@@ -144,6 +144,75 @@ __global__ void __launch_bounds__(1024) k_probe_slots_sharded(FrameArgs f)
     }
 }
 
+// Traversal order of the window's slots (one workgroup; a stable bucket sort).
+// The probes are cut into 8 blocks of the x-z plane (4 along x, 2 along z, or 8
+// along x for a one-layer slab) and each block's slots keep their window order,
+// whose slowest coordinate is y. The trace and shade queues hand the 8 per-XCD
+// partitions out in this order, so partition p sweeps block p bottom to top and
+// all XCDs work on the same few y-layers at any time: the chip-wide working set
+// of BVH nodes and triangles is one slice of the scene (Infinity Cache sized)
+// instead of eight. Only the order of work changes, never a result.
+__global__ void __launch_bounds__(1024) k_slot_order(FrameArgs f, uint32_t* __restrict__ order)
+{
+    __shared__ uint32_t waveCount[16][8];
+    __shared__ uint32_t bucketBase[8];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t n = f.window_probes;
+    const int zlo = f.sharded ? f.slab_z0 : 0, zhi = f.sharded ? f.slab_z1 : f.Z;
+    const int zext = max(1, zhi - zlo);
+    auto bucketOf = [&](uint32_t slot) -> uint32_t {
+        const uint32_t probeIdx = f.slots[slot].probe_index;
+        const uint32_t sheetProbeIdx = probeIdx % static_cast<uint32_t>(f.X * f.Z);
+        const int x = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(f.X));
+        const int z = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X)) - zlo;
+        if (zext >= 2) return static_cast<uint32_t>(x * 4 / f.X + 4 * min(1, z * 2 / zext));
+        return static_cast<uint32_t>(x * 8 / f.X);
+    };
+    if (threadIdx.x < 8) bucketBase[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < n; s += 1024u) atomicAdd(&bucketBase[bucketOf(s)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t c = bucketBase[b];
+            bucketBase[b] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += 1024u) {
+        const uint32_t s = c0 + threadIdx.x;
+        const bool valid = s < n;
+        const uint32_t b = valid ? bucketOf(s) : 8u;
+        uint32_t rank = 0;
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint64_t m = __ballot(b == k);
+            if (b == k) rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+            if (lane == 0) waveCount[wave][k] = static_cast<uint32_t>(__popcll(m));
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = bucketBase[b] + rank;
+            for (uint32_t w = 0; w < wave; ++w) pos += waveCount[w][b];
+            order[pos] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < 16; ++w) tot += waveCount[w][threadIdx.x];
+            bucketBase[threadIdx.x] += tot;
+        }
+        __syncthreads();
+    }
+}
+
+// queue position -> slot (identity without an order table)
+__device__ __forceinline__ uint32_t slotAt(const FrameArgs& f, uint32_t q)
+{
+    return f.slot_order ? f.slot_order[q] : q;
+}
+
 // ---------------------------------------------------------------------------
 // BVH traversal
 // ---------------------------------------------------------------------------
@@ -545,7 +614,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t lane = threadIdx.x & 63u;
     const float tmin = 0.0001f; // raygen.rgen:116
-    uint32_t cNodes = 0, cTris = 0, cHits = 0;
+    uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
     const uint32_t home = xccId();
@@ -580,8 +649,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 if (rank < avail) r = poolNext + rank;
                 else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
                 if (r != kNoHit) {
-                    const uint32_t slot = r / f.R;
-                    const float4 fv = f.fib_order[r - slot * f.R]; // (direction, sample index)
+                    const uint32_t q = r / f.R;
+                    const uint32_t slot = slotAt(f, q);
+                    const float4 fv = f.fib_order[r - q * f.R]; // (direction, sample index)
                     const GpuProbeSlot ps = f.slots[slot];
                     ray = slot * f.R + __float_as_uint(fv.w); // hit record index
                     o = { ps.pos[0], ps.pos[1], ps.pos[2] };
@@ -608,6 +678,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
         if (__ballot(active) == 0) break;
+        if (COUNT) cIter++;
         if (active) {
             // ---- one step: a pending leaf triangle, or the next node --------------
             if (!travDone(ts, st)) {
@@ -628,6 +699,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     h.backface = bf;
                 }
             }
+        }
+        if (active) {
             // ---- pass finished -----------------------------------------------------
             if (travDone(ts, st)) {
                 bool finished = true;
@@ -674,6 +747,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[2], static_cast<unsigned long long>(cHits));
+        if (lane == 0) atomicAdd(&f.counters[7], static_cast<unsigned long long>(cIter));
     }
 }
 
@@ -905,8 +979,9 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
         if (chunk >= chunkEnd) break;
         // ---- A. classify: misses and backfaces finish here ----------------------
         for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
-            const uint32_t ray = chunk + r;
-            if (ray >= chunkEnd) break;
+            if (chunk + r >= chunkEnd) break;
+            const uint32_t q = (chunk + r) / f.R;
+            const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
                 // miss (raygen.rgen:149-158)
@@ -1229,6 +1304,13 @@ static int shade_variant()
         return e ? std::atoi(e) : 4;
     }();
     return v;
+}
+
+hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
+{
+    if (f.window_probes == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_slot_order, dim3(1), dim3(1024), 0, s, f, order);
+    return hipGetLastError();
 }
 
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)

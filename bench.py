@@ -219,6 +219,7 @@ def main():
         "per_ray": {
             "primary_nodes": round(cnt.primary_node_visits / max(1, rays_rank), 2),
             "primary_tris": round(cnt.primary_tri_tests / max(1, rays_rank), 2),
+            "primary_lane_util": round((cnt.primary_node_visits + cnt.primary_tri_tests) / max(1, 64 * cnt.primary_wave_steps), 3),
             "hit_frac": round(cnt.hits / max(1, rays_rank), 4),
             "front_hit_frac": round(cnt.front_hits / max(1, rays_rank), 4),
             "shadow_rays": round(cnt.shadow_rays / max(1, rays_rank), 4),

@@ -236,7 +236,7 @@ typedef struct ArkDdgiCounters {
     uint64_t shadow_rays;         /* shadow rays traced */
     uint64_t shadow_node_visits;  /* BVH2 nodes fetched by shadow rays */
     uint64_t shadow_tri_tests;    /* triangle records fetched by shadow rays */
-    uint64_t reserved;
+    uint64_t primary_wave_steps;  /* wave iterations of the probe-ray traversal (lane utilisation = (node visits + tri tests) / (64 * this)) */
 } ArkDdgiCounters;
 
 /* Device-side views of the persistent resources, for an external collective
