@@ -20,6 +20,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
+
+#ifndef ARK_DDGI_GATHER_BATCH
+#define ARK_DDGI_GATHER_BATCH 1 // cage probes whose atlas taps are in flight together (sampleDDGI; 2 and 4 measured no faster on C4)
+#endif
 
 #include "../../include/ark_ddgi.h"
 #include "ddgi_device.h"
@@ -831,7 +836,77 @@ __device__ __forceinline__ void sampleAtlas(const uint16_t* __restrict__ atlas, 
     }
 }
 
-// probeSampling.glsl:64-163
+// One bilinear tap of an fp16 atlas, split into fetch and filter so that the taps of
+// several probes can be in flight at once. The two texels (xa, xb) of a row come
+// from one wide load at texel m = min(xa, W - 2) (xb is xa or xa + 1, both in
+// {m, m + 1}); `sel` says which half each one is. Same texels, weights and lerps as
+// sampleAtlas.
+template<int CH>
+struct AtlasTap {
+    using Row = typename std::conditional<CH == 4, uint4, uint2>::type;
+    Row r0, r1; // rows ya, yb: texels (m, m + 1)
+    float fx, fy;
+    uint32_t sel; // bit 0: texel a is m + 1, bit 1: texel b is m + 1
+};
+
+template<int CH>
+__device__ __forceinline__ AtlasTap<CH> atlasTap(const uint16_t* __restrict__ atlas, int W, int H, float u, float v)
+{
+    using Row = typename AtlasTap<CH>::Row;
+    AtlasTap<CH> t;
+    float x = u * static_cast<float>(W) - 0.5f;
+    float y = v * static_cast<float>(H) - 0.5f;
+    float x0f = floorf_(x), y0f = floorf_(y);
+    t.fx = x - x0f;
+    t.fy = y - y0f;
+    int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
+    int xa = min(max(x0, 0), W - 1), xb = min(max(x0 + 1, 0), W - 1);
+    int ya = min(max(y0, 0), H - 1), yb = min(max(y0 + 1, 0), H - 1);
+    const int m = min(xa, W - 2);
+    t.sel = (xa != m ? 1u : 0u) | (xb != m ? 2u : 0u);
+    t.r0 = *reinterpret_cast<const Row*>(atlas + (static_cast<size_t>(ya) * W + m) * CH);
+    t.r1 = *reinterpret_cast<const Row*>(atlas + (static_cast<size_t>(yb) * W + m) * CH);
+    return t;
+}
+
+template<int CH, int NOUT>
+__device__ __forceinline__ void atlasFilter(const AtlasTap<CH>& t, float* out)
+{
+    uint16_t q[4][CH];
+    auto split = [&](int k, const typename AtlasTap<CH>::Row& r) {
+        if constexpr (CH == 4) {
+            const uint2 lo = make_uint2(r.x, r.y), hi = make_uint2(r.z, r.w);
+            const uint2 wa = (t.sel & 1u) ? hi : lo, wb = (t.sel & 2u) ? hi : lo;
+            q[k][0] = static_cast<uint16_t>(wa.x & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(wa.x >> 16);
+            q[k][2] = static_cast<uint16_t>(wa.y & 0xffffu);
+            q[k][3] = static_cast<uint16_t>(wa.y >> 16);
+            q[k + 1][0] = static_cast<uint16_t>(wb.x & 0xffffu);
+            q[k + 1][1] = static_cast<uint16_t>(wb.x >> 16);
+            q[k + 1][2] = static_cast<uint16_t>(wb.y & 0xffffu);
+            q[k + 1][3] = static_cast<uint16_t>(wb.y >> 16);
+        } else {
+            const uint32_t wa = (t.sel & 1u) ? r.y : r.x, wb = (t.sel & 2u) ? r.y : r.x;
+            q[k][0] = static_cast<uint16_t>(wa & 0xffffu);
+            q[k][1] = static_cast<uint16_t>(wa >> 16);
+            q[k + 1][0] = static_cast<uint16_t>(wb & 0xffffu);
+            q[k + 1][1] = static_cast<uint16_t>(wb >> 16);
+        }
+    };
+    split(0, t.r0); // q[0] = (xa, ya), q[1] = (xb, ya)
+    split(2, t.r1); // q[2] = (xa, yb), q[3] = (xb, yb)
+    for (int c = 0; c < NOUT; ++c) {
+        float t00 = f16_to_f32(q[0][c]), t10 = f16_to_f32(q[1][c]);
+        float t01 = f16_to_f32(q[2][c]), t11 = f16_to_f32(q[3][c]);
+        out[c] = lerpf(lerpf(t00, t10, t.fx), lerpf(t01, t11, t.fx), t.fy);
+    }
+}
+
+// probeSampling.glsl:64-163. The 8 cage probes are gathered in three waves of loads
+// (visibility of all 8, then irradiance of probes 0-3 and 4-7) instead of one
+// dependent round trip per probe; every weight and sum is the same IEEE sequence
+// as the per-probe loop, and the irradiance sums still run in probe order.
+template<int GB>
 __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 {
     const V3 spacing = v3(f.spacing[0], f.spacing[1], f.spacing[2]);
@@ -849,52 +924,74 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
     const float invWv = 1.0f / static_cast<float>(f.Wv), invHv = 1.0f / static_cast<float>(f.Hv);
     const float minDistanceBetweenProbes = fminf_(spacing.x, fminf_(spacing.y, spacing.z));
     const V3 nN = normalize(N);
-    for (int i = 0; i < 8; ++i) {
-        int ox = i & 1, oy = (i >> 1) & 1, oz = (i >> 2) & 1;
-        int px = min(max(bx + ox, 0), f.X - 1);
-        int py = min(max(by + oy, 0), f.Y - 1);
-        int pz = min(max(bz + oz, 0), f.Z - 1);
-        V3 tri = { fmaxf_(0.001f, mixf(1.0f - alpha.x, alpha.x, static_cast<float>(ox))),
-                   fmaxf_(0.001f, mixf(1.0f - alpha.y, alpha.y, static_cast<float>(oy))),
-                   fmaxf_(0.001f, mixf(1.0f - alpha.z, alpha.z, static_cast<float>(oz))) };
-        float trilinearWeight = tri.x * tri.y * tri.z;
-        float weight = 1.0f;
-        const float tunableShadowBias = 0.3f;
-        V3 selfShadowBias = (N * 0.2f + Vw * 0.8f) * (0.75f * minDistanceBetweenProbes) * tunableShadowBias;
-        V3 biasedPosition = P + selfShadowBias;
-        V3 probePos = origin + v3(static_cast<float>(px), static_cast<float>(py), static_cast<float>(pz)) * spacing;
-        V3 pointToProbe = probePos - biasedPosition;
-        V3 directionToProbe = normalize(pointToProbe);
-        V3 unbiasedDirectionToProbe = normalize(probePos - P);
-        const float smoothFloor = 0.02f, additionalSmoothening = 0.25f;
-        weight *= smoothFloor + (1.0f - smoothFloor) * powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
-        {
+    const float tunableShadowBias = 0.3f;
+    const V3 selfShadowBias = (N * 0.2f + Vw * 0.8f) * (0.75f * minDistanceBetweenProbes) * tunableShadowBias;
+    const V3 biasedPosition = P + selfShadowBias;
+    auto probeOf = [&](int i, int& px, int& py, int& pz) {
+        px = min(max(bx + (i & 1), 0), f.X - 1);
+        py = min(max(by + ((i >> 1) & 1), 0), f.Y - 1);
+        pz = min(max(bz + ((i >> 2) & 1), 0), f.Z - 1);
+    };
+    auto probePosOf = [&](int px, int py, int pz) {
+        return origin + v3(static_cast<float>(px), static_cast<float>(py), static_cast<float>(pz)) * spacing;
+    };
+    // --- 4 probes at a time: visibility and irradiance taps issued together, then
+    // the weights, then the sums in probe order -----------------------------------
+#pragma unroll
+    for (int h = 0; h < 8; h += GB) {
+        AtlasTap<2> vt[GB];
+        AtlasTap<4> it[GB];
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            int px, py, pz;
+            probeOf(h + j, px, py, pz);
+            const V3 directionToProbe = normalize(probePosOf(px, py, pz) - biasedPosition);
             float u, v;
             atlasSampleUV(f, px, py, pz, -directionToProbe, ARK_DDGI_VISIBILITY_RES, invWv, invHv, &u, &v);
-            float vis[2];
-            sampleAtlas<2, 2>(f.vis, f.Wv, f.Hv, u, v, vis);
-            float meanDistanceToOccluder = vis[0];
-            float variance = fabsf_(vis[1] - square(vis[0]));
-            float distToProbe = length(pointToProbe);
-            float chebychevWeight = 1.0f;
-            if (distToProbe > meanDistanceToOccluder) {
-                chebychevWeight = variance / (variance + square(distToProbe - meanDistanceToOccluder));
-                chebychevWeight = chebychevWeight * chebychevWeight * chebychevWeight;
-            }
-            chebychevWeight = fmaxf_(0.05f, chebychevWeight);
-            weight *= chebychevWeight;
+            vt[j] = atlasTap<2>(f.vis, f.Wv, f.Hv, u, v);
+            atlasSampleUV(f, px, py, pz, nN, ARK_DDGI_IRRADIANCE_RES, invWi, invHi, &u, &v);
+            it[j] = atlasTap<4>(f.irr, f.Wi, f.Hi, u, v);
         }
-        weight = fmaxf_(0.000001f, weight);
-        const float crushThreshold = 0.2f;
-        if (weight < crushThreshold) weight *= square(weight) * (1.0f / square(crushThreshold));
-        weight *= trilinearWeight;
-        float u, v;
-        atlasSampleUV(f, px, py, pz, nN, ARK_DDGI_IRRADIANCE_RES, invWi, invHi, &u, &v);
-        float irr[3];
-        sampleAtlas<4, 3>(f.irr, f.Wi, f.Hi, u, v, irr);
-        V3 probeIrradiance = pow3(v3(irr[0], irr[1], irr[2]), 5.0f * 0.5f);
-        sumIrradiance = sumIrradiance + weight * probeIrradiance;
-        sumWeight += weight;
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const int i = h + j;
+            int px, py, pz;
+            probeOf(i, px, py, pz);
+            const int ox = i & 1, oy = (i >> 1) & 1, oz = (i >> 2) & 1;
+            V3 tri = { fmaxf_(0.001f, mixf(1.0f - alpha.x, alpha.x, static_cast<float>(ox))),
+                       fmaxf_(0.001f, mixf(1.0f - alpha.y, alpha.y, static_cast<float>(oy))),
+                       fmaxf_(0.001f, mixf(1.0f - alpha.z, alpha.z, static_cast<float>(oz))) };
+            float trilinearWeight = tri.x * tri.y * tri.z;
+            float weight = 1.0f;
+            const V3 probePos = probePosOf(px, py, pz);
+            const V3 pointToProbe = probePos - biasedPosition;
+            V3 unbiasedDirectionToProbe = normalize(probePos - P);
+            const float smoothFloor = 0.02f, additionalSmoothening = 0.25f;
+            weight *= smoothFloor + (1.0f - smoothFloor) * powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
+            {
+                float vis[2];
+                atlasFilter<2, 2>(vt[j], vis);
+                float meanDistanceToOccluder = vis[0];
+                float variance = fabsf_(vis[1] - square(vis[0]));
+                float distToProbe = length(pointToProbe);
+                float chebychevWeight = 1.0f;
+                if (distToProbe > meanDistanceToOccluder) {
+                    chebychevWeight = variance / (variance + square(distToProbe - meanDistanceToOccluder));
+                    chebychevWeight = chebychevWeight * chebychevWeight * chebychevWeight;
+                }
+                chebychevWeight = fmaxf_(0.05f, chebychevWeight);
+                weight *= chebychevWeight;
+            }
+            weight = fmaxf_(0.000001f, weight);
+            const float crushThreshold = 0.2f;
+            if (weight < crushThreshold) weight *= square(weight) * (1.0f / square(crushThreshold));
+            weight *= trilinearWeight;
+            float irr[3];
+            atlasFilter<4, 3>(it[j], irr);
+            V3 probeIrradiance = pow3(v3(irr[0], irr[1], irr[2]), 5.0f * 0.5f);
+            sumIrradiance = sumIrradiance + weight * probeIrradiance;
+            sumWeight += weight;
+        }
     }
     V3 irradiance = sumIrradiance / sumWeight;
     irradiance = irradiance * irradiance;
@@ -1115,7 +1212,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const V3 Vi = -dir;
             const V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
             const V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
-            const V3 irradiance = sampleDDGI(f, hitPoint, N, Vi);
+            const V3 irradiance = sampleDDGI<ARK_DDGI_GATHER_BATCH>(f, hitPoint, N, Vi);
             const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
             if (need == 0) {
@@ -1294,14 +1391,14 @@ static int trace_variant()
     return v;
 }
 
-// Occupancy variant of the shading kernel (minimum waves per SIMD): 4 by default
-// (128 VGPRs, 16 B/lane of spill; 2.05 vs 2.38 ms at the compiler's 3 on C4),
-// ARK_SHADE_WPE = 0 (compiler's choice) or 5 for tuning.
+// Occupancy variant of the shading kernel (minimum waves per SIMD): the compiler's
+// choice by default (161 VGPRs, 3 waves, no spill: 0.874 ms on C4 vs 0.905 ms at
+// 4 waves with 128 VGPRs and spills, profiles/r01s2_*), ARK_SHADE_WPE = 4 or 5 for tuning.
 static int shade_variant()
 {
     static const int v = [] {
         const char* e = std::getenv("ARK_SHADE_WPE");
-        return e ? std::atoi(e) : 4;
+        return e ? std::atoi(e) : 0;
     }();
     return v;
 }
