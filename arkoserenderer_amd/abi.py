@@ -229,6 +229,23 @@ class ArkDdgiBvhStats(C.Structure):
     ]
 
 
+class ArkBakeAoDesc(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("instance_index", C.c_uint32),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("sample_count", C.c_uint32),
+        ("bent_normals", C.c_int32),
+        ("reserved", C.c_int32 * 2),
+    ]
+
+
+ARK_BAKE_TRIANGLE_INDEX = 0
+ARK_BAKE_BARYCENTRICS = 1
+ARK_BAKE_OUTPUT = 2
+
+
 class ArkSoupParams(C.Structure):
     _fields_ = [
         ("struct_size", C.c_uint32),
@@ -250,7 +267,7 @@ class ArkSoupParams(C.Structure):
 ABI_STRUCTS = [
     ArkDdgiDesc, ArkRTVertex, ArkRTTriangleMesh, ArkShaderMaterial, ArkTexture, ArkRTInstance,
     ArkDirectionalLight, ArkSpotLight, ArkDdgiScene, ArkDdgiFrameParams, ArkDdgiCounters,
-    ArkDdgiDeviceViews, ArkDdgiBvhStats,
+    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc,
 ]
 
 # name -> (restype, argtypes)
@@ -273,6 +290,8 @@ EXPORTS = {
     "ark_ddgi_get_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int]),
     "ark_ddgi_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "ark_ddgi_get_bvh_stats": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiBvhStats)]),
+    "ark_ddgi_bake_ao": (C.c_int, [C.c_void_p, C.POINTER(ArkBakeAoDesc), C.c_void_p]),
+    "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     # ark_scene.h
     "ark_soup_default_params": (None, [C.POINTER(ArkSoupParams)]),
     "ark_soup_generate": (C.c_int, [C.POINTER(ArkSoupParams), C.POINTER(C.c_void_p)]),

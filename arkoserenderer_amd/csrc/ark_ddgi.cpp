@@ -118,7 +118,13 @@ struct ArkDdgiCtx {
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0;
     // scene
     bool hasScene = false;
-    DeviceBuffer nodes, tris, indices, vertices, meshes, materials, instances, texInfos, texels, spots;
+    DeviceBuffer nodes, tris, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
+    std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
+    std::vector<ArkRTTriangleMesh> meshHost;
+    // AO bake results (ark_ddgi_bake_ao)
+    DeviceBuffer bakeTri, bakeBary, bakeOut, bakePixels, bakeCounters;
+    uint32_t bakeW = 0, bakeH = 0;
+    int bakeBent = 0;
     SceneArgs scene {};
     ArkDdgiBvhStats bvhStats {};
     uint32_t bvhMaxDepth = 0;
@@ -285,7 +291,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
-                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->meshes, &ctx->materials, &ctx->instances,
+                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
     for (auto& ev : ctx->ev)
@@ -480,6 +486,9 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, ctx->tris, allTris.data(), allTris.size())) != 0) return rc;
     if ((rc = upload(ctx, ctx->indices, s->indices, s->index_count)) != 0) return rc;
     if ((rc = upload(ctx, ctx->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
+    if ((rc = upload(ctx, ctx->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
+    ctx->instHost.assign(s->instances, s->instances + s->instance_count);
+    ctx->meshHost.assign(s->meshes, s->meshes + s->mesh_count);
     if ((rc = upload(ctx, ctx->meshes, s->meshes, s->mesh_count)) != 0) return rc;
     if ((rc = upload(ctx, ctx->materials, s->materials, s->material_count)) != 0) return rc;
     if ((rc = upload(ctx, ctx->instances, ginst.data(), ginst.size())) != 0) return rc;
@@ -820,6 +829,76 @@ int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out)
 {
     if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
     *out = ctx->bvhStats;
+    return ARK_DDGI_OK;
+}
+
+// AO / bent-normal bake (include/ark_ddgi.h; BakeAmbientOcclusionNode.cpp:15-131):
+// raster -> barycentrics (+ covered-texel list) -> persistent AO rays, one stream.
+int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!d || d->struct_size != sizeof(ArkBakeAoDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkBakeAoDesc");
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: no scene");
+    if (d->instance_index >= ctx->instHost.size()) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: instance %u out of range", d->instance_index);
+    if (d->width == 0 || d->height == 0 || d->width > 16384 || d->height > 16384 || d->sample_count == 0)
+        return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: extent %ux%u / %u samples", d->width, d->height, d->sample_count);
+    const ArkRTInstance& inst = ctx->instHost[d->instance_index];
+    const ArkRTTriangleMesh& mesh = ctx->meshHost[inst.rt_mesh_index];
+    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    ARK_HIP(hipSetDevice(ctx->device));
+    const size_t texels = static_cast<size_t>(d->width) * d->height;
+    const size_t outBytes = texels * (d->bent_normals ? 4 : 1);
+    if (ctx->bakeTri.bytes < texels * 4) ARK_HIP(ctx->bakeTri.alloc(texels * 4));
+    if (ctx->bakeBary.bytes < texels * 8) ARK_HIP(ctx->bakeBary.alloc(texels * 8));
+    if (ctx->bakeOut.bytes < outBytes) ARK_HIP(ctx->bakeOut.alloc(outBytes));
+    if (ctx->bakePixels.bytes < texels * 4) ARK_HIP(ctx->bakePixels.alloc(texels * 4));
+    if (ctx->bakeCounters.bytes < 256) ARK_HIP(ctx->bakeCounters.alloc(256));
+    ARK_HIP(hipMemsetAsync(ctx->bakeTri.ptr, 0, texels * 4, s)); // ClearValue::blackAtMaxDepth
+    ARK_HIP(hipMemsetAsync(ctx->bakeCounters.ptr, 0, 256, s));
+    BakeArgs b {};
+    b.W = d->width;
+    b.H = d->height;
+    b.samples = d->sample_count;
+    b.tri_count = inst.triangle_count;
+    b.bent = d->bent_normals ? 1 : 0;
+    b.first_index = static_cast<uint32_t>(mesh.first_index);
+    b.first_vertex = static_cast<uint32_t>(mesh.first_vertex);
+    b.indices = ctx->indices.as<uint32_t>();
+    b.positions = ctx->positions.as<float>();
+    b.vertices = ctx->vertices.as<float>();
+    b.tri_idx = ctx->bakeTri.as<uint32_t>();
+    b.bary = ctx->bakeBary.as<uint16_t>();
+    b.out = ctx->bakeOut.as<uint8_t>();
+    b.pixels = ctx->bakePixels.as<uint32_t>();
+    b.counters = ctx->bakeCounters.as<uint32_t>();
+    b.spill = ctx->spill.as<uint32_t>();
+    if (b.tri_count > 0) ARK_HIP(launch_bake(ctx->scene, b, 0, 0, s));
+    ARK_HIP(launch_bake(ctx->scene, b, 0, 1, s));
+    // the persistent AO kernel uses the traversal spill area sized for shadowBlocks workgroups
+    ARK_HIP(launch_bake(ctx->scene, b, ctx->shadowBlocks, 2, s));
+    ctx->bakeW = d->width;
+    ctx->bakeH = d->height;
+    ctx->bakeBent = b.bent;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_bake_read(ArkDdgiCtx* ctx, int which, void* dst, uint64_t bytes)
+{
+    if (!ctx || !dst) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const size_t texels = static_cast<size_t>(ctx->bakeW) * ctx->bakeH;
+    const void* src = nullptr;
+    size_t n = 0;
+    switch (which) {
+    case ARK_BAKE_TRIANGLE_INDEX: src = ctx->bakeTri.ptr; n = texels * 4; break;
+    case ARK_BAKE_BARYCENTRICS: src = ctx->bakeBary.ptr; n = texels * 8; break;
+    case ARK_BAKE_OUTPUT: src = ctx->bakeOut.ptr; n = texels * (ctx->bakeBent ? 4 : 1); break;
+    default: return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake_read: unknown resource %d", which);
+    }
+    if (texels == 0) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake_read: no bake yet");
+    if (bytes != n) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake_read: %llu bytes, resource has %zu", static_cast<unsigned long long>(bytes), n);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return ARK_DDGI_OK;
 }
 

@@ -135,7 +135,25 @@ struct FrameArgs {
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };
 
+// AO / bent-normal bake of one mesh segment (ark_ddgi_bake_ao; ddgi_kernels.hip §5)
+struct BakeArgs {
+    uint32_t W, H, samples, tri_count;
+    int32_t bent;
+    uint32_t first_index, first_vertex;
+    const uint32_t* indices;
+    const float* positions; // vec3 pool (object space)
+    const float* vertices;  // RTVertex pool (9 floats)
+    uint32_t* tri_idx;      // [H][W] triangle + 1
+    uint16_t* bary;         // [H][W][4] fp16
+    uint8_t* out;           // [H][W] AO or [H][W][4] bent normal
+    uint32_t* pixels;       // covered texels (k_bake_bary appends)
+    uint32_t* counters;     // [0] covered count, [32] AO queue head
+    uint32_t* spill;
+};
+
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
+// stage 0: parameterization raster, 1: barycentrics + work list, 2: AO rays
+hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s);
 hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);

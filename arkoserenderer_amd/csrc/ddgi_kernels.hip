@@ -1365,6 +1365,275 @@ __global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t value)
         p[i] = value;
 }
 
+// ---------------------------------------------------------------------------
+// 5. AO / bent-normal bake (BakeAmbientOcclusionNode.cpp:15-131)
+// ---------------------------------------------------------------------------
+// Parameterization pass (bakeParameterization.vert/.frag) as a deterministic integer
+// rasterizer of the mesh's UV layout: a vertex lands at (fract(u) * W, fract(v) * H)
+// (the viewport transform of NDC = fract * 2 - 1), snapped to 1/256 texel with RNE
+// (8-bit subpixel precision); a texel is covered when its centre is inside the
+// triangle (exact 64-bit edge functions; a centre on an edge belongs to the triangle
+// that runs the edge "up, or right when horizontal" in positive orientation, so a
+// centre on an edge shared by two triangles is covered once). Where triangles
+// overlap the later primitive wins (draw order, no depth test): atomicMax of
+// triangle + 1. gl_BaryCoordEXT = edge function / area in fp32, stored RGBA16F.
+// The CPU oracle (oracle/ddgi_oracle.cpp, bake section) restates the same rules.
+
+
+__device__ __forceinline__ int64_t bakeSnap(float c, uint32_t extent)
+{
+    const float fr = c - floorf_(c); // GLSL fract
+    return static_cast<int64_t>(rintf(fr * static_cast<float>(extent) * 256.0f));
+}
+
+__device__ __forceinline__ int64_t bakeEdge(int64_t ax, int64_t ay, int64_t bx, int64_t by, int64_t px, int64_t py)
+{
+    return (bx - ax) * (py - ay) - (by - ay) * (px - ax);
+}
+
+// tie rule for a centre exactly on edge (a -> b) of a positively oriented triangle
+__device__ __forceinline__ bool bakeOwnsEdge(int64_t dx, int64_t dy) { return dy > 0 || (dy == 0 && dx > 0); }
+
+struct BakeTri {
+    int64_t x[3], y[3];
+    int64_t area; // bakeEdge(v0, v1, v2); 0 = degenerate
+};
+
+__device__ __forceinline__ BakeTri bakeTriangle(const BakeArgs& b, uint32_t t)
+{
+    BakeTri r;
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t idx = b.indices[static_cast<size_t>(b.first_index) + 3u * t + k];
+        const float* vx = b.vertices + (static_cast<size_t>(b.first_vertex) + idx) * 9;
+        r.x[k] = bakeSnap(vx[0], b.W);
+        r.y[k] = bakeSnap(vx[1], b.H);
+    }
+    r.area = bakeEdge(r.x[0], r.y[0], r.x[1], r.y[1], r.x[2], r.y[2]);
+    return r;
+}
+
+// edge functions at texel centre (px, py): w[k] is opposite vertex k; returns coverage
+__device__ __forceinline__ bool bakeCover(const BakeTri& t, int px, int py, int64_t* w)
+{
+    const int64_t cx = 256 * static_cast<int64_t>(px) + 128, cy = 256 * static_cast<int64_t>(py) + 128;
+    w[0] = bakeEdge(t.x[1], t.y[1], t.x[2], t.y[2], cx, cy);
+    w[1] = bakeEdge(t.x[2], t.y[2], t.x[0], t.y[0], cx, cy);
+    w[2] = bakeEdge(t.x[0], t.y[0], t.x[1], t.y[1], cx, cy);
+    const int64_t s = t.area > 0 ? 1 : -1;
+    bool in = true;
+    for (int k = 0; k < 3; ++k) {
+        const int a = (k + 1) % 3, c = (k + 2) % 3; // edge a -> c (as oriented when area > 0)
+        const int64_t e = s * w[k];
+        const int64_t dx = s * (t.x[c] - t.x[a]), dy = s * (t.y[c] - t.y[a]);
+        in = in && (e > 0 || (e == 0 && bakeOwnsEdge(dx, dy)));
+    }
+    return in;
+}
+
+__global__ void __launch_bounds__(256) k_bake_raster(BakeArgs b)
+{
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= b.tri_count) return;
+    const BakeTri tr = bakeTriangle(b, t);
+    if (tr.area == 0) return;
+    const int64_t xmin = min(tr.x[0], min(tr.x[1], tr.x[2])), xmax = max(tr.x[0], max(tr.x[1], tr.x[2]));
+    const int64_t ymin = min(tr.y[0], min(tr.y[1], tr.y[2])), ymax = max(tr.y[0], max(tr.y[1], tr.y[2]));
+    // texel centres 256 p + 128 inside [min, max]
+    const int px0 = static_cast<int>(max<int64_t>(0, (xmin - 128 + 255) >> 8));
+    const int px1 = static_cast<int>(min<int64_t>(static_cast<int64_t>(b.W) - 1, (xmax - 128) >> 8));
+    const int py0 = static_cast<int>(max<int64_t>(0, (ymin - 128 + 255) >> 8));
+    const int py1 = static_cast<int>(min<int64_t>(static_cast<int64_t>(b.H) - 1, (ymax - 128) >> 8));
+    for (int py = py0; py <= py1; ++py)
+        for (int px = px0; px <= px1; ++px) {
+            int64_t w[3];
+            if (bakeCover(tr, px, py, w)) atomicMax(&b.tri_idx[static_cast<size_t>(py) * b.W + px], t + 1u);
+        }
+}
+
+// barycentrics of the winning triangle; uncovered texels get their final output
+// here (bakeAmbientOcclusion.rgen:44-51), covered ones join the AO work list
+__global__ void __launch_bounds__(256) k_bake_bary(BakeArgs b)
+{
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= b.W * b.H) return;
+    const uint32_t t1 = b.tri_idx[p];
+    uint2 packed = make_uint2(0u, 0u);
+    if (t1 == 0) {
+        if (b.bent) reinterpret_cast<uint32_t*>(b.out)[p] = 128u | (128u << 8) | (128u << 16) | (255u << 24);
+        else b.out[p] = 0;
+    } else {
+        const BakeTri tr = bakeTriangle(b, t1 - 1u);
+        int64_t w[3];
+        bakeCover(tr, static_cast<int>(p % b.W), static_cast<int>(p / b.W), w);
+        const float A = static_cast<float>(tr.area);
+        const float b0 = static_cast<float>(w[0]) / A, b1 = static_cast<float>(w[1]) / A, b2 = static_cast<float>(w[2]) / A;
+        packed.x = static_cast<uint32_t>(f32_to_f16(b0)) | (static_cast<uint32_t>(f32_to_f16(b1)) << 16);
+        packed.y = static_cast<uint32_t>(f32_to_f16(b2)) | (0x3c00u << 16);
+        b.pixels[atomicAdd(&b.counters[0], 1u)] = p;
+    }
+    reinterpret_cast<uint2*>(b.bary)[p] = packed;
+}
+
+__device__ __forceinline__ uint8_t unorm8(float x) { return static_cast<uint8_t>(rintf(saturate(x) * 255.0f)); }
+
+// bakeAmbientOcclusion.rgen:93-98: one cosine-distributed direction by rejection,
+// bounded to kBakeMaxDraws draws (then the normal): a texel whose seed hashes to 0
+// (wang_hash(61) == 0) has a xorshift state stuck at 0 and would loop forever with a
+// +z normal, which on the reference is a GPU hang (DESIGN.md §AO bake).
+constexpr int kBakeMaxDraws = 16;
+__device__ __forceinline__ V3 bakeSampleDirection(V3 normal, uint32_t& rng)
+{
+    V3 dir;
+    int draws = 0;
+    do {
+        const float theta = kTwoPi * randomFloat(rng);
+        const float u = 2.0f * randomFloat(rng) - 1.0f;
+        const float sr = sqrtf_(1.0f - u * u);
+        float s, c;
+        sincosf_(theta, &s, &c);
+        dir = normal + v3(sr * c, sr * s, u);
+    } while (dot(dir, dir) <= 1e-4f && ++draws < kBakeMaxDraws);
+    if (dot(dir, dir) <= 1e-4f) dir = normal;
+    return normalize(dir);
+}
+
+// bakeAmbientOcclusion.rgen:33-118, persistent: every lane owns one texel and runs
+// its sample_count rays one after the other (one any-hit traversal each over the
+// three hit-mask classes, masked candidates alpha tested as .rahit does); lanes whose
+// texel is done take the next covered texel from a wave-private pool.
+template<int WPE>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_bake_ao(SceneArgs sc, BakeArgs b)
+{
+    __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
+    __shared__ uint4 ldsNodes[kLdsNodes * 5];
+    const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
+    const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
+    Stack<kTraceBlock> st { ldsStack + threadIdx.x, b.spill + gtid, gridDim.x * kTraceBlock, 0 };
+    const uint32_t lane = threadIdx.x & 63u;
+    const float tmin = 0.0005f, tmax = 100.0f;
+    const uint32_t total = b.counters[0];
+    const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
+    uint32_t cN = 0, cT = 0;
+
+    uint32_t poolNext = 0, poolEnd = 0;
+    bool exhausted = false, active = false;
+    uint32_t pixel = 0, rng = 0, sampleIdx = 0;
+    float aoAcc = 0.0f;
+    V3 dirAcc = splat(0.0f), P = splat(0.0f), Nrm = splat(0.0f);
+    int pass = 0;
+    TravState ts { 0u, 0u, 0u, 0u };
+    uint32_t oct = 0;
+    V3 d = { 0, 0, 1 }, idir = { 0, 0, 1 };
+    auto startRay = [&]() {
+        d = bakeSampleDirection(Nrm, rng);
+        idir = safeInv(d);
+        oct = rayOctant(idir);
+        st.depth = 0;
+        pass = 0;
+        while (pass < 3 && roots[pass] < 0) ++pass;
+        ts = pass < 3 ? TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u } : TravState { 0u, 0u, 0u, 0u };
+    };
+    for (;;) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && !exhausted) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(need));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
+            const uint32_t avail = poolEnd - poolNext;
+            uint32_t fb = 0, fe = 0;
+            if (avail < n) {
+                uint32_t s = 0;
+                if (lane == 0) s = atomicAdd(&b.counters[32], 64u);
+                fb = min(__shfl(s, 0), total);
+                fe = min(fb + 64u, total);
+            }
+            if (!active) {
+                uint32_t r = kNoHit;
+                if (rank < avail) r = poolNext + rank;
+                else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
+                if (r != kNoHit) {
+                    // texel setup (bakeAmbientOcclusion.rgen:53-86)
+                    pixel = b.pixels[r];
+                    const uint32_t tri = b.tri_idx[pixel] - 1u;
+                    const uint2 bw = reinterpret_cast<const uint2*>(b.bary)[pixel];
+                    const V3 bc = v3(f16_to_f32(static_cast<uint16_t>(bw.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(bw.x >> 16)),
+                                     f16_to_f32(static_cast<uint16_t>(bw.y & 0xffffu)));
+                    V3 p[3], nn[3];
+                    for (int k = 0; k < 3; ++k) {
+                        const uint32_t idx = b.indices[static_cast<size_t>(b.first_index) + 3u * tri + k];
+                        const size_t vi = static_cast<size_t>(b.first_vertex) + idx;
+                        p[k] = v3(b.positions[vi * 3 + 0], b.positions[vi * 3 + 1], b.positions[vi * 3 + 2]);
+                        const float* vx = b.vertices + vi * 9;
+                        nn[k] = v3(vx[2], vx[3], vx[4]);
+                    }
+                    P = p[0] * bc.x + p[1] * bc.y + p[2] * bc.z;
+                    Nrm = normalize(nn[0] * bc.x + nn[1] * bc.y + nn[2] * bc.z);
+                    rng = wang_hash(pixel); // seedRandom(x + y * W)
+                    sampleIdx = 0;
+                    aoAcc = 0.0f;
+                    dirAcc = splat(0.0f);
+                    active = true;
+                    startRay();
+                }
+            }
+            if (avail < n) {
+                if (fb >= fe) {
+                    exhausted = true;
+                    poolNext = poolEnd = 0;
+                } else {
+                    poolNext = min(fb + (n - avail), fe);
+                    poolEnd = fe;
+                }
+            } else {
+                poolNext += n;
+            }
+        }
+        if (__ballot(active) == 0) break;
+        if (active) {
+            bool hit = false;
+            if (!travDone(ts, st)) {
+                Fetch fx;
+                travFetch(sc, nc, ts, st, oct, fx);
+                uint32_t inst, prim;
+                float tt, uu, vv;
+                bool bf;
+                hit = travCompute(fx, ts, P, d, idir, oct, tmin, tmax, tt, uu, vv, bf, inst, prim, cN, cT) &&
+                      !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv)); // masked.rahit ignoreIntersection
+            }
+            bool rayDone = hit;
+            if (!hit && travDone(ts, st)) {
+                ++pass;
+                while (pass < 3 && roots[pass] < 0) ++pass;
+                if (pass < 3) {
+                    st.depth = 0;
+                    ts = TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u };
+                } else {
+                    rayDone = true;
+                }
+            }
+            if (rayDone) {
+                // bakeAmbientOcclusion.rgen:101-106 (hit distance <= tmax iff an accepted hit)
+                if (hit) aoAcc += 1.0f;
+                else dirAcc = dirAcc + d;
+                if (++sampleIdx < b.samples) {
+                    startRay();
+                } else {
+                    if (b.bent) { // :109-114
+                        const V3 bent = dirAcc / static_cast<float>(b.samples);
+                        const float cone = (kPi / 2.0f) / (kPi / 2.0f);
+                        const V3 enc = bent * v3(0.5f, 0.5f, 0.5f) + v3(0.5f, 0.5f, 0.5f);
+                        reinterpret_cast<uint32_t*>(b.out)[pixel] = static_cast<uint32_t>(unorm8(enc.x)) | (static_cast<uint32_t>(unorm8(enc.y)) << 8) |
+                                                                    (static_cast<uint32_t>(unorm8(enc.z)) << 16) | (static_cast<uint32_t>(unorm8(cone)) << 24);
+                    } else { // :115-118
+                        const float ao = aoAcc / static_cast<float>(b.samples);
+                        b.out[pixel] = unorm8(1.0f - ao);
+                    }
+                    active = false;
+                }
+            }
+        }
+    }
+}
+
 } // namespace dev
 
 // ---------------------------------------------------------------------------
@@ -1477,6 +1746,14 @@ const void* kernel_shade_ptr(bool count)
 const void* kernel_trace_shadow_ptr(bool count)
 {
     return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6>);
+}
+
+hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s)
+{
+    if (stage == 0) hipLaunchKernelGGL(dev::k_bake_raster, dim3((b.tri_count + 255) / 256), dim3(256), 0, s, b);
+    else if (stage == 1) hipLaunchKernelGGL(dev::k_bake_bary, dim3((b.W * b.H + 255) / 256), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((dev::k_bake_ao<6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, b);
+    return hipGetLastError();
 }
 
 } // namespace ark

@@ -175,6 +175,24 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_get_last_timings(self.h, out, 5), "ark_ddgi_get_last_timings")
         return list(out)
 
+    def bake_ao(self, instance_index: int, width: int, height: int, sample_count: int, bent_normals: bool,
+                stream: int | None = None):
+        """ark_ddgi_bake_ao: AO / bent-normal bake of one instance's mesh segment."""
+        d = abi.ArkBakeAoDesc()
+        d.struct_size = C.sizeof(abi.ArkBakeAoDesc)
+        d.instance_index, d.width, d.height, d.sample_count = int(instance_index), int(width), int(height), int(sample_count)
+        d.bent_normals = int(bool(bent_normals))
+        self.check(self.lib.ark_ddgi_bake_ao(self.h, C.byref(d), C.c_void_p(stream) if stream else None), "ark_ddgi_bake_ao")
+        self._bake = (int(width), int(height), bool(bent_normals))
+
+    def bake_read(self, which: int) -> np.ndarray:
+        w, h, bent = self._bake
+        shape, dt = {abi.ARK_BAKE_TRIANGLE_INDEX: ((h, w), np.uint32), abi.ARK_BAKE_BARYCENTRICS: ((h, w, 4), np.uint16),
+                     abi.ARK_BAKE_OUTPUT: ((h, w, 4 if bent else 1), np.uint8)}[which]
+        out = np.empty(shape, dt)
+        self.check(self.lib.ark_ddgi_bake_read(self.h, which, out.ctypes.data, out.nbytes), "ark_ddgi_bake_read")
+        return out
+
     def bvh_stats(self) -> abi.ArkDdgiBvhStats:
         s = abi.ArkDdgiBvhStats()
         self.check(self.lib.ark_ddgi_get_bvh_stats(self.h, C.byref(s)), "ark_ddgi_get_bvh_stats")
@@ -247,3 +265,28 @@ class DDGINode:
         self.ctx.update(p, stream)
         self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
         return p
+
+
+class BakeAmbientOcclusionNode:
+    """Python mirror of BakeAmbientOcclusionNode (name "Bake ambient occlusion",
+    arkose/rendering/baking/BakeAmbientOcclusionNode.{h,cpp}): bakes the mesh segment
+    of one instance; the output format selects AO (R8Uint) or bent normals (RGBA8)
+    (BakeAmbientOcclusionNode.cpp:20-31). The scene/BVH come from a DDGIContext."""
+
+    R8UINT = "R8Uint"
+    RGBA8 = "RGBA8"
+
+    def __init__(self, instance_index: int, sample_count: int = 500):
+        assert sample_count > 0  # BakeAmbientOcclusionNode.cpp:12
+        self.instance_index = instance_index
+        self.sample_count = sample_count
+
+    def name(self) -> str:
+        return "Bake ambient occlusion"
+
+    def execute(self, ctx: DDGIContext, width: int, height: int, output_format: str, stream: int | None = None) -> np.ndarray:
+        if output_format not in (self.R8UINT, self.RGBA8):
+            raise ValueError("BakeAmbientOcclusionNode: unknown AO texture format - only R8Uint & RGBA8 (bent normals)")
+        bent = output_format == self.RGBA8
+        ctx.bake_ao(self.instance_index, width, height, self.sample_count, bent, stream)
+        return ctx.bake_read(abi.ARK_BAKE_OUTPUT)

@@ -314,6 +314,16 @@ def cornell_box() -> tuple[SceneData, dict]:
     return scene, {"light_pre_exposure": pre, "environment_brightness": 3000.0, "z_far": 10000.0}
 
 
+def damaged_helmet() -> SceneData:
+    """BASELINE config C1 input: DamagedHelmet.gltf (15,452 triangles), baked in
+    object space at an identity instance transform, as MeshViewerApp.cpp:845-880 sets
+    up its bake scene (bakeScene->addMesh)."""
+    path = find_asset("DamagedHelmet", "DamagedHelmet.gltf")
+    if path is None:
+        raise FileNotFoundError("tests/assets/DamagedHelmet/DamagedHelmet.gltf missing")
+    return load_gltf(path)
+
+
 def soup(triangle_count: int = 10_000_000, **overrides) -> SceneData:
     """BASELINE config C4 synthetic triangle-strip soup (PCG32 seed 0xA2C05E00)."""
     lib = abi.load_library()

@@ -311,6 +311,41 @@ typedef struct ArkDdgiBvhStats {
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 
+/* ------------------------------------------------------------------------------
+ * Ambient-occlusion / bent-normal bake of one mesh segment of the current scene,
+ * on the same scene and BVH. Replaces the reference's
+ * BakeAmbientOcclusionNode (arkose/rendering/baking/BakeAmbientOcclusionNode.cpp:15-131):
+ *   1. the UV parameterization pass (bakeParameterization.vert/.frag): every texel
+ *      gets the index + 1 of the triangle covering it (0 = none) and its barycentrics
+ *      (RGBA16F), by a deterministic rasterizer (see DESIGN.md §AO bake);
+ *   2. the ray pass (baking/ao/bakeAmbientOcclusion.rgen:33-118): `sample_count`
+ *      cosine-distributed rays per covered texel from the object-space surface point,
+ *      tmin 0.0005, tmax 100, any accepted hit occludes (.rahit alpha test for the
+ *      masked class); output R8Uint AO (bent_normals = 0) or RGBA8 UNORM bent normal
+ *      (bent_normals = 1), as BakeAmbientOcclusionNode.cpp:20-31 selects by format.
+ * The mesh is the RT mesh of instance `instance_index` (its triangle_count
+ * triangles), baked in object space as MeshViewerApp.cpp:845-880 sets it up. */
+typedef struct ArkBakeAoDesc {
+    uint32_t struct_size;
+    uint32_t instance_index;
+    uint32_t width, height;   /* output texture extent */
+    uint32_t sample_count;    /* m_sampleCount (BakeAmbientOcclusionNode.h:21, default 500) */
+    int32_t bent_normals;     /* 0: R8Uint ambient occlusion, 1: RGBA8 bent normals */
+    int32_t reserved[2];
+} ArkBakeAoDesc;
+
+/* Runs both passes, enqueued on `hip_stream` (NULL = ctx stream). */
+int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* desc, void* hip_stream);
+
+/* Results of the last bake (blocking): width*height texels of
+ *   ARK_BAKE_TRIANGLE_INDEX  uint32 (triangle + 1, 0 = uncovered)
+ *   ARK_BAKE_BARYCENTRICS    4 x fp16 (b0, b1, b2, 1)
+ *   ARK_BAKE_OUTPUT          uint8 AO, or 4 x uint8 bent normal (xyz * 0.5 + 0.5, cone / (pi/2)) */
+#define ARK_BAKE_TRIANGLE_INDEX 0
+#define ARK_BAKE_BARYCENTRICS 1
+#define ARK_BAKE_OUTPUT 2
+int ark_ddgi_bake_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

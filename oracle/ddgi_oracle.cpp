@@ -598,6 +598,7 @@ struct Oracle {
     std::vector<WTri> tris;
     Bvh bvhOpaque, bvhMasked, bvhBlend;
     std::vector<uint32_t> indices;
+    std::vector<float> positions; // vec3 pool (object space; the AO bake)
     std::vector<ArkRTVertex> vertices;
     std::vector<ArkRTTriangleMesh> meshes;
     std::vector<ArkShaderMaterial> materials;
@@ -1065,6 +1066,145 @@ void resetHistory(Oracle& o)
     std::fill(o.surfels.begin(), o.surfels.end(), 0);
 }
 
+
+// ---------------------------------------------------------------------------
+// AO / bent-normal bake (BakeAmbientOcclusionNode.cpp:15-131).
+// Parameterization (bakeParameterization.vert/.frag): the rasterization rules are
+// implementation-defined in Vulkan; the build fixes them (DESIGN.md §AO bake):
+// vertex at (fract(u) * W, fract(v) * H) snapped to 1/256 texel (RNE), texel centre
+// coverage by exact integer edge functions with an "up, or right when horizontal"
+// tie rule, later primitives overwrite earlier ones (draw order without depth
+// test), barycentrics = edge function / area in fp32, stored fp16 (RGBA16F).
+// ---------------------------------------------------------------------------
+constexpr int kBakeMaxDraws = 16; // bound of the cosine-direction rejection loop
+
+struct BakeTri {
+    int64_t x[3], y[3];
+    int64_t area;
+};
+
+inline int64_t bakeSnap(float c, uint32_t extent)
+{
+    float fr = c - floorf_(c); // GLSL fract
+    return static_cast<int64_t>(std::nearbyint(fr * static_cast<float>(extent) * 256.0f));
+}
+inline int64_t bakeEdge(int64_t ax, int64_t ay, int64_t bx, int64_t by, int64_t px, int64_t py)
+{
+    return (bx - ax) * (py - ay) - (by - ay) * (px - ax);
+}
+
+BakeTri bakeTriangle(const Oracle& o, const ArkRTTriangleMesh& m, uint32_t t, uint32_t W, uint32_t H)
+{
+    BakeTri r;
+    for (int k = 0; k < 3; ++k) {
+        uint32_t idx = o.indices[static_cast<size_t>(m.first_index) + 3u * t + k];
+        const ArkRTVertex& v = o.vertices[static_cast<size_t>(m.first_vertex) + idx];
+        r.x[k] = bakeSnap(v.tex_coord[0], W);
+        r.y[k] = bakeSnap(v.tex_coord[1], H);
+    }
+    r.area = bakeEdge(r.x[0], r.y[0], r.x[1], r.y[1], r.x[2], r.y[2]);
+    return r;
+}
+
+bool bakeCover(const BakeTri& t, int px, int py, int64_t* w)
+{
+    int64_t cx = 256 * static_cast<int64_t>(px) + 128, cy = 256 * static_cast<int64_t>(py) + 128;
+    w[0] = bakeEdge(t.x[1], t.y[1], t.x[2], t.y[2], cx, cy);
+    w[1] = bakeEdge(t.x[2], t.y[2], t.x[0], t.y[0], cx, cy);
+    w[2] = bakeEdge(t.x[0], t.y[0], t.x[1], t.y[1], cx, cy);
+    int64_t sgn = t.area > 0 ? 1 : -1;
+    for (int k = 0; k < 3; ++k) {
+        int a = (k + 1) % 3, c = (k + 2) % 3;
+        int64_t e = sgn * w[k], dx = sgn * (t.x[c] - t.x[a]), dy = sgn * (t.y[c] - t.y[a]);
+        bool owns = dy > 0 || (dy == 0 && dx > 0);
+        if (!(e > 0 || (e == 0 && owns))) return false;
+    }
+    return true;
+}
+
+// any accepted hit in [tmin, tmax]; masked candidates pass the .rahit alpha test
+bool traverseAnyAccepted(const Oracle& o, const Bvh& bvh, const Ray& r, bool alphaTest, Stats& st)
+{
+    if (bvh.empty()) return false;
+    V3 inv = safeInv(r.d);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const BNode& n = bvh.nodes[stack[--sp]];
+        st.nodes++;
+        if (!boxHit(n.box, r.o, inv, r.tmin, r.tmax)) continue;
+        if (n.left < 0) {
+            for (uint32_t i = n.first; i < n.first + n.count; ++i) {
+                st.tris++;
+                const WTri& t = o.tris[bvh.order[i]];
+                float tt, u, v;
+                bool bf;
+                if (intersectTri(r, t, r.tmax, &tt, &u, &v, &bf) && (!alphaTest || alphaAccept(o, t, u, v))) return true;
+            }
+        } else {
+            if (sp + 2 > 128) { std::fprintf(stderr, "oracle: BVH stack overflow\n"); std::abort(); }
+            stack[sp++] = static_cast<uint32_t>(n.right);
+            stack[sp++] = static_cast<uint32_t>(n.left);
+        }
+    }
+    return false;
+}
+
+inline uint8_t unorm8(float x) { return static_cast<uint8_t>(std::nearbyint(saturate(x) * 255.0f)); }
+
+// bakeAmbientOcclusion.rgen:33-118 for texel p (covered: triIdx1 = triangle + 1)
+void bakeTexel(const Oracle& o, const ArkRTTriangleMesh& m, uint32_t p, uint32_t triIdx1, const uint16_t* bary, uint32_t samples,
+               bool bent, uint8_t* out, Stats& st)
+{
+    uint32_t tri = triIdx1 - 1u;
+    V3 bc = v3(f16_to_f32(bary[0]), f16_to_f32(bary[1]), f16_to_f32(bary[2]));
+    V3 pp[3], nn[3];
+    for (int k = 0; k < 3; ++k) {
+        uint32_t idx = o.indices[static_cast<size_t>(m.first_index) + 3u * tri + k];
+        size_t vi = static_cast<size_t>(m.first_vertex) + idx;
+        pp[k] = v3(o.positions[vi * 3 + 0], o.positions[vi * 3 + 1], o.positions[vi * 3 + 2]);
+        const ArkRTVertex& v = o.vertices[vi];
+        nn[k] = v3(v.normal[0], v.normal[1], v.normal[2]);
+    }
+    V3 position = pp[0] * bc.x + pp[1] * bc.y + pp[2] * bc.z;
+    V3 normal = normalize(nn[0] * bc.x + nn[1] * bc.y + nn[2] * bc.z);
+    const float tmin = 0.0005f, tmax = 100.0f;
+    float ambientOcclusionAcc = 0.0f;
+    V3 unoccludedDirectionAcc = splat(0.0f);
+    Rng rng(p); // seedRandom(x + y * W)
+    for (uint32_t sampleIdx = 0; sampleIdx < samples; ++sampleIdx) {
+        // rejection loop, bounded: a texel whose seed hashes to 0 (wang_hash(61) == 0)
+        // has a xorshift state stuck at 0, drawing (0, 0, -1) forever; with a +z normal
+        // the reference loops without end (a GPU hang). After kBakeMaxDraws rejected
+        // draws the normal itself is used (DESIGN.md §AO bake).
+        V3 sampleDirection;
+        int draws = 0;
+        do {
+            sampleDirection = normal + rng.randomPointOnSphere();
+        } while (dot(sampleDirection, sampleDirection) <= 1e-4f && ++draws < kBakeMaxDraws);
+        if (dot(sampleDirection, sampleDirection) <= 1e-4f) sampleDirection = normal;
+        sampleDirection = normalize(sampleDirection);
+        Ray r { position, sampleDirection, tmin, tmax };
+        bool hit = traverseAnyAccepted(o, o.bvhOpaque, r, false, st) || traverseAnyAccepted(o, o.bvhMasked, r, true, st) ||
+                   traverseAnyAccepted(o, o.bvhBlend, r, false, st);
+        if (hit) ambientOcclusionAcc += 1.0f;
+        else unoccludedDirectionAcc = unoccludedDirectionAcc + sampleDirection;
+    }
+    if (bent) {
+        V3 bentNormal = unoccludedDirectionAcc / static_cast<float>(samples);
+        float bentCone = (kPi / 2.0f) / (kPi / 2.0f);
+        V3 enc = bentNormal * v3(0.5f, 0.5f, 0.5f) + v3(0.5f, 0.5f, 0.5f);
+        out[0] = unorm8(enc.x);
+        out[1] = unorm8(enc.y);
+        out[2] = unorm8(enc.z);
+        out[3] = unorm8(bentCone);
+    } else {
+        float ambientOcclusion = ambientOcclusionAcc / static_cast<float>(samples);
+        out[0] = unorm8(1.0f - ambientOcclusion);
+    }
+}
+
 } // namespace
 
 // ===========================================================================
@@ -1116,6 +1256,7 @@ int oracle_set_scene(void* ctx, const ArkDdgiScene* s, int threads)
     Oracle& o = *static_cast<Oracle*>(ctx);
     if (!s) return ARK_DDGI_E_INVALID_ARGUMENT;
     o.indices.assign(s->indices, s->indices + s->index_count);
+    o.positions.assign(s->positions, s->positions + 3 * static_cast<size_t>(s->vertex_count));
     o.vertices.assign(s->vertices, s->vertices + s->vertex_count);
     o.meshes.assign(s->meshes, s->meshes + s->mesh_count);
     o.materials.assign(s->materials, s->materials + s->material_count);
@@ -1373,6 +1514,65 @@ void oracle_get_stats(void* ctx, uint64_t* nodes, uint64_t* tris)
 }
 
 // ---- helper KAT exports ----------------------------------------------------
+// AO / bent-normal bake of instance `instance`'s mesh segment (include/ark_ddgi.h
+// ark_ddgi_bake_ao). Outputs: tri_idx [H][W] u32, bary [H][W][4] fp16, out [H][W]
+// (AO) or [H][W][4] (bent normals). Rows [row0, row1) of the ray pass only (the
+// parameterization covers the whole texture); `threads` host threads over texels.
+int oracle_bake_ao(void* ctx, uint32_t instance, uint32_t W, uint32_t H, uint32_t samples, int bent, uint32_t row0, uint32_t row1,
+                   uint32_t* triIdx, uint16_t* bary, uint8_t* out, int threads)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!o.hasScene || instance >= o.instances.size() || W == 0 || H == 0 || samples == 0) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const ArkRTInstance& inst = o.instances[instance];
+    const ArkRTTriangleMesh& m = o.meshes[inst.rt_mesh_index];
+    std::fill(triIdx, triIdx + static_cast<size_t>(W) * H, 0u);
+    for (uint32_t t = 0; t < inst.triangle_count; ++t) { // draw order: later triangles overwrite
+        BakeTri tr = bakeTriangle(o, m, t, W, H);
+        if (tr.area == 0) continue;
+        int64_t xmin = std::min(tr.x[0], std::min(tr.x[1], tr.x[2])), xmax = std::max(tr.x[0], std::max(tr.x[1], tr.x[2]));
+        int64_t ymin = std::min(tr.y[0], std::min(tr.y[1], tr.y[2])), ymax = std::max(tr.y[0], std::max(tr.y[1], tr.y[2]));
+        int px0 = static_cast<int>(std::max<int64_t>(0, (xmin - 128 + 255) >> 8)), px1 = static_cast<int>(std::min<int64_t>(W - 1, (xmax - 128) >> 8));
+        int py0 = static_cast<int>(std::max<int64_t>(0, (ymin - 128 + 255) >> 8)), py1 = static_cast<int>(std::min<int64_t>(H - 1, (ymax - 128) >> 8));
+        for (int py = py0; py <= py1; ++py)
+            for (int px = px0; px <= px1; ++px) {
+                int64_t w[3];
+                if (bakeCover(tr, px, py, w)) triIdx[static_cast<size_t>(py) * W + px] = t + 1u;
+            }
+    }
+    const size_t texels = static_cast<size_t>(W) * H;
+    for (size_t p = 0; p < texels; ++p) {
+        uint16_t* b = bary + 4 * p;
+        b[0] = b[1] = b[2] = b[3] = 0;
+        if (!triIdx[p]) continue;
+        BakeTri tr = bakeTriangle(o, m, triIdx[p] - 1u, W, H);
+        int64_t w[3];
+        bakeCover(tr, static_cast<int>(p % W), static_cast<int>(p / W), w);
+        float A = static_cast<float>(tr.area);
+        b[0] = f32_to_f16(static_cast<float>(w[0]) / A);
+        b[1] = f32_to_f16(static_cast<float>(w[1]) / A);
+        b[2] = f32_to_f16(static_cast<float>(w[2]) / A);
+        b[3] = 0x3c00u;
+    }
+    const int cpp = bent ? 4 : 1;
+    row1 = std::min(row1, H);
+    std::vector<Stats> tst(std::max(threads, 1));
+    parallelFor(static_cast<int>((row1 > row0 ? row1 - row0 : 0) * W), threads, [&](int i, int tid) {
+        size_t p = static_cast<size_t>(row0) * W + static_cast<size_t>(i);
+        uint8_t* dst = out + p * cpp;
+        if (!triIdx[p]) { // bakeAmbientOcclusion.rgen:44-51
+            if (bent) { dst[0] = dst[1] = dst[2] = 128; dst[3] = 255; }
+            else dst[0] = 0;
+            return;
+        }
+        bakeTexel(o, m, static_cast<uint32_t>(p), triIdx[p], bary + 4 * p, samples, bent != 0, dst, tst[tid]);
+    });
+    for (const Stats& t : tst) {
+        o.stats.nodes += t.nodes;
+        o.stats.tris += t.tris;
+    }
+    return 0;
+}
+
 uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
 uint32_t oracle_rand_xorshift(uint32_t s) { return rand_xorshift(s); }
 

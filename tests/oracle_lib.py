@@ -45,6 +45,8 @@ def load():
         lib.oracle_f32_to_f16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         lib.oracle_f16_to_f32.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         lib.oracle_fmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        lib.oracle_bake_ao.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _lib = lib
     return _lib
 
@@ -100,6 +102,18 @@ class Oracle:
         data = np.ascontiguousarray(data)
         rc = self.lib.oracle_write(self.h, which, data.ctypes.data, data.nbytes)
         assert rc == 0, rc
+
+    def bake_ao(self, instance: int, width: int, height: int, samples: int, bent: bool, rows=None, threads: int = 8):
+        """AO / bent-normal bake (oracle_bake_ao): (triangle index + 1, fp16 barycentrics,
+        output) arrays; `rows` = (row0, row1) limits the ray pass (CPU baseline samples)."""
+        r0, r1 = rows if rows is not None else (0, height)
+        tri = np.zeros((height, width), np.uint32)
+        bary = np.zeros((height, width, 4), np.uint16)
+        out = np.zeros((height, width, 4 if bent else 1), np.uint8)
+        rc = self.lib.oracle_bake_ao(self.h, instance, width, height, samples, int(bent), r0, r1, tri.ctypes.data, bary.ctypes.data,
+                                     out.ctypes.data, threads)
+        assert rc == 0, rc
+        return tri, bary, out
 
     def stats(self):
         n, t = C.c_uint64(), C.c_uint64()
