@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ao-bake", action="store_true", help="skip the config C1 AO bake line (GPU + CPU oracle)")
+    ap.add_argument("--ao-size", type=int, default=1024)
+    ap.add_argument("--ao-samples", type=int, default=64)
+    ap.add_argument("--ao-cpu-seconds", type=float, default=8.0)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "latest_pmc.json"),
                     help="PMC traffic summary written by tools/profile_pmc.py (optional)")
     return ap.parse_args()
@@ -231,6 +235,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, grid, R, args, exposure)
 
+    if rank == 0 and world == 1 and not args.no_ao_bake:
+        result["ao_bake"] = ao_bake_c1(args, torch, device)
+
     if rank == 0:
         print(json.dumps(result), flush=True)
     node.ctx.close()
@@ -282,6 +289,65 @@ def cpu_baseline(scene, grid, R, args, exposure):
         "sample": f"{done_probes} probes x {R} rays of the same C4 workload (probes 0..{done_probes - 1}), full update incl. shading/indirect/blend, {spent:.1f} s; oracle BVH build {build_s:.1f} s excluded",
         "probes_updated_per_s": round(done_probes / spent, 2),
     }
+
+
+def ao_bake_c1(args, torch, device):
+    """Config C1: AO bake of DamagedHelmet (15,452 triangles) at
+    ao_size^2 texels x ao_samples rays, on the GPU (ark_ddgi_bake_ao, wall-clock
+    timed around the three passes) and on the host cores with the CPU
+    oracle (the repo's own CPU AO ray path; a bounded band of rows, same rules,
+    bit-identical results). Rays = covered texels x samples."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+    from arkoserenderer_amd import abi
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+    from parity import make_desc
+
+    W = H = args.ao_size
+    n_s = args.ao_samples
+    scene = S.damaged_helmet()
+    grid = D.ProbeGrid((1, 1, 1), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=1, probe_updates_per_frame=1, max_rays_per_probe=1, max_probe_updates=1)
+    ctx = D.DDGIContext(grid, 100.0, cfg, device=device.index or 0)
+    ctx.set_scene(scene)
+    ctx.bake_ao(0, W, H, n_s, False)  # warm-up (context stream)
+    ctx.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.bake_ao(0, W, H, n_s, False)
+    ctx.synchronize()
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    tri = ctx.bake_read(abi.ARK_BAKE_TRIANGLE_INDEX)
+    covered = int(np.count_nonzero(tri))
+    gpu_out = ctx.bake_read(abi.ARK_BAKE_OUTPUT)
+    ctx.close()
+    res = {"workload": f"C1: DamagedHelmet AO bake {W}x{H} texels x {n_s} samples ({covered} covered texels)",
+           "gpu_mrays_s": round(covered * n_s / (gpu_ms * 1e-3) / 1e6, 2), "gpu_ms": round(gpu_ms, 3)}
+    if args.no_cpu_baseline:
+        return res
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    orc = O.Oracle(make_desc(grid, 100.0, cfg))
+    orc.set_scene(scene, threads)
+    row0, rows, spent, rays, exact = 0, 4, 0.0, 0, True
+    while spent < args.ao_cpu_seconds and row0 < H:
+        r1 = min(H, row0 + rows)
+        t = time.perf_counter()
+        otri, _, out = orc.bake_ao(0, W, H, n_s, False, rows=(row0, r1), threads=threads)
+        el = time.perf_counter() - t
+        spent += el
+        rays += int(np.count_nonzero(otri[row0:r1])) * n_s
+        exact = exact and np.array_equal(out[row0:r1], gpu_out[row0:r1])
+        row0 = r1
+        rows = int(max(4, rows * min(4.0, args.ao_cpu_seconds / 3 / max(el, 1e-3))))
+    orc.close()
+    res["cpu_baseline"] = {"value": round(rays / spent / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                           "sample": f"rows 0..{row0 - 1} of the same bake ({rays} rays, {spent:.1f} s, parameterization passes included)",
+                           "bit_exact_vs_gpu": bool(exact)}
+    return res
 
 
 if __name__ == "__main__":
