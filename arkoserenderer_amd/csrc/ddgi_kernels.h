@@ -131,6 +131,7 @@ struct FrameArgs {
     uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
     uint32_t light_count;    // has_sun + spot lights
     uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
+    uint32_t grab_chunk;     // trace / shadow: rays a wave takes from its partition head at once (<= 64)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };

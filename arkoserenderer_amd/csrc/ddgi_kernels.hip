@@ -565,8 +565,7 @@ __device__ __forceinline__ uint32_t xccId()
 }
 
 // Same partitioned dequeue over a flat list of `total` items (shadow rays).
-template<uint32_t CHUNK>
-__device__ __forceinline__ void grabItems(uint32_t* heads, uint32_t total, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+__device__ __forceinline__ void grabItems(uint32_t* heads, uint32_t total, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e, uint32_t CHUNK)
 {
     b = e = 0;
     for (; tried < kRayParts; ++tried) {
@@ -591,8 +590,7 @@ __device__ __forceinline__ uint32_t partRayBegin(const FrameArgs& f, uint32_t p)
 // One lane only: next chunk of at most CHUNK consecutive rays from the head
 // counters at `heads`, or b >= e when every partition is drained.
 // `tried` = partitions already found empty (uniform over the caller's group).
-template<uint32_t CHUNK>
-__device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+__device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e, uint32_t CHUNK)
 {
     b = e = 0;
     for (; tried < kRayParts; ++tried) {
@@ -644,7 +642,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             uint32_t fb = 0, fe = 0; // fresh chunk [fb, fe)
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) grabRays<64u>(f, f.ray_counter, home, t, b, e);
+                if (lane == 0) grabRays(f, f.ray_counter, home, t, b, e, f.grab_chunk);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);
@@ -1066,7 +1064,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t b, e;
-            grabRays<static_cast<uint32_t>(kShadeChunk)>(f, heads, home, tried, b, e);
+            grabRays(f, heads, home, tried, b, e, static_cast<uint32_t>(kShadeChunk));
             counts[0] = 0;
             counts[2] = b;
             counts[3] = e;
@@ -1264,7 +1262,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             uint32_t fb = 0, fe = 0;
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) grabItems<64u>(f.shadow_heads, total, home, t, b, e);
+                if (lane == 0) grabItems(f.shadow_heads, total, home, t, b, e, f.grab_chunk);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);

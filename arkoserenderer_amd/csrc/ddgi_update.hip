@@ -101,7 +101,7 @@ __device__ __forceinline__ float visWeightAbs(float a, float sharp, int ns)
 struct UpdateLds {
     float4* ray;    // [P][R + pad]  rotated direction + clamped distance
     float* d2;      // [P][R + pad]  clamped distance squared
-    float4* rad;    // [P][R + pad]  surfel radiance + signed distance
+    uint2* rad;     // [P][R + pad]  raw fp16 surfel: radiance rgb + signed distance
     uint32_t* vis;  // [P][18*18]    visibility tile (interior + border)
     uint2* irr;     // [P][10*10]    irradiance tile
     uint8_t* cls;   // [P][R]        offset ray class
@@ -116,8 +116,8 @@ __device__ __forceinline__ UpdateLds updateLds(uint32_t R)
     unsigned char* p = smem;
     L.ray = reinterpret_cast<float4*>(p);
     p += sizeof(float4) * kUpdateProbes * L.stride;
-    L.rad = reinterpret_cast<float4*>(p);
-    p += sizeof(float4) * kUpdateProbes * L.stride;
+    L.rad = reinterpret_cast<uint2*>(p);
+    p += sizeof(uint2) * kUpdateProbes * L.stride;
     L.irr = reinterpret_cast<uint2*>(p);
     p += sizeof(uint2) * kUpdateProbes * 100;
     L.vis = reinterpret_cast<uint32_t*>(p);
@@ -131,7 +131,7 @@ __device__ __forceinline__ UpdateLds updateLds(uint32_t R)
 size_t probe_update_lds_bytes(uint32_t R)
 {
     const size_t stride = R + 4;
-    return kUpdateProbes * (stride * (16 + 16 + 4) + 100 * 8 + 324 * 4 + R);
+    return kUpdateProbes * (stride * (16 + 8 + 4) + 100 * 8 + 324 * 4 + R); // 38.6 KB at R = 256: 4 workgroups per CU
 }
 
 // the orbit of quadrant texel (qx, qy) of a res x res tile: t, x-mirror t', antipode -t, -t'
@@ -217,8 +217,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             const float dd = fminf_(fabsf_(a), maxDistance);
             L.ray[p * L.stride + s] = make_float4(d.x, d.y, d.z, dd);
             L.d2[p * L.stride + s] = square(dd);
-            L.rad[p * L.stride + s] = make_float4(f16_to_f32(static_cast<uint16_t>(sv.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(sv.x >> 16)),
-                                                  f16_to_f32(static_cast<uint16_t>(sv.y & 0xffffu)), a);
+            L.rad[p * L.stride + s] = sv; // fp16 as stored: converted where used (exact)
         }
     }
     __syncthreads();
@@ -276,13 +275,15 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             orbitTexels(IR, j & 3, j >> 2, tx, ty);
             const V3 t = texelDirection(IR, tx[0], ty[0]);
             const float4* ray = L.ray + p * L.stride;
-            const float4* rad = L.rad + p * L.stride;
+            const uint2* rad = L.rad + p * L.stride;
             V3 acc[4] = { splat(0.0f), splat(0.0f), splat(0.0f), splat(0.0f) };
             float tw[4] = { 0.0f, 0.0f, 0.0f, 0.0f };
 #pragma unroll 2
             for (uint32_t s = 0; s < R; ++s) {
                 const float4 r = ray[s];
-                const float4 c = rad[s];
+                const uint2 cw = rad[s];
+                const float4 c = make_float4(f16_to_f32(static_cast<uint16_t>(cw.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(cw.x >> 16)),
+                                             f16_to_f32(static_cast<uint16_t>(cw.y & 0xffffu)), 0.0f);
                 const float px = t.x * r.x, py = t.y * r.y, pz = t.z * r.z;
                 const float d1 = (px + py) + pz;
                 const float d2 = (py - px) + pz;
@@ -338,7 +339,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                     const uint32_t s = s0 + static_cast<uint32_t>(ln);
                     uint32_t cls = 0;
                     if (s < R) {
-                        const float a = L.rad[q * L.stride + s].w;
+                        const float a = f16_to_f32(static_cast<uint16_t>(L.rad[q * L.stride + s].y >> 16));
                         cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
                         L.cls[q * R + s] = static_cast<uint8_t>(cls);
                     }
