@@ -118,7 +118,7 @@ struct ArkDdgiCtx {
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0;
     // scene
     bool hasScene = false;
-    DeviceBuffer nodes, tris, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
+    DeviceBuffer nodes, tris, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
     std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
     std::vector<ArkRTTriangleMesh> meshHost;
     // AO bake results (ark_ddgi_bake_ao)
@@ -291,7 +291,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
-                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
+                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->triNormals, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
     for (auto& ev : ctx->ev)
@@ -495,9 +495,34 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, ctx->texInfos, infos.data(), infos.size())) != 0) return rc;
     if ((rc = upload(ctx, ctx->texels, texels.data(), texels.size())) != 0) return rc;
     if ((rc = upload(ctx, ctx->spots, gspots.data(), gspots.size())) != 0) return rc;
+    {
+        // per-triangle vertex normals for the shadow rays traced inside the primary
+        // traversal (hitShadingNormal); only needed when the scene has lights
+        std::vector<float> tn;
+        if (s->has_directional_light || s->spot_light_count > 0) {
+            tn.resize(allTris.size() * 12, 0.0f);
+            for (size_t t = 0; t < allTris.size(); ++t) {
+                uint32_t inst, prim;
+                std::memcpy(&inst, &allTris[t].t2[1], 4);
+                std::memcpy(&prim, &allTris[t].t2[2], 4);
+                const ArkRTTriangleMesh& mesh = s->meshes[s->instances[inst].rt_mesh_index];
+                float* o = tn.data() + t * 12;
+                for (int q = 0; q < 3; ++q) {
+                    const uint32_t idx = s->indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
+                    const float* v = reinterpret_cast<const float*>(s->vertices) + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+                    for (int k = 0; k < 3; ++k) o[q * 3 + k] = v[2 + k];
+                }
+                std::memcpy(o + 9, &inst, 4);
+            }
+        } else {
+            tn.assign(12, 0.0f);
+        }
+        if ((rc = upload(ctx, ctx->triNormals, tn.data(), tn.size())) != 0) return rc;
+    }
     SceneArgs& sc = ctx->scene;
     sc.nodes = ctx->nodes.as<GpuBvh8Node>();
     sc.tris = ctx->tris.as<GpuTriangle>();
+    sc.tri_normals = ctx->triNormals.as<float4>();
     sc.root_opaque = roots[0];
     sc.root_masked = roots[1];
     sc.root_blend = roots[2];
@@ -622,8 +647,26 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         f.front_recs = reinterpret_cast<FrontRec*>(w);
         f.front_lights = reinterpret_cast<FrontLight*>(w + rays * sizeof(FrontRec));
         f.shadow_rays = reinterpret_cast<ShadowRay*>(w + rays * (sizeof(FrontRec) + ctx->lightCount * sizeof(FrontLight)));
+        // fused path: per-ray light bits alias the (then unused) front records
+        f.shadow_bits = reinterpret_cast<uint32_t*>(w);
     }
     f.light_count = ctx->lightCount;
+    {
+        // shadow rays traced inside the primary traversal (default) or by their own
+        // persistent launch after shading (ARK_SHADOWS=split): same bits either way
+        // three equivalent schedules (identical bits): "pre" (default) generates and
+        // traces the shadow rays between traversal and shading, so shading finishes
+        // every surfel in one pass; "split" records per-light terms in shading and
+        // finishes them after the shadow launch; "fused" traces the shadow rays in
+        // the primary traversal's lanes (measured slower: DESIGN.md §3)
+        const char* se = std::getenv("ARK_SHADOWS"); // read per frame: tests flip it in-process
+        int mode = 2;
+        if (se && std::strcmp(se, "split") == 0) mode = 0;
+        else if (se && std::strcmp(se, "fused") == 0) mode = 1;
+        // the pre schedule packs (ray << 4 | light) into 32 bits
+        if (static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax >= (1ull << 28)) mode = 0;
+        f.fused_shadows = f.light_count > 0 ? mode : 0;
+    }
     {
         // refill idle trace lanes in batches of >= 8: the refill (pool atomic, slot and
         // direction loads) then stalls a wave once per 8 finished rays, and the rays it
@@ -668,10 +711,15 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
         // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
         // rank it waits here for the previous exchange (the traversal above did not)
+        if (f.fused_shadows == 2) {
+            ARK_HIP(launch_shadow_gen(ctx->scene, f, s));
+            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
+        }
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], s));
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
-        if (f.light_count > 0) {
+        if (f.fused_shadows == 0 && f.light_count > 0) {
             ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
             ARK_HIP(launch_shade_finish(f, s));
         }
@@ -681,6 +729,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
+            ARK_HIP(hipEventRecord(ctx->ev[5], s));
             ARK_HIP(hipEventRecord(ctx->ev[2], s));
             ARK_HIP(hipEventRecord(ctx->ev[4], s));
         }
@@ -826,9 +875,14 @@ int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out, int count)
     float ms[5] = {};
     ARK_HIP(hipEventElapsedTime(&ms[0], ctx->ev[0], ctx->ev[3]));
     ARK_HIP(hipEventElapsedTime(&ms[1], ctx->ev[0], ctx->ev[1]));
-    ARK_HIP(hipEventElapsedTime(&ms[2], ctx->ev[1], ctx->ev[2]));
+    // shade = ev5 -> ev2; shadow = (ev1 -> ev5) + (ev2 -> ev4): whichever side of
+    // shading the schedule put the shadow rays on (the other interval is ~0)
+    float pre = 0.0f, post = 0.0f;
+    ARK_HIP(hipEventElapsedTime(&ms[2], ctx->ev[5], ctx->ev[2]));
     ARK_HIP(hipEventElapsedTime(&ms[3], ctx->ev[4], ctx->ev[3]));
-    ARK_HIP(hipEventElapsedTime(&ms[4], ctx->ev[2], ctx->ev[4]));
+    ARK_HIP(hipEventElapsedTime(&pre, ctx->ev[1], ctx->ev[5]));
+    ARK_HIP(hipEventElapsedTime(&post, ctx->ev[2], ctx->ev[4]));
+    ms[4] = pre + post;
     for (int i = 0; i < count && i < 5; ++i) out[i] = ms[i];
     return ARK_DDGI_OK;
 }

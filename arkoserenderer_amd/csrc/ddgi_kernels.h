@@ -79,6 +79,10 @@ struct SceneArgs {
     float sun_color[3];
     float sun_dir[3];
     const GpuSpotLight* spots;
+    // [triangle] 3 x float4: object-space vertex normals n0, n1, n2 (9 floats) and the
+    // instance index; BVH triangle order. Lets k_trace_primary<SHADOWS> find the
+    // shading normal with two dependent loads instead of five (set when lights exist).
+    const float4* tri_normals;
 
     __device__ __forceinline__ int resolveTexture(int idx) const
     {
@@ -132,6 +136,8 @@ struct FrameArgs {
     uint32_t light_count;    // has_sun + spot lights
     uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
     uint32_t grab_chunk;     // trace / shadow: rays a wave takes from its partition head at once (<= 64)
+    int32_t fused_shadows;   // 0 split (records + k_shade_finish); 1 traced inside k_trace_primary; 2 k_shadow_gen + k_trace_shadow before shading
+    uint32_t* shadow_bits;   // [window_rays] lit light bits 0-15, occluded bits 16-31 (fused path)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };
@@ -159,6 +165,7 @@ hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
+hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s);
 hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s);
 size_t shade_work_bytes(uint64_t rays, uint32_t lights);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);

@@ -541,6 +541,54 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
     return false;
 }
 
+// opaque.rchit:118-131: world-space shading normal of a front hit. The trace
+// kernel's shadow phase and the shading kernel both evaluate exactly this
+// expression, so they agree on N (and on which lights need a shadow ray).
+__device__ __forceinline__ V3 hitShadingNormal(const SceneArgs& sc, uint32_t tri, float hu, float hv)
+{
+    const float4* tn = sc.tri_normals + 3u * static_cast<size_t>(tri);
+    const float4 a = tn[0], b = tn[1], c = tn[2];
+    const uint32_t inst = __float_as_uint(c.y);
+    const float* M = sc.instances[inst].normal_matrix;
+    const float bx = 1.0f - hu - hv, by = hu, bz = hv;
+    // same operation sequence as k_shade (opaque.rchit:118-131)
+    V3 N = normalize(v3(a.x, a.y, a.z) * bx + v3(a.w, b.x, b.y) * by + v3(b.z, b.w, c.x) * bz);
+    V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
+    return normalize(Nw);
+}
+
+// opaque.rchit:56-103: lights with LdotN > 0 (bit l: sun first, then spots in order)
+__device__ __forceinline__ uint32_t litLightMask(const SceneArgs& sc, V3 N)
+{
+    uint32_t need = 0, l = 0;
+    if (sc.has_sun) {
+        const V3 Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+        if (dot(Ld, N) > 0.0f) need |= 1u;
+        l++;
+    }
+    for (int li = 0; li < sc.spot_count; ++li, ++l) {
+        const V3 Ld = -normalize(v3(sc.spots[li].direction[0], sc.spots[li].direction[1], sc.spots[li].direction[2]));
+        if (dot(Ld, N) > 0.0f) need |= 1u << l;
+    }
+    return need;
+}
+
+// Shadow ray of light l from hit point X (opaque.rchit:35-54 + :56-103): sun toward
+// -sunDirection with tmax 2 zFar, spot toward its position with tmax distance - 0.001.
+__device__ __forceinline__ void shadowRayOf(const SceneArgs& sc, float zFar, uint32_t l, V3 X, V3* dir, float* tmax)
+{
+    if (sc.has_sun && l == 0) {
+        *dir = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+        *tmax = 2.0f * zFar;
+        return;
+    }
+    const GpuSpotLight& sl = sc.spots[l - (sc.has_sun ? 1u : 0u)];
+    const V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - X;
+    const float distanceToLight = length(toLight);
+    *dir = toLight / distanceToLight;
+    *tmax = distanceToLight - 0.001f;
+}
+
 // ---------------------------------------------------------------------------
 // 2. primary traversal (persistent, per-lane wave64 ballot refill)
 // ---------------------------------------------------------------------------
@@ -606,7 +654,12 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
     }
 }
 
-template<bool COUNT, int WPE>
+// SHADOWS: after a ray's closest hit is known, a front hit traces its shadow rays
+// (one per lit light, any-hit over all hit-mask classes, opaque.rchit:35-54) in the
+// same lane before the lane takes a new ray, and stores {lit, occluded} light bits
+// per ray; the shading kernel then finishes every surfel in one pass. One
+// persistent launch instead of two: no second ramp and tail.
+template<bool COUNT, int WPE, bool SHADOWS>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_primary(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
@@ -631,6 +684,36 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
+    // shadow phase (SHADOWS): pass 2 + class; o = hit point, d = light direction,
+    // h.t = the shadow ray's tmax; bits 0-15 lit lights, 16-31 occluded, sl = current light
+    uint32_t lightBits = 0, sl = 0;
+    const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
+    const float shadowTmin = 0.025f; // opaque.rchit:44
+    uint32_t cShadow = 0, cShNodes = 0, cShTris = 0;
+    // next lit light after sl with a non-empty interval: sets up its ray, or false
+    auto nextShadowRay = [&](uint32_t after) -> bool { // after = 32: from the first light
+        uint32_t rem = lightBits & 0xffffu;
+        if (after < 16u) rem &= ~((2u << after) - 1u);
+        while (rem) {
+            sl = static_cast<uint32_t>(__builtin_ctz(rem));
+            rem &= rem - 1u;
+            float tmaxS;
+            shadowRayOf(sc, f.z_far, sl, o, &d, &tmaxS);
+            if (!(tmaxS >= shadowTmin)) continue; // empty interval: miss shader, not occluded
+            h.t = tmaxS;
+            idir = safeInv(d);
+            oct = rayOctant(idir);
+            int c = 0;
+            while (c < 3 && roots[c] < 0) ++c;
+            if (c == 3) continue;
+            pass = 2 + c;
+            st.depth = 0;
+            ts = TravState { static_cast<uint32_t>(roots[c]), rootGroupBits(), 0u, 0u };
+            if (COUNT) cShadow++;
+            return true;
+        }
+        return false;
+    };
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
@@ -682,6 +765,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (__ballot(active) == 0) break;
         if (COUNT) cIter++;
+        bool shadowHit = false;
         if (active) {
             // ---- one step: a pending leaf triangle, or the next node --------------
             if (!travDone(ts, st)) {
@@ -690,7 +774,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 uint32_t inst, prim;
                 float tt, uu, vv;
                 bool bf;
-                if (travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, cNodes, cTris) &&
+                const bool shadowPass = SHADOWS && pass >= 2;
+                uint32_t& cN = shadowPass ? cShNodes : cNodes;
+                uint32_t& cT = shadowPass ? cShTris : cTris;
+                const bool cand = travCompute(fx, ts, o, d, idir, oct, shadowPass ? shadowTmin : tmin, h.t, tt, uu, vv, bf, inst, prim, cN, cT);
+                if (shadowPass) shadowHit = cand; // any hit occludes (Opaque flag: no alpha test)
+                else if (cand &&
                     !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
                     !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
                     h.t = tt;
@@ -703,7 +792,26 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 }
             }
         }
-        if (active) {
+        if (SHADOWS && active && pass >= 2 && (shadowHit || travDone(ts, st))) {
+            // ---- shadow ray of light sl finished: occluded, or its classes exhausted
+            bool rayDone = true;
+            if (shadowHit) {
+                lightBits |= 1u << (16 + sl);
+            } else {
+                int c = pass - 2 + 1;
+                while (c < 3 && roots[c] < 0) ++c;
+                if (c < 3) {
+                    pass = 2 + c;
+                    st.depth = 0;
+                    ts = TravState { static_cast<uint32_t>(roots[c]), rootGroupBits(), 0u, 0u };
+                    rayDone = false;
+                }
+            }
+            if (rayDone && !nextShadowRay(sl)) {
+                f.shadow_bits[ray] = lightBits;
+                active = false;
+            }
+        } else if (active) {
             // ---- pass finished -----------------------------------------------------
             if (travDone(ts, st)) {
                 bool finished = true;
@@ -723,11 +831,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     }
                 }
                 if (finished) {
+                    GpuHit out;
                     if (pass == 1 && h.tri == kNoHit) {
                         // masked pass found nothing: the opaque result (already stored) stands
-                        if (COUNT && f.hits[ray].tri != kNoHit) cHits++;
+                        out = f.hits[ray];
+                        if (COUNT && out.tri != kNoHit) cHits++;
                     } else {
-                        GpuHit out;
                         if (h.tri == kNoHit) {
                             out.t = __builtin_bit_cast(float, 0x7f800000u);
                             out.u = out.v = 0.0f;
@@ -742,6 +851,15 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                         f.hits[ray] = out;
                     }
                     active = false;
+                    if (SHADOWS && out.tri != kNoHit && !(out.t < 0.0f)) {
+                        // front hit (raygen.rgen:200-206): shadow rays of its lit lights
+                        lightBits = f.light_count ? litLightMask(sc, hitShadingNormal(sc, out.tri, out.u, out.v)) : 0u;
+                        if (lightBits) {
+                            o = o + out.t * d; // hit point as opaque.rchit computes it
+                            active = nextShadowRay(32u);
+                        }
+                        if (!active) f.shadow_bits[ray] = lightBits;
+                    }
                 }
             }
         }
@@ -751,6 +869,11 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[2], static_cast<unsigned long long>(cHits));
         if (lane == 0) atomicAdd(&f.counters[7], static_cast<unsigned long long>(cIter));
+        if (SHADOWS) {
+            atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
+            atomicAdd(&f.counters[4], static_cast<unsigned long long>(cShNodes));
+            atomicAdd(&f.counters[5], static_cast<unsigned long long>(cShTris));
+        }
     }
 }
 
@@ -1049,7 +1172,11 @@ __device__ __forceinline__ uint32_t waveAlloc(uint32_t* ctr, uint32_t n)
     return base + x - n;
 }
 
-template<bool COUNT, int WPE>
+// FUSED: the shadow rays were traced by k_trace_primary<..., SHADOWS = true>, whose
+// per-ray light bits say which lit lights are occluded: every surfel is finished
+// here, base (+ T or Z per lit light, in light order) + indirect, as k_shade_finish
+// adds them in the split path.
+template<bool COUNT, int WPE, bool FUSED>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
@@ -1154,9 +1281,14 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     if (dot(Ld, N) > 0.0f) need |= 1u << l;
                 }
             }
-            const uint32_t fk = waveAlloc(f.front_count, need != 0 ? 1u : 0u);
-            uint32_t sj = waveAlloc(f.shadow_count, static_cast<uint32_t>(__builtin_popcount(need)));
+            uint32_t fk = 0, sj = 0, occ = 0;
+            if (!FUSED) {
+                fk = waveAlloc(f.front_count, need != 0 ? 1u : 0u);
+                sj = waveAlloc(f.shadow_count, static_cast<uint32_t>(__builtin_popcount(need)));
+            }
             if (!valid) continue;
+            if (FUSED) occ = f.shadow_bits[ray] >> 16;
+            V3 color = base;
             const V3 V = -dir;
             const V3 hitPoint = origin + T * dir;
             uint32_t l = 0;
@@ -1168,9 +1300,13 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     const V3 lc = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]);
                     const V3 tT = brdf * LdotN * (lc * 1.0f);
                     const V3 tZ = brdf * LdotN * (lc * 0.0f);
-                    f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
-                    f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far),
-                                                      make_float4(Ld.x, Ld.y, Ld.z, __uint_as_float((fk << 4) | l)) };
+                    if (FUSED) {
+                        color = color + ((occ >> l) & 1u ? tZ : tT);
+                    } else {
+                        f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
+                        f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far),
+                                                          make_float4(Ld.x, Ld.y, Ld.z, __uint_as_float((fk << 4) | l)) };
+                    }
                 }
                 l++;
             }
@@ -1201,9 +1337,13 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                         V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
                         V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
                         V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
-                    f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
-                    f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f),
-                                                      make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, __uint_as_float((fk << 4) | l)) };
+                    if (FUSED) {
+                        color = color + ((occ >> l) & 1u ? tZ : tT);
+                    } else {
+                        f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
+                        f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f),
+                                                          make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, __uint_as_float((fk << 4) | l)) };
+                    }
                 }
             }
             // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
@@ -1213,7 +1353,9 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const V3 irradiance = sampleDDGI<ARK_DDGI_GATHER_BATCH>(f, hitPoint, N, Vi);
             const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
-            if (need == 0) {
+            if (FUSED) {
+                storeSurfel(f, ray, color + bi, T);
+            } else if (need == 0) {
                 storeSurfel(f, ray, base + bi, T);
             } else {
                 f.front_recs[fk] = FrontRec { make_float4(base.x, base.y, base.z, T), make_float4(bi.x, bi.y, bi.z, __uint_as_float(ray)), need, 0u };
@@ -1316,7 +1458,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 occluded = travCompute(fx, ts, o, d, idir, oct, tmin, tmax, tt, uu, vv, bf, inst, prim, cNodes, cTris);
             }
             if (occluded) {
-                atomicOr(&f.front_recs[owner >> 4].occ, 1u << (owner & 15u));
+                if (f.fused_shadows) atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
+                else atomicOr(&f.front_recs[owner >> 4].occ, 1u << (owner & 15u));
                 active = false;
             } else if (travDone(ts, st)) {
                 ++pass;
@@ -1334,6 +1477,90 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[5], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
+    }
+}
+
+// Shadow rays before shading (fused_shadows == 2): one thread per window ray in
+// slot order; a front hit (raygen.rgen:200-206) stores its lit-light mask
+// (opaque.rchit:56-103, LdotN > 0 with the shading normal) in shadow_bits[ray] and
+// appends one shadow ray per lit light, owner = (ray << 4) | light. k_trace_shadow
+// then sets the occluded bits 16 + light, and k_shade<FUSED> finishes every surfel
+// in one pass (no per-light records, no finishing kernel).
+// Block b owns the kGenSteps x 256 consecutive queue positions from b * kGenSpan:
+// pass 1 stores the light masks (LDS + shadow_bits) and counts; one global atomic
+// per block reserves the block's shadow rays (a per-wave atomic on the one list
+// counter serialises at L2: 1.45 ms for 131K waves on C4); pass 2 writes them in
+// position order (wave scans), so a shadow-kernel grab of 64 list entries holds the
+// neighbouring rays of one probe.
+constexpr uint32_t kGenSteps = 16, kGenSpan = kGenSteps * 256u;
+
+__device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
+{
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= static_cast<uint32_t>(off)) x += y;
+    }
+    return x;
+}
+
+__global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
+{
+    __shared__ uint32_t bitsL[kGenSpan];
+    __shared__ uint32_t waveOff[kGenSteps][4];
+    __shared__ uint32_t blockBase;
+    const uint32_t total = f.window_rays;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t first = blockIdx.x * kGenSpan;
+    for (uint32_t k = 0; k < kGenSteps; ++k) {
+        const uint32_t pos = first + k * 256u + threadIdx.x;
+        uint32_t bits = 0;
+        if (pos < total) {
+            const uint32_t q = pos / f.R;
+            const uint32_t ray = slotAt(f, q) * f.R + (pos - q * f.R);
+            const GpuHit hit = f.hits[ray];
+            if (hit.tri != kNoHit && !(hit.t < 0.0f)) {
+                bits = litLightMask(sc, hitShadingNormal(sc, hit.tri, hit.u, hit.v));
+                f.shadow_bits[ray] = bits;
+            }
+        }
+        bitsL[k * 256u + threadIdx.x] = bits;
+        const uint32_t x = waveInclusiveScan(static_cast<uint32_t>(__builtin_popcount(bits)));
+        if (__lane_id() == 63u) waveOff[k][wave] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < kGenSteps; ++k)
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t c = waveOff[k][w];
+                waveOff[k][w] = run;
+                run += c;
+            }
+        blockBase = run ? atomicAdd(f.shadow_count, run) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < kGenSteps; ++k) {
+        const uint32_t bits = bitsL[k * 256u + threadIdx.x];
+        const uint32_t c = static_cast<uint32_t>(__builtin_popcount(bits));
+        uint32_t sj = blockBase + waveOff[k][wave] + waveInclusiveScan(c) - c;
+        if (bits == 0) continue;
+        const uint32_t pos = first + k * 256u + threadIdx.x;
+        const uint32_t q = pos / f.R;
+        const uint32_t ray = slotAt(f, q) * f.R + (pos - q * f.R);
+        const float t = f.hits[ray].t;
+        V3 origin, dir;
+        rayOf(f, ray, &origin, &dir);
+        const V3 hitPoint = origin + t * dir;
+        for (uint32_t b = bits; b; b &= b - 1) {
+            const uint32_t l = static_cast<uint32_t>(__builtin_ctz(b));
+            V3 ld;
+            float tmax;
+            shadowRayOf(sc, f.z_far, l, hitPoint, &ld, &tmax);
+            f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax),
+                                              make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
+        }
     }
 }
 
@@ -1680,10 +1907,19 @@ hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     const int v = trace_variant();
-    if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_trace_primary<false, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    if (f.fused_shadows == 1) {
+        // the shadow state costs ~20 VGPRs: 6 waves/EU would spill, 5 is the default
+        static const int vf = [] { const char* e = std::getenv("ARK_TRACE_WPE_FUSED"); return e ? std::atoi(e) : 5; }();
+        if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+        else if (vf == 4) hipLaunchKernelGGL((dev::k_trace_primary<false, 4, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+        else if (vf == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+        else hipLaunchKernelGGL((dev::k_trace_primary<false, 5, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+        return hipGetLastError();
+    }
+    if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_trace_primary<false, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -1695,10 +1931,15 @@ size_t shade_work_bytes(uint64_t rays, uint32_t lights)
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     const int v = shade_variant();
-    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_shade<false, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    if (f.fused_shadows) {
+        if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+        else hipLaunchKernelGGL((dev::k_shade<false, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+        return hipGetLastError();
+    }
+    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_shade<false, 1, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -1706,6 +1947,14 @@ hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t
 {
     if (count) hipLaunchKernelGGL((dev::k_trace_shadow<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else hipLaunchKernelGGL((dev::k_trace_shadow<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s)
+{
+    const uint32_t blocks = (f.window_rays + dev::kGenSpan - 1u) / dev::kGenSpan;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_shadow_gen, dim3(blocks), dim3(256), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -1727,18 +1976,18 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
 const void* kernel_trace_primary_ptr(bool count)
 {
     const int v = trace_variant();
-    if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1>);
-    if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5>);
-    if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6>);
-    return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1>);
+    if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1, false>);
+    if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5, false>);
+    if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6, false>);
+    return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1, false>);
 }
 const void* kernel_shade_ptr(bool count)
 {
     const int v = shade_variant();
-    if (count) return reinterpret_cast<const void*>(&dev::k_shade<true, 1>);
-    if (v == 4) return reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
-    if (v == 5) return reinterpret_cast<const void*>(&dev::k_shade<false, 5>);
-    return reinterpret_cast<const void*>(&dev::k_shade<false, 1>);
+    if (count) return reinterpret_cast<const void*>(&dev::k_shade<true, 1, false>);
+    if (v == 4) return reinterpret_cast<const void*>(&dev::k_shade<false, 4, false>);
+    if (v == 5) return reinterpret_cast<const void*>(&dev::k_shade<false, 5, false>);
+    return reinterpret_cast<const void*>(&dev::k_shade<false, 1, false>);
 }
 
 const void* kernel_trace_shadow_ptr(bool count)

@@ -7,6 +7,6 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 i=0
 for cfg in "$@"; do
   i=$((i+1))
-  env $cfg timeout -k 10 240 python -u bench.py --no-cpu-baseline > $OUT/bench_$i.log 2>&1 || { echo "bench [$cfg] failed rc=$?"; tail -5 $OUT/bench_$i.log; exit 1; }
+  env $cfg timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-ao-bake > $OUT/bench_$i.log 2>&1 || { echo "bench [$cfg] failed rc=$?"; tail -5 $OUT/bench_$i.log; exit 1; }
   echo "[$cfg] $(tail -1 $OUT/bench_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["kernels_ms"], d["per_ray"].get("primary_lane_util"))')"
 done
