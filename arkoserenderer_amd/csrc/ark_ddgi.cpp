@@ -100,6 +100,8 @@ struct ArkDdgiCtx {
     ArkDdgiDesc desc {};
     std::string lastError;
     hipStream_t stream = nullptr;
+    hipStream_t auxStream = nullptr; // second stream of the sub-window pipeline
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -185,7 +187,8 @@ int ensureSpill(ArkDdgiCtx* ctx)
     // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
     uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
     uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the two traversal kernels
-    size_t bytes = static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
+    // two halves: one per stream of the sub-window pipeline
+    size_t bytes = 2 * static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
     if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
     ctx->spillEntries = need;
@@ -253,6 +256,9 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if (e != hipSuccess) return bad(e, "hipGetDeviceProperties");
     ctx->cuCount = prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipStreamCreateWithFlags(&ctx->auxStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate aux");
+    if ((e = hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
@@ -266,7 +272,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->fibOrder.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib order");
     if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
-    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4 * kMaxSubWindows)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0, occW = 0;
@@ -296,6 +302,10 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
         b->release();
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (ctx->auxStream) (void)hipStreamSynchronize(ctx->auxStream);
+    if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
+    if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
+    if (ctx->auxStream) (void)hipStreamDestroy(ctx->auxStream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -707,21 +717,65 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         }
     }
     if (f.window_probes > 0) {
-        ARK_HIP(launch_trace_primary(ctx->scene, f, ctx->traceBlocks, count, s));
-        if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
-        // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
-        // rank it waits here for the previous exchange (the traversal above did not)
-        if (f.fused_shadows == 2) {
-            ARK_HIP(launch_shadow_gen(ctx->scene, f, s));
-            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
+        // Sub-window pipeline: the window's queue positions are cut into S pieces run
+        // alternately on the context stream and an auxiliary one, each piece through
+        // trace -> shadow rays -> shading with its own counters, spill stack and
+        // shadow list. A persistent launch holds every CU until its last long ray
+        // finishes (~0.3 ms for traversal, ~0.2 ms for shadow rays); the other
+        // stream's launches were meant to take the CUs its retiring workgroups free.
+        // Measured, they do not fill those tails (each piece adds its own), so S = 1
+        // is the default and S > 1 a tested option. Results do not depend on S (every
+        // ray is computed the same way wherever it runs). Serial (S = 1) when timing,
+        // so that per-stage times stay separable.
+        const char* se = std::getenv("ARK_SUBWINDOWS"); // read per frame: tests flip it in-process
+        const int envS = se ? std::atoi(se) : 1; // measured: S = 2 +0.5 %, 3-4 slower; 1/8 slab slower
+        int S = timing || !f.slot_order ? 1 : std::max(1, std::min(kMaxSubWindows, envS));
+        S = static_cast<int>(std::min<uint32_t>(static_cast<uint32_t>(S), f.window_probes));
+        hipStream_t st[2] = { s, ctx->auxStream };
+        if (S > 1) {
+            ARK_HIP(hipEventRecord(ctx->evFork, s));
+            ARK_HIP(hipStreamWaitEvent(ctx->auxStream, ctx->evFork, 0));
         }
-        if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], s));
-        if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-        ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
-        if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
-        if (f.fused_shadows == 0 && f.light_count > 0) {
-            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
-            ARK_HIP(launch_shade_finish(f, s));
+        const size_t spillHalf = ctx->spill.bytes / 2 / sizeof(uint32_t);
+        for (int w = 0; w < S; ++w) {
+            const uint32_t qb = static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * w / S);
+            const uint32_t qe = static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * (w + 1) / S);
+            if (qb == qe) continue;
+            hipStream_t ss = st[w & 1];
+            FrameArgs g = f;
+            g.window_probes = qe - qb;
+            g.window_rays = g.window_probes * R;
+            if (S > 1) {
+                g.slot_order = f.slot_order + qb;
+                g.ray_counter = f.ray_counter + static_cast<size_t>(w) * kRayCounterWords;
+                g.front_count = g.ray_counter + kFrontCountWord;
+                g.shadow_count = g.ray_counter + kShadowCountWord;
+                g.shadow_heads = g.ray_counter + kShadowHeadWord;
+                g.shadow_rays = f.shadow_rays + static_cast<size_t>(qb) * R * f.light_count;
+                g.front_recs = f.front_recs + static_cast<size_t>(qb) * R; // split schedule
+                g.front_lights = f.front_lights + static_cast<size_t>(qb) * R * f.light_count;
+                g.spill = f.spill + (w & 1) * spillHalf;
+            }
+            ARK_HIP(launch_trace_primary(ctx->scene, g, ctx->traceBlocks, count, ss));
+            if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], ss));
+            if (g.fused_shadows == 2) {
+                ARK_HIP(launch_shadow_gen(ctx->scene, g, ss));
+                ARK_HIP(launch_trace_shadow(ctx->scene, g, ctx->shadowBlocks, count, ss));
+            }
+            if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], ss));
+            // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
+            // rank it waits here for the previous exchange (the traversal above did not)
+            if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(ss, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+            ARK_HIP(launch_shade(ctx->scene, g, ctx->shadeBlocks, count, ss));
+            if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], ss));
+            if (g.fused_shadows == 0 && g.light_count > 0) {
+                ARK_HIP(launch_trace_shadow(ctx->scene, g, ctx->shadowBlocks, count, ss));
+                ARK_HIP(launch_shade_finish(g, ss));
+            }
+        }
+        if (S > 1) {
+            ARK_HIP(hipEventRecord(ctx->evJoin, ctx->auxStream));
+            ARK_HIP(hipStreamWaitEvent(s, ctx->evJoin, 0));
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
         ARK_HIP(launch_probe_update(f, s));

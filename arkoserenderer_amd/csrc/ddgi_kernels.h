@@ -55,6 +55,7 @@ constexpr int kFrontCountWord = 2 * kRayParts * kRayCounterStride;
 constexpr int kShadowCountWord = kFrontCountWord + kRayCounterStride;
 constexpr int kShadowHeadWord = kShadowCountWord + kRayCounterStride; // kRayParts partition heads
 constexpr int kRayCounterWords = kShadowHeadWord + kRayParts * kRayCounterStride;
+constexpr int kMaxSubWindows = 4; // sub-window pipeline: one counter block each
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {

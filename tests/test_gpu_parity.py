@@ -102,3 +102,17 @@ def test_other_shadow_schedules(case, mode, monkeypatch):
                            max_rays_per_probe=256, max_probe_updates=512)
         reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
         _assert_exact(reps)
+
+
+@pytest.mark.parametrize("subwindows", ["2", "3", "4"])
+def test_subwindow_pipeline(subwindows, monkeypatch):
+    """ARK_SUBWINDOWS: the window cut into S pieces on two streams (default 1); every
+    S gives the oracle's bits (features scene: lights, masked, translucent, offsets)."""
+    monkeypatch.setenv("ARK_SUBWINDOWS", subwindows)
+    sc = scenes.features_scene()
+    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
+    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=100, compute_probe_offsets=True,
+                       max_rays_per_probe=128, max_probe_updates=144)
+    reps = run_pair(sc, grid, cfg, 3, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
+                                                  environment_brightness=0.5))
+    _assert_exact(reps, offsets_expected=True)
