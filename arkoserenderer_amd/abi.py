@@ -245,6 +245,50 @@ ARK_BAKE_TRIANGLE_INDEX = 0
 ARK_BAKE_BARYCENTRICS = 1
 ARK_BAKE_OUTPUT = 2
 
+# lighting compose flags (lightingCompose.comp:30-41 named uniforms)
+ARK_COMPOSE_DIRECT_LIGHT = 1 << 0
+ARK_COMPOSE_SKIN_DIFFUSE_LIGHT = 1 << 1
+ARK_COMPOSE_DIFFUSE_GI = 1 << 2
+ARK_COMPOSE_BAKED_OCCLUSION = 1 << 3
+ARK_COMPOSE_USE_BENT_NORMAL = 1 << 4
+ARK_COMPOSE_BENT_NORMAL_OCCLUSION = 1 << 5
+ARK_COMPOSE_SCREEN_SPACE_OCCLUSION = 1 << 6
+ARK_COMPOSE_GLOSSY_GI = 1 << 7
+ARK_COMPOSE_MATERIAL_COLOR = 1 << 8
+ARK_COMPOSE_DEFAULT_FLAGS = 0x1FF
+
+
+class ArkComposeDesc(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("view_from_pixel", C.c_float * 16),
+        ("view_from_world", C.c_float * 16),
+        ("world_from_view", C.c_float * 16),
+        ("depth", C.c_void_p),
+        ("base_color", C.c_void_p),
+        ("material", C.c_void_p),
+        ("normal_velocity", C.c_void_p),
+        ("bent_normal", C.c_void_p),
+        ("direct_light", C.c_void_p),
+        ("diffuse_irradiance", C.c_void_p),
+        ("reflections", C.c_void_p),
+        ("reflection_direction", C.c_void_p),
+        ("screen_space_occlusion", C.c_void_p),
+        ("out", C.c_void_p),
+    ]
+
+
+# G-buffer plane name -> (dtype, channels) in ArkComposeDesc order
+COMPOSE_PLANES = [
+    ("depth", "float32", 1), ("base_color", "uint8", 4), ("material", "uint8", 4),
+    ("normal_velocity", "float16", 4), ("bent_normal", "float16", 4), ("direct_light", "float16", 4),
+    ("diffuse_irradiance", "float16", 4), ("reflections", "float16", 4), ("reflection_direction", "float16", 4),
+    ("screen_space_occlusion", "float32", 1),
+]
+
 
 class ArkSoupParams(C.Structure):
     _fields_ = [
@@ -267,7 +311,7 @@ class ArkSoupParams(C.Structure):
 ABI_STRUCTS = [
     ArkDdgiDesc, ArkRTVertex, ArkRTTriangleMesh, ArkShaderMaterial, ArkTexture, ArkRTInstance,
     ArkDirectionalLight, ArkSpotLight, ArkDdgiScene, ArkDdgiFrameParams, ArkDdgiCounters,
-    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc,
+    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc, ArkComposeDesc,
 ]
 
 # name -> (restype, argtypes)
@@ -292,6 +336,7 @@ EXPORTS = {
     "ark_ddgi_get_bvh_stats": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiBvhStats)]),
     "ark_ddgi_bake_ao": (C.c_int, [C.c_void_p, C.POINTER(ArkBakeAoDesc), C.c_void_p]),
     "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
+    "ark_ddgi_lighting_compose": (C.c_int, [C.c_void_p, C.POINTER(ArkComposeDesc), C.c_void_p]),
     # ark_scene.h
     "ark_soup_default_params": (None, [C.POINTER(ArkSoupParams)]),
     "ark_soup_generate": (C.c_int, [C.POINTER(ArkSoupParams), C.POINTER(C.c_void_p)]),

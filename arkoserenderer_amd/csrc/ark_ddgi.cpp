@@ -1018,4 +1018,27 @@ int ark_ddgi_bake_read(ArkDdgiCtx* ctx, int which, void* dst, uint64_t bytes)
     return ARK_DDGI_OK;
 }
 
+int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!desc || desc->struct_size != sizeof(ArkComposeDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkComposeDesc");
+    if (!desc->out) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "lighting_compose: no output plane");
+    if (static_cast<uint64_t>(desc->width) * desc->height >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "lighting_compose: target too large");
+    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    ARK_HIP(hipSetDevice(ctx->device));
+    // the DDGISamplingSet (DDGINode.cpp:45-66): grid constants + both atlases
+    FrameArgs f {};
+    f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
+    f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
+    for (int k = 0; k < 3; ++k) {
+        f.spacing[k] = ctx->desc.probe_spacing[k];
+        f.origin[k] = ctx->desc.offset_to_first[k];
+    }
+    f.irr = ctx->irr.as<uint16_t>();
+    f.vis = ctx->vis.as<uint16_t>();
+    ArkComposeDesc c = *desc;
+    ARK_HIP(launch_lighting_compose(f, c, s));
+    return ARK_DDGI_OK;
+}
+
 } // extern "C"

@@ -1859,6 +1859,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     }
 }
 
+#include "ddgi_compose.inc"
+
 } // namespace dev
 
 // ---------------------------------------------------------------------------
@@ -2000,6 +2002,13 @@ hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, 
     if (stage == 0) hipLaunchKernelGGL(dev::k_bake_raster, dim3((b.tri_count + 255) / 256), dim3(256), 0, s, b);
     else if (stage == 1) hipLaunchKernelGGL(dev::k_bake_bary, dim3((b.W * b.H + 255) / 256), dim3(256), 0, s, b);
     else hipLaunchKernelGGL((dev::k_bake_ao<6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s)
+{
+    if (c.width == 0 || c.height == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_lighting_compose, dim3((c.width + 15u) / 16u, (c.height + 15u) / 16u), dim3(256), 0, s, f, c);
     return hipGetLastError();
 }
 

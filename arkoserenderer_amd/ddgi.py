@@ -193,6 +193,24 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_bake_read(self.h, which, out.ctypes.data, out.nbytes), "ark_ddgi_bake_read")
         return out
 
+    def lighting_compose(self, width: int, height: int, flags: int, camera: dict, planes: dict, out_ptr: int,
+                         stream: int | None = None):
+        """ark_ddgi_lighting_compose. `planes` maps ArkComposeDesc plane names to DEVICE
+        pointers (ints; absent = NULL); `camera` holds the three column-major 4x4
+        matrices (CameraState, shared/CameraState.h); `out_ptr` is the RGBA16F output."""
+        d = abi.ArkComposeDesc()
+        d.struct_size = C.sizeof(abi.ArkComposeDesc)
+        d.width, d.height, d.flags = int(width), int(height), int(flags)
+        for k in ("view_from_pixel", "view_from_world", "world_from_view"):
+            m = np.ascontiguousarray(camera[k], np.float32).reshape(16)
+            getattr(d, k)[:] = [float(v) for v in m]
+        for name, _, _ in abi.COMPOSE_PLANES:
+            ptr = planes.get(name)
+            setattr(d, name, int(ptr) if ptr else None)
+        d.out = int(out_ptr)
+        self.check(self.lib.ark_ddgi_lighting_compose(self.h, C.byref(d), C.c_void_p(stream) if stream else None),
+                   "ark_ddgi_lighting_compose")
+
     def bvh_stats(self) -> abi.ArkDdgiBvhStats:
         s = abi.ArkDdgiBvhStats()
         self.check(self.lib.ark_ddgi_get_bvh_stats(self.h, C.byref(s)), "ark_ddgi_get_bvh_stats")
@@ -290,3 +308,53 @@ class BakeAmbientOcclusionNode:
         bent = output_format == self.RGBA8
         ctx.bake_ao(self.instance_index, width, height, self.sample_count, bent, stream)
         return ctx.bake_read(abi.ARK_BAKE_OUTPUT)
+
+
+class LightingComposeNode:
+    """Python mirror of LightingComposeNode (name "Lighting compose",
+    arkose/rendering/lighting/LightingComposeNode.{h,cpp}) for the WITH_DDGI
+    configuration: the node's toggles (LightingComposeNode.h:16-25 defaults, GUI at
+    LightingComposeNode.cpp:9-44) become ArkComposeDesc flags; the G-buffer planes are
+    device tensors (torch) in the formats GpuScene.cpp:326-360 creates."""
+
+    def __init__(self):
+        self.include_direct_light = True
+        self.include_skin_diffuse_light = True
+        self.include_glossy_gi = True
+        self.include_diffuse_gi = True
+        self.with_baked_occlusion = True
+        self.use_bent_normal_direction = True
+        self.with_bent_normal_occlusion = True
+        self.with_screen_space_occlusion = True
+        self.include_material_color = True  # GpuScene::shouldIncludeMaterialColor
+
+    def name(self) -> str:
+        return "Lighting compose"
+
+    def flags(self, has_screen_space_occlusion: bool) -> int:
+        f = 0
+        f |= abi.ARK_COMPOSE_DIRECT_LIGHT if self.include_direct_light else 0
+        f |= abi.ARK_COMPOSE_SKIN_DIFFUSE_LIGHT if self.include_skin_diffuse_light else 0
+        f |= abi.ARK_COMPOSE_DIFFUSE_GI if self.include_diffuse_gi else 0
+        f |= abi.ARK_COMPOSE_BAKED_OCCLUSION if self.with_baked_occlusion else 0
+        f |= abi.ARK_COMPOSE_USE_BENT_NORMAL if self.use_bent_normal_direction else 0
+        f |= abi.ARK_COMPOSE_BENT_NORMAL_OCCLUSION if self.with_bent_normal_occlusion else 0
+        # no AmbientOcclusion texture: the option is forced off (LightingComposeNode.cpp:56-60)
+        f |= abi.ARK_COMPOSE_SCREEN_SPACE_OCCLUSION if (self.with_screen_space_occlusion and has_screen_space_occlusion) else 0
+        f |= abi.ARK_COMPOSE_GLOSSY_GI if self.include_glossy_gi else 0
+        f |= abi.ARK_COMPOSE_MATERIAL_COLOR if self.include_material_color else 0
+        return f
+
+    def execute(self, ctx: DDGIContext, camera: dict, gbuffer: dict, out, stream: int | None = None):
+        """gbuffer: plane name -> contiguous device tensor [H, W(, C)] (missing = NULL,
+        read as 0 like the node's black stand-ins); out: uint16/float16 device tensor
+        [H, W, 4] (SceneColorWithGI, RGBA16F)."""
+        h, w = int(out.shape[0]), int(out.shape[1])
+        planes = {}
+        for name, _, _ in abi.COMPOSE_PLANES:
+            t = gbuffer.get(name)
+            if t is not None:
+                if not t.is_contiguous() or int(t.shape[0]) != h or int(t.shape[1]) != w:
+                    raise ValueError(f"LightingComposeNode: plane {name} must be a contiguous [{h}, {w}, ...] tensor")
+                planes[name] = t.data_ptr()
+        ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(), stream)

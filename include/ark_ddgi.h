@@ -346,6 +346,55 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* desc, void* hip_strea
 #define ARK_BAKE_OUTPUT 2
 int ark_ddgi_bake_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);
 
+/* ---- DDGI consumer: lighting compose -------------------------
+ * Replaces LightingComposeNode (arkose/rendering/lighting/LightingComposeNode.cpp:60-110)
+ * and its compute shader lightingCompose.comp:22-135 (WITH_DDGI = 1): per pixel,
+ * direct light + skin diffuse + glossy reflections + the DDGI diffuse term sampled
+ * from this context's current atlases (probeSampling.glsl:64-163), written RGBA16F.
+ * Flags mirror the node's named uniforms (lightingCompose.comp:30-41). */
+#define ARK_COMPOSE_DIRECT_LIGHT           (1u << 0) /* includeDirectLight */
+#define ARK_COMPOSE_SKIN_DIFFUSE_LIGHT     (1u << 1) /* includeSkinDiffuseLight */
+#define ARK_COMPOSE_DIFFUSE_GI             (1u << 2) /* includeDiffuseGI */
+#define ARK_COMPOSE_BAKED_OCCLUSION        (1u << 3) /* withBakedOcclusion */
+#define ARK_COMPOSE_USE_BENT_NORMAL        (1u << 4) /* useBentNormalDirection */
+#define ARK_COMPOSE_BENT_NORMAL_OCCLUSION  (1u << 5) /* withBentNormalOcclusion */
+#define ARK_COMPOSE_SCREEN_SPACE_OCCLUSION (1u << 6) /* withScreenSpaceOcclusion */
+#define ARK_COMPOSE_GLOSSY_GI              (1u << 7) /* includeGlossyGI */
+#define ARK_COMPOSE_MATERIAL_COLOR         (1u << 8) /* withMaterialColor */
+/* The node's defaults (LightingComposeNode.h:16-25, GpuScene m_includeMaterialColor):
+ * all on. Screen-space occlusion is forced off when no AmbientOcclusion texture
+ * exists (LightingComposeNode.cpp:56-60); here: when screen_space_occlusion is NULL. */
+#define ARK_COMPOSE_DEFAULT_FLAGS 0x1ffu
+
+/* G-buffer planes are device pointers, width x height texels row-major, in the
+ * formats GpuScene.cpp:326-360 creates (RGBA16F as 4 x fp16, RGBA8 as 4 x u8 UNORM);
+ * depth is the sampled non-linear depth as float. NULL inputs read as 0, like the
+ * node's black stand-in textures (LightingComposeNode.cpp:62-71). Matrices are
+ * CameraState's (shared/CameraState.h), column-major as GLSL mat4. */
+typedef struct ArkComposeDesc {
+    uint32_t struct_size;
+    uint32_t width, height;          /* targetSize */
+    uint32_t flags;                  /* ARK_COMPOSE_* */
+    float view_from_pixel[16];
+    float view_from_world[16];
+    float world_from_view[16];
+    const float* depth;                    /* SceneDepth */
+    const uint8_t* base_color;             /* SceneBaseColor RGBA8: rgb base colour */
+    const uint8_t* material;               /* SceneMaterial RGBA8: roughness, metallic, occlusion */
+    const uint16_t* normal_velocity;       /* SceneNormalVelocity RGBA16F: rg = octahedral view-space normal */
+    const uint16_t* bent_normal;           /* SceneBentNormal RGBA16F: rgb world bent normal, a cone */
+    const uint16_t* direct_light;          /* SceneColor RGBA16F */
+    const uint16_t* diffuse_irradiance;    /* SceneDiffuseIrradiance RGBA16F */
+    const uint16_t* reflections;           /* DenoisedReflections RGBA16F */
+    const uint16_t* reflection_direction;  /* ReflectionDirection RGBA16F (world space) */
+    const float* screen_space_occlusion;   /* AmbientOcclusion .r */
+    uint16_t* out;                         /* SceneColorWithGI RGBA16F */
+} ArkComposeDesc;
+
+/* Enqueues the compose on `hip_stream` (NULL = ctx stream), after any update
+ * enqueued before it on that stream. */
+int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void* hip_stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

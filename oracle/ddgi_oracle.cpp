@@ -1573,6 +1573,102 @@ int oracle_bake_ao(void* ctx, uint32_t instance, uint32_t W, uint32_t H, uint32_
     return 0;
 }
 
+// DDGI consumer, lightingCompose.comp:22-135 (WITH_DDGI = 1) per pixel, on the
+// oracle's current atlases (include/ark_ddgi.h ark_ddgi_lighting_compose). The desc's
+// planes are HOST pointers here. Matrix products: columns summed left to right.
+int oracle_lighting_compose(void* ctx, const ArkComposeDesc* c, int threads)
+{
+    const Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!c || c->struct_size != sizeof(ArkComposeDesc) || !c->out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    auto half4 = [](const uint16_t* p, size_t i, float v[4]) {
+        for (int k = 0; k < 4; ++k) v[k] = p ? f16_to_f32(p[4 * i + k]) : 0.0f;
+    };
+    auto unorm4 = [](const uint8_t* p, size_t i, float v[4]) {
+        for (int k = 0; k < 4; ++k) v[k] = p ? static_cast<float>(p[4 * i + k]) / 255.0f : 0.0f;
+    };
+    auto mulDir = [](const float* M, V3 v) {
+        return V3 { M[0] * v.x + M[4] * v.y + M[8] * v.z, M[1] * v.x + M[5] * v.y + M[9] * v.z, M[2] * v.x + M[6] * v.y + M[10] * v.z };
+    };
+    auto mulPoint = [](const float* M, float x, float y, float z, float w, float r[4]) {
+        for (int i = 0; i < 4; ++i) r[i] = M[i] * x + M[4 + i] * y + M[8 + i] * z + M[12 + i] * w;
+    };
+    const uint32_t flags = c->flags;
+    const int n = static_cast<int>(static_cast<uint64_t>(c->width) * c->height);
+    parallelFor(n, threads, [&](int i, int) {
+        const uint32_t x = static_cast<uint32_t>(i) % c->width, y = static_cast<uint32_t>(i) / c->width;
+        const size_t p = static_cast<size_t>(i);
+        float t[4];
+        V3 materialBaseColor = splat(1.0f);
+        if (flags & ARK_COMPOSE_MATERIAL_COLOR) { // :49-52
+            unorm4(c->base_color, p, t);
+            materialBaseColor = v3(t[0], t[1], t[2]);
+        }
+        float sceneColor[4] = { 0.0f, 0.0f, 0.0f, 0.0f };
+        if (flags & ARK_COMPOSE_DIRECT_LIGHT) { // :56-58
+            half4(c->direct_light, p, t);
+            for (int k = 0; k < 4; ++k) sceneColor[k] = sceneColor[k] + t[k];
+        }
+        V3 rgb = v3(sceneColor[0], sceneColor[1], sceneColor[2]);
+        if (flags & ARK_COMPOSE_SKIN_DIFFUSE_LIGHT) { // :60-63, diffuseBRDF() = 1/pi
+            half4(c->diffuse_irradiance, p, t);
+            rgb = rgb + v3(t[0], t[1], t[2]) * materialBaseColor * splat(1.0f / kPi);
+        }
+        float ambientOcclusion = 1.0f;
+        if ((flags & ARK_COMPOSE_SCREEN_SPACE_OCCLUSION) && c->screen_space_occlusion) ambientOcclusion = c->screen_space_occlusion[p];
+        const float nonLinearDepth = c->depth ? c->depth[p] : 0.0f;
+        if (nonLinearDepth < 1.0f - 1e-6f) { // :70
+            float mp[4];
+            unorm4(c->material, p, mp);
+            const float metallic = mp[1], occlusion = mp[2];
+            if (flags & ARK_COMPOSE_BAKED_OCCLUSION) ambientOcclusion = fminf_(ambientOcclusion, occlusion);
+            float rr[4], rd[4];
+            half4(c->reflections, p, rr);
+            half4(c->reflection_direction, p, rd);
+            const V3 reflectionRadiance = v3(rr[0], rr[1], rr[2]);
+            const V3 reflectionWorldDirection = v3(rd[0], rd[1], rd[2]);
+            const bool hasReflections = dot(reflectionWorldDirection, reflectionWorldDirection) > 1e-4f;
+            float vp[4]; // camera.glsl:101-106
+            mulPoint(c->view_from_pixel, static_cast<float>(x) + 0.5f, static_cast<float>(y) + 0.5f, nonLinearDepth, 1.0f, vp);
+            const V3 pos = v3(vp[0] / vp[3], vp[1] / vp[3], vp[2] / vp[3]);
+            const V3 V = -normalize(pos);
+            float nv[4];
+            half4(c->normal_velocity, p, nv);
+            const V3 N = octahedralDecode(nv[0], nv[1]); // encoding.glsl decodeNormal
+            const V3 L = mulDir(c->view_from_world, reflectionWorldDirection);
+            const V3 H = normalize(L + V); // specularBRDF (brdf.glsl:70-89), F only
+            const float LdotH = clampf(dot(L, H), 0.0f, 1.0f);
+            const V3 F = F_Schlick3(LdotH, mix3(splat(DIELECTRIC_REFLECTANCE), materialBaseColor, metallic));
+            if (hasReflections && (flags & ARK_COMPOSE_GLOSSY_GI)) rgb = rgb + materialBaseColor * reflectionRadiance * 0.25f;
+            if (flags & ARK_COMPOSE_DIFFUSE_GI) { // :101-132
+                float bn[4];
+                half4(c->bent_normal, p, bn);
+                V3 dir;
+                if ((flags & ARK_COMPOSE_USE_BENT_NORMAL) && bn[3] >= 0.0f) {
+                    const V3 b = v3(bn[0], bn[1], bn[2]);
+                    const float len = length(b);
+                    dir = b / len;
+                    if (flags & ARK_COMPOSE_BENT_NORMAL_OCCLUSION) ambientOcclusion = fminf_(ambientOcclusion, len);
+                } else {
+                    dir = normalize(mulDir(c->world_from_view, N));
+                }
+                float wp[4];
+                mulPoint(c->world_from_view, pos.x, pos.y, pos.z, 1.0f, wp);
+                const V3 wview = normalize(mulDir(c->world_from_view, V));
+                const V3 irr = sampleDynamicDiffuseGlobalIllumination(o, v3(wp[0], wp[1], wp[2]), dir, wview);
+                const float fudge = hasReflections ? 1.0f : 0.0f;
+                const V3 colorForDiffuse = materialBaseColor * splat(1.0f - metallic * fudge) * (splat(1.0f) - F * fudge);
+                rgb = rgb + colorForDiffuse * irr * ambientOcclusion;
+            }
+        }
+        uint16_t* out = c->out + 4 * p;
+        out[0] = f32_to_f16(rgb.x);
+        out[1] = f32_to_f16(rgb.y);
+        out[2] = f32_to_f16(rgb.z);
+        out[3] = f32_to_f16(sceneColor[3]);
+    });
+    return 0;
+}
+
 uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
 uint32_t oracle_rand_xorshift(uint32_t s) { return rand_xorshift(s); }
 

@@ -47,6 +47,7 @@ def load():
         lib.oracle_fmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         lib.oracle_bake_ao.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        lib.oracle_lighting_compose.argtypes = [C.c_void_p, C.POINTER(abi.ArkComposeDesc), C.c_int]
         _lib = lib
     return _lib
 
@@ -114,6 +115,28 @@ class Oracle:
                                      out.ctypes.data, threads)
         assert rc == 0, rc
         return tri, bary, out
+
+    def lighting_compose(self, width: int, height: int, flags: int, camera: dict, planes: dict, threads: int = 8):
+        """oracle_lighting_compose on host arrays: planes maps ArkComposeDesc plane names
+        to numpy arrays (absent = NULL); returns the RGBA16F output as uint16 [H, W, 4]."""
+        d = abi.ArkComposeDesc()
+        d.struct_size = C.sizeof(abi.ArkComposeDesc)
+        d.width, d.height, d.flags = int(width), int(height), int(flags)
+        for k in ("view_from_pixel", "view_from_world", "world_from_view"):
+            m = np.ascontiguousarray(camera[k], np.float32).reshape(16)
+            getattr(d, k)[:] = [float(v) for v in m]
+        keep = []
+        for name, _, _ in abi.COMPOSE_PLANES:
+            a = planes.get(name)
+            if a is not None:
+                a = np.ascontiguousarray(a)
+                keep.append(a)
+                setattr(d, name, a.ctypes.data)
+        out = np.zeros((height, width, 4), np.uint16)
+        d.out = out.ctypes.data
+        rc = self.lib.oracle_lighting_compose(self.h, C.byref(d), threads)
+        assert rc == 0, rc
+        return out
 
     def stats(self):
         n, t = C.c_uint64(), C.c_uint64()
