@@ -281,6 +281,34 @@ class ArkComposeDesc(C.Structure):
     ]
 
 
+class ArkIesInfo(C.Structure):
+    _fields_ = [
+        ("photometric_type", C.c_int32),
+        ("units_type", C.c_int32),
+        ("lamp_count", C.c_int32),
+        ("num_angles_v", C.c_uint32),
+        ("num_angles_h", C.c_uint32),
+        ("lumens_per_lamp", C.c_float),
+        ("width", C.c_float),
+        ("length", C.c_float),
+        ("height", C.c_float),
+        ("ballast_factor", C.c_float),
+        ("input_watts", C.c_float),
+        ("first_angle_v", C.c_float),
+        ("last_angle_v", C.c_float),
+        ("first_angle_h", C.c_float),
+        ("last_angle_h", C.c_float),
+        ("max_candela", C.c_float),
+    ]
+
+
+ARK_IES_OK = 0
+ARK_IES_E_INVALID_ARGUMENT = -1
+ARK_IES_E_IO = -2
+ARK_IES_E_PARSE = -3
+ARK_IES_LUT_SIZE = 256
+
+
 # G-buffer plane name -> (dtype, channels) in ArkComposeDesc order
 COMPOSE_PLANES = [
     ("depth", "float32", 1), ("base_color", "uint8", 4), ("material", "uint8", 4),
@@ -337,6 +365,11 @@ EXPORTS = {
     "ark_ddgi_bake_ao": (C.c_int, [C.c_void_p, C.POINTER(ArkBakeAoDesc), C.c_void_p]),
     "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "ark_ddgi_lighting_compose": (C.c_int, [C.c_void_p, C.POINTER(ArkComposeDesc), C.c_void_p]),
+    # ark_ies.h
+    "ark_ies_lut_from_memory": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),
+    "ark_ies_lut_from_file": (C.c_int, [C.c_char_p, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),
+    "ark_ies_lookup": (C.c_int, [C.c_char_p, C.c_uint64, C.c_float, C.c_float, C.POINTER(C.c_float)]),
+    "ark_ies_last_error": (C.c_char_p, []),
     # ark_scene.h
     "ark_soup_default_params": (None, [C.POINTER(ArkSoupParams)]),
     "ark_soup_generate": (C.c_int, [C.POINTER(ArkSoupParams), C.POINTER(C.c_void_p)]),

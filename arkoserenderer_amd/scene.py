@@ -365,3 +365,31 @@ class _SoupHandle:
             self.lib.ark_soup_free(self.h)
         except Exception:
             pass
+
+
+def ies_lut(source, size: int = abi.ARK_IES_LUT_SIZE):
+    """IES profile -> (size x size float32 LUT, ArkIesInfo) through ark_ies_lut_*
+    (IESProfile.cpp + GpuScene.cpp:1101-1124). `source` is a path or the file's text.
+    Raises ValueError with the parser's reason where the reference logs Fatal."""
+    import ctypes as C
+    import os
+
+    import numpy as np
+
+    lib = abi.load_library()
+    out = np.empty((size, size), np.float32)
+    info = abi.ArkIesInfo()
+    if isinstance(source, (str, os.PathLike)) and os.path.exists(source):
+        rc = lib.ark_ies_lut_from_file(os.fsencode(source), size, out.ctypes.data, C.byref(info))
+    else:
+        data = source.encode() if isinstance(source, str) else bytes(source)
+        rc = lib.ark_ies_lut_from_memory(data, len(data), size, out.ctypes.data, C.byref(info))
+    if rc != abi.ARK_IES_OK:
+        raise ValueError(f"IES profile: {lib.ark_ies_last_error().decode()} (status {rc})")
+    return out, info
+
+
+def ies_texture(source, size: int = abi.ARK_IES_LUT_SIZE) -> Texture:
+    """The spot light's LUT texture (R32F, clamp to edge, GpuScene.cpp:1108-1115)."""
+    lut, _ = ies_lut(source, size)
+    return Texture(size, size, abi.ARK_TEX_R32F, lut, abi.ARK_WRAP_CLAMP_TO_EDGE)

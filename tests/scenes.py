@@ -12,7 +12,7 @@ def _quad(center, u, v):
     return np.stack([c - u - v, c + u - v, c + u + v, c - u + v]).astype(np.float32)
 
 
-def features_scene(seed: int = 7) -> S.SceneData:
+def features_scene(seed: int = 7, ies_lut: np.ndarray | None = None) -> S.SceneData:
     """Exercises every shading/traversal feature: an opaque room, alpha-masked
     textured quads (any-hit alpha test), a translucent quad (only shadow rays see
     it), a mirrored instance (negative determinant -> flipped facing), sRGB and
@@ -113,8 +113,11 @@ def features_scene(seed: int = 7) -> S.SceneData:
     a[..., 0], a[..., 1], a[..., 2] = 200, 180, 90
     a[..., 3] = np.where(((xx // 4 + yy // 4) % 2) == 0, 255, 20)  # checker alpha
     tex.append(S.Texture(16, 16, abi.ARK_TEX_RGBA8_SRGB, a, abi.ARK_WRAP_CLAMP_TO_EDGE))
-    ies = (0.5 + 0.5 * np.cos(np.linspace(0, 3, 16))[None, :] * np.ones((16, 1))).astype(np.float32)
-    tex.append(S.Texture(16, 16, abi.ARK_TEX_R32F, ies, abi.ARK_WRAP_CLAMP_TO_EDGE))
+    if ies_lut is None:
+        ies = (0.5 + 0.5 * np.cos(np.linspace(0, 3, 16))[None, :] * np.ones((16, 1))).astype(np.float32)
+        tex.append(S.Texture(16, 16, abi.ARK_TEX_R32F, ies, abi.ARK_WRAP_CLAMP_TO_EDGE))
+    else:  # a real profile's LUT (ark_ies_lut_*), scaled like a light's candela normalisation
+        tex.append(S.Texture(ies_lut.shape[1], ies_lut.shape[0], abi.ARK_TEX_R32F, ies_lut.astype(np.float32), abi.ARK_WRAP_CLAMP_TO_EDGE))
     mr = np.zeros((4, 4, 4), np.uint8)
     mr[..., 1] = rng.integers(50, 255, (4, 4))
     mr[..., 2] = rng.integers(50, 255, (4, 4))

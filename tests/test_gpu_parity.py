@@ -116,3 +116,18 @@ def test_subwindow_pipeline(subwindows, monkeypatch):
     reps = run_pair(sc, grid, cfg, 3, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
                                                   environment_brightness=0.5))
     _assert_exact(reps, offsets_expected=True)
+
+
+def test_features_scene_real_ies_lut():
+    """The spots sample a real profile's 256x256 LUT (multi-lobe.ies through
+    ark_ies_lut_from_file, normalised by its peak candela), as the C5 config's
+    lights do; bit-exact against the oracle."""
+    import os
+    lut, info = S.ies_lut(os.path.join(os.path.dirname(__file__), "golden", "ies", "multi-lobe.ies"))
+    sc = scenes.features_scene(ies_lut=lut / np.float32(info.max_candela))
+    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
+    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
+                       max_rays_per_probe=128, max_probe_updates=144)
+    reps = run_pair(sc, grid, cfg, 2, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
+                                                  environment_brightness=0.5))
+    _assert_exact(reps, offsets_expected=True)
