@@ -393,3 +393,90 @@ def ies_texture(source, size: int = abi.ARK_IES_LUT_SIZE) -> Texture:
     """The spot light's LUT texture (R32F, clamp to edge, GpuScene.cpp:1108-1115)."""
     lut, _ = ies_lut(source, size)
     return Texture(size, size, abi.ARK_TEX_R32F, lut, abi.ARK_WRAP_CLAMP_TO_EDGE)
+
+
+def _box_mesh():
+    """Unit cube [0,1]^3, 24 vertices (flat normals), 12 CCW triangles facing out."""
+    faces = [((0, 0, 1), [(0, 0, 1), (1, 0, 1), (1, 1, 1), (0, 1, 1)]), ((0, 0, -1), [(1, 0, 0), (0, 0, 0), (0, 1, 0), (1, 1, 0)]),
+             ((1, 0, 0), [(1, 0, 1), (1, 0, 0), (1, 1, 0), (1, 1, 1)]), ((-1, 0, 0), [(0, 0, 0), (0, 0, 1), (0, 1, 1), (0, 1, 0)]),
+             ((0, 1, 0), [(0, 1, 1), (1, 1, 1), (1, 1, 0), (0, 1, 0)]), ((0, -1, 0), [(0, 0, 0), (1, 0, 0), (1, 0, 1), (0, 0, 1)])]
+    pos, nrm, uv, idx = [], [], [], []
+    for n, quad in faces:
+        b = len(pos)
+        pos += quad
+        nrm += [n] * 4
+        uv += [(0, 0), (1, 0), (1, 1), (0, 1)]
+        idx += [b, b + 1, b + 2, b, b + 2, b + 3]
+    return np.array(pos, np.float32), np.array(nrm, np.float32), np.array(uv, np.float32), np.array(idx, np.uint32)
+
+
+def city_block(box_count: int = 250_000, extent: float = 240.0, seed: int = 0xB15780, ies_sources=None) -> SceneData:
+    """BASELINE config C5 substitute (Bistro is not in the reference's
+    assets): a synthetic city block of instanced boxes on a ground plane, ~12
+    triangles per box (250,000 boxes ~ 3 M triangles), 8 box meshes x 8 materials,
+    a sun and 4 IES spot lights at street level using the reference's sample
+    profiles (assets/sample/ies: multi-lobe.ies, simple.ies; LUTs via ark_ies).
+    Buildings (2 % of the boxes) stand on a street grid; the rest are props of
+    0.1-1.5 m scattered over streets and building fronts up to 30 m."""
+    rng = np.random.default_rng(seed)
+    bp, bn, buv, bi = _box_mesh()
+    n_mesh = 8
+    V = len(bp)
+    positions = [np.tile(bp, (n_mesh, 1)), np.array([[0, 0, 0], [extent, 0, 0], [extent, 0, extent], [0, 0, extent]], np.float32)]
+    verts = np.zeros(n_mesh * V + 4, dtype=VERTEX_DTYPE)
+    verts["normal"][: n_mesh * V] = np.tile(bn, (n_mesh, 1))
+    verts["tex_coord"][: n_mesh * V] = np.tile(buv, (n_mesh, 1))
+    verts["normal"][n_mesh * V:] = (0, 1, 0)
+    verts["tex_coord"][n_mesh * V:] = [(0, 0), (8, 0), (8, 8), (0, 8)]
+    indices = np.concatenate([np.tile(bi, n_mesh), np.array([0, 2, 1, 0, 3, 2], np.uint32)])
+    meshes = np.zeros(n_mesh + 1, dtype=MESH_DTYPE)
+    meshes["first_vertex"] = [m * V for m in range(n_mesh)] + [n_mesh * V]
+    meshes["first_index"] = [m * 36 for m in range(n_mesh)] + [n_mesh * 36]
+    meshes["material_index"] = list(range(n_mesh)) + [n_mesh]
+    mats = np.array([default_material() for _ in range(n_mesh + 1)], dtype=MATERIAL_DTYPE)
+    mats["color_tint"][:, :3] = rng.uniform(0.1, 0.9, (n_mesh + 1, 3))
+    mats["metallic_factor"] = rng.uniform(0.0, 0.3, n_mesh + 1)
+    mats["roughness_factor"] = rng.uniform(0.3, 1.0, n_mesh + 1)
+
+    n_build = max(1, box_count // 50)
+    n_prop = box_count - n_build
+    cell = extent / math.ceil(math.sqrt(n_build))
+    gx = rng.integers(0, int(extent // cell), n_build)
+    gz = rng.integers(0, int(extent // cell), n_build)
+    bsize = np.stack([rng.uniform(0.3, 0.75, n_build) * cell, rng.uniform(5, 35, n_build), rng.uniform(0.3, 0.75, n_build) * cell], -1)
+    borig = np.stack([gx * cell + rng.uniform(0.05, 0.2, n_build) * cell, np.zeros(n_build), gz * cell + rng.uniform(0.05, 0.2, n_build) * cell], -1)
+    psize = rng.uniform(0.1, 1.5, (n_prop, 3))
+    porig = np.stack([rng.uniform(0, extent, n_prop), np.minimum(rng.exponential(4.0, n_prop), 30.0), rng.uniform(0, extent, n_prop)], -1)
+    size = np.concatenate([bsize, psize]).astype(np.float32)
+    orig = np.concatenate([borig, porig]).astype(np.float32)
+    inst = np.zeros(box_count + 1, dtype=INSTANCE_DTYPE)
+    m = np.zeros((box_count, 3, 4), np.float32)
+    m[:, 0, 0], m[:, 1, 1], m[:, 2, 2] = size[:, 0], size[:, 1], size[:, 2]
+    m[:, :, 3] = orig
+    inst["object_to_world"][:box_count] = m.reshape(box_count, 12)
+    inst["rt_mesh_index"][:box_count] = rng.integers(0, n_mesh, box_count)
+    inst["triangle_count"][:box_count] = 12
+    inst["object_to_world"][box_count] = np.eye(3, 4, dtype=np.float32).reshape(12)
+    inst["rt_mesh_index"][box_count] = n_mesh
+    inst["triangle_count"][box_count] = 2
+    inst["hit_mask"] = abi.ARK_RT_HIT_MASK_OPAQUE
+
+    textures = []
+    if ies_sources is None:
+        here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "ies")
+        ies_sources = [os.path.join(here, "multi-lobe.ies"), os.path.join(here, "simple.ies")]
+    for src in ies_sources:
+        lut, info = ies_lut(src)
+        textures.append(Texture(lut.shape[1], lut.shape[0], abi.ARK_TEX_R32F, lut / np.float32(info.max_candela), abi.ARK_WRAP_CLAMP_TO_EDGE))
+    env = np.ones((4, 8, 4), np.float32)
+    env[..., :3] = np.linspace(0.3, 1.2, 4)[:, None, None] * np.array([0.6, 0.75, 1.0], np.float32)
+    textures.append(Texture(8, 4, abi.ARK_TEX_RGBA32F, env))
+    spots = []
+    for k in range(4):
+        px, pz = rng.uniform(0.2, 0.8, 2) * extent
+        spots.append(SpotLight((400.0, 380.0, 300.0), (0.0, -1.0, 0.0), (1.0, 0.0, 0.0), (0.0, 0.0, 1.0),
+                               (float(px), 6.0, float(pz)), 1.2, k % 2))
+    sun_dir = np.array([0.4, -1.0, 0.3]) / np.linalg.norm([0.4, -1.0, 0.3])
+    return SceneData(positions=np.concatenate(positions), vertices=verts, indices=indices, meshes=meshes, materials=mats,
+                     instances=inst, textures=textures, sun=((3.0, 2.9, 2.7), tuple(sun_dir)), spots=spots,
+                     environment_texture=len(ies_sources))

@@ -131,3 +131,16 @@ def test_features_scene_real_ies_lut():
     reps = run_pair(sc, grid, cfg, 2, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
                                                   environment_brightness=0.5))
     _assert_exact(reps, offsets_expected=True)
+
+
+def test_city_block_c5_like():
+    """BASELINE config C5 shape at test size: instanced boxes (2,000 instances, 8
+    meshes), sun + 4 spot lights with the reference's sample IES profiles (5 shadow
+    rays per lit hit), 8x4x8 probes x 64 rays, offsets on."""
+    sc = S.city_block(2000, extent=40.0)
+    grid = D.ProbeGrid((8, 4, 8), (40.0 / 8, 2.5, 40.0 / 8), (2.5, 0.5, 2.5))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=256, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=256)
+    reps = run_pair(sc, grid, cfg, 2, 1000.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.02,
+                                                   environment_brightness=1.0))
+    _assert_exact(reps, offsets_expected=True)

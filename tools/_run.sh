@@ -1,2 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-ao-bake > gpurun_out/r01s3_bench_compose.log 2>&1 && tail -1 gpurun_out/r01s3_bench_compose.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["lighting_compose"])'
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "city or real_ies" > gpurun_out/r01s3_pt2.log 2>&1; rc=$?; tail -3 gpurun_out/r01s3_pt2.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/r01s3_pt2.log | head -20; exit 1; }
+timeout -k 10 400 python -u tools/config_bench.py > gpurun_out/r01s3_configs.log 2>&1; tail -2 gpurun_out/r01s3_configs.log
