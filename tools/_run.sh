@@ -1,3 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "city or real_ies" > gpurun_out/r01s3_pt2.log 2>&1; rc=$?; tail -3 gpurun_out/r01s3_pt2.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/r01s3_pt2.log | head -20; exit 1; }
-timeout -k 10 400 python -u tools/config_bench.py > gpurun_out/r01s3_configs.log 2>&1; tail -2 gpurun_out/r01s3_configs.log
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r01s3_sortprof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-ao-bake --no-compose > gpurun_out/r01s3_sortprof.log 2>&1 && cut -d, -f1-4 gpurun_out/r01s3_sortprof/run_kernel_stats.csv | head -12
