@@ -42,6 +42,9 @@ __device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) c
 namespace dev {
 
 typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
+#ifndef ARK_NODE_PACKED
+#define ARK_NODE_PACKED 0 // 1: BVH8 slab tests as packed fp32 pairs (measured slower: 3.02 vs 2.72 ms, see visitNode8)
+#endif
 
 // ---------------------------------------------------------------------------
 // 1. window -> slots
@@ -362,7 +365,7 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // scene diagonal on top of its own relative margin (bvh_builder.cpp), which
 // covers that error, and the comparison keeps a relative margin for far boxes,
 // so a box holding an exact triangle hit is never culled. The near/far plane of
-// each axis is chosen by the ray octant. Two slots per packed fp32 operation.
+// each axis is chosen by the ray octant. Scalar fp32 by default (ARK_NODE_PACKED=1: packed pairs).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
@@ -382,6 +385,24 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
     uint32_t hitSlots = 0, insideSlots = 0;
+#if !ARK_NODE_PACKED
+    // one slot at a time in scalar fp32 (the packed form costs two issue slots per
+    // v_pk op on gfx950 plus the moves that pair its operands)
+    (void)Ax; (void)Ay; (void)Az; (void)Bx; (void)By; (void)Bz; (void)Tmin; (void)Tmax;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
+        const bool hiWord = s >= 4;
+        auto q = [&](uint32_t w0_, uint32_t w1_) { return static_cast<float>(((hiWord ? w1_ : w0_) >> sh) & 0xffu); };
+        const float tnx = fmaf(q(nX0, nX1), ax, bx), tny = fmaf(q(nY0, nY1), ay, by), tnz = fmaf(q(nZ0, nZ1), az, bz);
+        const float tfx = fmaf(q(fX0, fX1), ax, bx), tfy = fmaf(q(fY0, fY1), ay, by), tfz = fmaf(q(fZ0, fZ1), az, bz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+        const float lim = fmaf(tf, 1.00001f, 1e-7f);
+        hitSlots |= (tn <= lim ? 1u : 0u) << s;
+        insideSlots |= (tn <= tmin ? 1u : 0u) << (s + 16);
+    }
+#else
 #pragma unroll
     for (int s = 0; s < 8; s += 2) {
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
@@ -405,6 +426,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         insideSlots |= (tn.x <= tmin ? 1u : 0u) << (s + 16);
         insideSlots |= (tn.y <= tmin ? 1u : 0u) << (s + 17);
     }
+#endif
     // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
     // swapping bit pairs / pairs of pairs / nibbles per octant bit
     // (hit and inside masks permuted together: bits 0-7 and 16-23)
