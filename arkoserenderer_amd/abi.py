@@ -394,6 +394,13 @@ def load_library(path: str | None = None) -> C.CDLL:
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"libark_ddgi.so not found at {p}: run __graft_entry__.build() (no CPU fallback exists)")
+    # torch (ROCm) ships its own libamdhip64 with the same soname: load it first so
+    # the process has ONE HIP runtime. Loading ours first makes torch bind to it and
+    # report "No HIP GPUs are available" once it initialises.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(p)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

@@ -42,6 +42,10 @@ __device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) c
 namespace dev {
 
 typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#ifndef ARK_NODE_MIX
+#define ARK_NODE_MIX 0 // 1: plane bytes as f16 subnormals into v_fma_mix_f32 (visitNode8; bit-identical, measured 1 % slower)
+#endif
 #ifndef ARK_NODE_PACKED
 #define ARK_NODE_PACKED 0 // 1: BVH8 slab tests as packed fp32 pairs (measured slower: 3.02 vs 2.72 ms, see visitNode8)
 #endif
@@ -385,7 +389,36 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
     uint32_t hitSlots = 0, insideSlots = 0;
-#if !ARK_NODE_PACKED
+#if ARK_NODE_MIX
+    // Plane bytes become f16 subnormals (bits 0x00qq = q * 2^-24, exact) two at a time
+    // with one v_perm_b32, and feed v_fma_mix_f32 as its f16 operand: fma(q * 2^-24,
+    // a * 2^24, b) rounds the exact q*a + b once, bit-identical to fma(q, a, b) (a is
+    // never subnormal: |idir| >= 1 and the plane exponent is >= -100), without the
+    // byte-to-float conversion per plane.
+    (void)Ax; (void)Ay; (void)Az; (void)Bx; (void)By; (void)Bz; (void)Tmin; (void)Tmax;
+    const float ax24 = __uint_as_float(((w0.w & 0xffu) + 24u) << 23) * idir.x;
+    const float ay24 = __uint_as_float((((w0.w >> 8) & 0xffu) + 24u) << 23) * idir.y;
+    const float az24 = __uint_as_float((((w0.w >> 16) & 0xffu) + 24u) << 23) * idir.z;
+    (void)ax; (void)ay; (void)az;
+    auto pairOf = [](uint32_t w, bool upper) { return __builtin_bit_cast(h2, __builtin_amdgcn_perm(0u, w, upper ? 0x0c030c02u : 0x0c010c00u)); };
+#pragma unroll
+    for (int s = 0; s < 8; s += 2) {
+        const bool hiWord = s >= 4, upper = (s & 2) != 0;
+        const h2 pnx = pairOf(hiWord ? nX1 : nX0, upper), pny = pairOf(hiWord ? nY1 : nY0, upper), pnz = pairOf(hiWord ? nZ1 : nZ0, upper);
+        const h2 pfx = pairOf(hiWord ? fX1 : fX0, upper), pfy = pairOf(hiWord ? fY1 : fY0, upper), pfz = pairOf(hiWord ? fZ1 : fZ0, upper);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            auto hv = [&](h2 p) { return static_cast<float>(j ? p.y : p.x); };
+            const float tnx = fmaf(hv(pnx), ax24, bx), tny = fmaf(hv(pny), ay24, by), tnz = fmaf(hv(pnz), az24, bz);
+            const float tfx = fmaf(hv(pfx), ax24, bx), tfy = fmaf(hv(pfy), ay24, by), tfz = fmaf(hv(pfz), az24, bz);
+            const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+            const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+            const float lim = fmaf(tf, 1.00001f, 1e-7f);
+            hitSlots |= (tn <= lim ? 1u : 0u) << (s + j);
+            insideSlots |= (tn <= tmin ? 1u : 0u) << (s + j + 16);
+        }
+    }
+#elif !ARK_NODE_PACKED
     // one slot at a time in scalar fp32 (the packed form costs two issue slots per
     // v_pk op on gfx950 plus the moves that pair its operands)
     (void)Ax; (void)Ay; (void)Az; (void)Bx; (void)By; (void)Bz; (void)Tmin; (void)Tmax;
