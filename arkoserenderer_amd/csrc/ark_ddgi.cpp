@@ -493,7 +493,9 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     }
     int rc;
     if ((rc = upload(ctx, ctx->nodes, allNodes.data(), allNodes.size())) != 0) return rc;
+    allTris.push_back(GpuTriangle {}); // padding: a five-load fetch of the last triangle stays in bounds (ARK_FETCH5)
     if ((rc = upload(ctx, ctx->tris, allTris.data(), allTris.size())) != 0) return rc;
+    allTris.pop_back();
     if ((rc = upload(ctx, ctx->indices, s->indices, s->index_count)) != 0) return rc;
     if ((rc = upload(ctx, ctx->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
     if ((rc = upload(ctx, ctx->positions, s->positions, s->vertex_count * 3)) != 0) return rc;

@@ -43,6 +43,12 @@ namespace dev {
 
 typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#ifndef ARK_FLAT_FETCH
+#define ARK_FLAT_FETCH 0
+#endif
+#ifndef ARK_FETCH5
+#define ARK_FETCH5 1 // 0: node-only last two loads (measured 2 % slower)
+#endif
 #ifndef ARK_NODE_MIX
 #define ARK_NODE_MIX 0 // 1: plane bytes as f16 subnormals into v_fma_mix_f32 (visitNode8; bit-identical, measured 1 % slower)
 #endif
@@ -556,6 +562,16 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& 
         src = reinterpret_cast<const uint4*>(sc.nodes + child);
     }
     const uint32_t rel = static_cast<uint32_t>(reinterpret_cast<const GpuBvh8Node*>(src) - sc.nodes) - nc.base;
+#if ARK_FLAT_FETCH
+    // one generic (flat) pointer into LDS or HBM: five flat loads, no divergent paths
+    const uint4* p = (!fx.isTri && rel < nc.count) ? nc.lds + rel * 5u : src;
+    fx.w0 = p[0];
+    fx.w1 = p[1];
+    fx.w2 = p[2];
+    fx.w3 = p[3];
+    fx.w4 = p[4];
+    return;
+#endif
     if (!fx.isTri && rel < nc.count) {
         const uint4* l = nc.lds + rel * 5u;
         fx.w0 = l[0];
@@ -568,11 +584,17 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& 
     fx.w0 = src[0];
     fx.w1 = src[1];
     fx.w2 = src[2];
-    fx.w3 = fx.w4 = make_uint4(0, 0, 0, 0);
-    if (!fx.isTri) {
+#if ARK_FETCH5
+    // five loads whatever the step: a triangle step reads 32 B of the next record
+    // (the triangle array is padded), no branch around the node's last two loads
+    fx.w3 = src[3];
+    fx.w4 = src[4];
+#else
+    if (!fx.isTri) { // triangle steps leave w3/w4 unset: only node steps read them
         fx.w3 = src[3];
         fx.w4 = src[4];
     }
+#endif
 }
 
 // Returns true when a triangle step produced a candidate (tt, uu, vv, backface
