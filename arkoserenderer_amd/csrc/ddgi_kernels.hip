@@ -21,6 +21,8 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #ifndef ARK_DDGI_GATHER_BATCH
 #define ARK_DDGI_GATHER_BATCH 1 // cage probes whose atlas taps are in flight together (sampleDDGI; 2 and 4 measured no faster on C4)
@@ -2007,12 +2009,31 @@ size_t shade_work_bytes(uint64_t rays, uint32_t lights)
     return rays * (sizeof(FrontRec) + static_cast<uint64_t>(lights) * (sizeof(FrontLight) + sizeof(ShadowRay)));
 }
 
+// Co-resident workgroups of a persistent kernel on this device (cached per kernel).
+static uint32_t persistentBlocks(const void* fn, int block, uint32_t fallback)
+{
+    static thread_local std::vector<std::pair<const void*, uint32_t>> cache;
+    for (const auto& c : cache)
+        if (c.first == fn) return c.second;
+    int dev = 0, cus = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, block, 0) != hipSuccess || occ <= 0 || cus <= 0)
+        return fallback;
+    cache.emplace_back(fn, static_cast<uint32_t>(occ * cus));
+    return cache.back().second;
+}
+
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     const int v = shade_variant();
     if (f.fused_shadows) {
+        // one-pass shading at <= 128 VGPRs, 4 waves/SIMD, no spill (0.57 -> 0.50 ms at C4;
+        // ARK_SHADE_WPE=1: the compiler's 133 VGPRs, 3 waves)
         if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-        else hipLaunchKernelGGL((dev::k_shade<false, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+        else if (v != 1) {
+            const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, 4, true>);
+            hipLaunchKernelGGL((dev::k_shade<false, 4, true>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
+        } else hipLaunchKernelGGL((dev::k_shade<false, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
         return hipGetLastError();
     }
     if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
