@@ -1571,7 +1571,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 // counter serialises at L2: 1.45 ms for 131K waves on C4); pass 2 writes them in
 // position order (wave scans), so a shadow-kernel grab of 64 list entries holds the
 // neighbouring rays of one probe.
-constexpr uint32_t kGenSteps = 16, kGenSpan = kGenSteps * 256u;
+#ifndef ARK_GEN_STEPS
+#define ARK_GEN_STEPS 4 // queue positions per block = 256 x this (16: 0.185 ms, 4: 0.163, 2: 0.215 at C4)
+#endif
+constexpr uint32_t kGenSteps = ARK_GEN_STEPS, kGenSpan = kGenSteps * 256u;
 
 __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 {
