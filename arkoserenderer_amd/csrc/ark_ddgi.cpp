@@ -492,10 +492,19 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         g.ies_texture = sl.ies_profile_index;
     }
     int rc;
-    if ((rc = upload(ctx, ctx->nodes, allNodes.data(), allNodes.size())) != 0) return rc;
+    // nodes and triangles in ONE allocation (triangles after the nodes, 256-B aligned):
+    // the traversal addresses both through one buffer resource with a per-lane
+    // byte offset (32 bits: the pair must stay below 4 GiB)
+    const size_t nodeBytes = allNodes.size() * sizeof(GpuBvh8Node);
+    const size_t triOffset = (nodeBytes + 255) & ~static_cast<size_t>(255);
+    const size_t triBytes = (allTris.size() + 1) * sizeof(GpuTriangle); // + padding record
+    if (triOffset + triBytes >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "BVH nodes + triangles exceed 4 GiB");
+    ARK_HIP(ctx->nodes.alloc(triOffset + triBytes));
+    ARK_HIP(hipMemcpy(ctx->nodes.ptr, allNodes.data(), nodeBytes, hipMemcpyHostToDevice));
     allTris.push_back(GpuTriangle {}); // padding: a five-load fetch of the last triangle stays in bounds (ARK_FETCH5)
-    if ((rc = upload(ctx, ctx->tris, allTris.data(), allTris.size())) != 0) return rc;
+    ARK_HIP(hipMemcpy(static_cast<char*>(ctx->nodes.ptr) + triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
     allTris.pop_back();
+    ctx->tris.release();
     if ((rc = upload(ctx, ctx->indices, s->indices, s->index_count)) != 0) return rc;
     if ((rc = upload(ctx, ctx->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
     if ((rc = upload(ctx, ctx->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
@@ -533,7 +542,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     }
     SceneArgs& sc = ctx->scene;
     sc.nodes = ctx->nodes.as<GpuBvh8Node>();
-    sc.tris = ctx->tris.as<GpuTriangle>();
+    sc.tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(ctx->nodes.ptr) + triOffset);
+    sc.tri_byte_offset = static_cast<uint32_t>(triOffset);
     sc.tri_normals = ctx->triNormals.as<float4>();
     sc.root_opaque = roots[0];
     sc.root_masked = roots[1];

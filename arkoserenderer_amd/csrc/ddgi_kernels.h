@@ -60,7 +60,8 @@ constexpr int kMaxSubWindows = 4; // sub-window pipeline: one counter block each
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {
     const GpuBvh8Node* nodes;
-    const GpuTriangle* tris;
+    const GpuTriangle* tris;     // = (char*)nodes + tri_byte_offset (one allocation)
+    uint32_t tri_byte_offset;
     int32_t root_opaque; // -1 = no geometry of that hit-mask class
     int32_t root_masked;
     int32_t root_blend;
