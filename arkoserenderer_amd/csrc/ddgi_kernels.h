@@ -54,7 +54,8 @@ struct alignas(16) ShadowRay {
 constexpr int kFrontCountWord = 2 * kRayParts * kRayCounterStride;
 constexpr int kShadowCountWord = kFrontCountWord + kRayCounterStride;
 constexpr int kShadowHeadWord = kShadowCountWord + kRayCounterStride; // kRayParts partition heads
-constexpr int kRayCounterWords = kShadowHeadWord + kRayParts * kRayCounterStride;
+constexpr int kShade2HeadWord = kShadowHeadWord + kRayParts * kRayCounterStride; // second shading pass's heads
+constexpr int kRayCounterWords = kShade2HeadWord + kRayParts * kRayCounterStride;
 constexpr int kMaxSubWindows = 4; // sub-window pipeline: one counter block each
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
@@ -140,6 +141,7 @@ struct FrameArgs {
     uint32_t grab_chunk;     // trace / shadow: rays a wave takes from its partition head at once (<= 64)
     int32_t fused_shadows;   // 0 split (records + k_shade_finish); 1 traced inside k_trace_primary; 2 k_shadow_gen + k_trace_shadow before shading
     uint32_t* shadow_bits;   // [window_rays] lit light bits 0-15, occluded bits 16-31 (fused path)
+    int32_t shade_pass;      // one-pass shading: 0 every ray; 1 rays needing no shadow bit; 2 lit front hits
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };

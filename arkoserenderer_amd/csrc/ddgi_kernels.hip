@@ -1291,7 +1291,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     uint32_t cFront = 0;
 
     // chunks come from the second set of per-XCD partition heads (see grabRays)
-    uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
+    uint32_t* heads = f.ray_counter + (f.shade_pass == 2 ? kShade2HeadWord : kRayParts * kRayCounterStride);
     const uint32_t home = xccId();
     uint32_t tried = 0;
     for (;;) {
@@ -1311,6 +1311,12 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const uint32_t q = (chunk + r) / f.R;
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
+            if (FUSED && f.shade_pass != 0) {
+                // split shading: pass 1 = every ray that needs no shadow bit (it runs beside
+                // the shadow traversal), pass 2 = the front hits with lit lights, after it
+                const bool lit = hit.tri != kNoHit && !(hit.t < 0.0f) && (f.shadow_bits[ray] & 0xffffu) != 0u;
+                if (lit != (f.shade_pass == 2)) continue;
+            }
             if (hit.tri == kNoHit) {
                 // miss (raygen.rgen:149-158)
                 V3 origin, dir;

@@ -79,14 +79,17 @@ def test_small_soup_sun():
     _assert_exact(reps)
 
 
-@pytest.mark.parametrize("mode", ["split", "fused"])
+@pytest.mark.parametrize("mode", ["split", "fused", "shade2"])
 @pytest.mark.parametrize("case", ["features", "soup"])
 def test_other_shadow_schedules(case, mode, monkeypatch):
     """The two non-default shadow-ray schedules (ARK_SHADOWS): "split" = per-light
     records in shading, k_trace_shadow after it, k_shade_finish; "fused" = shadow rays
     traced inside k_trace_primary. Both give the oracle's bits, like the default
     "pre" schedule (k_shadow_gen + k_trace_shadow before one-pass shading)."""
-    monkeypatch.setenv("ARK_SHADOWS", mode)
+    if mode == "shade2":  # the default schedule with shading split in two passes around the shadow rays
+        monkeypatch.setenv("ARK_SHADE_SPLIT", "1")
+    else:
+        monkeypatch.setenv("ARK_SHADOWS", mode)
     if case == "features":
         sc = scenes.features_scene()
         grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))

@@ -1,4 +1,5 @@
 set -o pipefail
-L=$PWD/arkoserenderer_amd/lib
-ARK_TRACE_WPE=7 ARK_DDGI_LIB=$L/libark_ddgi_s4.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r01s3_pt4.log 2>&1; rc=$?; echo "s4w7: $(tail -1 gpurun_out/r01s3_pt4.log)"; [ $rc -eq 0 ] || exit 1
-bash tools/sweep_env.sh r01s3_occ "ARK_DDGI_LIB=$L/libark_ddgi.so" "ARK_DDGI_LIB=$L/libark_ddgi_s4.so" "ARK_TRACE_WPE=7 ARK_DDGI_LIB=$L/libark_ddgi_s4.so" "ARK_TRACE_WPE=7 ARK_DDGI_LIB=$L/libark_ddgi.so"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r01s3_pt.log 2>&1; rc=$?; tail -1 gpurun_out/r01s3_pt.log; [ $rc -eq 0 ] || { grep -E "assert|Error|FAILED" gpurun_out/r01s3_pt.log | head; exit 1; }
+bash tools/sweep_env.sh r01s3_split "ARK_SHADE_SPLIT=0" "ARK_SHADE_SPLIT=1" "ARK_SHADE_SPLIT=0" "ARK_SHADE_SPLIT=1" && \
+ARK_SHADE_SPLIT=0 timeout -k 10 300 python -u tools/shard_proxy.py --shards 8 > gpurun_out/r01s3_split/shard0.log 2>&1 && tail -n 1 gpurun_out/r01s3_split/shard0.log && \
+timeout -k 10 300 python -u tools/shard_proxy.py --shards 8 > gpurun_out/r01s3_split/shard1.log 2>&1 && tail -n 1 gpurun_out/r01s3_split/shard1.log
