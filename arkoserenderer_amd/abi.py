@@ -309,6 +309,24 @@ ARK_IES_E_PARSE = -3
 ARK_IES_LUT_SIZE = 256
 
 
+ARK_PROBE_DEBUG_DISABLED = 0
+ARK_PROBE_DEBUG_IRRADIANCE = 1
+ARK_PROBE_DEBUG_DISTANCE = 2
+ARK_PROBE_DEBUG_DISTANCE2 = 3
+
+
+class ArkProbeDebugDesc(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("visualisation", C.c_int32),
+        ("distance_scale", C.c_float),
+        ("count", C.c_uint32),
+        ("probe_indices", C.c_void_p),
+        ("directions", C.c_void_p),
+        ("out", C.c_void_p),
+    ]
+
+
 # G-buffer plane name -> (dtype, channels) in ArkComposeDesc order
 COMPOSE_PLANES = [
     ("depth", "float32", 1), ("base_color", "uint8", 4), ("material", "uint8", 4),
@@ -339,7 +357,7 @@ class ArkSoupParams(C.Structure):
 ABI_STRUCTS = [
     ArkDdgiDesc, ArkRTVertex, ArkRTTriangleMesh, ArkShaderMaterial, ArkTexture, ArkRTInstance,
     ArkDirectionalLight, ArkSpotLight, ArkDdgiScene, ArkDdgiFrameParams, ArkDdgiCounters,
-    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc, ArkComposeDesc,
+    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc, ArkComposeDesc, ArkProbeDebugDesc,
 ]
 
 # name -> (restype, argtypes)
@@ -365,6 +383,7 @@ EXPORTS = {
     "ark_ddgi_bake_ao": (C.c_int, [C.c_void_p, C.POINTER(ArkBakeAoDesc), C.c_void_p]),
     "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "ark_ddgi_lighting_compose": (C.c_int, [C.c_void_p, C.POINTER(ArkComposeDesc), C.c_void_p]),
+    "ark_ddgi_probe_debug": (C.c_int, [C.c_void_p, C.POINTER(ArkProbeDebugDesc), C.c_void_p]),
     # ark_ies.h
     "ark_ies_lut_from_memory": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),
     "ark_ies_lut_from_file": (C.c_int, [C.c_char_p, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),

@@ -1071,4 +1071,24 @@ int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void*
     return ARK_DDGI_OK;
 }
 
+int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!desc || desc->struct_size != sizeof(ArkProbeDebugDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkProbeDebugDesc");
+    if (desc->count && (!desc->probe_indices || !desc->directions || !desc->out)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "probe_debug: null plane");
+    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    ARK_HIP(hipSetDevice(ctx->device));
+    FrameArgs f {};
+    f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
+    f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
+    for (int k = 0; k < 3; ++k) {
+        f.spacing[k] = ctx->desc.probe_spacing[k];
+        f.origin[k] = ctx->desc.offset_to_first[k];
+    }
+    f.irr = ctx->irr.as<uint16_t>();
+    f.vis = ctx->vis.as<uint16_t>();
+    ARK_HIP(launch_probe_debug(f, *desc, s));
+    return ARK_DDGI_OK;
+}
+
 } // extern "C"

@@ -2139,6 +2139,13 @@ hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, 
     return hipGetLastError();
 }
 
+hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hipStream_t s)
+{
+    if (d.count == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_probe_debug, dim3((d.count + 255u) / 256u), dim3(256), 0, s, f, d);
+    return hipGetLastError();
+}
+
 hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s)
 {
     if (c.width == 0 || c.height == 0) return hipSuccess;

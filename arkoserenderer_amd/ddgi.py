@@ -211,6 +211,16 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_lighting_compose(self.h, C.byref(d), C.c_void_p(stream) if stream else None),
                    "ark_ddgi_lighting_compose")
 
+    def probe_debug(self, visualisation: int, distance_scale: float, count: int, probes_ptr: int, dirs_ptr: int, out_ptr: int,
+                    stream: int | None = None):
+        """ark_ddgi_probe_debug on device arrays (uint32 probe indices, float3 directions,
+        RGBA16F out)."""
+        d = abi.ArkProbeDebugDesc()
+        d.struct_size = C.sizeof(abi.ArkProbeDebugDesc)
+        d.visualisation, d.distance_scale, d.count = int(visualisation), float(distance_scale), int(count)
+        d.probe_indices, d.directions, d.out = int(probes_ptr), int(dirs_ptr), int(out_ptr)
+        self.check(self.lib.ark_ddgi_probe_debug(self.h, C.byref(d), C.c_void_p(stream) if stream else None), "ark_ddgi_probe_debug")
+
     def bvh_stats(self) -> abi.ArkDdgiBvhStats:
         s = abi.ArkDdgiBvhStats()
         self.check(self.lib.ark_ddgi_get_bvh_stats(self.h, C.byref(s)), "ark_ddgi_get_bvh_stats")
@@ -358,3 +368,40 @@ class LightingComposeNode:
                     raise ValueError(f"LightingComposeNode: plane {name} must be a contiguous [{h}, {w}, ...] tensor")
                 planes[name] = t.data_ptr()
         ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(), stream)
+
+
+class DDGIProbeDebug:
+    """Python mirror of DDGIProbeDebug (name "DDGI probe debug",
+    arkose/rendering/nodes/DDGIProbeDebug.{h,cpp}): the fragment stage of its probe
+    spheres (probeDebug.frag) on (probe, normal) samples - `sphere_samples` gives the
+    reference's 48x48 sphere vertices; rasterising them is the caller's."""
+
+    def __init__(self):
+        self.debug_visualisation = abi.ARK_PROBE_DEBUG_DISABLED  # m_debugVisualisation
+        self.probe_scale = 0.1
+        self.distance_scale = 0.01
+        self.use_probe_offset = True
+
+    def name(self) -> str:
+        return "DDGI probe debug"
+
+    @staticmethod
+    def sphere_samples(rings: int = 48, sectors: int = 48) -> np.ndarray:
+        """Unit-sphere vertex positions of createSphereRenderData (DDGIProbeDebug.cpp:75-98)."""
+        r = np.arange(rings, dtype=np.float32)[:, None]
+        s = np.arange(sectors, dtype=np.float32)[None, :]
+        R, S = np.float32(1.0 / (rings - 1)), np.float32(1.0 / (sectors - 1))
+        pi = np.float32(np.pi)
+        y = np.sin(-(pi / 2) + pi * r * R) * np.ones_like(s)
+        x = np.cos(2 * pi * s * S) * np.sin(pi * r * R)
+        z = np.sin(2 * pi * s * S) * np.sin(pi * r * R)
+        return np.stack([x, y, z], -1).reshape(-1, 3).astype(np.float32)
+
+    def execute(self, ctx: DDGIContext, probes, dirs, out, stream: int | None = None):
+        """probes: uint32/int32 device tensor [n]; dirs: float32 device tensor [n, 3];
+        out: 16-bit device tensor [n, 4]. A no-op when the visualisation is disabled
+        (DDGIProbeDebug.cpp:53-54)."""
+        if self.debug_visualisation == abi.ARK_PROBE_DEBUG_DISABLED:
+            return
+        ctx.probe_debug(self.debug_visualisation, self.distance_scale, int(probes.shape[0]), probes.data_ptr(), dirs.data_ptr(),
+                        out.data_ptr(), stream)

@@ -395,6 +395,27 @@ typedef struct ArkComposeDesc {
  * enqueued before it on that stream. */
 int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void* hip_stream);
 
+/* ---- DDGI probe debug visualisation --------------------------
+ * The fragment stage of DDGIProbeDebug (DDGIProbeDebug.cpp:34-71,
+ * ddgi/probeDebug.frag): for each (probe index, sphere normal) sample, the colour the
+ * reference's fragment writes: irradiance pow(texel, 5), distance or distance^2 x
+ * distance_scale (magenta for a negative distance), or magenta for an unknown mode.
+ * The sphere rasterisation itself stays with the caller (raster is out of scope). */
+#define ARK_PROBE_DEBUG_DISABLED   0 /* DDGI_PROBE_DEBUG_VISUALIZE_* (shared/DDGIData.h:17-20) */
+#define ARK_PROBE_DEBUG_IRRADIANCE 1
+#define ARK_PROBE_DEBUG_DISTANCE   2
+#define ARK_PROBE_DEBUG_DISTANCE2  3
+typedef struct ArkProbeDebugDesc {
+    uint32_t struct_size;
+    int32_t visualisation;          /* m_debugVisualisation */
+    float distance_scale;           /* m_distanceScale (default 0.01) */
+    uint32_t count;                 /* samples */
+    const uint32_t* probe_indices;  /* device [count]: gl_InstanceIndex */
+    const float* directions;        /* device [count][3]: vNormal */
+    uint16_t* out;                  /* device [count][4] RGBA16F */
+} ArkProbeDebugDesc;
+int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* hip_stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

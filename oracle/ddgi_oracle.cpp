@@ -1669,6 +1669,41 @@ int oracle_lighting_compose(void* ctx, const ArkComposeDesc* c, int threads)
     return 0;
 }
 
+// Probe debug fragment stage (ddgi/probeDebug.frag; include/ark_ddgi.h
+// ark_ddgi_probe_debug) on the oracle's current atlases; host arrays.
+int oracle_probe_debug(void* ctx, int mode, float distanceScale, uint32_t count, const uint32_t* probes, const float* dirs, uint16_t* out)
+{
+    const Oracle& o = *static_cast<Oracle*>(ctx);
+    const Grid& g = o.g;
+    for (uint32_t i = 0; i < count; ++i) {
+        const V3 dir = normalize(v3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]));
+        const V3 pos = probePosition(g, probes[i]) + splat(1e-4f); // calculateProbePosition + 1e-4
+        const V3 rel = (pos - g.origin) / g.spacing;                // baseGridCoord (probeSampling.glsl:52-57)
+        const int gx = std::min(std::max(static_cast<int>(rel.x), 0), g.X - 1);
+        const int gy = std::min(std::max(static_cast<int>(rel.y), 0), g.Y - 1);
+        const int gz = std::min(std::max(static_cast<int>(rel.z), 0), g.Z - 1);
+        float u, v, irr[3], vis[2];
+        atlasSampleUV(g, gx, gy, gz, dir, ARK_DDGI_IRRADIANCE_RES, ARK_DDGI_ATLAS_PADDING, 1.0f / static_cast<float>(o.Wi), 1.0f / static_cast<float>(o.Hi), &u, &v);
+        sampleAtlas(o.irr, o.Wi, o.Hi, 4, u, v, irr, 3);
+        atlasSampleUV(g, gx, gy, gz, dir, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, 1.0f / static_cast<float>(o.Wv), 1.0f / static_cast<float>(o.Hv), &u, &v);
+        sampleAtlas(o.vis, o.Wv, o.Hv, 2, u, v, vis, 2);
+        V3 c = v3(1.0f, 0.0f, 1.0f);
+        if (mode == ARK_PROBE_DEBUG_IRRADIANCE) {
+            c = pow3(v3(irr[0], irr[1], irr[2]), 5.0f);
+        } else if (mode == ARK_PROBE_DEBUG_DISTANCE) {
+            c = splat(distanceScale * vis[0]);
+            if (vis[0] < 0.0f) c = v3(1.0f, 0.0f, 1.0f);
+        } else if (mode == ARK_PROBE_DEBUG_DISTANCE2) {
+            c = splat(distanceScale * vis[1]);
+        }
+        out[4 * i] = f32_to_f16(c.x);
+        out[4 * i + 1] = f32_to_f16(c.y);
+        out[4 * i + 2] = f32_to_f16(c.z);
+        out[4 * i + 3] = 0x3c00u;
+    }
+    return 0;
+}
+
 uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
 uint32_t oracle_rand_xorshift(uint32_t s) { return rand_xorshift(s); }
 

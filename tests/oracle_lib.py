@@ -48,6 +48,7 @@ def load():
         lib.oracle_bake_ao.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         lib.oracle_lighting_compose.argtypes = [C.c_void_p, C.POINTER(abi.ArkComposeDesc), C.c_int]
+        lib.oracle_probe_debug.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = lib
     return _lib
 
@@ -136,6 +137,13 @@ class Oracle:
         d.out = out.ctypes.data
         rc = self.lib.oracle_lighting_compose(self.h, C.byref(d), threads)
         assert rc == 0, rc
+        return out
+
+    def probe_debug(self, mode: int, distance_scale: float, probes, dirs):
+        probes = np.ascontiguousarray(probes, np.uint32)
+        dirs = np.ascontiguousarray(dirs, np.float32)
+        out = np.zeros((len(probes), 4), np.uint16)
+        assert self.lib.oracle_probe_debug(self.h, mode, distance_scale, len(probes), probes.ctypes.data, dirs.ctypes.data, out.ctypes.data) == 0
         return out
 
     def stats(self):
