@@ -45,6 +45,9 @@ namespace dev {
 
 typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#ifndef ARK_BRANCHLESS_STEP
+#define ARK_BRANCHLESS_STEP 0 // 1: both tests every step, no divergent branch (bit-identical; neutral for traversal, slower for shadow rays)
+#endif
 #ifndef ARK_BUFFER_FETCH
 #define ARK_BUFFER_FETCH 0 // 1: ds_read + buffer_load paths (measured 1.5 % slower than the merged flat loads)
 #endif
@@ -629,9 +632,60 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& 
 // Returns true when a triangle step produced a candidate (tt, uu, vv, backface
 // with the instance's handedness applied, inst, prim) in [tmin, tmax]; node steps
 // update the group state and return false.
+// Both tests without early exits (same operation sequence as intersectTri, all
+// conditions evaluated): used by the branch-free step below.
+__device__ __forceinline__ bool intersectTriFlat(V3 o, V3 d, float tmin, float tmax, const GpuTriangle& tr, float* outT, float* outU, float* outV, bool* backfaceDet)
+{
+    V3 v0 = { tr.t0[0], tr.t0[1], tr.t0[2] };
+    V3 e1 = { tr.t0[3], tr.t1[0], tr.t1[1] };
+    V3 e2 = { tr.t1[2], tr.t1[3], tr.t2[0] };
+    V3 p = cross(d, e2);
+    float det = dot(e1, p);
+    float inv = 1.0f / det;
+    V3 s = o - v0;
+    float u = dot(s, p) * inv;
+    V3 q = cross(s, e1);
+    float v = dot(d, q) * inv;
+    float tt = dot(e2, q) * inv;
+    *outT = tt;
+    *outU = u;
+    *outV = v;
+    *backfaceDet = det < 0.0f;
+    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (tt >= tmin && tt <= tmax);
+}
+
 __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o, V3 d, V3 idir, uint32_t oct, float tmin, float tmax, float& tt,
                                             float& uu, float& vv, bool& backface, uint32_t& inst, uint32_t& prim, uint32_t& cNodes, uint32_t& cTris)
 {
+#if ARK_BRANCHLESS_STEP
+    // A wave almost always holds both kinds of step (28 % are triangle steps), so it
+    // runs both tests anyway; computing both for every lane and selecting drops the
+    // divergent branch and its exec-mask bookkeeping. The unused test reads the other
+    // kind's words (finite or not, its result is discarded).
+    {
+        const GpuTriangle tr = triFromWords(fx.w0, fx.w1, fx.w2);
+        bool bf;
+        float t2, u2, v2;
+        const bool ok = intersectTriFlat(o, d, tmin, tmax, tr, &t2, &u2, &v2, &bf);
+        uint32_t gB, gBits, tB, tBits;
+        visitNode8(fx.w0, fx.w1, fx.w2, fx.w3, fx.w4, o, idir, oct, tmin, tmax, gB, gBits, tB, tBits);
+        cTris += fx.isTri ? 1u : 0u;
+        cNodes += fx.isTri ? 0u : 1u;
+        if (!fx.isTri) {
+            ts.gBase = gB;
+            ts.gBits = gBits;
+            ts.tBase = tB;
+            ts.tBits = tBits;
+        }
+        tt = t2;
+        uu = u2;
+        vv = v2;
+        inst = fx.w2.y;
+        prim = fx.w2.z;
+        backface = bf != (fx.w2.w != 0u);
+        return fx.isTri && ok;
+    }
+#endif
     if (fx.isTri) {
         cTris++;
         const GpuTriangle tr = triFromWords(fx.w0, fx.w1, fx.w2);
@@ -2036,6 +2090,9 @@ hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_
     if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+#if ARK_LDS_NODES <= 64 // 7 waves/SIMD only fit the LDS with a smaller node cache
+    else if (v == 7) hipLaunchKernelGGL((dev::k_trace_primary<false, 7, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+#endif
     else hipLaunchKernelGGL((dev::k_trace_primary<false, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     return hipGetLastError();
 }
@@ -2115,6 +2172,9 @@ const void* kernel_trace_primary_ptr(bool count)
     if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1, false>);
     if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5, false>);
     if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6, false>);
+#if ARK_LDS_NODES <= 64
+    if (v == 7) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 7, false>);
+#endif
     return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1, false>);
 }
 const void* kernel_shade_ptr(bool count)

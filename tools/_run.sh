@@ -1,2 +1,4 @@
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r01s3_pt.log 2>&1; rc=$?; tail -1 gpurun_out/r01s3_pt.log; [ $rc -eq 0 ] || { grep -E "assert|Error|FAILED" gpurun_out/r01s3_pt.log | head; exit 1; }
+L=$PWD/arkoserenderer_amd/lib
+ARK_DDGI_LIB=$L/libark_ddgi_bl.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bake.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r01s3_pt4.log 2>&1; rc=$?; echo "bl: $(tail -1 gpurun_out/r01s3_pt4.log)"; [ $rc -eq 0 ] || exit 1
+bash tools/sweep_env.sh r01s3_bl "ARK_DDGI_LIB=$L/libark_ddgi.so" "ARK_DDGI_LIB=$L/libark_ddgi_bl.so" "ARK_DDGI_LIB=$L/libark_ddgi.so" "ARK_DDGI_LIB=$L/libark_ddgi_bl.so"
