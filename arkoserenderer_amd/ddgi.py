@@ -320,6 +320,21 @@ class BakeAmbientOcclusionNode:
         return ctx.bake_read(abi.ARK_BAKE_OUTPUT)
 
 
+
+def _tensor_stream(ctx: "DDGIContext", tensor, stream: int | None) -> int:
+    """Stream for a consumer node whose planes are torch tensors: the caller's, else
+    torch's current stream on the tensor's device. The context's own stream is
+    non-blocking, so launching there would race torch's producers of the planes (a
+    zero-filled output, for one) and its consumers; the reference records the node
+    into the frame's one command list, i.e. in order with both. The context's queued
+    work (an update writing the atlases) is finished first."""
+    if stream:
+        return stream
+    import torch
+
+    ctx.synchronize()
+    return torch.cuda.current_stream(tensor.device).cuda_stream
+
 class LightingComposeNode:
     """Python mirror of LightingComposeNode (name "Lighting compose",
     arkose/rendering/lighting/LightingComposeNode.{h,cpp}) for the WITH_DDGI
@@ -367,7 +382,8 @@ class LightingComposeNode:
                 if not t.is_contiguous() or int(t.shape[0]) != h or int(t.shape[1]) != w:
                     raise ValueError(f"LightingComposeNode: plane {name} must be a contiguous [{h}, {w}, ...] tensor")
                 planes[name] = t.data_ptr()
-        ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(), stream)
+        ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(),
+                            _tensor_stream(ctx, out, stream))
 
 
 class DDGIProbeDebug:
@@ -404,4 +420,4 @@ class DDGIProbeDebug:
         if self.debug_visualisation == abi.ARK_PROBE_DEBUG_DISABLED:
             return
         ctx.probe_debug(self.debug_visualisation, self.distance_scale, int(probes.shape[0]), probes.data_ptr(), dirs.data_ptr(),
-                        out.data_ptr(), stream)
+                        out.data_ptr(), _tensor_stream(ctx, out, stream))

@@ -23,7 +23,10 @@ def _run(ctx, orc, probes, dirs, mode, scale=0.01):
     ctx.synchronize()
     got = out.cpu().numpy().view(np.uint16)
     want = orc.probe_debug(mode, scale, probes, dirs)
-    assert np.array_equal(got, want), f"mode {mode}: {int((got != want).sum())} differ"
+    if not np.array_equal(got, want):
+        bad = np.nonzero(np.any(got != want, axis=1))[0]
+        rows = "; ".join(f"#{i} probe {probes[i]} got {got[i].view(np.float16)} want {want[i].view(np.float16)}" for i in bad[:6])
+        raise AssertionError(f"mode {mode}: {int((got != want).sum())} values in {bad.size} rows differ: {rows}")
     return got
 
 
