@@ -102,6 +102,15 @@ struct ArkDdgiCtx {
     hipStream_t stream = nullptr;
     hipStream_t auxStream = nullptr; // second stream of the sub-window pipeline
     hipEvent_t evFork = nullptr, evJoin = nullptr;
+    // Deferred probe update (ark_ddgi_set_deferred_update): a frame's probe update runs
+    // on updStream after its shading (evShaded) and signals evUpd; the next frame's
+    // traversal does not wait for it (it reads neither atlas), its shading does.
+    hipStream_t updStream = nullptr;
+    hipEvent_t evShaded = nullptr, evUpd = nullptr;
+    bool deferred = false;
+    bool updPending = false;       // evUpd guards a probe update not yet joined
+    bool updPendingOffsets = false; // ... which also writes the probe offsets
+    uint32_t slotFlip = 0;          // slot table half of the next deferred frame
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -259,13 +268,28 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipStreamCreateWithFlags(&ctx->auxStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate aux");
     if ((e = hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    {
+        // the deferred probe update should take the CUs the next frame's traversal
+        // leaves (its tail), not compete with its start: lowest stream priority
+        // (ARK_UPD_PRIORITY=normal for the default priority)
+        int least = 0, greatest = 0;
+        const char* pe = std::getenv("ARK_UPD_PRIORITY");
+        const bool low = !(pe && std::strcmp(pe, "normal") == 0);
+        if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+        if ((e = hipStreamCreateWithPriority(&ctx->updStream, hipStreamNonBlocking, low ? least : 0)) != hipSuccess) return bad(e, "hipStreamCreate update");
+        if (const char* pd = std::getenv("ARK_DEBUG_PRIORITY")) {
+            if (pd[0] == '1') std::fprintf(stderr, "ark_ddgi: stream priority range least %d greatest %d, update stream %d\n", least, greatest, low ? least : 0);
+        }
+    }
+    if ((e = hipEventCreateWithFlags(&ctx->evShaded, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evUpd, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
     if ((e = ctx->irr.alloc(static_cast<size_t>(ctx->Wi) * ctx->Hi * 8)) != hipSuccess) return bad(e, "alloc irradiance");
     if ((e = ctx->vis.alloc(static_cast<size_t>(ctx->Wv) * ctx->Hv * 4)) != hipSuccess) return bad(e, "alloc visibility");
     if ((e = ctx->offsets.alloc(static_cast<size_t>(ctx->N) * 16)) != hipSuccess) return bad(e, "alloc offsets");
-    if ((e = ctx->slots.alloc(K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
+    if ((e = ctx->slots.alloc(2 * K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
     if ((e = ctx->slotOrder.alloc(K * 4)) != hipSuccess) return bad(e, "alloc slot order");
     if ((e = ctx->fib.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib");
     if ((e = ctx->order.alloc(R * 4)) != hipSuccess) return bad(e, "alloc order");
@@ -296,6 +320,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->updStream) (void)hipStreamSynchronize(ctx->updStream);
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->triNormals, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
@@ -306,6 +331,9 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
     if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
     if (ctx->auxStream) (void)hipStreamDestroy(ctx->auxStream);
+    if (ctx->evShaded) (void)hipEventDestroy(ctx->evShaded);
+    if (ctx->evUpd) (void)hipEventDestroy(ctx->evUpd);
+    if (ctx->updStream) (void)hipStreamDestroy(ctx->updStream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -318,6 +346,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (!s || s->struct_size != sizeof(ArkDdgiScene)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiScene");
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipStreamSynchronize(ctx->stream));
+    ARK_HIP(hipStreamSynchronize(ctx->updStream));
     const auto t0 = std::chrono::steady_clock::now();
     // validate
     for (uint32_t i = 0; i < s->instance_count; ++i) {
@@ -600,6 +629,13 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
 
+// Orders `s` after a deferred probe update still in flight (atlases and offsets).
+static hipError_t joinPendingUpdate(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (!ctx->updPending) return hipSuccess;
+    return hipStreamWaitEvent(s, ctx->evUpd, 0);
+}
+
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
 {
     return updateImpl(ctx, p, hipStream, nullptr, nullptr);
@@ -650,7 +686,14 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
     f.offsets = ctx->offsets.as<float4>();
-    f.slots = ctx->slots.as<GpuProbeSlot>();
+    // Deferred probe update: this frame's update goes to updStream, and the next
+    // frame's traversal may run beside it. Off while timing stages or on the
+    // overlapped (multi-GPU) path, whose events already order the frames.
+    const bool deferNow = ctx->deferred && !ctx->timing && !shadeWaitEvent && !doneEvent;
+    // the traversal reads the probe offsets: it waits if the pending update writes them
+    const bool waitBeforeTrace = ctx->updPending && (!deferNow || ctx->updPendingOffsets);
+    const bool waitBeforeShade = ctx->updPending;
+    f.slots = ctx->slots.as<GpuProbeSlot>() + (deferNow ? static_cast<size_t>(ctx->slotFlip) * ctx->Kmax : 0);
     f.fib = ctx->fib.as<float4>();
     if (ctx->orderR != R) {
         sampleTraversalOrder(R, ctx->orderHost);
@@ -711,6 +754,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.counters = ctx->counters.as<unsigned long long>();
     const bool timing = ctx->timing;
     const bool count = ctx->counting;
+    if (waitBeforeTrace) ARK_HIP(joinPendingUpdate(ctx, s));
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
     ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, ctx->rayCounter.bytes, s));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
@@ -786,6 +830,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
                 FrameArgs p1 = g;
                 p1.shade_pass = 1;
                 ARK_HIP(hipStreamWaitEvent(ctx->auxStream, ctx->evFork, 0));
+                if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, ctx->auxStream));
                 if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(ctx->auxStream, static_cast<hipEvent_t>(shadeWaitEvent), 0));
                 ARK_HIP(launch_shade(ctx->scene, p1, ctx->shadeBlocks, count, ctx->auxStream));
                 ARK_HIP(hipEventRecord(ctx->evJoin, ctx->auxStream));
@@ -795,6 +840,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
             // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
             // rank it waits here for the previous exchange (the traversal above did not)
             if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(ss, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+            if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, ss)); // the previous frame's atlases
             ARK_HIP(launch_shade(ctx->scene, g, ctx->shadeBlocks, count, ss));
             if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], ss));
             if (g.fused_shadows == 0 && g.light_count > 0) {
@@ -808,8 +854,22 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
             ARK_HIP(hipStreamWaitEvent(s, ctx->evJoin, 0));
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
-        ARK_HIP(launch_probe_update(f, s));
+        if (deferNow) {
+            hipStream_t us = ctx->updStream;
+            ARK_HIP(hipEventRecord(ctx->evShaded, s));
+            ARK_HIP(hipStreamWaitEvent(us, ctx->evShaded, 0));
+            ARK_HIP(launch_probe_update(f, us));
+            ARK_HIP(hipEventRecord(ctx->evUpd, us));
+            ctx->updPending = true;
+            ctx->updPendingOffsets = f.update_offsets != 0;
+            ctx->slotFlip ^= 1u;
+        } else {
+            ARK_HIP(launch_probe_update(f, s));
+            ctx->updPending = false;
+        }
     } else {
+        if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, s));
+        ctx->updPending = false;
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
@@ -832,7 +892,9 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipStreamSynchronize(ctx->stream));
+    ARK_HIP(hipStreamSynchronize(ctx->updStream));
     ARK_HIP(hipDeviceSynchronize());
+    ctx->updPending = false;
     return ARK_DDGI_OK;
 }
 
@@ -940,6 +1002,21 @@ int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out)
         out->front_hits = c[6];
         out->primary_wave_steps = c[7];
     }
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_set_deferred_update(ArkDdgiCtx* ctx, int enabled)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->deferred = enabled != 0;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_join_update(ArkDdgiCtx* ctx, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(joinPendingUpdate(ctx, hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream));
     return ARK_DDGI_OK;
 }
 
@@ -1067,6 +1144,7 @@ int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void*
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
     ArkComposeDesc c = *desc;
+    ARK_HIP(joinPendingUpdate(ctx, s));
     ARK_HIP(launch_lighting_compose(f, c, s));
     return ARK_DDGI_OK;
 }
@@ -1087,6 +1165,7 @@ int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* h
     }
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
+    ARK_HIP(joinPendingUpdate(ctx, s));
     ARK_HIP(launch_probe_debug(f, *desc, s));
     return ARK_DDGI_OK;
 }

@@ -167,6 +167,13 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_get_counters(self.h, C.byref(c)), "ark_ddgi_get_counters")
         return c
 
+    def set_deferred_update(self, on: bool):
+        """Frame n's probe update beside frame n+1's traversal (include/ark_ddgi.h)."""
+        self.check(self.lib.ark_ddgi_set_deferred_update(self.h, int(on)), "ark_ddgi_set_deferred_update")
+
+    def join_update(self, stream: int | None = None):
+        self.check(self.lib.ark_ddgi_join_update(self.h, C.c_void_p(stream) if stream else None), "ark_ddgi_join_update")
+
     def set_timing(self, on: bool):
         self.check(self.lib.ark_ddgi_set_timing(self.h, int(on)), "ark_ddgi_set_timing")
 

@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--deferred-update", type=int, default=0,
+                    help="1: frame n's probe update beside frame n+1's traversal (ark_ddgi_set_deferred_update; "
+                         "N=1 only; measured 0.3-0.5 %% slower on C4, DESIGN.md §9)")
     ap.add_argument("--no-ao-bake", action="store_true", help="skip the config C1 AO bake line (GPU + CPU oracle)")
     ap.add_argument("--ao-size", type=int, default=1024)
     ap.add_argument("--ao-samples", type=int, default=64)
@@ -105,6 +108,8 @@ def main():
         from arkoserenderer_amd.collective import OverlappedSlabExchange
 
         exch = OverlappedSlabExchange(node, SlabExchange.from_views(ctx.device_views(), rank, world, device).exchange, device)
+    deferred = bool(args.deferred_update) and exch is None
+    ctx.set_deferred_update(deferred)
     setup_s = time.time() - t_setup
 
     frame = 0
@@ -203,6 +208,7 @@ def main():
             "rays_per_probe": R,
             "probe_updates_per_step": K,
             "parallelism": f"zslab{world}",
+            "deferred_update": deferred,
             "bvh_nodes": int(bvh.node_count),
             "bvh_max_depth": int(bvh.max_depth),
             "bvh_build_ms": round(bvh.build_ms, 1),

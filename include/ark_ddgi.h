@@ -296,6 +296,20 @@ int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out_counters);
  * [3] probe update (irradiance, visibility, borders, offsets), [4] shadow rays
  * (traversal + light-term finish). Milliseconds. */
 int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out_ms, int count);
+/* Deferred probe update (off by default). The reference records a frame's probe
+ * update behind a barrier after its traceRays (DDGINode.cpp:171-240), and the next
+ * frame's traceRays waits for it; but the traversal reads neither atlas (only the
+ * closest-hit indirect lookup does, raygen.rgen:94-106), so with this on, frame
+ * n's probe update runs on an internal stream beside frame n+1's traversal, and
+ * frame n+1's shading waits for it (its traversal too, when frame n moved the probe
+ * offsets). Results are identical. After ark_ddgi_update returns, the atlases are
+ * complete for: the next update, ark_ddgi_lighting_compose / ark_ddgi_probe_debug,
+ * ark_ddgi_read, ark_ddgi_synchronize; any other reader of the device views first
+ * calls ark_ddgi_join_update(ctx, its_stream). Not applied on the overlapped path
+ * or while stage timing is on. */
+int ark_ddgi_set_deferred_update(ArkDdgiCtx* ctx, int enabled);
+/* Makes `hip_stream` (NULL = ctx stream) wait for a deferred probe update in flight. */
+int ark_ddgi_join_update(ArkDdgiCtx* ctx, void* hip_stream);
 int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled);
 
 /* BVH statistics of the last set_scene (node count, leaf triangle count, depth, SAH cost, bytes). */
