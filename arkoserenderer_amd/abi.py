@@ -327,6 +327,27 @@ class ArkProbeDebugDesc(C.Structure):
     ]
 
 
+class ArkReflectionsDesc(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("no_tracing_roughness", C.c_float),
+        ("environment_multiplier", C.c_float),
+        ("ambient_amount", C.c_float),
+        ("world_from_view", C.c_float * 16),
+        ("view_from_projection", C.c_float * 16),
+        ("depth", C.c_void_p),
+        ("material", C.c_void_p),
+        ("normal_velocity", C.c_void_p),
+        ("blue_noise", C.c_void_p),
+        ("noise_width", C.c_uint32),
+        ("noise_height", C.c_uint32),
+        ("out_radiance", C.c_void_p),
+        ("out_direction", C.c_void_p),
+    ]
+
+
 # G-buffer plane name -> (dtype, channels) in ArkComposeDesc order
 COMPOSE_PLANES = [
     ("depth", "float32", 1), ("base_color", "uint8", 4), ("material", "uint8", 4),
@@ -357,7 +378,7 @@ class ArkSoupParams(C.Structure):
 ABI_STRUCTS = [
     ArkDdgiDesc, ArkRTVertex, ArkRTTriangleMesh, ArkShaderMaterial, ArkTexture, ArkRTInstance,
     ArkDirectionalLight, ArkSpotLight, ArkDdgiScene, ArkDdgiFrameParams, ArkDdgiCounters,
-    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc, ArkComposeDesc, ArkProbeDebugDesc,
+    ArkDdgiDeviceViews, ArkDdgiBvhStats, ArkBakeAoDesc, ArkComposeDesc, ArkProbeDebugDesc, ArkReflectionsDesc,
 ]
 
 # name -> (restype, argtypes)
@@ -386,6 +407,7 @@ EXPORTS = {
     "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "ark_ddgi_lighting_compose": (C.c_int, [C.c_void_p, C.POINTER(ArkComposeDesc), C.c_void_p]),
     "ark_ddgi_probe_debug": (C.c_int, [C.c_void_p, C.POINTER(ArkProbeDebugDesc), C.c_void_p]),
+    "ark_ddgi_rt_reflections": (C.c_int, [C.c_void_p, C.POINTER(ArkReflectionsDesc), C.c_void_p]),
     # ark_ies.h
     "ark_ies_lut_from_memory": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),
     "ark_ies_lut_from_file": (C.c_int, [C.c_char_p, C.c_uint32, C.c_void_p, C.POINTER(ArkIesInfo)]),

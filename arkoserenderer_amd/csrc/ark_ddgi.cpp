@@ -1149,6 +1149,36 @@ int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void*
     return ARK_DDGI_OK;
 }
 
+int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!desc || desc->struct_size != sizeof(ArkReflectionsDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkReflectionsDesc");
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "rt_reflections before ark_ddgi_set_scene");
+    if (!desc->out_radiance || !desc->out_direction) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: no output image");
+    if (desc->blue_noise && (desc->noise_width == 0 || desc->noise_height == 0)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: empty blue noise");
+    if (static_cast<uint64_t>(desc->width) * desc->height >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: target too large");
+    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    ARK_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = ensureSpill(ctx)) != 0) return rc;
+    FrameArgs f {};
+    f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
+    f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
+    for (int k = 0; k < 3; ++k) {
+        f.spacing[k] = ctx->desc.probe_spacing[k];
+        f.origin[k] = ctx->desc.offset_to_first[k];
+    }
+    f.irr = ctx->irr.as<uint16_t>();
+    f.vis = ctx->vis.as<uint16_t>();
+    f.z_far = ctx->desc.z_far;
+    f.ambient_amount = desc->ambient_amount;
+    f.environment_multiplier = desc->environment_multiplier;
+    f.spill = ctx->spill.as<uint32_t>();
+    ARK_HIP(joinPendingUpdate(ctx, s));
+    ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, s));
+    return ARK_DDGI_OK;
+}
+
 int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* hipStream)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;

@@ -166,6 +166,7 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 // stage 0: parameterization raster, 1: barycentrics + work list, 2: AO rays
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s);
 hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s);
+hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t blocks, hipStream_t s);
 hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hipStream_t s);
 hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
 hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);

@@ -2029,6 +2029,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 }
 
 #include "ddgi_compose.inc"
+#include "ddgi_reflections.inc"
 
 } // namespace dev
 
@@ -2203,6 +2204,13 @@ hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hi
 {
     if (d.count == 0) return hipSuccess;
     hipLaunchKernelGGL(dev::k_probe_debug, dim3((d.count + 255u) / 256u), dim3(256), 0, s, f, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t blocks, hipStream_t s)
+{
+    if (r.width == 0 || r.height == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_rt_reflections, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f, r);
     return hipGetLastError();
 }
 

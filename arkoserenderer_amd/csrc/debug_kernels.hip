@@ -74,7 +74,7 @@ extern "C" int ark_ddgi_debug_struct_sizes(uint32_t* out, int n)
 {
     const uint32_t sizes[] = { sizeof(ArkDdgiDesc), sizeof(ArkRTVertex), sizeof(ArkRTTriangleMesh), sizeof(ArkShaderMaterial), sizeof(ArkTexture),
                                sizeof(ArkRTInstance), sizeof(ArkDirectionalLight), sizeof(ArkSpotLight), sizeof(ArkDdgiScene), sizeof(ArkDdgiFrameParams),
-                               sizeof(ArkDdgiCounters), sizeof(ArkDdgiDeviceViews), sizeof(ArkDdgiBvhStats), sizeof(ArkBakeAoDesc), sizeof(ArkComposeDesc), sizeof(ArkProbeDebugDesc) };
+                               sizeof(ArkDdgiCounters), sizeof(ArkDdgiDeviceViews), sizeof(ArkDdgiBvhStats), sizeof(ArkBakeAoDesc), sizeof(ArkComposeDesc), sizeof(ArkProbeDebugDesc), sizeof(ArkReflectionsDesc) };
     int m = static_cast<int>(sizeof(sizes) / sizeof(sizes[0]));
     for (int i = 0; i < n && i < m; ++i) out[i] = sizes[i];
     return m < n ? m : n;

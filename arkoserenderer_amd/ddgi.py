@@ -77,6 +77,25 @@ def _check(lib, ctx, rc, what):
         raise abi.ArkDdgiError(rc, f"{what}: {msg.decode() if msg else ''}")
 
 
+def desc_for(grid: ProbeGrid, z_far: float, config: DDGIConfig, device: int = 0, shard_rank: int = 0,
+             shard_count: int = 1) -> abi.ArkDdgiDesc:
+    """The ArkDdgiDesc of a context (host only; the oracle takes it too)."""
+    d = abi.ArkDdgiDesc()
+    d.struct_size = C.sizeof(abi.ArkDdgiDesc)
+    for k in range(3):
+        d.grid_dims[k] = int(grid.grid_dimensions[k])
+        d.probe_spacing[k] = float(grid.probe_spacing[k])
+        d.offset_to_first[k] = float(grid.offset_to_first[k])
+    d.z_far = float(z_far)
+    d.max_rays_per_probe = int(config.max_rays_per_probe)
+    d.max_probe_updates = int(config.max_probe_updates)
+    d.device = int(device)
+    d.clear_overflow_mode = int(config.clear_overflow_mode)
+    d.shard_rank = int(shard_rank)
+    d.shard_count = int(shard_count)
+    return d
+
+
 class DDGIContext:
     """Owns one ark_ddgi context (device memory of one DDGI node on one GPU)."""
 
@@ -85,19 +104,7 @@ class DDGIContext:
         self.lib = abi.load_library()
         self.grid = grid
         self.config = config or DDGIConfig()
-        d = abi.ArkDdgiDesc()
-        d.struct_size = C.sizeof(abi.ArkDdgiDesc)
-        for k in range(3):
-            d.grid_dims[k] = int(grid.grid_dimensions[k])
-            d.probe_spacing[k] = float(grid.probe_spacing[k])
-            d.offset_to_first[k] = float(grid.offset_to_first[k])
-        d.z_far = float(z_far)
-        d.max_rays_per_probe = int(self.config.max_rays_per_probe)
-        d.max_probe_updates = int(self.config.max_probe_updates)
-        d.device = int(device)
-        d.clear_overflow_mode = int(self.config.clear_overflow_mode)
-        d.shard_rank = int(shard_rank)
-        d.shard_count = int(shard_count)
+        d = desc_for(grid, z_far, self.config, device, shard_rank, shard_count)
         self.desc = d
         h = C.c_void_p()
         rc = self.lib.ark_ddgi_create(C.byref(d), C.byref(h))
@@ -217,6 +224,11 @@ class DDGIContext:
         d.out = int(out_ptr)
         self.check(self.lib.ark_ddgi_lighting_compose(self.h, C.byref(d), C.c_void_p(stream) if stream else None),
                    "ark_ddgi_lighting_compose")
+
+    def rt_reflections(self, desc: abi.ArkReflectionsDesc, stream: int | None = None):
+        """ark_ddgi_rt_reflections: `desc` holds device pointers (include/ark_ddgi.h)."""
+        desc.struct_size = C.sizeof(abi.ArkReflectionsDesc)
+        self.check(self.lib.ark_ddgi_rt_reflections(self.h, C.byref(desc), C.c_void_p(stream) if stream else None), "ark_ddgi_rt_reflections")
 
     def probe_debug(self, visualisation: int, distance_scale: float, count: int, probes_ptr: int, dirs_ptr: int, out_ptr: int,
                     stream: int | None = None):
@@ -342,6 +354,13 @@ def _tensor_stream(ctx: "DDGIContext", tensor, stream: int | None) -> int:
     ctx.synchronize()
     return torch.cuda.current_stream(tensor.device).cuda_stream
 
+
+def _after_launch(ctx: "DDGIContext", stream: int | None):
+    """torch's legacy default stream has handle 0, which the C-ABI reads as the
+    context's (non-blocking) stream: finish the launch before torch reads the planes."""
+    if not stream:
+        ctx.synchronize()
+
 class LightingComposeNode:
     """Python mirror of LightingComposeNode (name "Lighting compose",
     arkose/rendering/lighting/LightingComposeNode.{h,cpp}) for the WITH_DDGI
@@ -389,8 +408,9 @@ class LightingComposeNode:
                 if not t.is_contiguous() or int(t.shape[0]) != h or int(t.shape[1]) != w:
                     raise ValueError(f"LightingComposeNode: plane {name} must be a contiguous [{h}, {w}, ...] tensor")
                 planes[name] = t.data_ptr()
-        ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(),
-                            _tensor_stream(ctx, out, stream))
+        s = _tensor_stream(ctx, out, stream)
+        ctx.lighting_compose(w, h, self.flags("screen_space_occlusion" in gbuffer), camera, planes, out.data_ptr(), s)
+        _after_launch(ctx, s)
 
 
 class DDGIProbeDebug:
@@ -426,5 +446,49 @@ class DDGIProbeDebug:
         (DDGIProbeDebug.cpp:53-54)."""
         if self.debug_visualisation == abi.ARK_PROBE_DEBUG_DISABLED:
             return
+        s = _tensor_stream(ctx, out, stream)
         ctx.probe_debug(self.debug_visualisation, self.distance_scale, int(probes.shape[0]), probes.data_ptr(), dirs.data_ptr(),
-                        out.data_ptr(), _tensor_stream(ctx, out, stream))
+                        out.data_ptr(), s)
+        _after_launch(ctx, s)
+
+
+def reflections_desc(width: int, height: int, camera: dict, planes: dict, no_tracing_roughness: float = 0.7,
+                     environment_multiplier: float = 1.0, ambient_amount: float = 0.0) -> abi.ArkReflectionsDesc:
+    """ArkReflectionsDesc from a camera dict (world_from_view, view_from_projection:
+    column-major 16 floats) and a plane dict of pointers (depth, material,
+    normal_velocity, blue_noise, out_radiance, out_direction; missing = NULL) plus
+    noise_width / noise_height. The defaults are RTReflectionsNode's
+    (RTReflectionsNode.h: m_noTracingRoughnessThreshold 0.7)."""
+    d = abi.ArkReflectionsDesc()
+    d.struct_size = C.sizeof(abi.ArkReflectionsDesc)
+    d.width, d.height = int(width), int(height)
+    d.no_tracing_roughness, d.environment_multiplier, d.ambient_amount = float(no_tracing_roughness), float(environment_multiplier), float(ambient_amount)
+    for k in ("world_from_view", "view_from_projection"):
+        getattr(d, k)[:] = [float(v) for v in np.asarray(camera[k], np.float32).reshape(16)]
+    for k in ("depth", "material", "normal_velocity", "blue_noise", "out_radiance", "out_direction"):
+        v = planes.get(k)
+        setattr(d, k, int(v) if v else None)
+    d.noise_width, d.noise_height = int(planes.get("noise_width", 0)), int(planes.get("noise_height", 0))
+    return d
+
+
+class RTReflectionsNode:
+    """Mirror of RTReflectionsNode's ray-tracing pass (RTReflectionsNode.cpp:60-82):
+    the raygen with WITH_DDGI on torch G-buffer planes; the temporal denoiser passes
+    are not on the path."""
+
+    def __init__(self):
+        self.no_tracing_roughness_threshold = 0.7  # m_noTracingRoughnessThreshold
+        self.mirror_roughness_threshold = 0.0      # parameter1: read by no code path of the raygen
+
+    def execute(self, ctx: DDGIContext, camera: dict, gbuffer: dict, blue_noise, out_radiance, out_direction,
+                environment_multiplier: float = 1.0, ambient_amount: float = 0.0, stream: int | None = None):
+        h, w = int(out_radiance.shape[0]), int(out_radiance.shape[1])
+        planes = {k: (t.data_ptr() if t is not None else None) for k, t in gbuffer.items()}
+        planes.update(out_radiance=out_radiance.data_ptr(), out_direction=out_direction.data_ptr())
+        if blue_noise is not None:
+            planes.update(blue_noise=blue_noise.data_ptr(), noise_width=int(blue_noise.shape[1]), noise_height=int(blue_noise.shape[0]))
+        d = reflections_desc(w, h, camera, planes, self.no_tracing_roughness_threshold, environment_multiplier, ambient_amount)
+        s = _tensor_stream(ctx, out_radiance, stream)
+        ctx.rt_reflections(d, s)
+        _after_launch(ctx, s)

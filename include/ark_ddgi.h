@@ -409,6 +409,40 @@ typedef struct ArkComposeDesc {
  * enqueued before it on that stream. */
 int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void* hip_stream);
 
+/* ---- DDGI consumer: RT reflections ray generation -----------
+ * Replaces the traceRays of RTReflectionsNode (RTReflectionsNode.cpp:60-82) and its
+ * raygen rt-reflections/raygen.rgen:54-166 with WITH_DDGI: per pixel of the G-buffer,
+ * one GGX-VNDF-sampled reflection ray (blue-noise driven) traced against the opaque
+ * class, shaded by the closest-hit program (opaque.rchit:105-176: emissive + ambient +
+ * sun + spots with shadow rays, on front AND back faces, hitT signed) plus the DDGI
+ * diffuse term read from this context's atlases (min(metallic, 0.6), F = 0.04), or
+ * the environment on a miss. Writes the reflection radiance + signed ray length and
+ * the world reflection direction as RGBA16F. Depth >= 1 - 1e-6: result 0, direction
+ * left as is; roughness >= no_tracing_roughness: both 0 (raygen.rgen:60-76). The
+ * temporal denoiser passes after it (reproject/resolve/prefilter) are not on the path. */
+typedef struct ArkReflectionsDesc {
+    uint32_t struct_size;
+    uint32_t width, height;              /* rt_LaunchSize */
+    float no_tracing_roughness;          /* parameter2 (m_noTracingRoughnessThreshold) */
+    float environment_multiplier;        /* constants.environmentMultiplier */
+    float ambient_amount;                /* constants.ambientAmount (closest hit) */
+    float world_from_view[16];           /* CameraState, column-major as GLSL mat4 */
+    float view_from_projection[16];
+    const float* depth;                  /* SceneDepth (non-linear) */
+    const uint8_t* material;             /* SceneMaterial RGBA8: r roughness, g metallic */
+    const uint16_t* normal_velocity;     /* SceneNormalVelocity RGBA16F: rg octahedral view-space normal */
+    const float* blue_noise;             /* one layer of the blue-noise array, RG32F, noise_width x noise_height;
+                                            the layer is frameIndex % layers (parameter3). Sampled at
+                                            pixelCenter / size at LOD 0 with repeat: texel (x mod w, y mod h) */
+    uint32_t noise_width, noise_height;
+    uint16_t* out_radiance;              /* resultImage RGBA16F: radiance, signed ray length */
+    uint16_t* out_direction;             /* reflectionDirectionImg RGBA16F: world direction, 0 */
+} ArkReflectionsDesc;
+
+/* Enqueues the reflection rays on `hip_stream` (NULL = ctx stream), after any update
+ * enqueued before it on that stream (it shares the update's traversal stack space). */
+int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, void* hip_stream);
+
 /* ---- DDGI probe debug visualisation --------------------------
  * The fragment stage of DDGIProbeDebug (DDGIProbeDebug.cpp:34-71,
  * ddgi/probeDebug.frag): for each (probe index, sphere normal) sample, the colour the

@@ -1669,6 +1669,119 @@ int oracle_lighting_compose(void* ctx, const ArkComposeDesc* c, int threads)
     return 0;
 }
 
+// RT reflections ray generation (rt-reflections/raygen.rgen:54-166, WITH_DDGI;
+// include/ark_ddgi.h ark_ddgi_rt_reflections) on host arrays, against the oracle's
+// scene and current atlases. Matrix products sum in index order (the HIP kernel's
+// ddgi_reflections.inc does the same).
+int oracle_rt_reflections(void* ctx, const ArkReflectionsDesc* r, int threads)
+{
+    const Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!r || r->struct_size != sizeof(ArkReflectionsDesc) || !r->out_radiance || !r->out_direction) return ARK_DDGI_E_INVALID_ARGUMENT;
+    auto store = [](uint16_t* out, size_t p, V3 c, float w) {
+        out[4 * p] = f32_to_f16(c.x);
+        out[4 * p + 1] = f32_to_f16(c.y);
+        out[4 * p + 2] = f32_to_f16(c.z);
+        out[4 * p + 3] = f32_to_f16(w);
+    };
+    auto mulPoint = [](const float* M, float x, float y, float z, float w, float out[4]) {
+        for (int i = 0; i < 4; ++i) out[i] = M[i] * x + M[4 + i] * y + M[8 + i] * z + M[12 + i] * w;
+    };
+    float PW[16]; // camera.worldFromView * camera.viewFromProjection
+    for (int c = 0; c < 4; ++c)
+        for (int q = 0; q < 4; ++q)
+            PW[c * 4 + q] = r->world_from_view[q] * r->view_from_projection[c * 4] + r->world_from_view[4 + q] * r->view_from_projection[c * 4 + 1] +
+                            r->world_from_view[8 + q] * r->view_from_projection[c * 4 + 2] + r->world_from_view[12 + q] * r->view_from_projection[c * 4 + 3];
+    const int n = static_cast<int>(static_cast<uint64_t>(r->width) * r->height);
+    parallelFor(n, threads, [&](int i, int) {
+        const size_t p = static_cast<size_t>(i);
+        const uint32_t px = static_cast<uint32_t>(i) % r->width, py = static_cast<uint32_t>(i) / r->width;
+        const float pcx = static_cast<float>(px) + 0.5f, pcy = static_cast<float>(py) + 0.5f;
+        const float inU = pcx / static_cast<float>(r->width), inV = pcy / static_cast<float>(r->height);
+        const float nonLinearDepth = r->depth ? r->depth[p] : 0.0f;
+        if (nonLinearDepth >= 1.0f - 1e-6f) { // :60-64
+            store(r->out_radiance, p, splat(0.0f), 0.0f);
+            return;
+        }
+        const float roughness = r->material ? static_cast<float>(r->material[4 * p]) / 255.0f : 0.0f; // :66-68
+        if (roughness >= r->no_tracing_roughness) { // :70-76
+            store(r->out_radiance, p, splat(0.0f), 0.0f);
+            store(r->out_direction, p, splat(0.0f), 0.0f);
+            return;
+        }
+        const float nvx = r->normal_velocity ? f16_to_f32(r->normal_velocity[4 * p]) : 0.0f;
+        const float nvy = r->normal_velocity ? f16_to_f32(r->normal_velocity[4 * p + 1]) : 0.0f;
+        const V3 vsn = octahedralDecode(nvx, nvy); // encoding.glsl decodeNormal
+        const float* Wv = r->world_from_view;
+        const V3 N = { Wv[0] * vsn.x + Wv[4] * vsn.y + Wv[8] * vsn.z, Wv[1] * vsn.x + Wv[5] * vsn.y + Wv[9] * vsn.z,
+                       Wv[2] * vsn.x + Wv[6] * vsn.y + Wv[10] * vsn.z };
+        float co[4], ct[4];
+        mulPoint(Wv, 0.0f, 0.0f, 0.0f, 1.0f, co);
+        mulPoint(PW, inU * 2.0f - 1.0f, inV * 2.0f - 1.0f, nonLinearDepth, 1.0f, ct);
+        const V3 target = v3(ct[0] / ct[3], ct[1] / ct[3], ct[2] / ct[3]);
+        const V3 rayOrigin = target;
+        const V3 viewRay = normalize(target - v3(co[0], co[1], co[2]));
+        float rx = 0.0f, ry = 0.0f; // textureLod(blueNoiseTexture, pixelCenter / size, 0) at a texel centre
+        if (r->blue_noise) {
+            const float* bn = r->blue_noise + 2 * (static_cast<size_t>(py % r->noise_height) * r->noise_width + px % r->noise_width);
+            rx = bn[0];
+            ry = bn[1];
+        }
+        V3 T; // createIsotropicTBN (:34-50): rows T, B, N
+        if (fabsf_(N.z) > 0.0f) {
+            const float k = sqrtf_(N.y * N.y + N.z * N.z);
+            T = v3(0.0f, -N.z / k, N.y / k);
+        } else {
+            const float k = sqrtf_(N.x * N.x + N.y * N.y);
+            T = v3(N.y / k, -N.x / k, 0.0f);
+        }
+        const V3 B = cross(N, T);
+        const V3 mv = -viewRay;
+        const V3 Ve = v3(dot(T, mv), dot(B, mv), dot(N, mv));
+        // sampleSpecularBRDF -> sampleGGXVNDF (brdf.glsl:99-125)
+        const float alpha = roughness * roughness;
+        const V3 Vh = normalize(v3(alpha * Ve.x, alpha * Ve.y, Ve.z));
+        const float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+        const V3 T1 = lensq > 0.0f ? v3(-Vh.y, Vh.x, 0.0f) * (1.0f / sqrtf_(lensq)) : v3(1.0f, 0.0f, 0.0f);
+        const V3 T2 = cross(Vh, T1);
+        const float rr = sqrtf_(rx);
+        const float phi = 2.0f * kPi * ry;
+        const float t1 = rr * cosf_(phi);
+        float t2 = rr * sinf_(phi);
+        const float sh = 0.5f * (1.0f + Vh.z);
+        t2 = (1.0f - sh) * sqrtf_(1.0f - t1 * t1) + sh * t2;
+        const V3 Nh = t1 * T1 + t2 * T2 + sqrtf_(fmaxf_(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
+        const V3 sampledNormal = normalize(v3(alpha * Nh.x, alpha * Nh.y, fmaxf_(0.0f, Nh.z)));
+        const V3 I = -Ve;
+        const V3 reflected = I - 2.0f * dot(sampledNormal, I) * sampledNormal; // reflect
+        const V3 rayDirection = T * reflected.x + B * reflected.y + N * reflected.z; // inverseTBN * reflected
+        float tmax = 10000.0f;
+        V3 radiance = splat(0.0f);
+        Stats st;
+        const Ray ray { rayOrigin, rayDirection, 0.01f, tmax };
+        Hit hit; // Opaque pass: RayFlags_Opaque, cullMask RT_HIT_MASK_OPAQUE (:108-119)
+        traverseClosest(o, o.bvhOpaque, ray, hit, false, st);
+        if (hit.hit) {
+            const Surface s = closestHit(o, ray, hit, r->ambient_amount, st, true);
+            tmax = s.hitT;
+            radiance = s.color;
+            const V3 P = rayOrigin + tmax * rayDirection; // :121-153
+            const float hitMetallic = fminf_(s.metallic, 0.6f);
+            const V3 irradiance = sampleDynamicDiffuseGlobalIllumination(o, P, s.normal, -rayDirection);
+            const V3 indirectDiffuse = splat(1.0f - hitMetallic) * splat(1.0f - DIELECTRIC_REFLECTANCE) * irradiance;
+            radiance = radiance + s.baseColor * indirectDiffuse;
+        } else { // :155-159
+            float u, v, c[4];
+            sphericalUvFromDirection(rayDirection, &u, &v);
+            const Tex& env = (o.envTex >= 0) ? o.textures[o.envTex] : o.envWhite;
+            sampleBilinear(env, u, v, c);
+            radiance = r->environment_multiplier * v3(c[0], c[1], c[2]);
+        }
+        store(r->out_radiance, p, radiance, tmax);
+        store(r->out_direction, p, rayDirection, 0.0f);
+    });
+    return 0;
+}
+
 // Probe debug fragment stage (ddgi/probeDebug.frag; include/ark_ddgi.h
 // ark_ddgi_probe_debug) on the oracle's current atlases; host arrays.
 int oracle_probe_debug(void* ctx, int mode, float distanceScale, uint32_t count, const uint32_t* probes, const float* dirs, uint16_t* out)

@@ -48,6 +48,7 @@ def load():
         lib.oracle_bake_ao.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         lib.oracle_lighting_compose.argtypes = [C.c_void_p, C.POINTER(abi.ArkComposeDesc), C.c_int]
+        lib.oracle_rt_reflections.argtypes = [C.c_void_p, C.POINTER(abi.ArkReflectionsDesc), C.c_int]
         lib.oracle_probe_debug.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = lib
     return _lib
@@ -138,6 +139,23 @@ class Oracle:
         rc = self.lib.oracle_lighting_compose(self.h, C.byref(d), threads)
         assert rc == 0, rc
         return out
+
+    def rt_reflections(self, width: int, height: int, camera: dict, planes: dict, threads: int = 8, **kw):
+        """oracle_rt_reflections on host arrays; returns (radiance, direction) RGBA16F
+        as uint16 [H, W, 4]; `planes` maps depth/material/normal_velocity/blue_noise to
+        numpy arrays."""
+        from arkoserenderer_amd.ddgi import reflections_desc
+        keep = {k: np.ascontiguousarray(v) for k, v in planes.items() if v is not None}
+        rad = np.zeros((height, width, 4), np.uint16)
+        dirs = np.zeros((height, width, 4), np.uint16)
+        ptrs = {k: v.ctypes.data for k, v in keep.items()}
+        ptrs.update(out_radiance=rad.ctypes.data, out_direction=dirs.ctypes.data)
+        if "blue_noise" in keep:
+            ptrs.update(noise_width=keep["blue_noise"].shape[1], noise_height=keep["blue_noise"].shape[0])
+        d = reflections_desc(width, height, camera, ptrs, **kw)
+        rc = self.lib.oracle_rt_reflections(self.h, C.byref(d), threads)
+        assert rc == 0, rc
+        return rad, dirs
 
     def probe_debug(self, mode: int, distance_scale: float, probes, dirs):
         probes = np.ascontiguousarray(probes, np.uint32)

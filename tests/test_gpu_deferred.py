@@ -81,10 +81,14 @@ def test_consumer_after_deferred_update():
     dirs[np.all(dirs == 0, axis=1)] = (0, 1, 0)
     node = D.DDGIProbeDebug()
     node.debug_visualisation = abi.ARK_PROBE_DEBUG_IRRADIANCE
-    out = torch.zeros((len(probes), 4), dtype=torch.int16, device="cuda")
-    # an explicit stream: no host sync in the node, the C entry's join orders the launch
-    node.execute(ctx, torch.from_numpy(probes.astype(np.int32)).cuda(), torch.from_numpy(dirs).cuda(), out,
-                 stream=torch.cuda.current_stream().cuda_stream)
+    # an explicit (non-null) stream: no host sync in the node, the C entry's join
+    # orders the launch after the pending update
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        out = torch.zeros((len(probes), 4), dtype=torch.int16, device="cuda")
+        node.execute(ctx, torch.from_numpy(probes.astype(np.int32)).cuda(), torch.from_numpy(dirs).cuda(), out,
+                     stream=side.cuda_stream)
+    side.synchronize()
     got = out.cpu().numpy().view(np.uint16)
     want = orc.probe_debug(abi.ARK_PROBE_DEBUG_IRRADIANCE, 0.01, probes, dirs)
     assert np.array_equal(got, want)

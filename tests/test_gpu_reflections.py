@@ -1,0 +1,51 @@
+"""RT reflections raygen (rt-reflections/raygen.rgen:54-166 with
+WITH_DDGI) through ark_ddgi_rt_reflections against the CPU oracle, bit for bit: the
+features scene (sun + 2 IES spots with shadow rays, masked and translucent geometry,
+mirrored instance, textures), atlases after two DDGI frames, a synthetic G-buffer
+with sky, untraced rough and traced pixels."""
+import numpy as np
+import pytest
+import torch
+
+from arkoserenderer_amd import ddgi as D
+import oracle_lib as O
+import reflection_inputs as RI
+import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("roughness", [None, 0])
+def test_reflections_features_scene(roughness):
+    sc = scenes.features_scene()
+    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=144, max_rays_per_probe=64, max_probe_updates=144)
+    ctx = D.DDGIContext(grid, 100.0, cfg)
+    ctx.set_scene(sc)
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(sc)
+    for f in range(2):
+        p = D.frame_params(cfg, grid, D.AppState(f), 0, light_pre_exposure=1.0, ambient_illuminance=0.05, environment_brightness=0.5)
+        ctx.update(p)
+        orc.update(p)
+    ctx.synchronize()
+    W, H = 96, 64
+    cam = RI.camera(W, H)
+    g, _ = RI.gbuffer(W, H, cam, seed=11, roughness=roughness)
+    kw = dict(environment_multiplier=0.5, ambient_amount=0.05)
+    want_rad, want_dir = orc.rt_reflections(W, H, cam, g, **kw)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in g.items()}
+    rad = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+    dirs = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+    node = D.RTReflectionsNode()
+    node.execute(ctx, cam, {k: dev[k] for k in ("depth", "material", "normal_velocity")}, dev["blue_noise"], rad, dirs, **kw)
+    got_rad, got_dir = rad.cpu().numpy().view(np.uint16), dirs.cpu().numpy().view(np.uint16)
+    for name, got, want in (("radiance", got_rad, want_rad), ("direction", got_dir, want_dir)):
+        bad = np.argwhere(np.any(got != want, axis=-1))
+        assert bad.size == 0, f"{name}: {len(bad)} pixels differ, first {bad[:4].tolist()}: got {got[tuple(bad[0])].view(np.float16)} want {want[tuple(bad[0])].view(np.float16)}"
+    traced = np.any(want_dir != 0, axis=-1)
+    assert traced.sum() > W * H // 2
+    rl = want_rad.view(np.float16)[..., 3].astype(np.float32)[traced]
+    assert (rl < 10000).any() and (rl == 10000).any()  # both hits and misses
+    ctx.close()
+    orc.close()

@@ -1,0 +1,41 @@
+"""RT reflections raygen (rt-reflections/raygen.rgen:54-166) in the CPU oracle:
+untraced pixels, unit reflection directions, and the mirror KAT (roughness 0: the
+GGX VNDF sample is the normal, so the ray is reflect(viewRay, N))."""
+import numpy as np
+
+from arkoserenderer_amd import ddgi as D
+import oracle_lib as O
+import reflection_inputs as RI
+import scenes
+
+
+def test_reflections_oracle_untraced_and_mirror():
+    sc = scenes.features_scene()
+    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
+    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=144, max_rays_per_probe=32, max_probe_updates=144)
+    orc = O.Oracle(D.desc_for(grid, 100.0, cfg))
+    orc.set_scene(sc)
+    W, H = 24, 16
+    cam = RI.camera(W, H)
+    g, n_view = RI.gbuffer(W, H, cam, roughness=0)
+    rad, dirs = orc.rt_reflections(W, H, cam, g, environment_multiplier=0.5)
+    rad, dirs = rad.view(np.float16).astype(np.float32), dirs.view(np.float16).astype(np.float32)
+    sky = g["depth"] >= 1.0 - 1e-6
+    rough = (g["material"][..., 0] / 255.0 >= 0.7) & ~sky
+    traced = ~sky & ~rough
+    assert (rad[sky] == 0).all() and (dirs[sky] == 0).all()  # direction untouched (zeros)
+    assert (rad[rough] == 0).all() and (dirs[rough] == 0).all()
+    d = dirs[traced][:, :3]
+    assert np.allclose(np.linalg.norm(d, axis=1), 1.0, atol=2e-3)
+    # mirror KAT: reflect(viewRay, N) with N = mat3(worldFromView) * viewSpaceNormal
+    Wv = cam["world_from_view"].reshape(4, 4).T
+    ys, xs = np.nonzero(traced)
+    ndc = np.stack([(xs + 0.5) / W * 2 - 1, (ys + 0.5) / H * 2 - 1, g["depth"][ys, xs], np.ones_like(xs, np.float64)], 1)
+    P = (Wv @ cam["view_from_projection"].reshape(4, 4).T @ ndc.T).T
+    P = P[:, :3] / P[:, 3:]
+    v = P - Wv[:3, 3]
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    N = (Wv[:3, :3] @ n_view[ys, xs].T).T
+    want = v - 2 * np.sum(N * v, axis=1, keepdims=True) * N
+    assert np.abs(d - want).max() < 5e-3
+    orc.close()
