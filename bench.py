@@ -248,6 +248,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_compose:
         result["lighting_compose"] = lighting_compose_line(args, torch, node.ctx)
+        result["rt_reflections"] = rt_reflections_line(args, torch, node.ctx)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -299,6 +300,50 @@ def cpu_baseline(scene, grid, R, args, exposure):
         "kind": "port",
         "sample": f"{done_probes} probes x {R} rays of the same C4 workload (probes 0..{done_probes - 1}), full update incl. shading/indirect/blend, {spent:.1f} s; oracle BVH build {build_s:.1f} s excluded",
         "probes_updated_per_s": round(done_probes / spent, 2),
+    }
+
+
+def rt_reflections_line(args, torch, ctx):
+    """The RT reflections consumer: ark_ddgi_rt_reflections at
+    compose_size on the C4 scene (10M triangles) and atlases after the timed steps, a
+    seeded synthetic G-buffer (10 % sky, 20 % too rough to trace) resident in HBM, one
+    reflection ray per traced pixel plus its shadow ray (sun). HIP events on the
+    stream the kernel runs on."""
+    import numpy as np
+
+    from arkoserenderer_amd import ddgi as D
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import reflection_inputs as RI
+
+    W, H = (int(v) for v in args.compose_size.split("x"))
+    cam = RI.camera(W, H, eye=(16.0, 16.0, -6.0), target=(16.0, 14.0, 16.0))
+    g, _ = RI.gbuffer(W, H, cam, seed=5)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in g.items()}
+    rad = torch.empty((H, W, 4), dtype=torch.int16, device="cuda")
+    dirs = torch.empty((H, W, 4), dtype=torch.int16, device="cuda")
+    planes = {k: dev[k].data_ptr() for k in ("depth", "material", "normal_velocity", "blue_noise")}
+    planes.update(out_radiance=rad.data_ptr(), out_direction=dirs.data_ptr(), noise_width=64, noise_height=64)
+    d = D.reflections_desc(W, H, cam, planes, environment_multiplier=1.0)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    for _ in range(2):
+        ctx.rt_reflections(d, side.cuda_stream)
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(side)
+    for _ in range(reps):
+        ctx.rt_reflections(d, side.cuda_stream)
+    e1.record(side)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    traced = int(((g["depth"] < 1.0 - 1e-6) & (g["material"][..., 0] / 255.0 < 0.7)).sum())
+    return {
+        "workload": f"{W}x{H} pixels ({traced} traced), synthetic G-buffer, C4 scene + atlases",
+        "gpu_ms": round(ms, 4),
+        "mrays_per_s": round(traced / ms / 1e3, 1),
+        "note": "one lane per pixel, no ray compaction: a first version, not tuned",
     }
 
 
