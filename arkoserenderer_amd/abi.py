@@ -400,8 +400,6 @@ EXPORTS = {
     "ark_ddgi_get_counters": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiCounters)]),
     "ark_ddgi_get_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int]),
     "ark_ddgi_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
-    "ark_ddgi_set_deferred_update": (C.c_int, [C.c_void_p, C.c_int]),
-    "ark_ddgi_join_update": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ark_ddgi_get_bvh_stats": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiBvhStats)]),
     "ark_ddgi_bake_ao": (C.c_int, [C.c_void_p, C.POINTER(ArkBakeAoDesc), C.c_void_p]),
     "ark_ddgi_bake_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),

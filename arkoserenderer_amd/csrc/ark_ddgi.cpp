@@ -99,18 +99,14 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 struct ArkDdgiCtx {
     ArkDdgiDesc desc {};
     std::string lastError;
-    hipStream_t stream = nullptr;
-    hipStream_t auxStream = nullptr; // second stream of the sub-window pipeline
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
-    // Deferred probe update (ark_ddgi_set_deferred_update): a frame's probe update runs
-    // on updStream after its shading (evShaded) and signals evUpd; the next frame's
-    // traversal does not wait for it (it reads neither atlas), its shading does.
-    hipStream_t updStream = nullptr;
-    hipEvent_t evShaded = nullptr, evUpd = nullptr;
-    bool deferred = false;
-    bool updPending = false;       // evUpd guards a probe update not yet joined
-    bool updPendingOffsets = false; // ... which also writes the probe offsets
-    uint32_t slotFlip = 0;          // slot table half of the next deferred frame
+    hipStream_t stream = nullptr; // internal (clears); synchronous use only
+    // Call order across streams: every operation records evOrder on its stream when
+    // enqueued, and the next one waits for it when given another stream (orderBegin).
+    hipEvent_t evOrder = nullptr;
+    hipStream_t orderStream = nullptr;
+    bool orderValid = false;
+    // traversal knobs, fixed at create: refill batch, grab chunk
+    uint32_t refillMin = 8, grabChunk = 64;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -195,12 +191,45 @@ int ensureSpill(ArkDdgiCtx* ctx)
 {
     // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
     uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
-    uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the two traversal kernels
-    // two halves: one per stream of the sub-window pipeline
-    size_t bytes = 2 * static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
+    uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the traversal kernels
+    size_t bytes = static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
     if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
     ctx->spillEntries = need;
+    return ARK_DDGI_OK;
+}
+
+// The stream of an asynchronous entry point: NULL is the legacy default (null)
+// stream, which orders against every blocking stream of the process (torch's
+// default stream among them), like any other HIP API taking a stream.
+hipStream_t streamOf(void* h) { return static_cast<hipStream_t>(h); }
+
+// Operations of one context execute in call order, whatever streams they are given
+// (they share the traversal spill area, the hit records and the atlases): an
+// operation on another stream than the previous one first waits for it.
+hipError_t orderBegin(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (ctx->orderValid && ctx->orderStream != s) return hipStreamWaitEvent(s, ctx->evOrder, 0);
+    return hipSuccess;
+}
+
+hipError_t orderEnd(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    const hipError_t e = hipEventRecord(ctx->evOrder, s);
+    ctx->orderStream = s;
+    ctx->orderValid = e == hipSuccess;
+    return e;
+}
+
+// Shading work set for the largest window: per-ray light bits, then k_shadow_gen's
+// shadow-ray list (at most one ray per probe ray and light).
+int ensureShadeWork(ArkDdgiCtx* ctx)
+{
+    const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
+    if (rays >= (1ull << 28) && ctx->lightCount > 0)
+        return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "%llu rays per update: shadow-ray owners pack (ray << 4) | light in 32 bits", static_cast<unsigned long long>(rays));
+    const uint64_t bytes = ((rays * 4 + 255) & ~static_cast<uint64_t>(255)) + rays * ctx->lightCount * sizeof(ShadowRay);
+    if (ctx->shadeWork.bytes < bytes) ARK_HIP(ctx->shadeWork.alloc(bytes));
     return ARK_DDGI_OK;
 }
 
@@ -265,24 +294,16 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if (e != hipSuccess) return bad(e, "hipGetDeviceProperties");
     ctx->cuCount = prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-    if ((e = hipStreamCreateWithFlags(&ctx->auxStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate aux");
-    if ((e = hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-    if ((e = hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evOrder, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     {
-        // the deferred probe update should take the CUs the next frame's traversal
-        // leaves (its tail), not compete with its start: lowest stream priority
-        // (ARK_UPD_PRIORITY=normal for the default priority)
-        int least = 0, greatest = 0;
-        const char* pe = std::getenv("ARK_UPD_PRIORITY");
-        const bool low = !(pe && std::strcmp(pe, "normal") == 0);
-        if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-        if ((e = hipStreamCreateWithPriority(&ctx->updStream, hipStreamNonBlocking, low ? least : 0)) != hipSuccess) return bad(e, "hipStreamCreate update");
-        if (const char* pd = std::getenv("ARK_DEBUG_PRIORITY")) {
-            if (pd[0] == '1') std::fprintf(stderr, "ark_ddgi: stream priority range least %d greatest %d, update stream %d\n", least, greatest, low ? least : 0);
-        }
+        // tuning knobs, read once: ARK_REFILL_MIN: refill idle trace lanes in batches
+        // of >= 8 (the refill then stalls a wave once per 8 finished rays, and the rays it
+        // starts descend from the root together: 2.98 vs 3.30 ms at 1 on C4; 16: 3.03);
+        // ARK_GRAB_CHUNK: rays per partition-head grab, 64 = a probe quarter of
+        // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
+        if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
+        if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
     }
-    if ((e = hipEventCreateWithFlags(&ctx->evShaded, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-    if ((e = hipEventCreateWithFlags(&ctx->evUpd, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
@@ -296,11 +317,11 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->fibOrder.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib order");
     if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
-    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4 * kMaxSubWindows)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0, occW = 0;
-    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_primary_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occS, kernel_shade_ptr(false), kShadeBlock, 0)) != hipSuccess) return bad(e, "occupancy shade");
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occW, kernel_trace_shadow_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy shadow");
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
@@ -319,21 +340,14 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->updStream) (void)hipStreamSynchronize(ctx->updStream);
+    (void)hipDeviceSynchronize();
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->triNormals, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
-    if (ctx->auxStream) (void)hipStreamSynchronize(ctx->auxStream);
-    if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
-    if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
-    if (ctx->auxStream) (void)hipStreamDestroy(ctx->auxStream);
-    if (ctx->evShaded) (void)hipEventDestroy(ctx->evShaded);
-    if (ctx->evUpd) (void)hipEventDestroy(ctx->evUpd);
-    if (ctx->updStream) (void)hipStreamDestroy(ctx->updStream);
+    if (ctx->evOrder) (void)hipEventDestroy(ctx->evOrder);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -345,8 +359,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!s || s->struct_size != sizeof(ArkDdgiScene)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiScene");
     ARK_HIP(hipSetDevice(ctx->device));
-    ARK_HIP(hipStreamSynchronize(ctx->stream));
-    ARK_HIP(hipStreamSynchronize(ctx->updStream));
+    ARK_HIP(hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
     // validate
     for (uint32_t i = 0; i < s->instance_count; ++i) {
@@ -598,8 +611,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     ctx->bvhMaxDepth = maxDepth;
     if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
     ctx->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
-    // shading work lists for the largest window (front records, light terms, shadow rays)
-    ARK_HIP(ctx->shadeWork.alloc(std::max<size_t>(16, shade_work_bytes(static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax, ctx->lightCount))));
+    if ((rc = ensureShadeWork(ctx)) != 0) return rc;
     if ((rc = ensureSpill(ctx)) != 0) return rc;
     ctx->hasScene = true;
     const auto t1 = std::chrono::steady_clock::now();
@@ -629,13 +641,6 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
 
-// Orders `s` after a deferred probe update still in flight (atlases and offsets).
-static hipError_t joinPendingUpdate(ArkDdgiCtx* ctx, hipStream_t s)
-{
-    if (!ctx->updPending) return hipSuccess;
-    return hipStreamWaitEvent(s, ctx->evUpd, 0);
-}
-
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
 {
     return updateImpl(ctx, p, hipStream, nullptr, nullptr);
@@ -656,7 +661,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     const uint32_t R = p->rays_per_probe;
     if (K == 0 || R == 0 || K > static_cast<uint32_t>(ctx->Kmax) || R > static_cast<uint32_t>(ctx->Rmax))
         return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "probe_updates %u / rays_per_probe %u outside [1,%d] / [1,%d]", K, R, ctx->Kmax, ctx->Rmax);
-    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     FrameArgs f {};
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
@@ -686,15 +691,9 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
     f.offsets = ctx->offsets.as<float4>();
-    // Deferred probe update: this frame's update goes to updStream, and the next
-    // frame's traversal may run beside it. Off while timing stages or on the
-    // overlapped (multi-GPU) path, whose events already order the frames.
-    const bool deferNow = ctx->deferred && !ctx->timing && !shadeWaitEvent && !doneEvent;
-    // the traversal reads the probe offsets: it waits if the pending update writes them
-    const bool waitBeforeTrace = ctx->updPending && (!deferNow || ctx->updPendingOffsets);
-    const bool waitBeforeShade = ctx->updPending;
-    f.slots = ctx->slots.as<GpuProbeSlot>() + (deferNow ? static_cast<size_t>(ctx->slotFlip) * ctx->Kmax : 0);
+    f.slots = ctx->slots.as<GpuProbeSlot>();
     f.fib = ctx->fib.as<float4>();
+    ARK_HIP(orderBegin(ctx, s));
     if (ctx->orderR != R) {
         sampleTraversalOrder(R, ctx->orderHost);
         ARK_HIP(hipMemcpyAsync(ctx->order.ptr, ctx->orderHost.data(), R * 4, hipMemcpyHostToDevice, s));
@@ -705,171 +704,51 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.hits = ctx->hits.as<GpuHit>();
     f.surfels = ctx->surfels.as<uint16_t>();
     f.spill = ctx->spill.as<uint32_t>();
+    f.light_count = ctx->lightCount;
+    f.refill_min = ctx->refillMin;
+    f.grab_chunk = ctx->grabChunk;
+    f.ray_counter = ctx->rayCounter.as<uint32_t>();
+    f.counters = ctx->counters.as<unsigned long long>();
+    // shading work set (ensureShadeWork): per-ray light bits | shadow-ray list
     {
-        // work lists carved from one buffer sized for the largest window at set_scene
         const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
         char* w = static_cast<char*>(ctx->shadeWork.ptr);
-        f.front_recs = reinterpret_cast<FrontRec*>(w);
-        f.front_lights = reinterpret_cast<FrontLight*>(w + rays * sizeof(FrontRec));
-        f.shadow_rays = reinterpret_cast<ShadowRay*>(w + rays * (sizeof(FrontRec) + ctx->lightCount * sizeof(FrontLight)));
-        // fused path: per-ray light bits alias the (then unused) front records
         f.shadow_bits = reinterpret_cast<uint32_t*>(w);
+        f.shadow_rays = reinterpret_cast<ShadowRay*>(w + ((rays * 4 + 255) & ~static_cast<uint64_t>(255)));
     }
-    f.light_count = ctx->lightCount;
-    {
-        // shadow rays traced inside the primary traversal (default) or by their own
-        // persistent launch after shading (ARK_SHADOWS=split): same bits either way
-        // three equivalent schedules (identical bits): "pre" (default) generates and
-        // traces the shadow rays between traversal and shading, so shading finishes
-        // every surfel in one pass; "split" records per-light terms in shading and
-        // finishes them after the shadow launch; "fused" traces the shadow rays in
-        // the primary traversal's lanes (measured slower: DESIGN.md §3)
-        const char* se = std::getenv("ARK_SHADOWS"); // read per frame: tests flip it in-process
-        int mode = 2;
-        if (se && std::strcmp(se, "split") == 0) mode = 0;
-        else if (se && std::strcmp(se, "fused") == 0) mode = 1;
-        // the pre schedule packs (ray << 4 | light) into 32 bits
-        if (static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax >= (1ull << 28)) mode = 0;
-        f.fused_shadows = f.light_count > 0 ? mode : 0;
-    }
-    {
-        // refill idle trace lanes in batches of >= 8: the refill (pool atomic, slot and
-        // direction loads) then stalls a wave once per 8 finished rays, and the rays it
-        // starts descend from the root together (2.98 vs 3.30 ms at 1 on C4; 16: 3.03)
-        const char* e = std::getenv("ARK_REFILL_MIN");
-        f.refill_min = e ? static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(e)))) : 8u;
-    }
-    {
-        // rays per partition-head grab (tuning knob): 64 = one probe quarter of
-        // direction-clustered rays per wave pool; 16 and 8 measured slower on 1/8-size
-        // slabs (1.31 / 1.41 vs 1.18 ms per step): the rays of a wave lose coherence
-        const char* e = std::getenv("ARK_GRAB_CHUNK");
-        const uint32_t g = 64;
-        f.grab_chunk = e ? static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(e)))) : g;
-    }
-    f.ray_counter = ctx->rayCounter.as<uint32_t>();
-    f.front_count = f.ray_counter + kFrontCountWord;
     f.shadow_count = f.ray_counter + kShadowCountWord;
     f.shadow_heads = f.ray_counter + kShadowHeadWord;
-    f.counters = ctx->counters.as<unsigned long long>();
     const bool timing = ctx->timing;
     const bool count = ctx->counting;
-    if (waitBeforeTrace) ARK_HIP(joinPendingUpdate(ctx, s));
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
     ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, ctx->rayCounter.bytes, s));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
     ARK_HIP(launch_probe_slots(f, s));
     {
         // slot traversal order (k_slot_order): rebuilt when the window moves
-        static const bool useOrder = [] { const char* e = std::getenv("ARK_SLOT_ORDER"); return !(e && e[0] == '0'); }();
-        f.slot_order = nullptr;
-        if (useOrder) {
-            const int64_t key = (static_cast<int64_t>(f.first) << 32) | K;
-            if (key != ctx->slotOrderKey) {
-                ARK_HIP(launch_slot_order(f, ctx->slotOrder.as<uint32_t>(), s));
-                ctx->slotOrderKey = key;
-            }
-            f.slot_order = ctx->slotOrder.as<uint32_t>();
+        f.slot_order = ctx->slotOrder.as<uint32_t>();
+        const int64_t key = (static_cast<int64_t>(f.first) << 32) | K;
+        if (key != ctx->slotOrderKey) {
+            ARK_HIP(launch_slot_order(f, ctx->slotOrder.as<uint32_t>(), s));
+            ctx->slotOrderKey = key;
         }
     }
     if (f.window_probes > 0) {
-        // Sub-window pipeline: the window's queue positions are cut into S pieces run
-        // alternately on the context stream and an auxiliary one, each piece through
-        // trace -> shadow rays -> shading with its own counters, spill stack and
-        // shadow list. A persistent launch holds every CU until its last long ray
-        // finishes (~0.3 ms for traversal, ~0.2 ms for shadow rays); the other
-        // stream's launches were meant to take the CUs its retiring workgroups free.
-        // Measured, they do not fill those tails (each piece adds its own), so S = 1
-        // is the default and S > 1 a tested option. Results do not depend on S (every
-        // ray is computed the same way wherever it runs). Serial (S = 1) when timing,
-        // so that per-stage times stay separable.
-        const char* se = std::getenv("ARK_SUBWINDOWS"); // read per frame: tests flip it in-process
-        const int envS = se ? std::atoi(se) : 1; // measured: S = 2 +0.5 %, 3-4 slower; 1/8 slab slower
-        int S = timing || !f.slot_order ? 1 : std::max(1, std::min(kMaxSubWindows, envS));
-        S = static_cast<int>(std::min<uint32_t>(static_cast<uint32_t>(S), f.window_probes));
-        hipStream_t st[2] = { s, ctx->auxStream };
-        if (S > 1) {
-            ARK_HIP(hipEventRecord(ctx->evFork, s));
-            ARK_HIP(hipStreamWaitEvent(ctx->auxStream, ctx->evFork, 0));
+        ARK_HIP(launch_trace(ctx->scene, f, ctx->traceBlocks, count, s));
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
+        if (f.light_count > 0) {
+            ARK_HIP(launch_shadow_gen(ctx->scene, f, s));
+            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
         }
-        const size_t spillHalf = ctx->spill.bytes / 2 / sizeof(uint32_t);
-        for (int w = 0; w < S; ++w) {
-            const uint32_t qb = static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * w / S);
-            const uint32_t qe = static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * (w + 1) / S);
-            if (qb == qe) continue;
-            hipStream_t ss = st[w & 1];
-            FrameArgs g = f;
-            g.window_probes = qe - qb;
-            g.window_rays = g.window_probes * R;
-            if (S > 1) {
-                g.slot_order = f.slot_order + qb;
-                g.ray_counter = f.ray_counter + static_cast<size_t>(w) * kRayCounterWords;
-                g.front_count = g.ray_counter + kFrontCountWord;
-                g.shadow_count = g.ray_counter + kShadowCountWord;
-                g.shadow_heads = g.ray_counter + kShadowHeadWord;
-                g.shadow_rays = f.shadow_rays + static_cast<size_t>(qb) * R * f.light_count;
-                g.front_recs = f.front_recs + static_cast<size_t>(qb) * R; // split schedule
-                g.front_lights = f.front_lights + static_cast<size_t>(qb) * R * f.light_count;
-                g.spill = f.spill + (w & 1) * spillHalf;
-            }
-            ARK_HIP(launch_trace_primary(ctx->scene, g, ctx->traceBlocks, count, ss));
-            if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], ss));
-            // Split shading (S = 1, not timing): the rays that need no shadow bit (misses,
-            // backfaces, front hits with no lit light) are shaded on the auxiliary stream
-            // beside the shadow traversal, whose workgroups leave the CUs to them as they
-            // retire (its tail); the lit front hits are shaded after it. Off by default
-            // (ARK_SHADE_SPLIT=1): measured 1 % slower on C4, neutral on 1/8 slabs.
-            const char* sp = std::getenv("ARK_SHADE_SPLIT");
-            const bool splitShade = g.fused_shadows == 2 && S == 1 && !timing && sp && sp[0] == '1';
-            if (g.fused_shadows == 2) {
-                ARK_HIP(launch_shadow_gen(ctx->scene, g, ss));
-                if (splitShade) ARK_HIP(hipEventRecord(ctx->evFork, ss));
-                ARK_HIP(launch_trace_shadow(ctx->scene, g, ctx->shadowBlocks, count, ss));
-            }
-            if (splitShade) {
-                FrameArgs p1 = g;
-                p1.shade_pass = 1;
-                ARK_HIP(hipStreamWaitEvent(ctx->auxStream, ctx->evFork, 0));
-                if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, ctx->auxStream));
-                if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(ctx->auxStream, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-                ARK_HIP(launch_shade(ctx->scene, p1, ctx->shadeBlocks, count, ctx->auxStream));
-                ARK_HIP(hipEventRecord(ctx->evJoin, ctx->auxStream));
-                g.shade_pass = 2;
-            }
-            if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], ss));
-            // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
-            // rank it waits here for the previous exchange (the traversal above did not)
-            if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(ss, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-            if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, ss)); // the previous frame's atlases
-            ARK_HIP(launch_shade(ctx->scene, g, ctx->shadeBlocks, count, ss));
-            if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], ss));
-            if (g.fused_shadows == 0 && g.light_count > 0) {
-                ARK_HIP(launch_trace_shadow(ctx->scene, g, ctx->shadowBlocks, count, ss));
-                ARK_HIP(launch_shade_finish(g, ss));
-            }
-            if (splitShade) ARK_HIP(hipStreamWaitEvent(ss, ctx->evJoin, 0)); // pass 1 done before the update
-        }
-        if (S > 1) {
-            ARK_HIP(hipEventRecord(ctx->evJoin, ctx->auxStream));
-            ARK_HIP(hipStreamWaitEvent(s, ctx->evJoin, 0));
-        }
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], s));
+        // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
+        // rank it waits here for the previous exchange (the traversal above did not)
+        if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+        ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
+        if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
-        if (deferNow) {
-            hipStream_t us = ctx->updStream;
-            ARK_HIP(hipEventRecord(ctx->evShaded, s));
-            ARK_HIP(hipStreamWaitEvent(us, ctx->evShaded, 0));
-            ARK_HIP(launch_probe_update(f, us));
-            ARK_HIP(hipEventRecord(ctx->evUpd, us));
-            ctx->updPending = true;
-            ctx->updPendingOffsets = f.update_offsets != 0;
-            ctx->slotFlip ^= 1u;
-        } else {
-            ARK_HIP(launch_probe_update(f, s));
-            ctx->updPending = false;
-        }
+        ARK_HIP(launch_probe_update(f, s));
     } else {
-        if (waitBeforeShade) ARK_HIP(joinPendingUpdate(ctx, s));
-        ctx->updPending = false;
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
@@ -880,6 +759,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     }
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
     if (doneEvent) ARK_HIP(hipEventRecord(static_cast<hipEvent_t>(doneEvent), s));
+    ARK_HIP(orderEnd(ctx, s));
     ctx->timingValid = timing;
     ctx->countersPending = count;
     ctx->lastRays = f.window_rays;
@@ -891,10 +771,7 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ARK_HIP(hipSetDevice(ctx->device));
-    ARK_HIP(hipStreamSynchronize(ctx->stream));
-    ARK_HIP(hipStreamSynchronize(ctx->updStream));
     ARK_HIP(hipDeviceSynchronize());
-    ctx->updPending = false;
     return ARK_DDGI_OK;
 }
 
@@ -1005,21 +882,6 @@ int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out)
     return ARK_DDGI_OK;
 }
 
-int ark_ddgi_set_deferred_update(ArkDdgiCtx* ctx, int enabled)
-{
-    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
-    ctx->deferred = enabled != 0;
-    return ARK_DDGI_OK;
-}
-
-int ark_ddgi_join_update(ArkDdgiCtx* ctx, void* hipStream)
-{
-    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
-    ARK_HIP(hipSetDevice(ctx->device));
-    ARK_HIP(joinPendingUpdate(ctx, hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream));
-    return ARK_DDGI_OK;
-}
-
 int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
@@ -1067,8 +929,9 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
         return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: extent %ux%u / %u samples", d->width, d->height, d->sample_count);
     const ArkRTInstance& inst = ctx->instHost[d->instance_index];
     const ArkRTTriangleMesh& mesh = ctx->meshHost[inst.rt_mesh_index];
-    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(orderBegin(ctx, s));
     const size_t texels = static_cast<size_t>(d->width) * d->height;
     const size_t outBytes = texels * (d->bent_normals ? 4 : 1);
     if (ctx->bakeTri.bytes < texels * 4) ARK_HIP(ctx->bakeTri.alloc(texels * 4));
@@ -1099,6 +962,7 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
     ARK_HIP(launch_bake(ctx->scene, b, 0, 1, s));
     // the persistent AO kernel uses the traversal spill area sized for shadowBlocks workgroups
     ARK_HIP(launch_bake(ctx->scene, b, ctx->shadowBlocks, 2, s));
+    ARK_HIP(orderEnd(ctx, s));
     ctx->bakeW = d->width;
     ctx->bakeH = d->height;
     ctx->bakeBent = b.bent;
@@ -1131,7 +995,7 @@ int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void*
     if (!desc || desc->struct_size != sizeof(ArkComposeDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkComposeDesc");
     if (!desc->out) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "lighting_compose: no output plane");
     if (static_cast<uint64_t>(desc->width) * desc->height >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "lighting_compose: target too large");
-    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     // the DDGISamplingSet (DDGINode.cpp:45-66): grid constants + both atlases
     FrameArgs f {};
@@ -1144,8 +1008,9 @@ int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void*
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
     ArkComposeDesc c = *desc;
-    ARK_HIP(joinPendingUpdate(ctx, s));
+    ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(launch_lighting_compose(f, c, s));
+    ARK_HIP(orderEnd(ctx, s));
     return ARK_DDGI_OK;
 }
 
@@ -1157,7 +1022,7 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     if (!desc->out_radiance || !desc->out_direction) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: no output image");
     if (desc->blue_noise && (desc->noise_width == 0 || desc->noise_height == 0)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: empty blue noise");
     if (static_cast<uint64_t>(desc->width) * desc->height >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "rt_reflections: target too large");
-    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     int rc;
     if ((rc = ensureSpill(ctx)) != 0) return rc;
@@ -1174,8 +1039,9 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.ambient_amount = desc->ambient_amount;
     f.environment_multiplier = desc->environment_multiplier;
     f.spill = ctx->spill.as<uint32_t>();
-    ARK_HIP(joinPendingUpdate(ctx, s));
+    ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, s));
+    ARK_HIP(orderEnd(ctx, s));
     return ARK_DDGI_OK;
 }
 
@@ -1184,7 +1050,7 @@ int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* h
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!desc || desc->struct_size != sizeof(ArkProbeDebugDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkProbeDebugDesc");
     if (desc->count && (!desc->probe_indices || !desc->directions || !desc->out)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "probe_debug: null plane");
-    hipStream_t s = hipStream ? static_cast<hipStream_t>(hipStream) : ctx->stream;
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     FrameArgs f {};
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
@@ -1195,8 +1061,9 @@ int ark_ddgi_probe_debug(ArkDdgiCtx* ctx, const ArkProbeDebugDesc* desc, void* h
     }
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
-    ARK_HIP(joinPendingUpdate(ctx, s));
+    ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(launch_probe_debug(f, *desc, s));
+    ARK_HIP(orderEnd(ctx, s));
     return ARK_DDGI_OK;
 }
 

@@ -28,35 +28,18 @@ constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in
 constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
 
-// Lit front hit awaiting its shadow rays (k_shade -> k_shade_finish), 48 B.
-struct alignas(16) FrontRec {
-    float4 base_T; // emissive + ambient, w = hit distance T
-    float4 bi_ray; // baseColor * indirect, w = probe ray index (bits)
-    uint32_t need; // lit lights (one shadow ray each)
-    uint32_t occ;  // occluded lights (k_trace_shadow atomicOr)
-    uint32_t _pad[2];
-};
-
-// Per lit light of a front record: the light term with shadowFactor 1 and 0.
-struct alignas(16) FrontLight {
-    float4 T;
-    float4 Z;
-};
-
-// One shadow ray: origin + tmax, direction + owner ((front record << 4) | light).
+// One shadow ray: origin + tmax, direction + owner ((probe ray << 4) | light).
 struct alignas(16) ShadowRay {
     float4 origin_tmax;
     float4 dir_owner;
 };
 
-// Word offsets in the ray-counter buffer: 2 x kRayParts partition heads, then the
-// shading work-list counters (each on its own 128-B line).
-constexpr int kFrontCountWord = 2 * kRayParts * kRayCounterStride;
-constexpr int kShadowCountWord = kFrontCountWord + kRayCounterStride;
+// Word offsets in the ray-counter buffer (each counter on its own 128-B line): the
+// probe-ray partition heads, the shading heads, the shadow list (count + partition heads).
+constexpr int kShadeHeadWord = kRayParts * kRayCounterStride;
+constexpr int kShadowCountWord = 2 * kRayParts * kRayCounterStride;
 constexpr int kShadowHeadWord = kShadowCountWord + kRayCounterStride; // kRayParts partition heads
-constexpr int kShade2HeadWord = kShadowHeadWord + kRayParts * kRayCounterStride; // second shading pass's heads
-constexpr int kRayCounterWords = kShade2HeadWord + kRayParts * kRayCounterStride;
-constexpr int kMaxSubWindows = 4; // sub-window pipeline: one counter block each
+constexpr int kRayCounterWords = kShadowHeadWord + kRayParts * kRayCounterStride;
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {
@@ -83,8 +66,8 @@ struct SceneArgs {
     float sun_dir[3];
     const GpuSpotLight* spots;
     // [triangle] 3 x float4: object-space vertex normals n0, n1, n2 (9 floats) and the
-    // instance index; BVH triangle order. Lets k_trace_primary<SHADOWS> find the
-    // shading normal with two dependent loads instead of five (set when lights exist).
+    // instance index; BVH triangle order. Lets k_trace find the shading normal of a
+    // front hit with two dependent loads instead of five (set when lights exist).
     const float4* tri_normals;
 
     __device__ __forceinline__ int resolveTexture(int idx) const
@@ -130,18 +113,13 @@ struct FrameArgs {
     GpuHit* hits;
     uint16_t* surfels;
     uint32_t* spill;
-    FrontRec* front_recs;    // [window_rays] worst case
-    FrontLight* front_lights; // [front record][light_count]
-    ShadowRay* shadow_rays;  // [window_rays * light_count] worst case
-    uint32_t* front_count;   // = ray_counter + kFrontCountWord
-    uint32_t* shadow_count;  // = ray_counter + kShadowCountWord
-    uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
     uint32_t light_count;    // has_sun + spot lights
     uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
     uint32_t grab_chunk;     // trace / shadow: rays a wave takes from its partition head at once (<= 64)
-    int32_t fused_shadows;   // 0 split (records + k_shade_finish); 1 traced inside k_trace_primary; 2 k_shadow_gen + k_trace_shadow before shading
-    uint32_t* shadow_bits;   // [window_rays] lit light bits 0-15, occluded bits 16-31 (fused path)
-    int32_t shade_pass;      // one-pass shading: 0 every ray; 1 rays needing no shadow bit; 2 lit front hits
+    uint32_t* shadow_bits;   // [window_rays] lit light bits 0-15, occluded bits 16-31 (front hits)
+    ShadowRay* shadow_rays;  // k_shadow_gen's list: [window_rays * light_count] worst case
+    uint32_t* shadow_count;  // = ray_counter + kShadowCountWord
+    uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
 };
@@ -169,15 +147,13 @@ hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, 
 hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t blocks, hipStream_t s);
 hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hipStream_t s);
 hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
-hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
+hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s);
-hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s);
-size_t shade_work_bytes(uint64_t rays, uint32_t lights);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
-const void* kernel_trace_primary_ptr(bool count);
+const void* kernel_trace_ptr(bool count);
 const void* kernel_shade_ptr(bool count);
 const void* kernel_trace_shadow_ptr(bool count);
 

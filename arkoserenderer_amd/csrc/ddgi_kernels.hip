@@ -1,21 +1,24 @@
 // ddgi_kernels.hip — the DDGI probe-update hot path as HIP kernels for gfx950.
 //
-// One update (DDGINode.cpp:171-298) is four launches on one stream:
+// One update (DDGINode.cpp:132-259) is these launches on one stream:
 //   1. k_probe_slots    window -> slot table (probe position + offset, per-probe
-//                       ray rotation) and the spherical-Fibonacci table.
-//   2. k_trace_primary  persistent traversal of all K*R probe rays: opaque pass
+//                       ray rotation) and the spherical-Fibonacci table
+//                       (+ k_slot_order when the window moves).
+//   2. k_trace          persistent traversal of all K*R probe rays: opaque pass
 //                       (closest hit) then masked pass (alpha-tested any-hit),
 //                       software 8-wide quantized BVH (80 B nodes) with a per-lane
 //                       LDS ring stack of node groups (spilling to HBM only beyond
-//                       kStackLds entries) and wave64 ballot
-//                       refill of finished lanes (raygen.rgen:114-171).
-//   3. k_shade          closest-hit shading (opaque.rchit:105-176) with shadow
-//                       rays (any-hit traversal), environment on miss
-//                       (raygen.rgen:149-158), indirect from the previous frame's
-//                       atlases (probeSampling.glsl:64-163) -> fp16 surfels.
-//   4. k_probe_update   (ddgi_update.hip) irradiance + visibility blend,
+//                       kStackLds entries) and wave64 ballot refill of finished
+//                       lanes (raygen.rgen:35-92).
+//   3. k_shadow_gen     lit lights of every front hit -> shadow-ray list
+//      k_trace_shadow   persistent any-hit traversal of that list (opaque.rchit:35-54).
+//   4. k_shade          closest-hit shading (opaque.rchit:105-176) with the shadow
+//                       bits, environment on miss (raygen.rgen:71-80), indirect from
+//                       the previous frame's atlases (probeSampling.glsl:64-163)
+//                       -> fp16 surfels.
+//   5. k_probe_update   (ddgi_update.hip) irradiance + visibility blend,
 //                       tile border copy, probe offsets.
-// No MFMA: the path is traversal/gather, HBM/latency bound.
+// No MFMA: the path is traversal/gather, latency/issue bound.
 
 #include <hip/hip_runtime.h>
 
@@ -42,27 +45,6 @@ __device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) c
 }
 
 namespace dev {
-
-typedef float f2 __attribute__((ext_vector_type(2))); // packed fp32 pair (v_pk_*_f32)
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-#ifndef ARK_BRANCHLESS_STEP
-#define ARK_BRANCHLESS_STEP 0 // 1: both tests every step, no divergent branch (bit-identical; neutral for traversal, slower for shadow rays)
-#endif
-#ifndef ARK_BUFFER_FETCH
-#define ARK_BUFFER_FETCH 0 // 1: ds_read + buffer_load paths (measured 1.5 % slower than the merged flat loads)
-#endif
-#ifndef ARK_FLAT_FETCH
-#define ARK_FLAT_FETCH 0
-#endif
-#ifndef ARK_FETCH5
-#define ARK_FETCH5 1 // 0: node-only last two loads (measured 2 % slower)
-#endif
-#ifndef ARK_NODE_MIX
-#define ARK_NODE_MIX 0 // 1: plane bytes as f16 subnormals into v_fma_mix_f32 (visitNode8; bit-identical, measured 1 % slower)
-#endif
-#ifndef ARK_NODE_PACKED
-#define ARK_NODE_PACKED 0 // 1: BVH8 slab tests as packed fp32 pairs (measured slower: 3.02 vs 2.72 ms, see visitNode8)
-#endif
 
 // ---------------------------------------------------------------------------
 // 1. window -> slots
@@ -383,7 +365,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // scene diagonal on top of its own relative margin (bvh_builder.cpp), which
 // covers that error, and the comparison keeps a relative margin for far boxes,
 // so a box holding an exact triangle hit is never culled. The near/far plane of
-// each axis is chosen by the ray octant. Scalar fp32 by default (ARK_NODE_PACKED=1: packed pairs).
+// each axis is chosen by the ray octant. Scalar fp32, one slot at a time: a packed
+// v_pk_fma_f32 pair issues in two slots on gfx950 and needs moves to pair its
+// operands (measured 3.02 vs 2.72 ms traversal at C4 in round 1).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
@@ -395,47 +379,12 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const float bx = (__uint_as_float(w0.x) - o.x) * idir.x;
     const float by = (__uint_as_float(w0.y) - o.y) * idir.y;
     const float bz = (__uint_as_float(w0.z) - o.z) * idir.z;
-    const f2 Ax = { ax, ax }, Ay = { ay, ay }, Az = { az, az }, Bx = { bx, bx }, By = { by, by }, Bz = { bz, bz };
-    const f2 Tmin = { tmin, tmin }, Tmax = { tmax, tmax };
     const uint32_t imask = w0.w >> 24;
     const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
     const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
     uint32_t hitSlots = 0, insideSlots = 0;
-#if ARK_NODE_MIX
-    // Plane bytes become f16 subnormals (bits 0x00qq = q * 2^-24, exact) two at a time
-    // with one v_perm_b32, and feed v_fma_mix_f32 as its f16 operand: fma(q * 2^-24,
-    // a * 2^24, b) rounds the exact q*a + b once, bit-identical to fma(q, a, b) (a is
-    // never subnormal: |idir| >= 1 and the plane exponent is >= -100), without the
-    // byte-to-float conversion per plane.
-    (void)Ax; (void)Ay; (void)Az; (void)Bx; (void)By; (void)Bz; (void)Tmin; (void)Tmax;
-    const float ax24 = __uint_as_float(((w0.w & 0xffu) + 24u) << 23) * idir.x;
-    const float ay24 = __uint_as_float((((w0.w >> 8) & 0xffu) + 24u) << 23) * idir.y;
-    const float az24 = __uint_as_float((((w0.w >> 16) & 0xffu) + 24u) << 23) * idir.z;
-    (void)ax; (void)ay; (void)az;
-    auto pairOf = [](uint32_t w, bool upper) { return __builtin_bit_cast(h2, __builtin_amdgcn_perm(0u, w, upper ? 0x0c030c02u : 0x0c010c00u)); };
-#pragma unroll
-    for (int s = 0; s < 8; s += 2) {
-        const bool hiWord = s >= 4, upper = (s & 2) != 0;
-        const h2 pnx = pairOf(hiWord ? nX1 : nX0, upper), pny = pairOf(hiWord ? nY1 : nY0, upper), pnz = pairOf(hiWord ? nZ1 : nZ0, upper);
-        const h2 pfx = pairOf(hiWord ? fX1 : fX0, upper), pfy = pairOf(hiWord ? fY1 : fY0, upper), pfz = pairOf(hiWord ? fZ1 : fZ0, upper);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            auto hv = [&](h2 p) { return static_cast<float>(j ? p.y : p.x); };
-            const float tnx = fmaf(hv(pnx), ax24, bx), tny = fmaf(hv(pny), ay24, by), tnz = fmaf(hv(pnz), az24, bz);
-            const float tfx = fmaf(hv(pfx), ax24, bx), tfy = fmaf(hv(pfy), ay24, by), tfz = fmaf(hv(pfz), az24, bz);
-            const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-            const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-            const float lim = fmaf(tf, 1.00001f, 1e-7f);
-            hitSlots |= (tn <= lim ? 1u : 0u) << (s + j);
-            insideSlots |= (tn <= tmin ? 1u : 0u) << (s + j + 16);
-        }
-    }
-#elif !ARK_NODE_PACKED
-    // one slot at a time in scalar fp32 (the packed form costs two issue slots per
-    // v_pk op on gfx950 plus the moves that pair its operands)
-    (void)Ax; (void)Ay; (void)Az; (void)Bx; (void)By; (void)Bz; (void)Tmin; (void)Tmax;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
@@ -447,33 +396,9 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
         const float lim = fmaf(tf, 1.00001f, 1e-7f);
         hitSlots |= (tn <= lim ? 1u : 0u) << s;
+        // origin inside the box: every near-plane distance <= tmin
         insideSlots |= (tn <= tmin ? 1u : 0u) << (s + 16);
     }
-#else
-#pragma unroll
-    for (int s = 0; s < 8; s += 2) {
-        const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
-        const bool hiWord = s >= 4;
-        auto q2 = [&](uint32_t w0_, uint32_t w1_) {
-            const uint32_t w = hiWord ? w1_ : w0_;
-            return f2 { static_cast<float>((w >> sh) & 0xffu), static_cast<float>((w >> (sh + 8u)) & 0xffu) };
-        };
-        const f2 tnx = __builtin_elementwise_fma(q2(nX0, nX1), Ax, Bx);
-        const f2 tny = __builtin_elementwise_fma(q2(nY0, nY1), Ay, By);
-        const f2 tnz = __builtin_elementwise_fma(q2(nZ0, nZ1), Az, Bz);
-        const f2 tfx = __builtin_elementwise_fma(q2(fX0, fX1), Ax, Bx);
-        const f2 tfy = __builtin_elementwise_fma(q2(fY0, fY1), Ay, By);
-        const f2 tfz = __builtin_elementwise_fma(q2(fZ0, fZ1), Az, Bz);
-        const f2 tn = __builtin_elementwise_max(__builtin_elementwise_max(tnx, tny), __builtin_elementwise_max(tnz, Tmin));
-        const f2 tf = __builtin_elementwise_min(__builtin_elementwise_min(tfx, tfy), __builtin_elementwise_min(tfz, Tmax));
-        const f2 lim = __builtin_elementwise_fma(tf, f2 { 1.00001f, 1.00001f }, f2 { 1e-7f, 1e-7f });
-        hitSlots |= (tn.x <= lim.x ? 1u : 0u) << s;
-        hitSlots |= (tn.y <= lim.y ? 1u : 0u) << (s + 1);
-        // origin inside the box: every near-plane distance <= tmin
-        insideSlots |= (tn.x <= tmin ? 1u : 0u) << (s + 16);
-        insideSlots |= (tn.y <= tmin ? 1u : 0u) << (s + 17);
-    }
-#endif
     // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
     // swapping bit pairs / pairs of pairs / nibbles per octant bit
     // (hit and inside masks permuted together: bits 0-7 and 16-23)
@@ -570,40 +495,6 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& 
         src = reinterpret_cast<const uint4*>(sc.nodes + child);
     }
     const uint32_t rel = static_cast<uint32_t>(reinterpret_cast<const GpuBvh8Node*>(src) - sc.nodes) - nc.base;
-#if ARK_BUFFER_FETCH
-    // LDS-cached nodes by ds_read; everything else by buffer_load_dwordx4 through one
-    // resource over nodes + triangles (per-lane byte offset), so the two paths stay
-    // distinct instructions instead of being merged into flat loads
-    if (!fx.isTri && rel < nc.count) {
-        const uint4* l = nc.lds + rel * 5u;
-        fx.w0 = l[0];
-        fx.w1 = l[1];
-        fx.w2 = l[2];
-        fx.w3 = l[3];
-        fx.w4 = l[4];
-        return;
-    }
-    {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<GpuBvh8Node*>(sc.nodes), 0, 0xffffffff, 0x00020000);
-        const uint32_t off = static_cast<uint32_t>(reinterpret_cast<const char*>(src) - reinterpret_cast<const char*>(sc.nodes));
-        fx.w0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-        fx.w1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16u, 0, 0));
-        fx.w2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 32u, 0, 0));
-        fx.w3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 48u, 0, 0));
-        fx.w4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 64u, 0, 0));
-        return;
-    }
-#endif
-#if ARK_FLAT_FETCH
-    // one generic (flat) pointer into LDS or HBM: five flat loads, no divergent paths
-    const uint4* p = (!fx.isTri && rel < nc.count) ? nc.lds + rel * 5u : src;
-    fx.w0 = p[0];
-    fx.w1 = p[1];
-    fx.w2 = p[2];
-    fx.w3 = p[3];
-    fx.w4 = p[4];
-    return;
-#endif
     if (!fx.isTri && rel < nc.count) {
         const uint4* l = nc.lds + rel * 5u;
         fx.w0 = l[0];
@@ -616,76 +507,18 @@ __device__ __forceinline__ void travFetch(const SceneArgs& sc, const NodeCache& 
     fx.w0 = src[0];
     fx.w1 = src[1];
     fx.w2 = src[2];
-#if ARK_FETCH5
     // five loads whatever the step: a triangle step reads 32 B of the next record
     // (the triangle array is padded), no branch around the node's last two loads
     fx.w3 = src[3];
     fx.w4 = src[4];
-#else
-    if (!fx.isTri) { // triangle steps leave w3/w4 unset: only node steps read them
-        fx.w3 = src[3];
-        fx.w4 = src[4];
-    }
-#endif
 }
 
 // Returns true when a triangle step produced a candidate (tt, uu, vv, backface
 // with the instance's handedness applied, inst, prim) in [tmin, tmax]; node steps
 // update the group state and return false.
-// Both tests without early exits (same operation sequence as intersectTri, all
-// conditions evaluated): used by the branch-free step below.
-__device__ __forceinline__ bool intersectTriFlat(V3 o, V3 d, float tmin, float tmax, const GpuTriangle& tr, float* outT, float* outU, float* outV, bool* backfaceDet)
-{
-    V3 v0 = { tr.t0[0], tr.t0[1], tr.t0[2] };
-    V3 e1 = { tr.t0[3], tr.t1[0], tr.t1[1] };
-    V3 e2 = { tr.t1[2], tr.t1[3], tr.t2[0] };
-    V3 p = cross(d, e2);
-    float det = dot(e1, p);
-    float inv = 1.0f / det;
-    V3 s = o - v0;
-    float u = dot(s, p) * inv;
-    V3 q = cross(s, e1);
-    float v = dot(d, q) * inv;
-    float tt = dot(e2, q) * inv;
-    *outT = tt;
-    *outU = u;
-    *outV = v;
-    *backfaceDet = det < 0.0f;
-    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (tt >= tmin && tt <= tmax);
-}
-
 __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o, V3 d, V3 idir, uint32_t oct, float tmin, float tmax, float& tt,
                                             float& uu, float& vv, bool& backface, uint32_t& inst, uint32_t& prim, uint32_t& cNodes, uint32_t& cTris)
 {
-#if ARK_BRANCHLESS_STEP
-    // A wave almost always holds both kinds of step (28 % are triangle steps), so it
-    // runs both tests anyway; computing both for every lane and selecting drops the
-    // divergent branch and its exec-mask bookkeeping. The unused test reads the other
-    // kind's words (finite or not, its result is discarded).
-    {
-        const GpuTriangle tr = triFromWords(fx.w0, fx.w1, fx.w2);
-        bool bf;
-        float t2, u2, v2;
-        const bool ok = intersectTriFlat(o, d, tmin, tmax, tr, &t2, &u2, &v2, &bf);
-        uint32_t gB, gBits, tB, tBits;
-        visitNode8(fx.w0, fx.w1, fx.w2, fx.w3, fx.w4, o, idir, oct, tmin, tmax, gB, gBits, tB, tBits);
-        cTris += fx.isTri ? 1u : 0u;
-        cNodes += fx.isTri ? 0u : 1u;
-        if (!fx.isTri) {
-            ts.gBase = gB;
-            ts.gBits = gBits;
-            ts.tBase = tB;
-            ts.tBits = tBits;
-        }
-        tt = t2;
-        uu = u2;
-        vv = v2;
-        inst = fx.w2.y;
-        prim = fx.w2.z;
-        backface = bf != (fx.w2.w != 0u);
-        return fx.isTri && ok;
-    }
-#endif
     if (fx.isTri) {
         cTris++;
         const GpuTriangle tr = triFromWords(fx.w0, fx.w1, fx.w2);
@@ -750,14 +583,8 @@ __device__ __forceinline__ void shadowRayOf(const SceneArgs& sc, float zFar, uin
 }
 
 // ---------------------------------------------------------------------------
-// 2. primary traversal (persistent, per-lane wave64 ballot refill)
+// 2. traversal work distribution
 // ---------------------------------------------------------------------------
-// Every lane owns one probe ray at a time. One outer iteration visits one BVH8
-// node per active lane and tests the triangles of its hit leaf children; lanes
-// whose ray finished are refilled at the top of the next iteration from a wave-private
-// pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays),
-// so the SIMD stays full until the global ray counter runs out.
-
 // XCD-aware work split: the window's probes are cut into kRayParts contiguous
 // partitions with one head counter each (ray_counter[p * kRayCounterStride]).
 // A wave drains the partition of the XCD it runs on first (read from
@@ -814,13 +641,16 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
     }
 }
 
-// SHADOWS: after a ray's closest hit is known, a front hit traces its shadow rays
-// (one per lit light, any-hit over all hit-mask classes, opaque.rchit:35-54) in the
-// same lane before the lane takes a new ray, and stores {lit, occluded} light bits
-// per ray; the shading kernel then finishes every surfel in one pass. One
-// persistent launch instead of two: no second ramp and tail.
-template<bool COUNT, int WPE, bool SHADOWS>
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_primary(SceneArgs sc, FrameArgs f)
+// ---------------------------------------------------------------------------
+// 2b. k_trace: probe-ray traversal (persistent, per-lane wave64 ballot refill)
+// ---------------------------------------------------------------------------
+// Every lane owns one probe ray at a time (pass 0 opaque, 1 masked). One outer
+// iteration visits one BVH8 node or one leaf triangle per active lane; lanes whose
+// ray finished are refilled at the top of the next iteration from a wave-private
+// pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays), so
+// the SIMD stays full until the global ray counter runs out.
+template<bool COUNT, int WPE>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     __shared__ uint4 ldsNodes[kLdsNodes * 5];
@@ -829,7 +659,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t lane = threadIdx.x & 63u;
-    const float tmin = 0.0001f; // raygen.rgen:116
+    const float tmin = 0.0001f; // raygen.rgen:37
     uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
@@ -844,36 +674,6 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
-    // shadow phase (SHADOWS): pass 2 + class; o = hit point, d = light direction,
-    // h.t = the shadow ray's tmax; bits 0-15 lit lights, 16-31 occluded, sl = current light
-    uint32_t lightBits = 0, sl = 0;
-    const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
-    const float shadowTmin = 0.025f; // opaque.rchit:44
-    uint32_t cShadow = 0, cShNodes = 0, cShTris = 0;
-    // next lit light after sl with a non-empty interval: sets up its ray, or false
-    auto nextShadowRay = [&](uint32_t after) -> bool { // after = 32: from the first light
-        uint32_t rem = lightBits & 0xffffu;
-        if (after < 16u) rem &= ~((2u << after) - 1u);
-        while (rem) {
-            sl = static_cast<uint32_t>(__builtin_ctz(rem));
-            rem &= rem - 1u;
-            float tmaxS;
-            shadowRayOf(sc, f.z_far, sl, o, &d, &tmaxS);
-            if (!(tmaxS >= shadowTmin)) continue; // empty interval: miss shader, not occluded
-            h.t = tmaxS;
-            idir = safeInv(d);
-            oct = rayOctant(idir);
-            int c = 0;
-            while (c < 3 && roots[c] < 0) ++c;
-            if (c == 3) continue;
-            pass = 2 + c;
-            st.depth = 0;
-            ts = TravState { static_cast<uint32_t>(roots[c]), rootGroupBits(), 0u, 0u };
-            if (COUNT) cShadow++;
-            return true;
-        }
-        return false;
-    };
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
@@ -895,9 +695,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 if (rank < avail) r = poolNext + rank;
                 else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
                 if (r != kNoHit) {
-                    const uint32_t q = r / f.R;
-                    const uint32_t slot = slotAt(f, q);
-                    const float4 fv = f.fib_order[r - q * f.R]; // (direction, sample index)
+                    const uint32_t qp = r / f.R;
+                    const uint32_t slot = slotAt(f, qp);
+                    const float4 fv = f.fib_order[r - qp * f.R]; // (direction, sample index)
                     const GpuProbeSlot ps = f.slots[slot];
                     ray = slot * f.R + __float_as_uint(fv.w); // hit record index
                     o = { ps.pos[0], ps.pos[1], ps.pos[2] };
@@ -925,102 +725,65 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (__ballot(active) == 0) break;
         if (COUNT) cIter++;
-        bool shadowHit = false;
-        if (active) {
-            // ---- one step: a pending leaf triangle, or the next node --------------
-            if (!travDone(ts, st)) {
-                Fetch fx;
-                travFetch(sc, nc, ts, st, oct, fx);
-                uint32_t inst, prim;
-                float tt, uu, vv;
-                bool bf;
-                const bool shadowPass = SHADOWS && pass >= 2;
-                uint32_t& cN = shadowPass ? cShNodes : cNodes;
-                uint32_t& cT = shadowPass ? cShTris : cTris;
-                const bool cand = travCompute(fx, ts, o, d, idir, oct, shadowPass ? shadowTmin : tmin, h.t, tt, uu, vv, bf, inst, prim, cN, cT);
-                if (shadowPass) shadowHit = cand; // any hit occludes (Opaque flag: no alpha test)
-                else if (cand &&
-                    !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
-                    !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
-                    h.t = tt;
-                    h.u = uu;
-                    h.v = vv;
-                    h.tri = fx.i;
-                    h.inst = inst;
-                    h.prim = prim;
-                    h.backface = bf;
-                }
+        // ---- one step: a pending leaf triangle, or the next node ------------------
+        if (active && !travDone(ts, st)) {
+            Fetch fx;
+            travFetch(sc, nc, ts, st, oct, fx);
+            uint32_t inst, prim;
+            float tt, uu, vv;
+            bool bf;
+            const bool cand = travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, cNodes, cTris);
+            if (cand &&
+                     !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
+                     !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
+                h.t = tt;
+                h.u = uu;
+                h.v = vv;
+                h.tri = fx.i;
+                h.inst = inst;
+                h.prim = prim;
+                h.backface = bf;
             }
         }
-        if (SHADOWS && active && pass >= 2 && (shadowHit || travDone(ts, st))) {
-            // ---- shadow ray of light sl finished: occluded, or its classes exhausted
-            bool rayDone = true;
-            if (shadowHit) {
-                lightBits |= 1u << (16 + sl);
-            } else {
-                int c = pass - 2 + 1;
-                while (c < 3 && roots[c] < 0) ++c;
-                if (c < 3) {
-                    pass = 2 + c;
+        // ---- pass finished -------------------------------------------------------------
+        if (active && travDone(ts, st)) {
+            bool finished = true;
+            if (pass == 0) {
+                // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
+                // cullMask 0x02, tmax = previous hit T (:64-92); a negative tmax
+                // (backface) is an empty interval.
+                opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
+                if (sc.root_masked >= 0 && opaqueT >= tmin) {
+                    pass = 1;
+                    finished = false;
+                    ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
                     st.depth = 0;
-                    ts = TravState { static_cast<uint32_t>(roots[c]), rootGroupBits(), 0u, 0u };
-                    rayDone = false;
+                    // stash the opaque hit; the masked pass searches [tmin, opaqueT]
+                    f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
+                    h = RayHit { opaqueT, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                 }
             }
-            if (rayDone && !nextShadowRay(sl)) {
-                f.shadow_bits[ray] = lightBits;
-                active = false;
-            }
-        } else if (active) {
-            // ---- pass finished -----------------------------------------------------
-            if (travDone(ts, st)) {
-                bool finished = true;
-                if (pass == 0) {
-                    // opaque pass done (raygen.rgen:122-134); masked pass: RayFlags_NoOpaque,
-                    // cullMask 0x02, tmax = previous hit T (:136-147); a negative tmax
-                    // (backface) is an empty interval.
-                    opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
-                    if (sc.root_masked >= 0 && opaqueT >= tmin) {
-                        pass = 1;
-                        finished = false;
-                        ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
-                        st.depth = 0;
-                        // stash the opaque hit; the masked pass searches [tmin, opaqueT]
-                        f.hits[ray] = GpuHit { h.tri == kNoHit ? __builtin_bit_cast(float, 0x7f800000u) : opaqueT, h.u, h.v, h.tri };
-                        h = RayHit { opaqueT, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-                    }
-                }
-                if (finished) {
-                    GpuHit out;
-                    if (pass == 1 && h.tri == kNoHit) {
-                        // masked pass found nothing: the opaque result (already stored) stands
-                        out = f.hits[ray];
-                        if (COUNT && out.tri != kNoHit) cHits++;
+            if (finished) {
+                GpuHit out;
+                if (pass == 1 && h.tri == kNoHit) {
+                    // masked pass found nothing: the opaque result (already stored) stands
+                    out = f.hits[ray];
+                    if (COUNT && out.tri != kNoHit) cHits++;
+                } else {
+                    if (h.tri == kNoHit) {
+                        out.t = __builtin_bit_cast(float, 0x7f800000u);
+                        out.u = out.v = 0.0f;
+                        out.tri = kNoHit;
                     } else {
-                        if (h.tri == kNoHit) {
-                            out.t = __builtin_bit_cast(float, 0x7f800000u);
-                            out.u = out.v = 0.0f;
-                            out.tri = kNoHit;
-                        } else {
-                            out.t = h.backface ? -h.t : h.t;
-                            out.u = h.u;
-                            out.v = h.v;
-                            out.tri = h.tri;
-                            if (COUNT) cHits++;
-                        }
-                        f.hits[ray] = out;
+                        out.t = h.backface ? -h.t : h.t;
+                        out.u = h.u;
+                        out.v = h.v;
+                        out.tri = h.tri;
+                        if (COUNT) cHits++;
                     }
-                    active = false;
-                    if (SHADOWS && out.tri != kNoHit && !(out.t < 0.0f)) {
-                        // front hit (raygen.rgen:200-206): shadow rays of its lit lights
-                        lightBits = f.light_count ? litLightMask(sc, hitShadingNormal(sc, out.tri, out.u, out.v)) : 0u;
-                        if (lightBits) {
-                            o = o + out.t * d; // hit point as opaque.rchit computes it
-                            active = nextShadowRay(32u);
-                        }
-                        if (!active) f.shadow_bits[ray] = lightBits;
-                    }
+                    f.hits[ray] = out;
                 }
+                active = false;
             }
         }
     }
@@ -1029,11 +792,6 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
         atomicAdd(&f.counters[2], static_cast<unsigned long long>(cHits));
         if (lane == 0) atomicAdd(&f.counters[7], static_cast<unsigned long long>(cIter));
-        if (SHADOWS) {
-            atomicAdd(&f.counters[3], static_cast<unsigned long long>(cShadow));
-            atomicAdd(&f.counters[4], static_cast<unsigned long long>(cShNodes));
-            atomicAdd(&f.counters[5], static_cast<unsigned long long>(cShTris));
-        }
     }
 }
 
@@ -1282,18 +1040,15 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 
 
 // ---------------------------------------------------------------------------
-// 3. shading: surface kernel -> shadow-ray kernel -> finish kernel
+// 3. shading
 // ---------------------------------------------------------------------------
 // k_shade takes chunks of kShadeChunk consecutive probe rays. Misses and backface
 // hits are finished in a classify pass; front hits are compacted into an LDS list
-// and shaded densely (material, textures, BRDF per lit light, DDGI indirect).
-// A front hit with no lit light stores its surfel at once. One with lit lights
-// (opaque.rchit:56-103: LdotN > 0) gets a front record - base and indirect terms
-// and, per lit light, the light term for shadowFactor = 1 (T) and 0 (Z) - and one
-// shadow ray per lit light in a global list. k_trace_shadow traces that list
-// densely (persistent, refilled lanes, any-hit over all hit-mask classes) and
-// sets occlusion bits; k_shade_finish adds base (+ T or Z per lit light) +
-// indirect: the same IEEE sequence as the single-pass closest-hit shader.
+// and shaded densely (material, textures, BRDF per lit light, DDGI indirect). The
+// shadow rays were traced before (k_shadow_gen + k_trace_shadow), and their per-ray light bits say
+// which lit lights are occluded: base (+ T or Z per lit light, in light order) +
+// indirect, the IEEE sequence of the single-pass closest-hit shader
+// (opaque.rchit:105-176 with traceShadowRay's shadowFactor 1 or 0).
 __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3 color, float dist)
 {
     const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
@@ -1312,40 +1067,15 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
     *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
 }
 
-// Wave-aggregated allocation: every lane of the converged, full wave passes its
-// count; returns this lane's first index in [*ctr, *ctr + sum). One atomic per wave.
-__device__ __forceinline__ uint32_t waveAlloc(uint32_t* ctr, uint32_t n)
-{
-    const uint32_t lane = __lane_id();
-    uint32_t x = n;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= static_cast<uint32_t>(off)) x += y;
-    }
-    const uint32_t total = __shfl(x, 63);
-    uint32_t base = 0;
-    if (total != 0) {
-        if (lane == 63) base = atomicAdd(ctr, total);
-        base = __shfl(base, 63);
-    }
-    return base + x - n;
-}
-
-// FUSED: the shadow rays were traced by k_trace_primary<..., SHADOWS = true>, whose
-// per-ray light bits say which lit lights are occluded: every surfel is finished
-// here, base (+ T or Z per lit light, in light order) + indirect, as k_shade_finish
-// adds them in the split path.
-template<bool COUNT, int WPE, bool FUSED>
+template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
     __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
-    const uint32_t L = f.light_count;
     uint32_t cFront = 0;
 
     // chunks come from the second set of per-XCD partition heads (see grabRays)
-    uint32_t* heads = f.ray_counter + (f.shade_pass == 2 ? kShade2HeadWord : kRayParts * kRayCounterStride);
+    uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
     const uint32_t home = xccId();
     uint32_t tried = 0;
     for (;;) {
@@ -1365,12 +1095,6 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const uint32_t q = (chunk + r) / f.R;
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
-            if (FUSED && f.shade_pass != 0) {
-                // split shading: pass 1 = every ray that needs no shadow bit (it runs beside
-                // the shadow traversal), pass 2 = the front hits with lit lights, after it
-                const bool lit = hit.tri != kNoHit && !(hit.t < 0.0f) && (f.shadow_bits[ray] & 0xffffu) != 0u;
-                if (lit != (f.shade_pass == 2)) continue;
-            }
             if (hit.tri == kNoHit) {
                 // miss (raygen.rgen:149-158)
                 V3 origin, dir;
@@ -1391,7 +1115,6 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
         __syncthreads();
         const uint32_t nA = counts[0];
         // ---- B. dense surface shading of front hits -----------------------------
-        // (every lane runs every iteration so that the record allocation sees full waves)
         for (uint32_t k0 = 0; k0 < nA; k0 += kShadeBlock) {
             const uint32_t kk = k0 + threadIdx.x;
             const bool valid = kk < nA;
@@ -1447,13 +1170,8 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     if (dot(Ld, N) > 0.0f) need |= 1u << l;
                 }
             }
-            uint32_t fk = 0, sj = 0, occ = 0;
-            if (!FUSED) {
-                fk = waveAlloc(f.front_count, need != 0 ? 1u : 0u);
-                sj = waveAlloc(f.shadow_count, static_cast<uint32_t>(__builtin_popcount(need)));
-            }
             if (!valid) continue;
-            if (FUSED) occ = f.shadow_bits[ray] >> 16;
+            const uint32_t occ = need ? f.shadow_bits[ray] >> 16 : 0u;
             V3 color = base;
             const V3 V = -dir;
             const V3 hitPoint = origin + T * dir;
@@ -1466,13 +1184,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     const V3 lc = v3(sc.sun_color[0], sc.sun_color[1], sc.sun_color[2]);
                     const V3 tT = brdf * LdotN * (lc * 1.0f);
                     const V3 tZ = brdf * LdotN * (lc * 0.0f);
-                    if (FUSED) {
-                        color = color + ((occ >> l) & 1u ? tZ : tT);
-                    } else {
-                        f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
-                        f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 2.0f * f.z_far),
-                                                          make_float4(Ld.x, Ld.y, Ld.z, __uint_as_float((fk << 4) | l)) };
-                    }
+                    color = color + ((occ >> l) & 1u ? tZ : tT);
                 }
                 l++;
             }
@@ -1503,13 +1215,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                         V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
                         V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
                         V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
-                    if (FUSED) {
-                        color = color + ((occ >> l) & 1u ? tZ : tT);
-                    } else {
-                        f.front_lights[static_cast<size_t>(fk) * L + l] = FrontLight { make_float4(tT.x, tT.y, tT.z, 0.0f), make_float4(tZ.x, tZ.y, tZ.z, 0.0f) };
-                        f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, distanceToLight - 0.001f),
-                                                          make_float4(normalizedToLight.x, normalizedToLight.y, normalizedToLight.z, __uint_as_float((fk << 4) | l)) };
-                    }
+                    color = color + ((occ >> l) & 1u ? tZ : tT);
                 }
             }
             // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
@@ -1519,13 +1225,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const V3 irradiance = sampleDDGI<ARK_DDGI_GATHER_BATCH>(f, hitPoint, N, Vi);
             const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
-            if (FUSED) {
-                storeSurfel(f, ray, color + bi, T);
-            } else if (need == 0) {
-                storeSurfel(f, ray, base + bi, T);
-            } else {
-                f.front_recs[fk] = FrontRec { make_float4(base.x, base.y, base.z, T), make_float4(bi.x, bi.y, bi.z, __uint_as_float(ray)), need, 0u };
-            }
+            storeSurfel(f, ray, color + bi, T);
         }
         __syncthreads();
     }
@@ -1535,8 +1235,8 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
 // Persistent any-hit traversal of the shadow-ray list (opaque.rchit:35-54:
 // TerminateOnFirstHit | SkipClosestHit | Opaque, cullMask 0xff, tmin 0.025): the
 // three hit-mask classes in turn, no alpha test. Lanes are refilled from a
-// wave-private pool like k_trace_primary; an occluded ray sets its light's bit in
-// its front record.
+// wave-private pool like k_trace; an occluded ray sets bit 16 + light of its probe
+// ray's word.
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
@@ -1624,8 +1324,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 occluded = travCompute(fx, ts, o, d, idir, oct, tmin, tmax, tt, uu, vv, bf, inst, prim, cNodes, cTris);
             }
             if (occluded) {
-                if (f.fused_shadows) atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
-                else atomicOr(&f.front_recs[owner >> 4].occ, 1u << (owner & 15u));
+                atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
                 active = false;
             } else if (travDone(ts, st)) {
                 ++pass;
@@ -1646,11 +1345,11 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     }
 }
 
-// Shadow rays before shading (fused_shadows == 2): one thread per window ray in
+// Shadow-ray list: one thread per window ray in
 // slot order; a front hit (raygen.rgen:200-206) stores its lit-light mask
 // (opaque.rchit:56-103, LdotN > 0 with the shading normal) in shadow_bits[ray] and
 // appends one shadow ray per lit light, owner = (ray << 4) | light. k_trace_shadow
-// then sets the occluded bits 16 + light, and k_shade<FUSED> finishes every surfel
+// then sets the occluded bits 16 + light, and k_shade finishes every surfel
 // in one pass (no per-light records, no finishing kernel).
 // Block b owns the kGenSteps x 256 consecutive queue positions from b * kGenSpan:
 // pass 1 stores the light masks (LDS + shadow_bits) and counts; one global atomic
@@ -1730,25 +1429,6 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax),
                                               make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
         }
-    }
-}
-
-// Lit front hits: base (+ T or Z per lit light, in light order) + indirect.
-__global__ void __launch_bounds__(256) k_shade_finish(FrameArgs f)
-{
-    const uint32_t n = *f.front_count;
-    const uint32_t L = f.light_count;
-    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < n; k += gridDim.x * 256u) {
-        const FrontRec fr = f.front_recs[k];
-        V3 color = v3(fr.base_T.x, fr.base_T.y, fr.base_T.z);
-        for (uint32_t b = fr.need; b; b &= b - 1) {
-            const uint32_t ll = static_cast<uint32_t>(__builtin_ctz(b));
-            const FrontLight& fl = f.front_lights[static_cast<size_t>(k) * L + ll];
-            const float4 t = (fr.occ >> ll) & 1u ? fl.Z : fl.T;
-            color = color + v3(t.x, t.y, t.z);
-        }
-        color = color + v3(fr.bi_ray.x, fr.bi_ray.y, fr.bi_ray.z);
-        storeSurfel(f, __float_as_uint(fr.bi_ray.w), color, fr.base_T.w);
     }
 }
 
@@ -2045,30 +1725,6 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
     return hipGetLastError();
 }
 
-// Occupancy variant of the trace kernel (minimum waves per SIMD the register
-// allocation must allow): 6 by default (80 VGPRs, no spill; 3.43 vs 3.61 ms at the
-// compiler's 5 on C4; 8 spilled and took 5.4 ms), ARK_TRACE_WPE = 0 or 5 for tuning.
-static int trace_variant()
-{
-    static const int v = [] {
-        const char* e = std::getenv("ARK_TRACE_WPE");
-        return e ? std::atoi(e) : 6;
-    }();
-    return v;
-}
-
-// Occupancy variant of the shading kernel (minimum waves per SIMD): the compiler's
-// choice by default (161 VGPRs, 3 waves, no spill: 0.874 ms on C4 vs 0.905 ms at
-// 4 waves with 128 VGPRs and spills, profiles/r01s2_*), ARK_SHADE_WPE = 4 or 5 for tuning.
-static int shade_variant()
-{
-    static const int v = [] {
-        const char* e = std::getenv("ARK_SHADE_WPE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
 hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
 {
     if (f.window_probes == 0) return hipSuccess;
@@ -2076,31 +1732,14 @@ hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_trace_primary(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
+// Persistent traversal at 6 waves/SIMD (80 VGPRs, no spill; round 1: 3.43 vs 3.61 ms
+// at the compiler's 5 on C4, 8 spilled and took 5.4 ms); COUNT variants run at the
+// compiler's occupancy.
+hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    const int v = trace_variant();
-    if (f.fused_shadows == 1) {
-        // the shadow state costs ~20 VGPRs: 6 waves/EU would spill, 5 is the default
-        static const int vf = [] { const char* e = std::getenv("ARK_TRACE_WPE_FUSED"); return e ? std::atoi(e) : 5; }();
-        if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-        else if (vf == 4) hipLaunchKernelGGL((dev::k_trace_primary<false, 4, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-        else if (vf == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-        else hipLaunchKernelGGL((dev::k_trace_primary<false, 5, true>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-        return hipGetLastError();
-    }
-    if (count) hipLaunchKernelGGL((dev::k_trace_primary<true, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else if (v == 5) hipLaunchKernelGGL((dev::k_trace_primary<false, 5, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else if (v == 6) hipLaunchKernelGGL((dev::k_trace_primary<false, 6, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-#if ARK_LDS_NODES <= 64 // 7 waves/SIMD only fit the LDS with a smaller node cache
-    else if (v == 7) hipLaunchKernelGGL((dev::k_trace_primary<false, 7, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-#endif
-    else hipLaunchKernelGGL((dev::k_trace_primary<false, 1, false>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    if (count) hipLaunchKernelGGL((dev::k_trace<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
+    else hipLaunchKernelGGL((dev::k_trace<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
     return hipGetLastError();
-}
-
-size_t shade_work_bytes(uint64_t rays, uint32_t lights)
-{
-    return rays * (sizeof(FrontRec) + static_cast<uint64_t>(lights) * (sizeof(FrontLight) + sizeof(ShadowRay)));
 }
 
 // Co-resident workgroups of a persistent kernel on this device (cached per kernel).
@@ -2117,23 +1756,16 @@ static uint32_t persistentBlocks(const void* fn, int block, uint32_t fallback)
     return cache.back().second;
 }
 
+// One-pass shading at <= 128 VGPRs, 4 waves/SIMD, no spill (round 1: 0.57 -> 0.50 ms
+// at C4 against the compiler's 133 VGPRs, 3 waves).
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    const int v = shade_variant();
-    if (f.fused_shadows) {
-        // one-pass shading at <= 128 VGPRs, 4 waves/SIMD, no spill (0.57 -> 0.50 ms at C4;
-        // ARK_SHADE_WPE=1: the compiler's 133 VGPRs, 3 waves)
-        if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-        else if (v != 1) {
-            const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, 4, true>);
-            hipLaunchKernelGGL((dev::k_shade<false, 4, true>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
-        } else hipLaunchKernelGGL((dev::k_shade<false, 1, true>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-        return hipGetLastError();
+    if (count) {
+        hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
+    } else {
+        const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
+        hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
     }
-    if (count) hipLaunchKernelGGL((dev::k_shade<true, 1, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else if (v == 4) hipLaunchKernelGGL((dev::k_shade<false, 4, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else if (v == 5) hipLaunchKernelGGL((dev::k_shade<false, 5, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_shade<false, 1, false>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -2152,12 +1784,6 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_shade_finish(const FrameArgs& f, hipStream_t s)
-{
-    hipLaunchKernelGGL(dev::k_shade_finish, dim3(2048), dim3(256), 0, s, f);
-    return hipGetLastError();
-}
-
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
@@ -2167,24 +1793,13 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
     return hipGetLastError();
 }
 
-const void* kernel_trace_primary_ptr(bool count)
+const void* kernel_trace_ptr(bool count)
 {
-    const int v = trace_variant();
-    if (count) return reinterpret_cast<const void*>(&dev::k_trace_primary<true, 1, false>);
-    if (v == 5) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 5, false>);
-    if (v == 6) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 6, false>);
-#if ARK_LDS_NODES <= 64
-    if (v == 7) return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 7, false>);
-#endif
-    return reinterpret_cast<const void*>(&dev::k_trace_primary<false, 1, false>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6>);
 }
 const void* kernel_shade_ptr(bool count)
 {
-    const int v = shade_variant();
-    if (count) return reinterpret_cast<const void*>(&dev::k_shade<true, 1, false>);
-    if (v == 4) return reinterpret_cast<const void*>(&dev::k_shade<false, 4, false>);
-    if (v == 5) return reinterpret_cast<const void*>(&dev::k_shade<false, 5, false>);
-    return reinterpret_cast<const void*>(&dev::k_shade<false, 1, false>);
+    return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
 }
 
 const void* kernel_trace_shadow_ptr(bool count)

@@ -51,9 +51,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--deferred-update", type=int, default=0,
-                    help="1: frame n's probe update beside frame n+1's traversal (ark_ddgi_set_deferred_update; "
-                         "N=1 only; measured 0.3-0.5 %% slower on C4, DESIGN.md §9)")
     ap.add_argument("--no-ao-bake", action="store_true", help="skip the config C1 AO bake line (GPU + CPU oracle)")
     ap.add_argument("--ao-size", type=int, default=1024)
     ap.add_argument("--ao-samples", type=int, default=64)
@@ -108,8 +105,6 @@ def main():
         from arkoserenderer_amd.collective import OverlappedSlabExchange
 
         exch = OverlappedSlabExchange(node, SlabExchange.from_views(ctx.device_views(), rank, world, device).exchange, device)
-    deferred = bool(args.deferred_update) and exch is None
-    ctx.set_deferred_update(deferred)
     setup_s = time.time() - t_setup
 
     frame = 0
@@ -166,13 +161,13 @@ def main():
     avg = [sum(k[i] for k in ktimes) / len(ktimes) for i in range(5)]
     rays_rank = cnt.rays
     kernel_bytes = {
-        "k_trace_primary": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays_rank,
+        "k_trace": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays_rank,
         "k_shade": HIT_RECORD_BYTES * rays_rank + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays_rank - cnt.hits)
-                   + SURFEL_BYTES * rays_rank + SHADOW_RAY_BYTES * cnt.shadow_rays,
+                   + SURFEL_BYTES * rays_rank,
         "k_trace_shadow": NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests + SHADOW_RAY_BYTES * cnt.shadow_rays,
         "k_probe_update": cnt.probes * (R * SURFEL_BYTES + 2 * (64 * 8 + 256 * 4) + (36 * 8 + 68 * 4) + 32),
     }
-    kernel_ms = {"k_trace_primary": avg[1], "k_shade": avg[2], "k_trace_shadow": avg[4], "k_probe_update": avg[3]}
+    kernel_ms = {"k_trace": avg[1], "k_shade": avg[2], "k_trace_shadow": avg[4], "k_probe_update": avg[3]}
     dom = max(kernel_ms, key=kernel_ms.get)
     achieved = kernel_bytes[dom] / (kernel_ms[dom] * 1e-3) / 1e9
     traffic = None
@@ -208,7 +203,6 @@ def main():
             "rays_per_probe": R,
             "probe_updates_per_step": K,
             "parallelism": f"zslab{world}",
-            "deferred_update": deferred,
             "bvh_nodes": int(bvh.node_count),
             "bvh_max_depth": int(bvh.max_depth),
             "bvh_build_ms": round(bvh.build_ms, 1),

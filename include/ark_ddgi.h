@@ -30,8 +30,17 @@
  * reference's ARKOSE_LOG(Error)+NullExecuteCallback handling (DDGINode.cpp:78-81):
  * the node maps a negative status to an Error log and a no-op.
  *
- * Threading: one context per GPU, used from one host thread. All device work is
- * enqueued on the caller's stream (or the context's own stream when NULL).
+ * Threading: one context per GPU, used from one host thread.
+ *
+ * Streams: every asynchronous entry point takes a hipStream_t as `void*`; NULL is
+ * the legacy default (null) stream, as for any HIP API, so work on it is ordered
+ * against every blocking stream of the process (torch's default stream among
+ * them). Operations of one context execute in the order they are called, whatever
+ * streams they are given: an operation enqueued on another stream than the
+ * previous one waits for it on the device (they share the traversal spill area,
+ * the hit records and the atlases). Work of other producers on another stream
+ * (e.g. the caller filling a G-buffer plane) is the caller's to order, as with any
+ * kernel launch.
  */
 #ifndef ARK_DDGI_H
 #define ARK_DDGI_H
@@ -263,8 +272,9 @@ const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx);
 /* Copies the scene arrays to HBM and builds the BVH (host arrays are not retained). */
 int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
 
-/* One DDGI update (DDGINode.cpp:171-298) enqueued on `hip_stream` (NULL = ctx stream).
- * Asynchronous: call ark_ddgi_synchronize or synchronize the stream before reading. */
+/* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null
+ * stream). Asynchronous: call ark_ddgi_synchronize or synchronize the stream before
+ * reading. */
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
@@ -292,24 +302,11 @@ int ark_ddgi_set_counting(ArkDdgiCtx* ctx, int enabled);
 int ark_ddgi_get_counters(ArkDdgiCtx* ctx, ArkDdgiCounters* out_counters);
 
 /* Device time of the last update's kernels, from HIP events on the update stream:
- * [0] whole update, [1] primary traversal (+ slot table), [2] surface shading,
- * [3] probe update (irradiance, visibility, borders, offsets), [4] shadow rays
- * (traversal + light-term finish). Milliseconds. */
+ * [0] whole update, [1] traversal (slot table + probe rays, and the shadow rays with
+ * the shadow queue), [2] surface shading, [3] probe update (irradiance, visibility,
+ * borders, offsets), [4] shadow rays traced in their own launch (0 with the queue).
+ * Milliseconds. */
 int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out_ms, int count);
-/* Deferred probe update (off by default). The reference records a frame's probe
- * update behind a barrier after its traceRays (DDGINode.cpp:171-240), and the next
- * frame's traceRays waits for it; but the traversal reads neither atlas (only the
- * closest-hit indirect lookup does, raygen.rgen:94-106), so with this on, frame
- * n's probe update runs on an internal stream beside frame n+1's traversal, and
- * frame n+1's shading waits for it (its traversal too, when frame n moved the probe
- * offsets). Results are identical. After ark_ddgi_update returns, the atlases are
- * complete for: the next update, ark_ddgi_lighting_compose / ark_ddgi_probe_debug,
- * ark_ddgi_read, ark_ddgi_synchronize; any other reader of the device views first
- * calls ark_ddgi_join_update(ctx, its_stream). Not applied on the overlapped path
- * or while stage timing is on. */
-int ark_ddgi_set_deferred_update(ArkDdgiCtx* ctx, int enabled);
-/* Makes `hip_stream` (NULL = ctx stream) wait for a deferred probe update in flight. */
-int ark_ddgi_join_update(ArkDdgiCtx* ctx, void* hip_stream);
 int ark_ddgi_set_timing(ArkDdgiCtx* ctx, int enabled);
 
 /* BVH statistics of the last set_scene (node count, leaf triangle count, depth, SAH cost, bytes). */
@@ -348,7 +345,7 @@ typedef struct ArkBakeAoDesc {
     int32_t reserved[2];
 } ArkBakeAoDesc;
 
-/* Runs both passes, enqueued on `hip_stream` (NULL = ctx stream). */
+/* Runs both passes, enqueued on `hip_stream` (NULL = the null stream). */
 int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* desc, void* hip_stream);
 
 /* Results of the last bake (blocking): width*height texels of
@@ -405,8 +402,8 @@ typedef struct ArkComposeDesc {
     uint16_t* out;                         /* SceneColorWithGI RGBA16F */
 } ArkComposeDesc;
 
-/* Enqueues the compose on `hip_stream` (NULL = ctx stream), after any update
- * enqueued before it on that stream. */
+/* Enqueues the compose on `hip_stream` (NULL = the null stream), after every
+ * operation of this context called before it. */
 int ark_ddgi_lighting_compose(ArkDdgiCtx* ctx, const ArkComposeDesc* desc, void* hip_stream);
 
 /* ---- DDGI consumer: RT reflections ray generation -----------
@@ -439,8 +436,9 @@ typedef struct ArkReflectionsDesc {
     uint16_t* out_direction;             /* reflectionDirectionImg RGBA16F: world direction, 0 */
 } ArkReflectionsDesc;
 
-/* Enqueues the reflection rays on `hip_stream` (NULL = ctx stream), after any update
- * enqueued before it on that stream (it shares the update's traversal stack space). */
+/* Enqueues the reflection rays on `hip_stream` (NULL = the null stream), after every
+ * operation of this context called before it (it shares the update's traversal
+ * stack space). */
 int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, void* hip_stream);
 
 /* ---- DDGI probe debug visualisation --------------------------

@@ -1775,6 +1775,11 @@ int oracle_rt_reflections(void* ctx, const ArkReflectionsDesc* r, int threads)
             const Tex& env = (o.envTex >= 0) ? o.textures[o.envTex] : o.envWhite;
             sampleBilinear(env, u, v, c);
             radiance = r->environment_multiplier * v3(c[0], c[1], c[2]);
+            // miss.rmiss:12 hitT = zFar + 1 passes `payload.hitT <= tmax` (:114) when
+            // zFar + 1 <= 10000: ray length zFar + 1; the reference's radiance is then an
+            // unwritten payload's (undefined), the environment stands in for it
+            const float missT = o.desc.z_far + 1.0f;
+            if (missT <= tmax) tmax = missT;
         }
         store(r->out_radiance, p, radiance, tmax);
         store(r->out_direction, p, rayDirection, 0.0f);

@@ -51,15 +51,13 @@ def diff_report(name, g, o):
     return {"name": name, "mismatch": n, "total": int(g.size), "linf": linf}
 
 
-def run_pair(scene, grid, cfg, frames, z_far=10000.0, exposure=None, threads=8, check_each_frame=True, deferred=False):
+def run_pair(scene, grid, cfg, frames, z_far=10000.0, exposure=None, threads=8, check_each_frame=True):
     """Runs `frames` updates through the HIP path and the oracle; returns the
-    per-frame diff reports."""
+    per-frame diff reports (every frame, or the last one only: frames are then
+    queued back to back without a host sync between them)."""
     exposure = exposure or {}
     ctx = D.DDGIContext(grid, z_far, cfg)
     ctx.set_scene(scene)
-    # deferred: frames are queued back to back (no host sync between them), so frame
-    # n's probe update really runs beside frame n+1's traversal
-    ctx.set_deferred_update(deferred)
     orc = O.Oracle(ctx.desc)
     orc.set_scene(scene, threads)
     node_idx = 0
@@ -67,7 +65,7 @@ def run_pair(scene, grid, cfg, frames, z_far=10000.0, exposure=None, threads=8, 
     for f in range(frames):
         p = D.frame_params(cfg, grid, D.AppState(f), node_idx, **exposure)
         ctx.update(p)
-        if not deferred or check_each_frame or f == frames - 1:
+        if check_each_frame or f == frames - 1:
             ctx.synchronize()
         orc.update(p, threads)
         node_idx = (node_idx + p.probe_updates) % grid.probe_count()

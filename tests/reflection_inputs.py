@@ -53,6 +53,7 @@ def gbuffer(width, height, cam, seed=5, sky_frac=0.1, rough_frac=0.2, roughness=
     nv[..., 0], nv[..., 1] = ex, ey
     mat = rng.integers(0, 256, (height, width, 4)).astype(np.uint8)
     mat[..., 0] = rng.integers(0, 150, (height, width)) if roughness is None else roughness
-    mat[rng.random((height, width)) < rough_frac, 0] = 230  # >= 0.7: not traced
+    mat[rng.random((height, width)) < rough_frac, 0] = 230  # >= 0.6: not traced
+    mat[rng.random((height, width)) < rough_frac / 2, 0] = 160  # 0.627, in [0.6, 0.7): not traced at the node's 0.6 (RTReflectionsNode.h:20)
     noise = rng.random((64, 64, 2)).astype(np.float32)
     return {"depth": depth, "material": mat, "normal_velocity": nv.view(np.uint16), "blue_noise": noise}, n.astype(np.float32)

@@ -79,48 +79,6 @@ def test_small_soup_sun():
     _assert_exact(reps)
 
 
-@pytest.mark.parametrize("mode", ["split", "fused", "shade2"])
-@pytest.mark.parametrize("case", ["features", "soup"])
-def test_other_shadow_schedules(case, mode, monkeypatch):
-    """The two non-default shadow-ray schedules (ARK_SHADOWS): "split" = per-light
-    records in shading, k_trace_shadow after it, k_shade_finish; "fused" = shadow rays
-    traced inside k_trace_primary. Both give the oracle's bits, like the default
-    "pre" schedule (k_shadow_gen + k_trace_shadow before one-pass shading)."""
-    if mode == "shade2":  # the default schedule with shading split in two passes around the shadow rays
-        monkeypatch.setenv("ARK_SHADE_SPLIT", "1")
-    else:
-        monkeypatch.setenv("ARK_SHADOWS", mode)
-    if case == "features":
-        sc = scenes.features_scene()
-        grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
-        cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
-                           max_rays_per_probe=128, max_probe_updates=144)
-        reps = run_pair(sc, grid, cfg, 2, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
-                                                      environment_brightness=0.5))
-        _assert_exact(reps, offsets_expected=True)
-    else:
-        sc = S.soup(64_000, extent=7.0)
-        grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
-        cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=512, compute_probe_offsets=False,
-                           max_rays_per_probe=256, max_probe_updates=512)
-        reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
-        _assert_exact(reps)
-
-
-@pytest.mark.parametrize("subwindows", ["2", "3", "4"])
-def test_subwindow_pipeline(subwindows, monkeypatch):
-    """ARK_SUBWINDOWS: the window cut into S pieces on two streams (default 1); every
-    S gives the oracle's bits (features scene: lights, masked, translucent, offsets)."""
-    monkeypatch.setenv("ARK_SUBWINDOWS", subwindows)
-    sc = scenes.features_scene()
-    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
-    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=100, compute_probe_offsets=True,
-                       max_rays_per_probe=128, max_probe_updates=144)
-    reps = run_pair(sc, grid, cfg, 3, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
-                                                  environment_brightness=0.5))
-    _assert_exact(reps, offsets_expected=True)
-
-
 def test_features_scene_real_ies_lut():
     """The spots sample a real profile's 256x256 LUT (multi-lobe.ies through
     ark_ies_lut_from_file, normalised by its peak candela), as the C5 config's

@@ -15,12 +15,15 @@ import scenes
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("roughness", [None, 0])
-def test_reflections_features_scene(roughness):
+@pytest.mark.parametrize("roughness,size,z_far", [(None, (96, 64), 100.0), (0, (96, 64), 100.0), (None, (97, 61), 10000.0)])
+def test_reflections_features_scene(roughness, size, z_far):
+    """(97, 61): partial 8 x 8 tiles on both edges. z_far 100: a miss passes the
+    raygen's hitT <= 10000 test with hitT = zFar + 1 (miss.rmiss:12), ray length 101;
+    z_far 10000 (the camera default): misses keep 10000."""
     sc = scenes.features_scene()
     grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=144, max_rays_per_probe=64, max_probe_updates=144)
-    ctx = D.DDGIContext(grid, 100.0, cfg)
+    ctx = D.DDGIContext(grid, z_far, cfg)
     ctx.set_scene(sc)
     orc = O.Oracle(ctx.desc)
     orc.set_scene(sc)
@@ -29,7 +32,7 @@ def test_reflections_features_scene(roughness):
         ctx.update(p)
         orc.update(p)
     ctx.synchronize()
-    W, H = 96, 64
+    W, H = size
     cam = RI.camera(W, H)
     g, _ = RI.gbuffer(W, H, cam, seed=11, roughness=roughness)
     kw = dict(environment_multiplier=0.5, ambient_amount=0.05)
@@ -46,6 +49,9 @@ def test_reflections_features_scene(roughness):
     traced = np.any(want_dir != 0, axis=-1)
     assert traced.sum() > W * H // 2
     rl = want_rad.view(np.float16)[..., 3].astype(np.float32)[traced]
-    assert (rl < 10000).any() and (rl == 10000).any()  # both hits and misses
+    miss_t = min(z_far + 1.0, 10000.0)
+    assert (rl < miss_t).any() and (rl == np.float32(np.float16(miss_t))).any()  # both hits and misses
+    rough = (g["material"][..., 0] / 255.0 >= 0.6) & (g["depth"] < 1.0 - 1e-6)
+    assert ((g["material"][..., 0] == 160) & rough).any() and (got_rad[rough] == 0).all() and (got_dir[rough] == 0).all()
     ctx.close()
     orc.close()

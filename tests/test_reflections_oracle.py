@@ -21,7 +21,8 @@ def test_reflections_oracle_untraced_and_mirror():
     rad, dirs = orc.rt_reflections(W, H, cam, g, environment_multiplier=0.5)
     rad, dirs = rad.view(np.float16).astype(np.float32), dirs.view(np.float16).astype(np.float32)
     sky = g["depth"] >= 1.0 - 1e-6
-    rough = (g["material"][..., 0] / 255.0 >= 0.7) & ~sky
+    rough = (g["material"][..., 0] / 255.0 >= 0.6) & ~sky
+    assert ((g["material"][..., 0] == 160) & ~sky).any()  # roughness in [0.6, 0.7) is not traced either
     traced = ~sky & ~rough
     assert (rad[sky] == 0).all() and (dirs[sky] == 0).all()  # direction untouched (zeros)
     assert (rad[rough] == 0).all() and (dirs[rough] == 0).all()
