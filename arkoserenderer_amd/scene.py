@@ -395,6 +395,30 @@ def ies_texture(source, size: int = abi.ARK_IES_LUT_SIZE) -> Texture:
     return Texture(size, size, abi.ARK_TEX_R32F, lut, abi.ARK_WRAP_CLAMP_TO_EDGE)
 
 
+def sponza_substitute(ies_dir: str | None = None) -> SceneData:
+    """BASELINE config C3 substitute (Sponza.bin is not in the reference's
+    assets, .MISSING_LARGE_BLOBS): a 262,272-triangle strip soup over [0, 31] m (the
+    C4 generator at Sponza's triangle count) with the C4 sun and three spot lights
+    from 20 m, pointing down, lit by the reference's multi-lobe.ies profile (LUT
+    normalised by its peak candela), for the 24x12x24-probe grid of
+    sponza_substitute_grid()."""
+    import os
+
+    sc = soup(262_272, extent=31.0)
+    here = ies_dir or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "ies")
+    lut, info = ies_lut(os.path.join(here, "multi-lobe.ies"))
+    sc.textures.append(Texture(256, 256, abi.ARK_TEX_R32F, lut / np.float32(info.max_candela), abi.ARK_WRAP_CLAMP_TO_EDGE))
+    t = len(sc.textures) - 1
+    sc.spots = [SpotLight((200.0, 190.0, 170.0), (0.0, -1.0, 0.0), (1.0, 0.0, 0.0), (0.0, 0.0, 1.0), (x, 20.0, z), 1.0, t)
+                for x, z in ((8.0, 8.0), (16.0, 24.0), (24.0, 12.0))]
+    return sc
+
+
+def sponza_substitute_grid():
+    """(grid dims, spacing, origin) of config C3: 24x12x24 probes over the [0.5, 31.5] m box."""
+    return (24, 12, 24), (31.0 / 24, 31.0 / 12, 31.0 / 24), (0.5, 0.5, 0.5)
+
+
 def _box_mesh():
     """Unit cube [0,1]^3, 24 vertices (flat normals), 12 CCW triangles facing out."""
     faces = [((0, 0, 1), [(0, 0, 1), (1, 0, 1), (1, 1, 1), (0, 1, 1)]), ((0, 0, -1), [(1, 0, 0), (0, 0, 0), (0, 1, 0), (1, 1, 0)]),

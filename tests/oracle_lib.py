@@ -79,6 +79,10 @@ class Oracle:
         assert rc == 0, rc
         self._scene = scene
 
+    def reset_history(self):
+        """The creation-time clears (atlases, offsets), as ark_ddgi_reset_history."""
+        assert self.lib.oracle_reset_history(self.h) == 0
+
     def update(self, params, threads: int = 8):
         rc = self.lib.oracle_update(self.h, C.byref(params), threads)
         assert rc == 0, rc

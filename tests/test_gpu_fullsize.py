@@ -1,0 +1,117 @@
+"""Full-size parity of the BASELINE configs the bench and the config lines run:
+C4 (10 M-triangle strip soup, 32x32x32 probes x 256 rays, sun) and the C3
+substitute (262,272-triangle soup, 24x12x24 x 256, sun + 3 IES spots), through the
+HIP path with the whole grid in one window (K = N), against the CPU oracle on a
+subset of probes spread over every Z-slab and every slot-order block.
+
+Why a subset is exact: a probe's frame-f surfels, atlas tile and offset depend only
+on its index, the frame index, the scene, its own previous tile and offset, and
+the previous frame's full atlases (raygen.rgen:94-139, probeUpdate*.comp). So the
+oracle runs each subset window from the same start state as the GPU's frame:
+  frame 0 - a reset oracle (cleared atlases, zero offsets), windows of 32 probes;
+  frame 1 - the GPU's frame-0 atlases and offsets written into the oracle, the same
+            windows at frame 1 (hysteresis on: the indirect term and the blends
+            read real frame-0 data at full size).
+Compared bit for bit: the window probes' surfels, atlas tiles (interior + border)
+and offsets."""
+import numpy as np
+import pytest
+
+from arkoserenderer_amd import abi
+from arkoserenderer_amd import ddgi as D
+from arkoserenderer_amd import scene as S
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _tile_mask(dims, probes, res):
+    """Boolean atlas mask of the (res + 2)^2 tiles of `probes` (ddgi/common.glsl:36-67)."""
+    X, Y, Z = dims
+    t = res + 2
+    m = np.zeros((Z * t, X * Y * t), bool)
+    for p in probes:
+        y, rem = divmod(int(p), X * Z)
+        z, x = divmod(rem, X)
+        tx, ty = x + y * X, z
+        m[ty * t:(ty + 1) * t, tx * t:(tx + 1) * t] = True
+    return m
+
+
+def _windows(dims, count):
+    """`count` windows of 32 consecutive probes (one x run at fixed y, z; x spans all
+    four x blocks of k_slot_order) with z covering every Z-slab of 8 and y spread."""
+    X, Y, Z = dims
+    n = min(32, X)
+    out = []
+    for k in range(count):
+        z = (k * Z) // count + (k % 2) * (Z // count // 2)
+        y = (k * 5 + 3) % Y
+        out.append(X * z + X * Z * y)
+    return [(f, n) for f in out]
+
+
+def _run(scene, dims, spacing, origin, R, z_far, exposure, windows):
+    grid = D.ProbeGrid(dims, spacing, origin)
+    N = grid.probe_count()
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+    ctx = D.DDGIContext(grid, z_far, cfg)
+    ctx.set_scene(scene)
+    ocfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=32, max_rays_per_probe=R, max_probe_updates=32, compute_probe_offsets=True)
+    orc = O.Oracle(D.desc_for(grid, z_far, ocfg))
+    orc.set_scene(scene, threads=16)
+    checked = 0
+    for frame in range(2):
+        p = D.frame_params(cfg, grid, D.AppState(frame), 0, **exposure)
+        ctx.update(p)
+        ctx.synchronize()
+        g = {w: ctx.read(w) for w in (abi.ARK_DDGI_SURFELS, abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS)}
+        for first, k in windows:
+            if frame == 0:
+                orc.reset_history()
+            else:
+                for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS):
+                    orc.write(w, start[w])
+            ocfg.probe_updates_per_frame = k
+            orc.update(D.frame_params(ocfg, grid, D.AppState(frame), first, **exposure), threads=16)
+            probes = np.arange(first, first + k)
+            # surfels: GPU slot = probe index (window from 0, K = N); oracle slot = probe - first
+            gs = g[abi.ARK_DDGI_SURFELS].reshape(N, R, 4)[probes]
+            os_ = orc.read(abi.ARK_DDGI_SURFELS).reshape(32, R, 4)[:k]
+            bad = np.argwhere(np.any(gs != os_, axis=-1))
+            assert bad.size == 0, f"frame {frame} window {first}: {len(bad)} surfels differ, first (slot, ray) {bad[:4].tolist()}"
+            for w, res, ch in ((abi.ARK_DDGI_ATLAS_IRRADIANCE, 8, 4), (abi.ARK_DDGI_ATLAS_VISIBILITY, 16, 2)):
+                m = _tile_mask(dims, probes, res)
+                ga = g[w].reshape(m.shape[0], m.shape[1], ch)[m]
+                oa = orc.read(w).reshape(m.shape[0], m.shape[1], ch)[m]
+                same = (ga == oa) | (np.isnan(O.f16_to_f32(ga)) & np.isnan(O.f16_to_f32(oa)))
+                assert same.all(), f"frame {frame} window {first}: {int((~same).sum())} atlas values of {w} differ"
+            go = g[abi.ARK_DDGI_PROBE_OFFSETS].reshape(N, 4)[probes]
+            oo = orc.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[probes]
+            assert np.array_equal(go.view(np.uint32), oo.view(np.uint32)), f"frame {frame} window {first}: offsets differ"
+            assert np.count_nonzero(os_) > 0
+            checked += k
+        start = g
+    ctx.close()
+    orc.close()
+    return checked
+
+
+def test_c4_full_size_probe_subset():
+    """C4 as bench.py runs it: 10 M triangles, 32^3 x 256, sun, offsets on; 8 windows
+    of 32 probes (256 probes, one x row per Z-slab of 4) for frames 0 and 1."""
+    scene = S.soup(10_000_000)
+    dims = (32, 32, 32)
+    n = _run(scene, dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), 256, 10000.0,
+             dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), _windows(dims, 8))
+    assert n == 2 * 256
+
+
+def test_c3_substitute_full_grid_probe_subset():
+    """C3 substitute at its full 24x12x24 grid x 256 rays with the sun and 3 IES spot
+    lights (4 shadow rays per lit hit), offsets on; 8 windows of 24 probes."""
+    scene = S.sponza_substitute()
+    dims, spacing, origin = S.sponza_substitute_grid()
+    n = _run(scene, dims, spacing, origin, 256, 10000.0,
+             dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), _windows(dims, 8))
+    assert n == 2 * 8 * 24

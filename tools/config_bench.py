@@ -24,15 +24,8 @@ def build(cfg_name):
         grid = D.ProbeGrid((48, 16, 48), (5.0, 2.5, 5.0), (2.5, 0.5, 2.5))
         R, zf = 512, 1000.0
     else:
-        sc = S.soup(262_272, extent=31.0)
-        import numpy as np
-        here = os.path.join(ROOT, "tests", "golden", "ies")
-        lut, info = S.ies_lut(os.path.join(here, "multi-lobe.ies"))
-        sc.textures.append(S.Texture(256, 256, 2, lut / np.float32(info.max_candela), 1))
-        t = len(sc.textures) - 1
-        sc.spots = [S.SpotLight((200.0, 190.0, 170.0), (0.0, -1.0, 0.0), (1.0, 0.0, 0.0), (0.0, 0.0, 1.0), (x, 20.0, z), 1.0, t)
-                    for x, z in ((8.0, 8.0), (16.0, 24.0), (24.0, 12.0))]
-        grid = D.ProbeGrid((24, 12, 24), (31.0 / 24, 31.0 / 12, 31.0 / 24), (0.5, 0.5, 0.5))
+        sc = S.sponza_substitute()
+        grid = D.ProbeGrid(*S.sponza_substitute_grid())
         R, zf = 256, 10000.0
     return sc, grid, R, zf
 
