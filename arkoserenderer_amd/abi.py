@@ -426,6 +426,11 @@ EXPORTS = {
 _lib = None
 
 
+def library_path() -> str:
+    """Path of the libark_ddgi.so this process loads (ARK_DDGI_LIB overrides)."""
+    return LIB_PATH
+
+
 def load_library(path: str | None = None) -> C.CDLL:
     """Loads libark_ddgi.so (built in-tree by __graft_entry__.build()). Raises if
     it is missing: there is no fallback implementation of the DDGI path."""

@@ -8,6 +8,14 @@ update (trace -> shade -> irradiance/visibility/border/offset update) of every
 probe; with N GPUs the grid is split in Z-slabs (strong scaling: fixed total
 work) and the atlases are all-gathered over RCCL after each update.
 
+Besides `value`, rank 0 at N = 1 reports: the reference's own windows (K = 4096,
+the node's cap, DDGINode.h:23; K = 2048, its default, DDGINode.h:31) with per-kernel
+times; config C2 (Cornell 8^3 x 64) on the GPU; the CPU baseline (the oracle on the
+box's host cores, one warm-up then the median of >= 5 frames, C4 and C2); the C1 AO
+bake; the DDGI consumers. The roofline object carries the algorithmic-bytes
+fraction (SURVEY §8d model) and, from a rocprofv3 PMC pass of this same library
+build (matched by its sha256), the measured HBM traffic and its fraction.
+
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
@@ -16,9 +24,11 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
-import ctypes as C
+import hashlib
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -48,8 +58,10 @@ def parse():
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--rays", type=int, default=256)
     ap.add_argument("--probe-updates", type=int, default=0, help="0 = whole grid per step")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-probes", type=int, default=512, help="C4 CPU-baseline frame: a window of this many probes")
+    ap.add_argument("--cpu-frames", type=int, default=5, help="timed CPU frames (median reported) after one warm-up")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores this process may use (see cpu_cores())")
+    ap.add_argument("--no-windows", action="store_true", help="skip the reference-window (K = 4096 / 2048) and C2 lines")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ao-bake", action="store_true", help="skip the config C1 AO bake line (GPU + CPU oracle)")
     ap.add_argument("--ao-size", type=int, default=1024)
@@ -58,7 +70,9 @@ def parse():
     ap.add_argument("--no-compose", action="store_true", help="skip the DDGI consumer (lighting compose) line")
     ap.add_argument("--compose-size", default="1920x1080")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "latest_pmc.json"),
-                    help="PMC traffic summary written by tools/profile_pmc.py (optional)")
+                    help="PMC traffic summary (tools/pmc_summary.py --latest); used only if its library hash matches")
+    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "latest_sq.json"),
+                    help="SQ counter summary (tools/sq_summary.py --json); used only if its library hash matches")
     return ap.parse_args()
 
 
@@ -156,31 +170,30 @@ def main():
     total_rays = args.steps * K * R
     total_probes = args.steps * K
     mrays = total_rays / dt / 1e6
+    lib_sha = library_sha16()
 
     # roofline of the dominant kernel (per launch, this rank's share)
     avg = [sum(k[i] for k in ktimes) / len(ktimes) for i in range(5)]
-    rays_rank = cnt.rays
-    kernel_bytes = {
-        "k_trace": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays_rank,
-        "k_shade": HIT_RECORD_BYTES * rays_rank + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays_rank - cnt.hits)
-                   + SURFEL_BYTES * rays_rank,
-        "k_trace_shadow": NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests + SHADOW_RAY_BYTES * cnt.shadow_rays,
-        "k_probe_update": cnt.probes * (R * SURFEL_BYTES + 2 * (64 * 8 + 256 * 4) + (36 * 8 + 68 * 4) + 32),
-    }
-    kernel_ms = {"k_trace": avg[1], "k_shade": avg[2], "k_trace_shadow": avg[4], "k_probe_update": avg[3]}
+    kernel_bytes = algorithmic_bytes(cnt, R)
+    kernel_ms = {"k_trace": avg[1], "k_shade": avg[2], "k_shadow": avg[4], "k_probe_update": avg[3]}
     dom = max(kernel_ms, key=kernel_ms.get)
     achieved = kernel_bytes[dom] / (kernel_ms[dom] * 1e-3) / 1e9
-    traffic = None
-    pmc_note = None
-    if os.path.exists(args.pmc):
-        try:
-            with open(args.pmc) as fh:
-                pm = json.load(fh)
-            if pm.get("config", {}).get("triangles") == args.triangles and pm.get("config", {}).get("grid") == G and dom in pm.get("kernels", {}):
-                traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
-                pmc_note = pm.get("source")
-        except Exception as e:  # noqa: BLE001
-            pmc_note = f"unreadable: {e}"
+    roof = {
+        # the roofline the kernel is priced against is HBM (no dense contraction: no
+        # MFMA); what limits it is instruction issue and dependent-fetch latency (SQ
+        # counters below): 83 % of its algorithmic bytes are L2/MALL hits
+        "bound": "latency",
+        "roofline": "hbm",
+        "kernel": dom,
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "algorithmic_bytes_per_launch": int(kernel_bytes[dom]),
+        "avg_launch_ms": round(kernel_ms[dom], 4),
+    }
+    roof.update(measured_traffic(args.pmc, dom, lib_sha, args, G, kernel_ms[dom]))
+    roof.update(sq_limiter(args.sq, dom, lib_sha))
 
     result = {
         "metric": "Mrays/s + probes-updated/s, DDGI 32^3 grid x 256 rays, at 1/2/4/8 MI355X",
@@ -207,32 +220,17 @@ def main():
             "bvh_max_depth": int(bvh.max_depth),
             "bvh_build_ms": round(bvh.build_ms, 1),
             "setup_s": round(setup_s, 2),
+            "lib_sha16": lib_sha,
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_source": pmc_note,
-            "algorithmic_bytes_per_launch": int(kernel_bytes[dom]),
-            "avg_launch_ms": round(kernel_ms[dom], 4),
-        },
+        "roofline": roof,
         "kernels_ms": {k: round(v, 4) for k, v in kernel_ms.items()},
         "update_ms": round(avg[0], 4),
-        "per_ray": {
-            "primary_nodes": round(cnt.primary_node_visits / max(1, rays_rank), 2),
-            "primary_tris": round(cnt.primary_tri_tests / max(1, rays_rank), 2),
-            "primary_lane_util": round((cnt.primary_node_visits + cnt.primary_tri_tests) / max(1, 64 * cnt.primary_wave_steps), 3),
-            "hit_frac": round(cnt.hits / max(1, rays_rank), 4),
-            "front_hit_frac": round(cnt.front_hits / max(1, rays_rank), 4),
-            "shadow_rays": round(cnt.shadow_rays / max(1, rays_rank), 4),
-            "shadow_nodes": round(cnt.shadow_node_visits / max(1, rays_rank), 2),
-            "shadow_tris": round(cnt.shadow_tri_tests / max(1, rays_rank), 2),
-        },
+        "per_ray": per_ray(cnt),
     }
+
+    if rank == 0 and world == 1 and not args.no_windows:
+        result["reference_windows"] = reference_windows(node, ctx, torch, device, sptr, frame)
+        result["c2"] = c2_line(args, torch, device)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, grid, R, args, exposure)
@@ -251,50 +249,252 @@ def main():
         dist.destroy_process_group()
 
 
+def library_sha16() -> str:
+    """sha256 (16 hex) of the HIP library this process runs: ties PMC/SQ summaries to a build."""
+    from arkoserenderer_amd import abi
+
+    path = abi.library_path()
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for chunk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def algorithmic_bytes(cnt, R):
+    """Algorithmic bytes per launch (SURVEY §8d model with this build's layouts)."""
+    rays = cnt.rays
+    return {
+        "k_trace": NODE_BYTES * cnt.primary_node_visits + TRI_BYTES * cnt.primary_tri_tests + HIT_RECORD_BYTES * rays,
+        "k_shade": HIT_RECORD_BYTES * rays + SHADE_HIT_BYTES * cnt.front_hits + MISS_BYTES * (rays - cnt.hits) + SURFEL_BYTES * rays,
+        "k_shadow": NODE_BYTES * cnt.shadow_node_visits + TRI_BYTES * cnt.shadow_tri_tests + 2 * SHADOW_RAY_BYTES * cnt.shadow_rays,
+        "k_probe_update": cnt.probes * (R * SURFEL_BYTES + 2 * (64 * 8 + 256 * 4) + (36 * 8 + 68 * 4) + 32),
+    }
+
+
+def per_ray(cnt):
+    rays = max(1, cnt.rays)
+    return {
+        "primary_nodes": round(cnt.primary_node_visits / rays, 2),
+        "primary_tris": round(cnt.primary_tri_tests / rays, 2),
+        "primary_lane_util": round((cnt.primary_node_visits + cnt.primary_tri_tests) / max(1, 64 * cnt.primary_wave_steps), 3),
+        "hit_frac": round(cnt.hits / rays, 4),
+        "front_hit_frac": round(cnt.front_hits / rays, 4),
+        "shadow_rays": round(cnt.shadow_rays / rays, 4),
+        "shadow_nodes": round(cnt.shadow_node_visits / rays, 2),
+        "shadow_tris": round(cnt.shadow_tri_tests / rays, 2),
+    }
+
+
+# rocprofv3 kernel names -> the bench's kernel keys
+PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow"], "k_probe_update": ["k_probe_update"]}
+
+
+def measured_traffic(path, dom, lib_sha, args, G, launch_ms):
+    """HBM bytes per launch from the PMC summary of THIS library build
+    (tools/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction of
+    MI355X_MICROARCH.md), on the same workload; null otherwise."""
+    out = {"traffic": None, "traffic_frac": None, "traffic_source": None}
+    if not os.path.exists(path):
+        out["traffic_source"] = "no PMC summary"
+        return out
+    try:
+        with open(path) as fh:
+            pm = json.load(fh)
+    except (OSError, ValueError) as e:
+        out["traffic_source"] = f"unreadable PMC summary: {e}"
+        return out
+    cfg = pm.get("config", {})
+    if cfg.get("lib_sha16") != lib_sha:
+        out["traffic_source"] = f"PMC summary {pm.get('tag')} is of another build ({cfg.get('lib_sha16')}): not used"
+        return out
+    if cfg.get("triangles") != args.triangles or cfg.get("grid") != G:
+        out["traffic_source"] = f"PMC summary {pm.get('tag')} is of another workload: not used"
+        return out
+    ks = [pm["kernels"].get(k) for k in PMC_KERNELS[dom]]
+    if any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
+        out["traffic_source"] = f"PMC summary {pm.get('tag')} lacks {dom}"
+        return out
+    traffic = sum(k["hbm_bytes_per_launch"] for k in ks)
+    out["traffic"] = int(traffic)
+    out["traffic_frac"] = round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    out["traffic_source"] = pm.get("source")
+    return out
+
+
+def sq_limiter(path, dom, lib_sha):
+    """SQ counter evidence for the limiter (tools/sq_summary.py --json) of this build."""
+    if not os.path.exists(path):
+        return {"limiter_evidence": None}
+    try:
+        with open(path) as fh:
+            sq = json.load(fh)
+    except (OSError, ValueError):
+        return {"limiter_evidence": None}
+    if sq.get("lib_sha16") != lib_sha:
+        return {"limiter_evidence": f"SQ summary {sq.get('tag')} is of another build: not used"}
+    k = sq.get("kernels", {}).get(PMC_KERNELS[dom][0] if dom != "k_shadow" else "k_trace_shadow")
+    if k is None:
+        return {"limiter_evidence": None}
+    return {"limiter_evidence": {key: k[key] for key in ("valu_active_per_wave", "wait_inst_any_per_wave", "wait_any_per_wave",
+                                                          "valu_insts_per_launch", "l2_hit") if key in k}
+            | {"source": sq.get("source")}}
+
+
+def reference_windows(node, ctx, torch, device, sptr, frame0):
+    """The reference node's own rolling windows on the same C4 context: K = 4096
+    (MaxNumProbeUpdates, DDGINode.h:23) and K = 2048 (m_probeUpdatesPerFrame default,
+    DDGINode.h:31), 256 rays, a window advancing each frame as the node's does; two
+    warm-up frames, then `reps` timed frames (wall clock) and the per-kernel HIP-event
+    times of 3 more."""
+    from arkoserenderer_amd import ddgi as D
+
+    out = {}
+    full = node.config.probe_updates_per_frame
+    frame = frame0
+    R = node.config.rays_per_probe
+    for K in (4096, 2048):
+        node.config.probe_updates_per_frame = K
+        for _ in range(2):
+            node.execute(D.AppState(frame), sptr)
+            frame += 1
+        torch.cuda.synchronize(device)
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            node.execute(D.AppState(frame), sptr)
+            frame += 1
+        torch.cuda.synchronize(device)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        ctx.set_timing(True)
+        kt = []
+        for _ in range(3):
+            node.execute(D.AppState(frame), sptr)
+            frame += 1
+            kt.append(ctx.last_timings())
+        ctx.set_timing(False)
+        torch.cuda.synchronize(device)
+        a = [sum(k[i] for k in kt) / len(kt) for i in range(5)]
+        out[f"K{K}"] = {"mrays_per_s": round(K * R / ms / 1e3, 1), "probes_updated_per_s": round(K / ms * 1e3, 1), "ms_per_frame": round(ms, 4),
+                        "kernels_ms": {"k_trace": round(a[1], 4), "k_shadow": round(a[4], 4), "k_shade": round(a[2], 4),
+                                       "k_probe_update": round(a[3], 4)}}
+    node.config.probe_updates_per_frame = full
+    return out
+
+
+def c2_line(args, torch, device):
+    """Config C2: Cornell box, 8^3 probes x 64 rays, all 512 probes per
+    frame, the level's exposure (preExposure 2.2e-4, env x 3000), offsets off; GPU
+    wall clock over 50 frames after 5 warm-up frames."""
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False, max_rays_per_probe=64, max_probe_updates=512)
+    node = D.DDGINode(cfg)
+    node.construct(sc, grid, ex["z_far"], device=device.index or 0, light_pre_exposure=ex["light_pre_exposure"],
+                   environment_brightness=ex["environment_brightness"])
+    sptr = torch.cuda.current_stream(device).cuda_stream
+    for f in range(5):
+        node.execute(D.AppState(f), sptr)
+    torch.cuda.synchronize(device)
+    reps = 50
+    t0 = time.perf_counter()
+    for f in range(reps):
+        node.execute(D.AppState(5 + f), sptr)
+    torch.cuda.synchronize(device)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    node.ctx.close()
+    return {"workload": "C2: Cornell box (100 triangles), 8x8x8 probes x 64 rays, all probes per frame",
+            "gpu_ms_per_frame": round(ms, 4), "gpu_mrays_per_s": round(512 * 64 / ms / 1e3, 1),
+            "note": "32,768 rays per frame: launch-bound on the GPU (five launches)"}
+
+
+def cpu_cores():
+    """Host cores for the CPU baseline: the CPUs this process may run on
+    (os.sched_getaffinity), capped at the GPU box's per-GPU CPU share where the
+    box sets it (OMP_NUM_THREADS / MAX_JOBS = 16 there: nproc shows the whole
+    machine), plus what the machine reports."""
+    allowed = len(os.sched_getaffinity(0))
+    share = None
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var)
+        if v and v.isdigit() and int(v) > 0:
+            share = int(v)
+            break
+    use = min(allowed, share) if share else allowed
+    model = None
+    try:
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in txt.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc", "--all"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except (OSError, subprocess.SubprocessError, ValueError):
+        nproc = os.cpu_count()
+    return use, {"nproc_all": nproc, "affinity": allowed, "share": share, "model": model}
+
+
+def _median_frames(orc, make_params, frames, threads):
+    """One warm-up frame, then the median wall time of `frames` frames."""
+    orc.update(make_params(0), threads)
+    ts = []
+    for f in range(1, frames + 1):
+        t = time.perf_counter()
+        orc.update(make_params(f), threads)
+        ts.append(time.perf_counter() - t)
+    return statistics.median(ts), ts
+
+
 def cpu_baseline(scene, grid, R, args, exposure):
-    """The CPU oracle (C++ restatement of the reference shaders, `port`) on a
-    bounded sample of the same workload: the first probes of the window of the
-    same scene/grid/R, all stages of the update, `threads` host threads."""
+    """The CPU oracle (the C++ restatement of the reference shaders, `port`) on the
+    host cores (cpu_cores()): config C4 on a window of `cpu_probes` probes of the
+    same scene / grid / R (a bounded sample: one warm-up frame + the median of
+    `cpu_frames` frames, all stages of the update), and config C2 whole (Cornell,
+    8^3 x 64, the same protocol)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     from arkoserenderer_amd import ddgi as D
-    from parity import make_desc
+    from arkoserenderer_amd import scene as S
 
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    kmax = 4096
-    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=kmax, max_rays_per_probe=R, max_probe_updates=kmax,
-                       compute_probe_offsets=True)
-    orc = O.Oracle(make_desc(grid, 10000.0, cfg))
+    threads, host = cpu_cores()
+    threads = args.cpu_threads or threads
+    k = args.cpu_probes
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=k, max_rays_per_probe=R, max_probe_updates=k, compute_probe_offsets=True)
+    orc = O.Oracle(D.desc_for(grid, 10000.0, cfg))
     t = time.time()
     orc.set_scene(scene, threads)
     build_s = time.time() - t
-    probes = 16
-    spent, rays, done_probes = 0.0, 0, 0
-    first = 0
-    frame = 0
-    while spent < args.cpu_seconds:
-        cfg.probe_updates_per_frame = probes
-        p = D.frame_params(cfg, grid, D.AppState(frame), first, **exposure)
-        t = time.perf_counter()
-        orc.update(p, threads)
-        el = time.perf_counter() - t
-        spent += el
-        rays += probes * R
-        done_probes += probes
-        first += probes
-        frame += 1
-        # grow the chunk towards ~1/4 of the budget
-        rate = probes / max(el, 1e-6)
-        probes = int(min(kmax, max(16, rate * args.cpu_seconds / 4)))
+    N = grid.probe_count()
+    med, ts = _median_frames(orc, lambda f: D.frame_params(cfg, grid, D.AppState(f), (f * k) % N, **exposure), args.cpu_frames, threads)
     orc.close()
-    return {
-        "value": round(rays / spent / 1e6, 4),
+    res = {
+        "value": round(k * R / med / 1e6, 4),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{done_probes} probes x {R} rays of the same C4 workload (probes 0..{done_probes - 1}), full update incl. shading/indirect/blend, {spent:.1f} s; oracle BVH build {build_s:.1f} s excluded",
-        "probes_updated_per_s": round(done_probes / spent, 2),
+        "sample": (f"C4: windows of {k} probes x {R} rays of the same workload (rolling, K = {k}), full update incl. shading/indirect/blend; "
+                   f"1 warm-up + median of {len(ts)} frames ({', '.join(f'{x:.2f}' for x in ts)} s); oracle BVH build {build_s:.1f} s excluded"),
+        "probes_updated_per_s": round(k / med, 2),
+        "host": host,
     }
+    sc, ex = S.cornell_box()
+    g2 = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    c2cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False, max_rays_per_probe=64, max_probe_updates=512)
+    orc = O.Oracle(D.desc_for(g2, ex["z_far"], c2cfg))
+    orc.set_scene(sc, threads)
+    kw = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    med2, ts2 = _median_frames(orc, lambda f: D.frame_params(c2cfg, g2, D.AppState(f), 0, **kw), args.cpu_frames, threads)
+    orc.close()
+    res["c2"] = {"value": round(512 * 64 / med2 / 1e6, 4), "unit": "Mrays/s", "cores": threads,
+                 "sample": f"C2: Cornell 8^3 x 64, all 512 probes per frame; 1 warm-up + median of {len(ts2)} frames",
+                 "ms_per_frame": round(med2 * 1e3, 3)}
+    return res
 
 
 def rt_reflections_line(args, torch, ctx):
@@ -420,7 +620,7 @@ def ao_bake_c1(args, torch, device):
            "gpu_mrays_s": round(covered * n_s / (gpu_ms * 1e-3) / 1e6, 2), "gpu_ms": round(gpu_ms, 3)}
     if args.no_cpu_baseline:
         return res
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads or cpu_cores()[0]
     orc = O.Oracle(make_desc(grid, 100.0, cfg))
     orc.set_scene(scene, threads)
     row0, rows, spent, rays, exact = 0, 4, 0.0, 0, True

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    """ark::dev::k_trace_primary<false, 6>(...) -> k_trace_primary; <true, ...> -> k_trace_primary_counting."""
+    """ark::dev::k_trace<false, 6>(...) -> k_trace; <true, ...> -> k_trace_counting."""
     m = re.search(r"\b(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
     if not m:
         return name
@@ -66,7 +66,7 @@ def main():
                 try:
                     j = json.loads(line)
                     cfg = {"triangles": j["config"]["triangles"], "grid": j["config"]["grid"],
-                           "rays_per_probe": j["config"]["rays_per_probe"], "bench": j}
+                           "rays_per_probe": j["config"]["rays_per_probe"], "lib_sha16": j["config"].get("lib_sha16"), "bench": j}
                 except Exception:
                     pass
     out = {"tag": tag, "source": f"rocprofv3 --kernel-trace --stats + --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), profiles/{tag}_*",

@@ -2,17 +2,34 @@
 summed over its dispatches and the derived ratios (per-wave fractions of
 SQ_WAVE_CYCLES, VALU issue per SIMD-quad-cycle, L2 hit rate).
 
-    python tools/sq_summary.py gpurun_out/<tag> [> profiles/<tag>_sq.txt]
+    python tools/sq_summary.py gpurun_out/<tag> [<tag> --json [--latest]] [> profiles/<tag>_sq.txt]
+
+--json writes profiles/<tag>_sq.json (per kernel ratios + the library hash of the
+profiled bench run); --latest also copies it to profiles/latest_sq.json, which
+bench.py reads when the hash matches its own library.
 """
 import collections
 import csv
 import glob
+import json
+import os
+import re
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
     name = name.split("(")[0].replace("void ", "").replace("ark::dev::", "")
     return name
+
+
+def base_name(name):
+    """k_trace<false, 6> -> k_trace (timed variants only; counting ones are skipped)."""
+    m = re.match(r"(k_[a-z0-9_]+)(<([a-z]+))?", name)
+    if not m or m.group(3) == "true":
+        return None
+    return m.group(1)
 
 
 def main():
@@ -36,6 +53,41 @@ def main():
         print("   insts: valu %.3g  salu %.3g  vmem_rd %.3g  lds %.3g   L2 hit %.3f  TCP accesses %.3g" % (
             v.get("SQ_INSTS_VALU", 0), v.get("SQ_INSTS_SALU", 0), v.get("SQ_INSTS_VMEM_RD", 0), v.get("SQ_INSTS_LDS", 0),
             hit / (hit + miss) if hit + miss else 0.0, v.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0)))
+    if "--json" in sys.argv:
+        tag = sys.argv[2]
+        lib_sha, launches = None, {}
+        for line in open(os.path.join(d, "sq1.log")):
+            if line.startswith("{"):
+                try:
+                    lib_sha = json.loads(line)["config"].get("lib_sha16")
+                except (ValueError, KeyError):
+                    pass
+        calls = collections.Counter()
+        for r in csv.DictReader(open(glob.glob(f"{d}/sq1/run_counter_collection.csv")[0])):
+            if r["Counter_Name"] == "SQ_WAVES":
+                calls[short(r["Kernel_Name"])] += 1
+        kernels = {}
+        for k, v in agg.items():
+            b = base_name(k)
+            wc = v.get("SQ_WAVE_CYCLES", 0)
+            if b is None or wc <= 0:
+                continue
+            hit, miss = v.get("TCC_HIT_sum", 0.0), v.get("TCC_MISS_sum", 0.0)
+            n = max(1, calls[k])
+            kernels[b] = {"valu_active_per_wave": round(v.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3),
+                          "wait_inst_any_per_wave": round(v.get("SQ_WAIT_INST_ANY", 0) / wc, 3),
+                          "wait_any_per_wave": round(v.get("SQ_WAIT_ANY", 0) / wc, 3),
+                          "valu_insts_per_launch": round(v.get("SQ_INSTS_VALU", 0) / n),
+                          "salu_insts_per_launch": round(v.get("SQ_INSTS_SALU", 0) / n),
+                          "vmem_rd_insts_per_launch": round(v.get("SQ_INSTS_VMEM_RD", 0) / n),
+                          "l2_hit": round(hit / (hit + miss), 3) if hit + miss else None}
+        out = {"tag": tag, "lib_sha16": lib_sha, "source": f"rocprofv3 --pmc SQ_*/TCC_* passes (tools/prof_sq.sh), profiles/{tag}_sq.*",
+               "kernels": kernels}
+        with open(os.path.join(ROOT, "profiles", f"{tag}_sq.json"), "w") as fh:
+            json.dump(out, fh, indent=1)
+        if "--latest" in sys.argv:
+            with open(os.path.join(ROOT, "profiles", "latest_sq.json"), "w") as fh:
+                json.dump(out, fh, indent=1)
 
 
 if __name__ == "__main__":
