@@ -1,7 +1,7 @@
 // ark_ddgi.cpp — the C-ABI context of the MI355X DDGI path (include/ark_ddgi.h).
 //
 // Owns all device memory of one DDGI node instance on one GPU: the persistent
-// atlases/offsets (the DDGISamplingSet, DDGINode.cpp:101-105), the per-update
+// atlases/offsets (the DDGISamplingSet, DDGINode.cpp:62-66), the per-update
 // working set (slot table, hit records, surfels) and the scene (BVH + RT mesh
 // data + materials + lights). Every update is enqueued on one HIP stream.
 #include <hip/hip_runtime.h>
@@ -171,7 +171,7 @@ namespace {
 
 int clearHistory(ArkDdgiCtx* ctx)
 {
-    // DDGINode.cpp:89-94: irradiance cleared to 0, visibility to (zFar, zFar^2) in RG16F;
+    // DDGINode.cpp:50-55: irradiance cleared to 0, visibility to (zFar, zFar^2) in RG16F;
     // zFar^2 = 1e8 overflows fp16: +inf by RNE, or 65504 if saturating.
     uint16_t zf = f32_to_f16_host(ctx->desc.z_far);
     uint16_t zf2 = f32_to_f16_host(ctx->desc.z_far * ctx->desc.z_far);

@@ -79,7 +79,7 @@ struct SceneArgs {
     __device__ __forceinline__ float4 sample(int idx, float u, float v) const;
 };
 
-// Per-update arguments (push constants of DDGINode.cpp:193-292 + resources).
+// Per-update arguments (push constants of DDGINode.cpp:154-253 + resources).
 struct FrameArgs {
     int32_t X, Y, Z;
     int32_t Wi, Hi, Wv, Hv;

@@ -61,7 +61,7 @@ __device__ V3 sphericalFibonacciSample(uint32_t i, uint32_t n)
 }
 
 // Writes slot `slot` for probe `probeIdx` (ddgi/common.glsl:12-25 seed/rotation,
-// :69-77 position, raygen.rgen:196-197 offset).
+// :69-77 position, raygen.rgen:117-118 offset).
 __device__ void writeSlot(const FrameArgs& f, uint32_t slot, uint32_t probeIdx)
 {
     uint32_t tilesPerSheet = static_cast<uint32_t>(f.X * f.Z);
@@ -105,7 +105,7 @@ __device__ __forceinline__ bool inSlab(const FrameArgs& f, uint32_t probeIdx)
     return z >= f.slab_z0 && z < f.slab_z1;
 }
 
-// Unsharded: slot s <-> probe (first + s) % N (raygen.rgen:192). Sharded (Z-slab):
+// Unsharded: slot s <-> probe (first + s) % N (raygen.rgen:113). Sharded (Z-slab):
 // a single workgroup compacts the window in order, so slots are deterministic.
 __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
 {
@@ -813,7 +813,7 @@ __device__ __forceinline__ void atlasSampleUV(const FrameArgs& f, int px, int py
     *v = ay * invH;
 }
 
-// Linear filter, clamp to edge, over an fp16 atlas (DDGINode.cpp:313).
+// Linear filter, clamp to edge, over an fp16 atlas (DDGINode.cpp:274).
 template<int CH, int NOUT>
 __device__ __forceinline__ void sampleAtlas(const uint16_t* __restrict__ atlas, int W, int H, float u, float v, float* out)
 {
@@ -1096,7 +1096,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
-                // miss (raygen.rgen:149-158)
+                // miss (raygen.rgen:70-79)
                 V3 origin, dir;
                 rayOf(f, ray, &origin, &dir);
                 float u, v;
@@ -1104,7 +1104,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                 float4 c = sc.sample(sc.env_texture, u, v);
                 storeSurfel(f, ray, f.environment_multiplier * v3(c.x, c.y, c.z), f.z_far);
             } else if (hit.t < 0.0f) {
-                // backface: colour 0, depth x 0.2 (raygen.rgen:208-213); the closest-hit
+                // backface: colour 0, depth x 0.2 (raygen.rgen:129-134); the closest-hit
                 // colour and the indirect term are overwritten, so they are not evaluated.
                 storeSurfel(f, ray, splat(0.0f), hit.t * 0.2f);
             } else {
@@ -1218,7 +1218,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     color = color + ((occ >> l) & 1u ? tZ : tT);
                 }
             }
-            // raygen.rgen:204-206 + evaluateIndirectLightFromPreviousFrame (:173-185)
+            // raygen.rgen:125-127 + evaluateIndirectLightFromPreviousFrame (:94-106)
             const V3 Vi = -dir;
             const V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
             const V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
@@ -1346,7 +1346,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 }
 
 // Shadow-ray list: one thread per window ray in
-// slot order; a front hit (raygen.rgen:200-206) stores its lit-light mask
+// slot order; a front hit (raygen.rgen:121-127) stores its lit-light mask
 // (opaque.rchit:56-103, LdotN > 0 with the shading normal) in shadow_bits[ray] and
 // appends one shadow ray per lit light, owner = (ray << 4) | light. k_trace_shadow
 // then sets the occluded bits 16 + light, and k_shade finishes every surfel
@@ -1432,7 +1432,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     }
 }
 
-// Atlas clears (DDGINode.cpp:89-94) as 32-bit fills.
+// Atlas clears (DDGINode.cpp:50-55) as 32-bit fills.
 __global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t value)
 {
     for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x)

@@ -1,9 +1,11 @@
-// ddgi_headless.cpp — headless driver of the C++ DDGI node: builds a
-// RenderPipeline {DDGINode} on the HIP backend, runs F frames the way
-// MeshViewerApp::performAmbientOcclusionBake submits a pipeline
-// (MeshViewerApp.cpp:845-893), optionally rebuilds the pipeline mid-run (history
-// carried through the Registry like Registry.cpp:120-150), and dumps the
-// DDGISamplingSet contents as raw files for comparison.
+// ddgi_headless.cpp — headless driver of the C++ DDGI node: loads a scene into the
+// engine-shaped GpuScene (vertex pools, static meshes of LOD segments, instances,
+// materials, textures, uploaded light data), builds a RenderPipeline {DDGINode} on
+// the HIP backend, runs F frames the way MeshViewerApp::performAmbientOcclusionBake
+// submits a pipeline (MeshViewerApp.cpp:845-893), optionally rebuilds the pipeline
+// mid-run (history carried through the Registry like Registry.cpp:120-150), and
+// dumps the DDGISamplingSet contents as raw files for comparison. The node reads the
+// scene through GpuScene::rtScene(), the GpuScene -> ArkDdgiScene adapter.
 //
 //   ddgi_headless --scene s.arkscn | --soup N   --grid X Y Z --spacing sx sy sz --origin ox oy oz
 //                 [--rays R] [--updates K] [--frames F] [--zfar Z] [--exposure E] [--env B]
@@ -88,6 +90,67 @@ bool loadScene(const char* path, SceneFile& s)
     return true;
 }
 
+// The flat RT arrays of a scene file (or the soup generator) as the engine holds them:
+// the pools as VertexManager's, one static mesh per TLAS instance with one LOD of one
+// segment (its RT mesh's vertex allocation and material), the instance transform as a
+// column-major world matrix, the lights as the uploaded light buffers (the file holds
+// pre-exposed colours, as GpuScene uploads them).
+void populate(GpuScene& gs, const ArkDdgiScene& s)
+{
+    gs.setVertexPools(std::vector<uint32_t>(s.indices, s.indices + s.index_count),
+                      std::vector<float>(s.positions, s.positions + 3 * s.vertex_count),
+                      std::vector<ArkRTVertex>(s.vertices, s.vertices + s.vertex_count));
+    for (uint32_t m = 0; m < s.material_count; ++m) gs.registerMaterial(s.materials[m]);
+    for (uint32_t t = 0; t < s.texture_count; ++t) {
+        const ArkTexture& tx = s.textures[t];
+        const size_t texel = tx.format == ARK_TEX_RGBA32F ? 16 : 4;
+        const uint8_t* p = static_cast<const uint8_t*>(tx.data);
+        gs.registerTexture(tx.width, tx.height, tx.format, tx.wrap, std::vector<uint8_t>(p, p + static_cast<size_t>(tx.width) * tx.height * texel));
+    }
+    for (uint32_t i = 0; i < s.instance_count; ++i) {
+        const ArkRTInstance& ri = s.instances[i];
+        const ArkRTTriangleMesh& rm = s.meshes[ri.rt_mesh_index];
+        StaticMeshSegment seg;
+        seg.vertexAllocation.firstVertex = rm.first_vertex;
+        seg.vertexAllocation.firstIndex = static_cast<uint32_t>(rm.first_index);
+        seg.vertexAllocation.indexCount = 3 * ri.triangle_count;
+        seg.material = rm.material_index;
+        StaticMesh mesh;
+        mesh.LODs.push_back(StaticMeshLOD { { seg } });
+        StaticMeshInstance inst;
+        inst.mesh = gs.addStaticMesh(std::move(mesh));
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) inst.worldMatrix[c * 4 + r] = r < 3 ? ri.object_to_world[r * 4 + c] : (c == 3 ? 1.0f : 0.0f);
+        gs.addStaticMeshInstance(inst);
+    }
+    std::vector<DirectionalLightData> dir;
+    if (s.has_directional_light) {
+        DirectionalLightData d {};
+        for (int k = 0; k < 3; ++k) {
+            d.color[k] = s.directional_light.color[k];
+            d.worldSpaceDirection[k] = s.directional_light.world_space_direction[k];
+        }
+        dir.push_back(d);
+    }
+    std::vector<SpotLightData> spots;
+    for (uint32_t l = 0; l < s.spot_light_count; ++l) {
+        const ArkSpotLight& a = s.spot_lights[l];
+        SpotLightData d {};
+        for (int k = 0; k < 3; ++k) {
+            d.color[k] = a.color[k];
+            d.worldSpaceDirection[k] = a.world_space_direction[k];
+            d.worldSpaceRight[k] = a.world_space_right[k];
+            d.worldSpaceUp[k] = a.world_space_up[k];
+            d.worldSpacePosition[k] = a.world_space_position[k];
+        }
+        d.outerConeHalfAngle = a.outer_cone_half_angle;
+        d.iesProfileIndex = a.ies_profile_index;
+        spots.push_back(d);
+    }
+    gs.setLightData(std::move(dir), std::move(spots));
+    gs.setEnvironmentMap(s.environment_texture);
+}
+
 bool dump(ArkDdgiCtx* ctx, int which, const std::string& path)
 {
     uint64_t bytes = 0;
@@ -149,7 +212,9 @@ int main(int argc, char** argv)
     }
 
     HipBackend backend(device);
-    GpuScene scene(backend, *rt);
+    GpuScene scene(backend);
+    populate(scene, *rt);
+    if (scene.rtScene().instance_count != rt->instance_count) ARKOSE_LOG(Fatal, "GpuScene adapter dropped instances");
     scene.scene().setProbeGrid(grid);
     scene.scene().setAmbientIlluminance(ambient);
     scene.scene().setEnvironmentBrightness(env);

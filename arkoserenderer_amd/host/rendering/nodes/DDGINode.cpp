@@ -15,7 +15,7 @@ struct DDGIProbeGridData {
 
 RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registry& reg)
 {
-    // DDGINode.cpp:78-81
+    // DDGINode.cpp:39-42
     if (!scene.scene().hasProbeGrid()) {
         ARKOSE_LOG(Error, "DDGINode is used but no probe grid is available, will no-op");
         return RenderPipelineNode::NullExecuteCallback;
@@ -32,7 +32,7 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
 
     // Atlases (RGBA16F irradiance cleared to 0, RG16F visibility cleared to (zFar, zFar^2)),
     // probe offsets (zeros) and the surfel store live in the context; reused across
-    // pipeline rebuilds like createOrReuseTexture2D (DDGINode.cpp:89-94, Registry.cpp:120-150).
+    // pipeline rebuilds like createOrReuseTexture2D (DDGINode.cpp:50-55, Registry.cpp:120-150).
     ArkDdgiDesc desc {};
     desc.struct_size = sizeof(ArkDdgiDesc);
     for (int k = 0; k < 3; ++k) {
@@ -55,7 +55,7 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
     }
     m_ctx = ctx;
     if (created.second == Registry::ReuseMode::Reused) {
-        // atlases carry over; the offsets buffer is created anew with zeros (DDGINode.cpp:96-99)
+        // atlases carry over; the offsets buffer is created anew with zeros (DDGINode.cpp:57-60)
         uint64_t bytes = 0;
         ark_ddgi_resource_size(ctx, ARK_DDGI_PROBE_OFFSETS, &bytes);
         std::vector<uint8_t> zeros(bytes, 0);
@@ -79,7 +79,7 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
                                                                 ShaderBinding::sampledTexture(visibility) });
     reg.publish("DDGISamplingSet", ddgiSamplingBindingSet);
 
-    // DDGINode.cpp:171-298
+    // DDGINode.cpp:132-259
     return [&, ctx](const AppState& appState, CommandList& cmdList, UploadBuffer&) {
         const ProbeGrid& grid = scene.scene().probeGrid();
         const uint32_t frameIdx = appState.frameIndex();

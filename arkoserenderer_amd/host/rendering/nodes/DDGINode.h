@@ -1,7 +1,7 @@
 // DDGINode.h — drop-in DDGI node on the HIP backend. Same name ("DDGI"), same
 // members and defaults as arkose/rendering/nodes/DDGINode.h:10-39, same published
 // resource ("DDGISamplingSet" = {grid CB, probe offsets SB, irradiance atlas,
-// visibility atlas}, DDGINode.cpp:101-105). The GPU work is the C-ABI of
+// visibility atlas}, DDGINode.cpp:62-66). The GPU work is the C-ABI of
 // libark_ddgi (include/ark_ddgi.h) instead of a Vulkan RT pipeline.
 #pragma once
 
@@ -15,7 +15,7 @@ public:
 
     ExecuteCallback construct(GpuScene&, Registry&) override;
 
-    // Settings the reference edits through ImGui (DDGINode.cpp:56-74); exposed as setters here.
+    // Settings the reference edits through ImGui (DDGINode.cpp:17-35); exposed as setters here.
     void setRaysPerProbe(int r) { m_raysPerProbeInt = r; }
     void setProbeUpdatesPerFrame(int n) { m_probeUpdatesPerFrame = n; }
     void setHysteresis(float irradiance, float visibility) { m_hysteresisIrradiance = irradiance; m_hysteresisVisibility = visibility; }

@@ -9,25 +9,25 @@
  * Every entry point replaces a piece of the reference's Vulkan-RT DDGI node:
  *
  *   ark_ddgi_create      <- DDGINode::construct resource creation
- *                           (arkose/rendering/nodes/DDGINode.cpp:76-169): grid CB,
- *                           atlases + clear values (:89-94), offsets buffer (:96-99),
- *                           surfel image 4096x512 (:107).
+ *                           (arkose/rendering/nodes/DDGINode.cpp:37-130): grid CB,
+ *                           atlases + clear values (:50-55), offsets buffer (:57-60),
+ *                           surfel image 4096x512 (:68).
  *   ark_ddgi_set_scene   <- the scene contract DDGINode binds at construct
- *                           (DDGINode.cpp:110-142): TLAS (GpuScene.cpp:872-1010),
+ *                           (DDGINode.cpp:71-103): TLAS (GpuScene.cpp:872-1010),
  *                           SceneRTMeshDataSet (rayTracing.glsl:9-18), material set
  *                           (material.glsl:9-14), SceneLightSet (lighting.glsl:8-17),
  *                           environment map (GpuScene.cpp:1041-1048). The BVH that the
  *                           Vulkan driver builds is built here instead.
- *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:171-298):
+ *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:132-259):
  *                           traceRays -> irradiance update -> visibility update ->
  *                           border copies -> probe offsets.
  *   ark_ddgi_read, ark_ddgi_write <- the published DDGISamplingSet contents
- *                           (DDGINode.cpp:101-105) and the Registry texture reuse that
+ *                           (DDGINode.cpp:62-66) and the Registry texture reuse that
  *                           carries DDGI history across rebuilds (Registry.cpp:120-150).
  *
  * Status convention: 0 = OK, negative = error (ARK_DDGI_E_*); the message of the
  * last error is available from ark_ddgi_last_error(ctx). This mirrors the
- * reference's ARKOSE_LOG(Error)+NullExecuteCallback handling (DDGINode.cpp:78-81):
+ * reference's ARKOSE_LOG(Error)+NullExecuteCallback handling (DDGINode.cpp:39-42):
  * the node maps a negative status to an Error log and a no-op.
  *
  * Threading: one context per GPU, used from one host thread.
@@ -92,7 +92,7 @@ enum {
 };
 
 /* How the visibility atlas clear value (zFar, zFar^2) is stored in RG16F
- * (DDGINode.cpp:92-94). zFar^2 = 1e8 overflows fp16. */
+ * (DDGINode.cpp:53-55). zFar^2 = 1e8 overflows fp16. */
 enum {
     ARK_DDGI_CLEAR_OVERFLOW_INF = 0,       /* IEEE RNE: +inf (default) */
     ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE = 1 /* saturate to 65504 */
@@ -216,15 +216,15 @@ typedef struct ArkDdgiScene {
     int32_t reserved[4];
 } ArkDdgiScene;
 
-/* Per-frame inputs (the push constants of DDGINode.cpp:193-292). */
+/* Per-frame inputs (the push constants of DDGINode.cpp:154-253). */
 typedef struct ArkDdgiFrameParams {
     uint32_t struct_size;
     uint32_t frame_index;        /* parameter1 / frameIdx */
     uint32_t first_probe_index;  /* parameter3 / firstProbeIdx (window start) */
     uint32_t probe_updates;      /* K = min(updatesPerFrame, N) */
     uint32_t rays_per_probe;     /* parameter2 / raysPerProbe (R) */
-    float hysteresis_irradiance; /* 0 on the first frame (DDGINode.cpp:215) */
-    float hysteresis_visibility; /* 0 on the first frame (DDGINode.cpp:230) */
+    float hysteresis_irradiance; /* 0 on the first frame (DDGINode.cpp:176) */
+    float hysteresis_visibility; /* 0 on the first frame (DDGINode.cpp:191) */
     float visibility_sharpness;  /* default 50 */
     float ambient_amount;        /* ambientLx * lightPreExposure */
     float environment_multiplier;/* preExposedEnvironmentBrightnessFactor */
@@ -262,9 +262,9 @@ typedef struct ArkDdgiCtx ArkDdgiCtx;
 
 int32_t ark_ddgi_abi_version(void);
 
-/* Allocates atlases (cleared as DDGINode.cpp:89-94), offsets (zeros, :96-99) and the
+/* Allocates atlases (cleared as DDGINode.cpp:50-55), offsets (zeros, :57-60) and the
  * surfel store (max_probe_updates x max_rays_per_probe, :107). Returns
- * ARK_DDGI_E_NO_PROBE_GRID for an empty grid (DDGINode.cpp:78-81). */
+ * ARK_DDGI_E_NO_PROBE_GRID for an empty grid (DDGINode.cpp:39-42). */
 int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** out_ctx);
 void ark_ddgi_destroy(ArkDdgiCtx* ctx);
 const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx);
@@ -280,11 +280,11 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
 /* ark_ddgi_update for a Z-slab rank that overlaps the atlas exchange with the next
  * frame's primary traversal: the traversal is enqueued at once, the shading work
- * (which samples the previous frame's atlases, raygen.rgen:173-185) first waits on
+ * (which samples the previous frame's atlases, raygen.rgen:94-106) first waits on
  * hipEvent_t shade_wait_event (e.g. recorded after the previous all-gather; NULL =
  * no wait), and hipEvent_t done_event (NULL = none) is recorded after the probe
  * update so the caller's exchange can start from it. Same work and results as
- * ark_ddgi_update (DDGINode.cpp:171-298). */
+ * ark_ddgi_update (DDGINode.cpp:132-259). */
 int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream, void* shade_wait_event,
                                void* done_event);
 

@@ -47,7 +47,7 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // fp16 (RNE) — the storage format of the surfel image and both atlases
-// (DDGINode.cpp:90,94,107: RGBA16F / RG16F).
+// (DDGINode.cpp:51,55,68: RGBA16F / RG16F).
 // ---------------------------------------------------------------------------
 uint16_t f32_to_f16(float f)
 {
@@ -340,7 +340,7 @@ void sampleBilinear(const Tex& t, float u, float v, float out[4])
         out[c] = lerpf(lerpf(t00[c], t10[c], fx), lerpf(t01[c], t11[c], fx), fy);
 }
 
-// Atlas fetch: linear filter, clamp to edge (DDGINode.cpp:313), fp16 texels.
+// Atlas fetch: linear filter, clamp to edge (DDGINode.cpp:274), fp16 texels.
 // `ch` = channels per texel in storage (4 for irradiance, 2 for visibility).
 void sampleAtlas(const std::vector<uint16_t>& atlas, int W, int H, int ch, float u, float v, float* out, int nout)
 {
@@ -814,7 +814,7 @@ Surface closestHit(const Oracle& o, const Ray& ray, const Hit& h, float ambientA
     Surface s {};
     const WTri& t = o.tris[h.tri];
     s.hitT = h.backface ? -h.t : h.t;
-    if (!shade) return s; // backface: raygen overwrites the colour with 0 (raygen.rgen:208-213)
+    if (!shade) return s; // backface: raygen overwrites the colour with 0 (raygen.rgen:129-134)
     Attribs a = fetchAttribs(o, t);
     const ArkShaderMaterial& mat = *a.mat;
     const ArkRTInstance& inst = o.instances[t.inst];
@@ -961,7 +961,7 @@ V3 sampleDynamicDiffuseGlobalIllumination(const Oracle& o, V3 P, V3 N, V3 Vw)
     return irradiance;
 }
 
-// raygen.rgen:173-185
+// raygen.rgen:94-106
 V3 evaluateIndirectLightFromPreviousFrame(const Oracle& o, V3 P, V3 V, V3 N, V3 baseColor, float metallic)
 {
     V3 H = N;
@@ -971,7 +971,7 @@ V3 evaluateIndirectLightFromPreviousFrame(const Oracle& o, V3 P, V3 V, V3 N, V3 
     return splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
 }
 
-// raygen.rgen:114-171 (tracePrimaryRay) + :187-218 (main) for one (probe, sample).
+// raygen.rgen:35-92 (tracePrimaryRay) + :108-139 (main) for one (probe, sample).
 void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const ArkDdgiFrameParams& p, float out[4], Stats& st)
 {
     const float zFar = o.desc.z_far;
@@ -979,7 +979,7 @@ void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const 
     int numHits = 0;
     V3 color = splat(0.0f);
     Ray ray { origin, dir, tmin, tmax };
-    // Opaque pass: RayFlags_Opaque, cullMask RT_HIT_MASK_OPAQUE (raygen.rgen:122-134)
+    // Opaque pass: RayFlags_Opaque, cullMask RT_HIT_MASK_OPAQUE (raygen.rgen:43-55)
     Hit hit;
     traverseClosest(o, o.bvhOpaque, ray, hit, false, st);
     Hit accepted;
@@ -989,7 +989,7 @@ void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const 
         numHits += 1;
     }
     // Masked pass: RayFlags_NoOpaque, cullMask RT_HIT_MASK_MASKED, tmax = previous hit T
-    // (raygen.rgen:136-147). A negative tmax (backface) leaves [tmin,tmax] empty: no hit.
+    // (raygen.rgen:57-68). A negative tmax (backface) leaves [tmin,tmax] empty: no hit.
     if (tmax >= tmin) {
         Ray r2 { origin, dir, tmin, tmax };
         Hit mh;
@@ -1001,7 +1001,7 @@ void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const 
         }
     }
     float dist;
-    if (numHits == 0) { // raygen.rgen:149-158
+    if (numHits == 0) { // raygen.rgen:70-79
         dist = zFar;
         float u, v;
         sphericalUvFromDirection(dir, &u, &v);
@@ -1018,7 +1018,7 @@ void traceProbeRay(const Oracle& o, uint32_t probeIdx, V3 origin, V3 dir, const 
             V3 indirect = evaluateIndirectLightFromPreviousFrame(o, hitPos, -dir, s.normal, s.baseColor, s.metallic);
             color = color + s.baseColor * indirect;
         } else {
-            color = splat(0.0f); // raygen.rgen:208-213
+            color = splat(0.0f); // raygen.rgen:129-134
             dist = dist * 0.2f;
         }
     }
@@ -1051,7 +1051,7 @@ void parallelFor(int n, int threads, F&& fn)
 
 void resetHistory(Oracle& o)
 {
-    // DDGINode.cpp:89-94 clear values; DDGINode.cpp:96-97 zero offsets
+    // DDGINode.cpp:50-55 clear values; DDGINode.cpp:57-58 zero offsets
     std::fill(o.irr.begin(), o.irr.end(), 0);
     uint16_t zf = f32_to_f16(o.desc.z_far);
     float zf2 = o.desc.z_far * o.desc.z_far;
@@ -1225,7 +1225,7 @@ void* oracle_create(const ArkDdgiDesc* desc)
     if (o->g.X <= 0 || o->g.Y <= 0 || o->g.Z <= 0) { delete o; return nullptr; }
     o->g.spacing = v3(desc->probe_spacing[0], desc->probe_spacing[1], desc->probe_spacing[2]);
     o->g.origin = v3(desc->offset_to_first[0], desc->offset_to_first[1], desc->offset_to_first[2]);
-    // DDGINode.cpp:301-320
+    // DDGINode.cpp:262-281
     const int si = ARK_DDGI_IRRADIANCE_RES + 2 * ARK_DDGI_ATLAS_PADDING;
     const int sv = ARK_DDGI_VISIBILITY_RES + 2 * ARK_DDGI_ATLAS_PADDING;
     o->Wi = o->g.X * si * o->g.Y;
@@ -1300,7 +1300,7 @@ int oracle_set_scene(void* ctx, const ArkDdgiScene* s, int threads)
     return 0;
 }
 
-// One DDGI update: DDGINode.cpp:171-298. `threads` host threads, parallel over probes.
+// One DDGI update: DDGINode.cpp:132-259. `threads` host threads, parallel over probes.
 int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
 {
     Oracle& o = *static_cast<Oracle*>(ctx);
@@ -1330,7 +1330,7 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
     });
 
     // 2+3. irradiance & visibility update (probeUpdateIrradiance.comp / probeUpdateVisibility.comp)
-    const float gridMaxSpacing = fmaxf_(g.spacing.x, fmaxf_(g.spacing.y, g.spacing.z)); // DDGINode.cpp:187
+    const float gridMaxSpacing = fmaxf_(g.spacing.x, fmaxf_(g.spacing.y, g.spacing.z)); // DDGINode.cpp:148
     parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
         uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
         std::vector<V3> dirs(R);
@@ -1431,7 +1431,7 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
     // 6. probe offsets (probeUpdateOffset.comp:27-96), full barrier semantics
     if (p->update_offsets) {
         const float minAxialSpacing = fminf_(g.spacing.x, fminf_(g.spacing.y, g.spacing.z));
-        const float maxOffset = minAxialSpacing / 2.0f; // DDGINode.cpp:287-289
+        const float maxOffset = minAxialSpacing / 2.0f; // DDGINode.cpp:248-250
         parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
             uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
             const uint16_t* sf = &o.surfels[static_cast<size_t>(slot) * o.Rmax * 4];

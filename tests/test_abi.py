@@ -52,7 +52,7 @@ def test_invalid_arguments_fail_cleanly():
     h = C.c_void_p()
     assert lib.ark_ddgi_create(None, C.byref(h)) == -1
     d = abi.ArkDdgiDesc()
-    d.struct_size = C.sizeof(d)  # empty grid -> no probe grid (DDGINode.cpp:78-81)
+    d.struct_size = C.sizeof(d)  # empty grid -> no probe grid (DDGINode.cpp:39-42)
     assert lib.ark_ddgi_create(C.byref(d), C.byref(h)) == -2
     d.struct_size = 3
     assert lib.ark_ddgi_create(C.byref(d), C.byref(h)) == -1

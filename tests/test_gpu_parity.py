@@ -37,7 +37,7 @@ def test_cornell_c2_strict():
 
 
 def test_cornell_window_and_offsets():
-    """Rolling window K < N (DDGINode.cpp:177-179,297) with probe offsets on."""
+    """Rolling window K < N (DDGINode.cpp:138-140,258) with probe offsets on."""
     sc, ex = S.cornell_box()
     grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
     cfg = D.DDGIConfig(rays_per_probe=96, probe_updates_per_frame=200, compute_probe_offsets=True,

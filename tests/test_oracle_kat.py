@@ -209,7 +209,7 @@ def test_inside_emissive_cube_front_faces():
 
 def test_inside_outward_cube_all_backfaces():
     """Faces CCW seen from outside: from the centre every hit is a backface ->
-    radiance 0 and depth * 0.2 (raygen.rgen:208-213), stored negative."""
+    radiance 0 and depth * 0.2 (raygen.rgen:129-134), stored negative."""
     sc = _cube_scene(inward=False, emissive=1.0)
     grid = D.ProbeGrid((1, 1, 1), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=1, max_rays_per_probe=64, max_probe_updates=1, compute_probe_offsets=True)
