@@ -534,6 +534,93 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
     return false;
 }
 
+// Dual step (k_trace): one lane tests a pending leaf triangle AND visits the next
+// node in the same iteration. A divergent wave runs the node and the triangle code
+// every iteration anyway (28 % of the steps are triangle steps, spread over its
+// lanes), so letting each lane do both roughly turns nodes + triangles iterations
+// per ray into max(nodes, triangles) + a short tail. Leaf hits of a node visited
+// while the lane's triangle group is still pending wait in a second group (nBase,
+// nBits); the node side pauses while that one is full. The closest hit does not
+// depend on the order (equal t: smaller (instance, primitive) wins). ANY (shadow
+// rays): the step reports a triangle hit in [tmin, h.t] instead of recording it.
+template<int BLOCK>
+__device__ __forceinline__ bool travDoneDual(const TravState& ts, uint32_t nBits, const Stack<BLOCK>& st)
+{
+    return ts.tBits == 0 && nBits == 0 && (ts.gBits & 0xffu) == 0 && st.depth == 0;
+}
+
+template<int BLOCK, bool ANY>
+__device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCache& nc, TravState& ts, uint32_t& nBase, uint32_t& nBits, Stack<BLOCK>& st,
+                                             V3 o, V3 d, V3 idir, uint32_t oct, float tmin, RayHit& h, int pass, uint32_t& cNodes, uint32_t& cTris)
+{
+    bool anyHit = false;
+    const bool doTri = ts.tBits != 0;
+    const bool doNode = nBits == 0 && ((ts.gBits & 0xffu) != 0 || st.depth != 0);
+    uint4 a = make_uint4(0, 0, 0, 0), b = a, c = a;
+    uint32_t ti = 0;
+    if (doTri) {
+        ti = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
+        ts.tBits &= ts.tBits - 1u;
+        const uint4* src = reinterpret_cast<const uint4*>(sc.tris + ti);
+        a = src[0];
+        b = src[1];
+        c = src[2];
+    }
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0, w2 = w0, w3 = w0, w4 = w0;
+    if (doNode) {
+        if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
+        const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
+        if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
+        const uint32_t rel = child - nc.base;
+        const uint4* src = rel < nc.count ? nc.lds + rel * 5u : reinterpret_cast<const uint4*>(sc.nodes + child);
+        w0 = src[0];
+        w1 = src[1];
+        w2 = src[2];
+        w3 = src[3];
+        w4 = src[4];
+    }
+    if (doTri) {
+        cTris++;
+        const GpuTriangle tr = triFromWords(a, b, c);
+        bool bf;
+        float tt, uu, vv;
+        if (intersectTri(o, d, tmin, h.t, tr, &tt, &uu, &vv, &bf)) {
+            const uint32_t inst = c.y, prim = c.z;
+            if (ANY) anyHit = true;
+            else if (!(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
+                !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
+                h.t = tt;
+                h.u = uu;
+                h.v = vv;
+                h.tri = ti;
+                h.inst = inst;
+                h.prim = prim;
+                h.backface = bf != (c.w != 0u); // GpuTriangle t2.w: instance flips facing
+            }
+        }
+    }
+    if (doNode) {
+        cNodes++;
+        uint32_t lb, lbits;
+        visitNode8(w0, w1, w2, w3, w4, o, idir, oct, tmin, h.t, ts.gBase, ts.gBits, lb, lbits);
+        if (lbits) {
+            if (ts.tBits == 0) {
+                ts.tBase = lb;
+                ts.tBits = lbits;
+            } else {
+                nBase = lb;
+                nBits = lbits;
+            }
+        }
+    }
+    if (ts.tBits == 0 && nBits != 0) {
+        ts.tBase = nBase;
+        ts.tBits = nBits;
+        nBits = 0;
+    }
+    return anyHit;
+}
+
 // opaque.rchit:118-131: world-space shading normal of a front hit. The trace
 // kernel's shadow phase and the shading kernel both evaluate exactly this
 // expression, so they agree on N (and on which lights need a shadow ray).
@@ -649,7 +736,7 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 // ray finished are refilled at the top of the next iteration from a wave-private
 // pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays), so
 // the SIMD stays full until the global ray counter runs out.
-template<bool COUNT, int WPE>
+template<bool COUNT, int WPE, bool DUAL>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
@@ -670,10 +757,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     uint32_t ray = 0;
     int pass = 0;
     TravState ts { 0u, 0u, 0u, 0u };
+    uint32_t nBase = 0, nBits = 0; // DUAL: the next triangle group
     uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
+    auto done = [&]() { return DUAL ? travDoneDual(ts, nBits, st) : travDone(ts, st); };
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
@@ -708,6 +797,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                     pass = 0;
                     st.depth = 0;
+                    nBits = 0;
                     ts = TravState { static_cast<uint32_t>(sc.root_opaque), sc.root_opaque >= 0 ? rootGroupBits() : 0u, 0u, 0u };
                 }
             }
@@ -725,8 +815,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (__ballot(active) == 0) break;
         if (COUNT) cIter++;
-        // ---- one step: a pending leaf triangle, or the next node ------------------
-        if (active && !travDone(ts, st)) {
+        // ---- one step: a pending leaf triangle and/or the next node ---------------
+        if (DUAL && active && !done()) {
+            travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
+        } else if (!DUAL && active && !done()) {
             Fetch fx;
             travFetch(sc, nc, ts, st, oct, fx);
             uint32_t inst, prim;
@@ -746,7 +838,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
         // ---- pass finished -------------------------------------------------------------
-        if (active && travDone(ts, st)) {
+        if (active && done()) {
             bool finished = true;
             if (pass == 0) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
@@ -1237,7 +1329,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
 // three hit-mask classes in turn, no alpha test. Lanes are refilled from a
 // wave-private pool like k_trace; an occluded ray sets bit 16 + light of its probe
 // ray's word.
-template<bool COUNT, int WPE>
+template<bool COUNT, int WPE, bool DUAL>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
@@ -1259,8 +1351,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     int pass = 0;
     float tmax = 0.0f;
     TravState ts { 0u, 0u, 0u, 0u };
+    uint32_t nBase = 0, nBits = 0; // DUAL: the next triangle group
     uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
+    auto done = [&]() { return DUAL ? travDoneDual(ts, nBits, st) : travDone(ts, st); };
     for (;;) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
@@ -1290,6 +1384,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     st.depth = 0;
                     pass = 0;
                     ts = TravState { 0u, 0u, 0u, 0u };
+                    nBits = 0;
                     active = true;
                     if (tmax >= tmin) {
                         if (COUNT) cShadow++;
@@ -1315,7 +1410,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         if (__ballot(active) == 0) break;
         if (active) {
             bool occluded = false;
-            if (!travDone(ts, st)) {
+            if (DUAL && !done()) {
+                RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                occluded = travStepDual<kTraceBlock, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
+            } else if (!DUAL && !done()) {
                 Fetch fx;
                 travFetch(sc, nc, ts, st, oct, fx);
                 uint32_t inst, prim;
@@ -1326,7 +1424,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             if (occluded) {
                 atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
                 active = false;
-            } else if (travDone(ts, st)) {
+            } else if (done()) {
                 ++pass;
                 while (pass < 3 && roots[pass] < 0) ++pass;
                 if (pass < 3) {
@@ -1735,11 +1833,34 @@ hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
 // Persistent traversal at 6 waves/SIMD (80 VGPRs, no spill; round 1: 3.43 vs 3.61 ms
 // at the compiler's 5 on C4, 8 spilled and took 5.4 ms); COUNT variants run at the
 // compiler's occupancy.
+// Traversal variant (tuning knob ARK_TRACE_DUAL, read once, default 1): 1 = dual step
+// (travStepDual) at 5 waves/SIMD, its extra fetch registers do not fit 6; 0 = one
+// step (a triangle or a node) per lane and iteration at 6 waves/SIMD. Measured at
+// C4: 2.57 vs 2.65 ms.
+static int traceDual()
+{
+    static const int v = [] { const char* e = std::getenv("ARK_TRACE_DUAL"); return e ? std::atoi(e) : 1; }();
+    return v;
+}
+
+// Same choice for the shadow traversal (ARK_SHADOW_DUAL, default 1; 6 waves/SIMD
+// either way; C4: 0.79 vs 0.83 ms with k_shadow_gen).
+static int shadowDual()
+{
+    static const int v = [] { const char* e = std::getenv("ARK_SHADOW_DUAL"); return e ? std::atoi(e) : 1; }();
+    return v;
+}
+
+const void* kernel_trace_ptr(bool count)
+{
+    if (traceDual()) return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1, true>) : reinterpret_cast<const void*>(&dev::k_trace<false, 5, true>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1, false>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6, false>);
+}
+
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    if (count) hipLaunchKernelGGL((dev::k_trace<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_trace<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    return hipGetLastError();
+    void* args[] = { const_cast<SceneArgs*>(&sc), const_cast<FrameArgs*>(&f) };
+    return hipLaunchKernel(kernel_trace_ptr(count), dim3(blocks), dim3(kTraceBlock), args, 0, s);
 }
 
 // Co-resident workgroups of a persistent kernel on this device (cached per kernel).
@@ -1771,9 +1892,8 @@ hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks
 
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
-    if (count) hipLaunchKernelGGL((dev::k_trace_shadow<true, 1>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    else hipLaunchKernelGGL((dev::k_trace_shadow<false, 6>), dim3(blocks), dim3(kTraceBlock), 0, s, sc, f);
-    return hipGetLastError();
+    void* args[] = { const_cast<SceneArgs*>(&sc), const_cast<FrameArgs*>(&f) };
+    return hipLaunchKernel(kernel_trace_shadow_ptr(count), dim3(blocks), dim3(kTraceBlock), args, 0, s);
 }
 
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s)
@@ -1793,10 +1913,6 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
     return hipGetLastError();
 }
 
-const void* kernel_trace_ptr(bool count)
-{
-    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6>);
-}
 const void* kernel_shade_ptr(bool count)
 {
     return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
@@ -1804,7 +1920,9 @@ const void* kernel_shade_ptr(bool count)
 
 const void* kernel_trace_shadow_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6>);
+    if (shadowDual())
+        return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, true>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6, true>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, false>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6, false>);
 }
 
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s)

@@ -56,12 +56,13 @@ __device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, i
 // antipode -t, exactly: every coordinate is a dyadic rational, the decode's fold
 // and normalize are sign-symmetric (tests/test_oracle_kat.py pins both tables).
 // So {t, t', -t, -t'} is an orbit of four texels, one of them in the quadrant
-// tx, ty < res/2; for a ray r with p = t*r (per component):
-//     dot(t, r)   = (px + py) + pz =  d1       dot(-t, r)  = -d1
-//     dot(t', r)  = (py - px) + pz =  d2       dot(-t', r) = -d2
-// each the same IEEE operations as the reference's dot on that texel (negation is
-// exact; for z = 0 texels only the sign of a zero dot can differ, whose weight is 0
-// either way). At most one of d and -d is positive, so one pow(|d|, sharpness)
+// tx, ty < res/2; for a ray r with p = t*r (per component) and the dot contracted
+// as a shader compiler does (last product fused, the oracle's dotFma):
+//     dot(t, r)   = fma(tz, rz, px + py) =  d1       dot(-t, r)  = -d1
+//     dot(t', r)  = fma(tz, rz, py - px) =  d2       dot(-t', r) = -d2
+// each the same IEEE operations as that dot on that texel (negation is exact and
+// commutes with round-to-nearest-even; for z = 0 texels only the sign of a zero dot
+// can differ, whose weight is 0 either way). Sums of weighted terms are fmas too. At most one of d and -d is positive, so one pow(|d|, sharpness)
 // serves both texels of a pair: the texel on the negative side gets weight +0,
 // which adds exactly nothing (finite distances; radiance is multiplied by the
 // same +0 as in the reference). One lane owns one orbit: 3 products, 4 sums and
@@ -161,18 +162,18 @@ __device__ __forceinline__ void visibilityOrbit(const UpdateLds& L, int p, uint3
     for (uint32_t s = 0; s < R; ++s) {
         const float4 r = ray[s];
         const float dd2 = d2[s];
-        const float px = t.x * r.x, py = t.y * r.y, pz = t.z * r.z;
-        const float d1 = (px + py) + pz;
-        const float d2v = (py - px) + pz;
+        const float px = t.x * r.x, py = t.y * r.y;
+        const float d1 = fmaf(t.z, r.z, px + py);
+        const float d2v = fmaf(t.z, r.z, py - px);
         const float w1 = visWeightAbs<MODE>(fabsf_(d1), sharp, ns);
         const float w2 = visWeightAbs<MODE>(fabsf_(d2v), sharp, ns);
         const float w0 = d1 > 0.0f ? w1 : 0.0f, w2n = d1 > 0.0f ? 0.0f : w1;
         const float w1p = d2v > 0.0f ? w2 : 0.0f, w3 = d2v > 0.0f ? 0.0f : w2;
         // texel order: t, t', -t, -t'
-        nv0[0] += w0 * r.w;  nv1[0] += w0 * dd2;  tw[0] += w0;
-        nv0[1] += w1p * r.w; nv1[1] += w1p * dd2; tw[1] += w1p;
-        nv0[2] += w2n * r.w; nv1[2] += w2n * dd2; tw[2] += w2n;
-        nv0[3] += w3 * r.w;  nv1[3] += w3 * dd2;  tw[3] += w3;
+        nv0[0] = fmaf(w0, r.w, nv0[0]);  nv1[0] = fmaf(w0, dd2, nv1[0]);  tw[0] += w0;
+        nv0[1] = fmaf(w1p, r.w, nv0[1]); nv1[1] = fmaf(w1p, dd2, nv1[1]); tw[1] += w1p;
+        nv0[2] = fmaf(w2n, r.w, nv0[2]); nv1[2] = fmaf(w2n, dd2, nv1[2]); tw[2] += w2n;
+        nv0[3] = fmaf(w3, r.w, nv0[3]);  nv1[3] = fmaf(w3, dd2, nv1[3]);  tw[3] += w3;
     }
 }
 
@@ -185,9 +186,9 @@ __device__ __forceinline__ void visibilityOrbitGeneric(const UpdateLds& L, int p
         const float4 r = ray[s];
         const V3 rd = v3(r.x, r.y, r.z);
         for (int k = 0; k < 4; ++k) {
-            const float weight = powf_(fmaxf_(0.0f, dot(dir[k], rd)), sharp);
-            nv0[k] += weight * r.w;
-            nv1[k] += weight * d2[s];
+            const float weight = powf_(fmaxf_(0.0f, fmaf(dir[k].z, rd.z, dir[k].x * rd.x + dir[k].y * rd.y)), sharp);
+            nv0[k] = fmaf(weight, r.w, nv0[k]);
+            nv1[k] = fmaf(weight, d2[s], nv1[k]);
             tw[k] += weight;
         }
     }
@@ -284,9 +285,9 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 const uint2 cw = rad[s];
                 const float4 c = make_float4(f16_to_f32(static_cast<uint16_t>(cw.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(cw.x >> 16)),
                                              f16_to_f32(static_cast<uint16_t>(cw.y & 0xffffu)), 0.0f);
-                const float px = t.x * r.x, py = t.y * r.y, pz = t.z * r.z;
-                const float d1 = (px + py) + pz;
-                const float d2 = (py - px) + pz;
+                const float px = t.x * r.x, py = t.y * r.y;
+                const float d1 = fmaf(t.z, r.z, px + py);
+                const float d2 = fmaf(t.z, r.z, py - px);
                 float w[4];
                 w[0] = fmaxf_(0.0f, d1);
                 w[1] = fmaxf_(0.0f, d2);
@@ -294,7 +295,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 w[3] = fmaxf_(0.0f, -d2);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    acc[k] = acc[k] + w[k] * v3(c.x, c.y, c.z);
+                    acc[k] = v3(fmaf(w[k], c.x, acc[k].x), fmaf(w[k], c.y, acc[k].y), fmaf(w[k], c.z, acc[k].z));
                     tw[k] += w[k];
                 }
             }

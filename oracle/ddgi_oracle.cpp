@@ -102,6 +102,10 @@ inline V3 operator*(float s, V3 a) { return { s * a.x, s * a.y, s * a.z }; }
 inline V3 operator/(V3 a, float s) { return { a.x / s, a.y / s, a.z / s }; }
 inline V3 operator/(V3 a, V3 b) { return { a.x / b.x, a.y / b.y, a.z / b.z }; }
 inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// The probe update's dot with its last product contracted, (ax*bx + ay*by) + az*bz
+// as one fma, the form a shader compiler emits for GLSL dot() (SPIR-V without
+// NoContraction); k_probe_update evaluates the same expression.
+inline float dotFma(V3 a, V3 b) { return fmaf(a.z, b.z, a.x * b.x + a.y * b.y); }
 inline V3 cross(V3 a, V3 b) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x }; }
 inline float length(V3 a) { return sqrtf_(dot(a, a)); }
 // GLSL normalize(v) = v * inversesqrt(dot(v,v)); restated as v * (1/sqrt(dot)).
@@ -1348,9 +1352,10 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                 V3 newIrr = splat(0.0f);
                 float totalWeight = 0.0f;
                 for (uint32_t s = 0; s < R; ++s) {
-                    float weight = fmaxf_(0.0f, dot(texelDirection, dirs[s]));
+                    float weight = fmaxf_(0.0f, dotFma(texelDirection, dirs[s]));
                     V3 rad = v3(f16_to_f32(sf[s * 4 + 0]), f16_to_f32(sf[s * 4 + 1]), f16_to_f32(sf[s * 4 + 2]));
-                    newIrr = newIrr + weight * rad;
+                    // newIrr += weight * rad, contracted (fma per component)
+                    newIrr = v3(fmaf(weight, rad.x, newIrr.x), fmaf(weight, rad.y, newIrr.y), fmaf(weight, rad.z, newIrr.z));
                     totalWeight += weight;
                 }
                 newIrr = newIrr / fmaxf_(totalWeight, epsilon);
@@ -1374,11 +1379,11 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                 atlasTexelCoord(g, probeIdx, tx, ty, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, &ax, &ay);
                 float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
                 for (uint32_t s = 0; s < R; ++s) {
-                    float weight = powf_(fmaxf_(0.0f, dot(texelDirection, dirs[s])), p->visibility_sharpness);
+                    float weight = powf_(fmaxf_(0.0f, dotFma(texelDirection, dirs[s])), p->visibility_sharpness);
                     float d = f16_to_f32(sf[s * 4 + 3]);
                     d = fminf_(fabsf_(d), maxDistance);
-                    nv0 += weight * d;
-                    nv1 += weight * square(d);
+                    nv0 = fmaf(weight, d, nv0);
+                    nv1 = fmaf(weight, square(d), nv1);
                     totalWeight += weight;
                 }
                 float den = fmaxf_(totalWeight, epsilon);
