@@ -387,6 +387,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         g.rt_mesh_index = static_cast<int32_t>(inst.rt_mesh_index);
         g.flip_facing = det < 0.0f ? 1 : 0;
         g.hit_mask = static_cast<int32_t>(inst.hit_mask);
+        g.material_index = m.material_index;
         const int c = (inst.hit_mask & ARK_RT_HIT_MASK_OPAQUE) ? 0 : (inst.hit_mask & ARK_RT_HIT_MASK_MASKED) ? 1 : 2;
         for (uint32_t p = 0; p < inst.triangle_count; ++p) {
             BuildTriangle t;
@@ -559,27 +560,27 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, ctx->texels, texels.data(), texels.size())) != 0) return rc;
     if ((rc = upload(ctx, ctx->spots, gspots.data(), gspots.size())) != 0) return rc;
     {
-        // per-triangle vertex normals for the shadow rays traced inside the primary
-        // traversal (hitShadingNormal); only needed when the scene has lights
-        std::vector<float> tn;
-        if (s->has_directional_light || s->spot_light_count > 0) {
-            tn.resize(allTris.size() * 12, 0.0f);
-            for (size_t t = 0; t < allTris.size(); ++t) {
-                uint32_t inst, prim;
-                std::memcpy(&inst, &allTris[t].t2[1], 4);
-                std::memcpy(&prim, &allTris[t].t2[2], 4);
-                const ArkRTTriangleMesh& mesh = s->meshes[s->instances[inst].rt_mesh_index];
-                float* o = tn.data() + t * 12;
-                for (int q = 0; q < 3; ++q) {
-                    const uint32_t idx = s->indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
-                    const float* v = reinterpret_cast<const float*>(s->vertices) + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
-                    for (int k = 0; k < 3; ++k) o[q * 3 + k] = v[2 + k];
-                }
-                std::memcpy(o + 9, &inst, 4);
+        // per-triangle shading records (GpuTriangle order, 64 B): the three vertex
+        // normals, the instance and the three UVs, copied from the vertex pool, so
+        // the shading and shadow-ray kernels reach a hit's surface in one fetch
+        // instead of instance -> mesh -> indices -> vertices
+        std::vector<float> tn(allTris.size() * 16, 0.0f);
+        for (size_t t = 0; t < allTris.size(); ++t) {
+            uint32_t inst, prim;
+            std::memcpy(&inst, &allTris[t].t2[1], 4);
+            std::memcpy(&prim, &allTris[t].t2[2], 4);
+            const ArkRTTriangleMesh& mesh = s->meshes[s->instances[inst].rt_mesh_index];
+            float* o = tn.data() + t * 16;
+            for (int q = 0; q < 3; ++q) {
+                const uint32_t idx = s->indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
+                const float* v = reinterpret_cast<const float*>(s->vertices) + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
+                for (int k = 0; k < 3; ++k) o[q * 3 + k] = v[2 + k];
+                o[10 + 2 * q] = v[0];
+                o[11 + 2 * q] = v[1];
             }
-        } else {
-            tn.assign(12, 0.0f);
+            std::memcpy(o + 9, &inst, 4);
         }
+        if (tn.empty()) tn.assign(16, 0.0f);
         if ((rc = upload(ctx, ctx->triNormals, tn.data(), tn.size())) != 0) return rc;
     }
     SceneArgs& sc = ctx->scene;

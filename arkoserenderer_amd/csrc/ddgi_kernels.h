@@ -68,7 +68,7 @@ struct SceneArgs {
     // [triangle] 3 x float4: object-space vertex normals n0, n1, n2 (9 floats) and the
     // instance index; BVH triangle order. Lets k_trace find the shading normal of a
     // front hit with two dependent loads instead of five (set when lights exist).
-    const float4* tri_normals;
+    const float4* tri_normals; // per-triangle shading records [4]: n0 n1 n2 (9), instance, uv0 uv1 uv2
 
     __device__ __forceinline__ int resolveTexture(int idx) const
     {

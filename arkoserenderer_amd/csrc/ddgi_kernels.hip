@@ -466,12 +466,12 @@ struct NodeCache {
     uint32_t count;
 };
 
-template<int BLOCK>
+template<int BLOCK, int NODES = kLdsNodes>
 __device__ __forceinline__ NodeCache loadNodeCache(const SceneArgs& sc, uint4* lds)
 {
     NodeCache nc { lds, sc.root_opaque >= 0 ? static_cast<uint32_t>(sc.root_opaque) : 0u, 0u };
     if (sc.root_opaque >= 0) {
-        nc.count = min(static_cast<uint32_t>(kLdsNodes), sc.opaque_nodes);
+        nc.count = min(static_cast<uint32_t>(NODES), sc.opaque_nodes);
         const uint4* src = reinterpret_cast<const uint4*>(sc.nodes + nc.base);
         for (uint32_t i = threadIdx.x; i < nc.count * 5u; i += BLOCK) lds[i] = src[i];
     }
@@ -626,7 +626,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
 // expression, so they agree on N (and on which lights need a shadow ray).
 __device__ __forceinline__ V3 hitShadingNormal(const SceneArgs& sc, uint32_t tri, float hu, float hv)
 {
-    const float4* tn = sc.tri_normals + 3u * static_cast<size_t>(tri);
+    const float4* tn = sc.tri_normals + 4u * static_cast<size_t>(tri);
     const float4 a = tn[0], b = tn[1], c = tn[2];
     const uint32_t inst = __float_as_uint(c.y);
     const float* M = sc.instances[inst].normal_matrix;
@@ -736,9 +736,16 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 // ray finished are refilled at the top of the next iteration from a wave-private
 // pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays), so
 // the SIMD stays full until the global ray counter runs out.
+#ifdef ARK_TAIL_PROBE
+__device__ unsigned long long g_tail[2][32768][6];
+#endif
 template<bool COUNT, int WPE, bool DUAL>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
+#ifdef ARK_TAIL_PROBE
+    const unsigned long long tStart = wall_clock64();
+    unsigned long long tEx = 0, itAll = 0, itEx = 0;
+#endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     __shared__ uint4 ldsNodes[kLdsNodes * 5];
     const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
@@ -815,6 +822,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (__ballot(active) == 0) break;
         if (COUNT) cIter++;
+#ifdef ARK_TAIL_PROBE
+        itAll++;
+        if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
+#endif
         // ---- one step: a pending leaf triangle and/or the next node ---------------
         if (DUAL && active && !done()) {
             travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
@@ -879,6 +890,15 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
     }
+#ifdef ARK_TAIL_PROBE
+    {
+        const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
+        if (lane == 0 && w < 32768) {
+            unsigned long long* r = g_tail[0][w];
+            r[0] = tStart; r[1] = tEx; r[2] = wall_clock64(); r[3] = itAll; r[4] = itEx; r[5] = 0;
+        }
+    }
+#endif
     if (COUNT) {
         atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
@@ -1220,25 +1240,19 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                 const GpuHit hit = f.hits[ray];
                 rayOf(f, ray, &origin, &dir);
                 T = hit.t;
-                const GpuTriangle tr = loadTri(sc.tris, hit.tri);
-                const uint32_t inst = __builtin_bit_cast(uint32_t, tr.t2[1]);
-                const uint32_t prim = __builtin_bit_cast(uint32_t, tr.t2[2]);
-                const GpuInstance gi = sc.instances[inst];
-                const ArkRTTriangleMesh mesh = sc.meshes[gi.rt_mesh_index];
-                const ArkShaderMaterial& mat = sc.materials[mesh.material_index];
+                // the triangle's shading record: vertex normals, instance, UVs
+                const float4* rec = sc.tri_normals + 4u * static_cast<size_t>(hit.tri);
+                const float4 ra = rec[0], rb = rec[1], rc = rec[2], rd = rec[3];
+                const GpuInstance gi = sc.instances[__float_as_uint(rc.y)];
+                const ArkShaderMaterial& mat = sc.materials[gi.material_index];
                 const float bx = 1.0f - hit.u - hit.v, by = hit.u, bz = hit.v;
-                const float* vx[3];
-                for (int q = 0; q < 3; ++q) {
-                    uint32_t idx = sc.indices[static_cast<size_t>(mesh.first_index) + 3u * prim + q];
-                    vx[q] = sc.vertices + (static_cast<size_t>(mesh.first_vertex) + idx) * 9;
-                }
                 // opaque.rchit:118-131 (front face: no flip)
-                N = normalize(v3(vx[0][2], vx[0][3], vx[0][4]) * bx + v3(vx[1][2], vx[1][3], vx[1][4]) * by + v3(vx[2][2], vx[2][3], vx[2][4]) * bz);
+                N = normalize(v3(ra.x, ra.y, ra.z) * bx + v3(ra.w, rb.x, rb.y) * by + v3(rb.z, rb.w, rc.x) * bz);
                 const float* M = gi.normal_matrix;
                 V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
                 N = normalize(Nw);
-                const float uvx = vx[0][0] * bx + vx[1][0] * by + vx[2][0] * bz;
-                const float uvy = vx[0][1] * bx + vx[1][1] * by + vx[2][1] * bz;
+                const float uvx = rc.z * bx + rd.x * by + rd.z * bz;
+                const float uvy = rc.w * bx + rd.y * by + rd.w * bz;
                 float4 c = sc.sample(mat.base_color, uvx, uvy);
                 baseColor = v3(c.x, c.y, c.z) * v3(mat.color_tint[0], mat.color_tint[1], mat.color_tint[2]);
                 c = sc.sample(mat.emissive, uvx, uvy);
@@ -1324,20 +1338,108 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     if (COUNT) atomicAdd(&f.counters[6], static_cast<unsigned long long>(cFront));
 }
 
+// ---------------------------------------------------------------------------
+// Intra-wave splitting of the traversal tail
+// ---------------------------------------------------------------------------
+// Once the ray supply has run dry, a persistent traversal wave only runs its last,
+// longest rays, one dependent node fetch per iteration, while most of its lanes
+// idle (C4: the shadow kernel spent 0.28 of 0.64 ms draining). So an idle lane of
+// an exhausted wave takes work from a lane that is still traversing: the donor
+// hands over the bottom entry of its node-group stack (the oldest deferred group,
+// usually the largest subtree left) and the helper traverses that group with a
+// copy of the donor's ray. Helpers can donate again; every helper reports to the
+// ray's root lane, which finishes the ray only when its helper count is back to
+// zero. The result does not depend on who visits which subtree: any-hit rays OR
+// their occlusion, closest-hit rays keep the nearest hit with the (instance,
+// primitive) tie rule, and box culling is conservative for any tmax that bounds
+// the closest hit.
+// Per wave LDS: a 64-entry donor table (rank -> donor lane) and, per lane, a byte
+// with its outstanding helper count (bits 0-6) and a "ray resolved" flag (bit 7).
+struct TailLds {
+    uint8_t* table;  // [kTraceBlock]
+    uint32_t* bytes; // [kTraceBlock / 4], one byte per lane
+};
+
+__device__ __forceinline__ uint32_t tailByte(const TailLds& tl, uint32_t t)
+{
+    return (__hip_atomic_load(tl.bytes + (t >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> (8u * (t & 3u))) & 0xffu;
+}
+
+__device__ __forceinline__ void tailAdd(const TailLds& tl, uint32_t t, uint32_t v)
+{
+    __hip_atomic_fetch_add(tl.bytes + (t >> 2), v << (8u * (t & 3u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__device__ __forceinline__ void tailSub(const TailLds& tl, uint32_t t, uint32_t v)
+{
+    __hip_atomic_fetch_sub(tl.bytes + (t >> 2), v << (8u * (t & 3u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__device__ __forceinline__ void tailOr(const TailLds& tl, uint32_t t, uint32_t v)
+{
+    __hip_atomic_fetch_or(tl.bytes + (t >> 2), v << (8u * (t & 3u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__device__ __forceinline__ void tailClear(const TailLds& tl, uint32_t t)
+{
+    __hip_atomic_fetch_and(tl.bytes + (t >> 2), ~(0xffu << (8u * (t & 3u))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// Removes the bottom entry (entry 0) of a non-empty stack and returns it; the top
+// entry moves into its place (visiting order only affects speed).
+template<int BLOCK>
+__device__ __forceinline__ void stackTakeBottom(Stack<BLOCK>& st, uint32_t& a, uint32_t& b)
+{
+    // entry i is in LDS slot i % kStackLds while i >= depth - kStackLds, else at spill[i]
+    if (st.depth <= kStackLds) {
+        a = st.lds[0];
+        b = st.lds[BLOCK];
+    } else {
+        a = st.spill[0];
+        b = st.spill[st.spillStride];
+    }
+    uint32_t ta, tb;
+    st.pop(ta, tb);
+    if (st.depth > 0) {
+        if (st.depth <= kStackLds) {
+            st.lds[0] = ta;
+            st.lds[BLOCK] = tb;
+        } else {
+            st.spill[0] = ta;
+            st.spill[st.spillStride] = tb;
+        }
+    }
+}
+
+__device__ __forceinline__ V3 shfl3(V3 v, uint32_t src)
+{
+    return v3(__shfl(v.x, static_cast<int>(src)), __shfl(v.y, static_cast<int>(src)), __shfl(v.z, static_cast<int>(src)));
+}
+
 // Persistent any-hit traversal of the shadow-ray list (opaque.rchit:35-54:
 // TerminateOnFirstHit | SkipClosestHit | Opaque, cullMask 0xff, tmin 0.025): the
-// three hit-mask classes in turn, no alpha test. Lanes are refilled from a
-// wave-private pool like k_trace; an occluded ray sets bit 16 + light of its probe
-// ray's word.
-template<bool COUNT, int WPE, bool DUAL>
+// three hit-mask classes in turn, no alpha test, dual steps. Lanes are refilled
+// from a wave-private pool like k_trace; an occluded ray sets bit 16 + light of its
+// probe ray's word. `pass` of a helper lane holds (root lane + 1) << 8.
+template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
+#ifdef ARK_TAIL_PROBE
+    const unsigned long long tStart = wall_clock64();
+    unsigned long long tEx = 0, itAll = 0, itEx = 0;
+#endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
-    __shared__ uint4 ldsNodes[kLdsNodes * 5];
-    const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
+    // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
+    constexpr int kNodes = kLdsNodes - 8;
+    __shared__ uint4 ldsNodes[kNodes * 5];
+    __shared__ uint8_t ldsTable[kTraceBlock];
+    __shared__ uint32_t ldsBytes[kTraceBlock / 4];
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    if (lane < 16u) ldsBytes[(wbase >> 2) + lane] = 0u; // wave-private
+    const NodeCache nc = loadNodeCache<kTraceBlock, kNodes>(sc, ldsNodes);
+    const TailLds tl { ldsTable, ldsBytes };
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
-    const uint32_t lane = threadIdx.x & 63u;
     const float tmin = 0.025f;
     const uint32_t total = *f.shadow_count;
     const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
@@ -1351,10 +1453,11 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     int pass = 0;
     float tmax = 0.0f;
     TravState ts { 0u, 0u, 0u, 0u };
-    uint32_t nBase = 0, nBits = 0; // DUAL: the next triangle group
+    uint32_t nBase = 0, nBits = 0; // the next triangle group (dual step)
     uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
-    auto done = [&]() { return DUAL ? travDoneDual(ts, nBits, st) : travDone(ts, st); };
+    auto done = [&]() { return travDoneDual(ts, nBits, st); };
+    auto stop = [&]() { ts = TravState { 0u, 0u, 0u, 0u }; nBits = 0; st.depth = 0; };
     for (;;) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
@@ -1381,10 +1484,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     owner = __float_as_uint(sr.dir_owner.w);
                     idir = safeInv(d);
                     oct = rayOctant(idir);
-                    st.depth = 0;
+                    stop();
                     pass = 0;
-                    ts = TravState { 0u, 0u, 0u, 0u };
-                    nBits = 0;
                     active = true;
                     if (tmax >= tmin) {
                         if (COUNT) cShadow++;
@@ -1408,34 +1509,89 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
         if (__ballot(active) == 0) break;
+#ifdef ARK_TAIL_PROBE
+        itAll++;
+        if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
+#endif
+        if (exhausted) {
+            // ---- tail: resolved rays stop, idle lanes take stack bottoms --------------
+            const uint32_t root = pass >= 256 ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
+            if (active && (tailByte(tl, wbase + root) & 0x80u)) stop();
+            const uint64_t idle = __ballot(!active);
+            const bool can = active && st.depth > 0;
+            const uint64_t donors = __ballot(can);
+            const uint32_t m = min(static_cast<uint32_t>(__popcll(idle)), static_cast<uint32_t>(__popcll(donors)));
+            if (m != 0) {
+                const uint32_t dr = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(donors >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(donors), 0u));
+                const uint32_t ir = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(idle >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(idle), 0u));
+                uint32_t gB = 0, gBits = 0;
+                if (can && dr < m) {
+                    stackTakeBottom(st, gB, gBits);
+                    tl.table[wbase + dr] = static_cast<uint8_t>(lane);
+                    tailAdd(tl, wbase + root, 1u);
+                }
+                // every lane shuffles (a lane that takes nothing reads its own values)
+                const bool take = !active && ir < m;
+                const uint32_t src = take ? tl.table[wbase + ir] : lane;
+                o = shfl3(o, src);
+                d = shfl3(d, src);
+                tmax = __shfl(tmax, static_cast<int>(src));
+                owner = __shfl(owner, static_cast<int>(src));
+                const uint32_t sroot = __shfl(root, static_cast<int>(src));
+                gB = __shfl(gB, static_cast<int>(src));
+                gBits = __shfl(gBits, static_cast<int>(src));
+                if (take) {
+                    idir = safeInv(d);
+                    oct = rayOctant(idir);
+                    pass = static_cast<int>((sroot + 1u) << 8);
+                    stop();
+                    ts = TravState { gB, gBits, 0u, 0u };
+                    active = true;
+                }
+            }
+        }
         if (active) {
             bool occluded = false;
-            if (DUAL && !done()) {
+            if (!done()) {
                 RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                 occluded = travStepDual<kTraceBlock, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
-            } else if (!DUAL && !done()) {
-                Fetch fx;
-                travFetch(sc, nc, ts, st, oct, fx);
-                uint32_t inst, prim;
-                float tt, uu, vv;
-                bool bf;
-                occluded = travCompute(fx, ts, o, d, idir, oct, tmin, tmax, tt, uu, vv, bf, inst, prim, cNodes, cTris);
             }
+            const bool helper = pass >= 256;
+            const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
             if (occluded) {
                 atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
-                active = false;
-            } else if (done()) {
-                ++pass;
-                while (pass < 3 && roots[pass] < 0) ++pass;
-                if (pass < 3) {
-                    st.depth = 0;
-                    ts = TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u };
-                } else {
+                if (exhausted) tailOr(tl, wbase + root, 0x80u);
+                stop();
+                if (!helper) pass = 3; // no further hit-mask classes
+            }
+            if (done()) {
+                if (helper) {
+                    tailSub(tl, wbase + root, 1u);
                     active = false;
+                } else if (!exhausted || (tailByte(tl, wbase + lane) & 0x7fu) == 0) {
+                    if (exhausted && (tailByte(tl, wbase + lane) & 0x80u)) pass = 3; // a helper found the occluder
+                    ++pass;
+                    while (pass < 3 && roots[pass] < 0) ++pass;
+                    if (pass < 3) {
+                        st.depth = 0;
+                        ts = TravState { static_cast<uint32_t>(roots[pass]), rootGroupBits(), 0u, 0u };
+                    } else {
+                        if (exhausted) tailClear(tl, wbase + lane);
+                        active = false;
+                    }
                 }
             }
         }
     }
+#ifdef ARK_TAIL_PROBE
+    {
+        const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
+        if (lane == 0 && w < 32768) {
+            unsigned long long* r = g_tail[1][w];
+            r[0] = tStart; r[1] = tEx; r[2] = wall_clock64(); r[3] = itAll; r[4] = itEx; r[5] = 0;
+        }
+    }
+#endif
     if (COUNT) {
         atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[5], static_cast<unsigned long long>(cTris));
@@ -1479,20 +1635,34 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     const uint32_t total = f.window_rays;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t first = blockIdx.x * kGenSpan;
+    // pass 1 in stages over the thread's kGenSteps rays, so that each stage's
+    // dependent loads (slot order -> hit -> triangle normals -> instance) are in
+    // flight for all of them at once (the kernel is latency bound)
+    uint32_t rays[kGenSteps];
+    GpuHit hits[kGenSteps];
+#pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         const uint32_t pos = first + k * 256u + threadIdx.x;
+        const uint32_t q = pos / f.R;
+        rays[k] = pos < total ? slotAt(f, q) * f.R + (pos - q * f.R) : kNoHit;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kGenSteps; ++k) {
+        hits[k] = rays[k] != kNoHit ? f.hits[rays[k]] : GpuHit { 0.0f, 0.0f, 0.0f, kNoHit };
+        if (hits[k].t < 0.0f) hits[k].tri = kNoHit; // backface: no shading, no shadow ray
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kGenSteps; ++k) {
         uint32_t bits = 0;
-        if (pos < total) {
-            const uint32_t q = pos / f.R;
-            const uint32_t ray = slotAt(f, q) * f.R + (pos - q * f.R);
-            const GpuHit hit = f.hits[ray];
-            if (hit.tri != kNoHit && !(hit.t < 0.0f)) {
-                bits = litLightMask(sc, hitShadingNormal(sc, hit.tri, hit.u, hit.v));
-                f.shadow_bits[ray] = bits;
-            }
+        if (hits[k].tri != kNoHit) {
+            bits = litLightMask(sc, hitShadingNormal(sc, hits[k].tri, hits[k].u, hits[k].v));
+            f.shadow_bits[rays[k]] = bits;
         }
         bitsL[k * 256u + threadIdx.x] = bits;
-        const uint32_t x = waveInclusiveScan(static_cast<uint32_t>(__builtin_popcount(bits)));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kGenSteps; ++k) {
+        const uint32_t x = waveInclusiveScan(static_cast<uint32_t>(__builtin_popcount(bitsL[k * 256u + threadIdx.x])));
         if (__lane_id() == 63u) waveOff[k][wave] = x;
     }
     __syncthreads();
@@ -1843,13 +2013,6 @@ static int traceDual()
     return v;
 }
 
-// Same choice for the shadow traversal (ARK_SHADOW_DUAL, default 1; 6 waves/SIMD
-// either way; C4: 0.79 vs 0.83 ms with k_shadow_gen).
-static int shadowDual()
-{
-    static const int v = [] { const char* e = std::getenv("ARK_SHADOW_DUAL"); return e ? std::atoi(e) : 1; }();
-    return v;
-}
 
 const void* kernel_trace_ptr(bool count)
 {
@@ -1920,9 +2083,7 @@ const void* kernel_shade_ptr(bool count)
 
 const void* kernel_trace_shadow_ptr(bool count)
 {
-    if (shadowDual())
-        return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, true>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6, true>);
-    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, false>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6, false>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6>);
 }
 
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s)
@@ -1955,3 +2116,10 @@ hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, 
 }
 
 } // namespace ark
+
+#ifdef ARK_TAIL_PROBE
+extern "C" __attribute__((visibility("default"))) int ark_debug_tail(unsigned long long* out, size_t bytes)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(ark::dev::g_tail), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -73,7 +73,7 @@ struct alignas(16) GpuInstance {
     int32_t rt_mesh_index;
     int32_t flip_facing;     // det(ObjectToWorld) < 0
     int32_t hit_mask;
-    int32_t _pad;
+    int32_t material_index;  // meshes[rt_mesh_index].material_index, resolved at upload
 };
 
 struct GpuTextureInfo {
