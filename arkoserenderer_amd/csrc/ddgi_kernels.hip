@@ -270,9 +270,14 @@ struct RayHit {
     bool backface;
 };
 
+// Inverse ray direction for the box tests only (triangle tests use d): v_rcp_f32
+// (1 ulp) instead of an IEEE divide (~10 VALU each). Every slab distance of an axis
+// then carries the same relative factor 1 +- 6e-8, far inside the box test's 1e-5
+// relative margin (visitNode8), so culling stays conservative; the sign, and with
+// it the ray octant, is exact.
 __device__ __forceinline__ V3 safeInv(V3 d)
 {
-    auto f = [](float x) { return 1.0f / (fabsf_(x) < 1e-20f ? (x < 0.0f ? -1e-20f : 1e-20f) : x); };
+    auto f = [](float x) { return __builtin_amdgcn_rcpf(fabsf_(x) < 1e-20f ? (x < 0.0f ? -1e-20f : 1e-20f) : x); };
     return { f(d.x), f(d.y), f(d.z) };
 }
 
@@ -361,7 +366,8 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // Tests the 8 children of one BVH8 node against [tmin, tmax]. A slab distance is
 // one fma of the 8-bit plane index q:  t = q * (step * idir) + (p - o) * idir,
 // where step * idir is exact (a power of two) and (p - o) * idir carries at most
-// about 2 ulp of |p - o| * |idir|; the build inflates every box by 1e-6 of the
+// about 2 ulp of |p - o| * |idir| (idir itself within 1 ulp of 1/d, safeInv); the
+// build inflates every box by 1e-6 of the
 // scene diagonal on top of its own relative margin (bvh_builder.cpp), which
 // covers that error, and the comparison keeps a relative margin for far boxes,
 // so a box holding an exact triangle hit is never culled. The near/far plane of
