@@ -747,7 +747,7 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 #ifdef ARK_TAIL_PROBE
 __device__ unsigned long long g_tail[2][32768][6];
 #endif
-template<bool COUNT, int WPE, bool DUAL>
+template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
 #ifdef ARK_TAIL_PROBE
@@ -772,12 +772,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     uint32_t ray = 0;
     int pass = 0;
     TravState ts { 0u, 0u, 0u, 0u };
-    uint32_t nBase = 0, nBits = 0; // DUAL: the next triangle group
+    uint32_t nBase = 0, nBits = 0; // the next triangle group (dual step)
     uint32_t oct = 0;
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
-    auto done = [&]() { return DUAL ? travDoneDual(ts, nBits, st) : travDone(ts, st); };
+    auto done = [&]() { return travDoneDual(ts, nBits, st); };
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
@@ -834,28 +834,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         itAll++;
         if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
 #endif
-        // ---- one step: a pending leaf triangle and/or the next node ---------------
-        if (DUAL && active && !done()) {
-            travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
-        } else if (!DUAL && active && !done()) {
-            Fetch fx;
-            travFetch(sc, nc, ts, st, oct, fx);
-            uint32_t inst, prim;
-            float tt, uu, vv;
-            bool bf;
-            const bool cand = travCompute(fx, ts, o, d, idir, oct, tmin, h.t, tt, uu, vv, bf, inst, prim, cNodes, cTris);
-            if (cand &&
-                     !(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
-                     !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
-                h.t = tt;
-                h.u = uu;
-                h.v = vv;
-                h.tri = fx.i;
-                h.inst = inst;
-                h.prim = prim;
-                h.backface = bf;
-            }
-        }
+        // ---- one step: a pending leaf triangle and the next node -------------------
+        if (active && !done()) travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
@@ -2011,21 +1991,12 @@ hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
 // Persistent traversal at 6 waves/SIMD (80 VGPRs, no spill; round 1: 3.43 vs 3.61 ms
 // at the compiler's 5 on C4, 8 spilled and took 5.4 ms); COUNT variants run at the
 // compiler's occupancy.
-// Traversal variant (tuning knob ARK_TRACE_DUAL, read once, default 1): 1 = dual step
-// (travStepDual) at 5 waves/SIMD, its extra fetch registers do not fit 6; 0 = one
-// step (a triangle or a node) per lane and iteration at 6 waves/SIMD. Measured at
-// C4: 2.57 vs 2.65 ms.
-static int traceDual()
-{
-    static const int v = [] { const char* e = std::getenv("ARK_TRACE_DUAL"); return e ? std::atoi(e) : 1; }();
-    return v;
-}
-
-
+// Dual-step traversal at 6 waves/SIMD (80 VGPRs): the only spills (4 VGPRs) sit in
+// the masked pass's alpha test. C4: 2.39 ms, against 2.51 at 5 waves (96 VGPRs, no
+// spill) and 2.65 for one step per iteration at 6 waves.
 const void* kernel_trace_ptr(bool count)
 {
-    if (traceDual()) return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1, true>) : reinterpret_cast<const void*>(&dev::k_trace<false, 5, true>);
-    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1, false>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6, false>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6>);
 }
 
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
