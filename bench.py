@@ -42,11 +42,11 @@ NODE_BYTES = 80        # GpuBvh8Node (8 quantized child boxes + bases + leaf cod
 TRI_BYTES = 48         # GpuTriangle (v0, e1, e2, instance, primitive)
 HIT_RECORD_BYTES = 16  # GpuHit
 SURFEL_BYTES = 8       # RGBA16F surfel
-# per shaded (front) hit: triangle 48 + instance 64 + RT mesh 12 + material 96 + 3 indices 12
-# + 3 RTVertex 108 + 3 texel fetches 48 + 8-probe DDGI gather 8*(4*4 + 4*8) = 384
-SHADE_HIT_BYTES = 48 + 64 + 12 + 96 + 12 + 108 + 48 + 384
+# per shaded (front) hit: shading record 64 (vertex normals, instance, UVs) + instance 64
+# + material 96 + 3 texel fetches 48 + 8-probe DDGI gather 8*(4*4 + 4*8) = 384
+SHADE_HIT_BYTES = 64 + 64 + 96 + 48 + 384
 MISS_BYTES = 16        # environment texel
-SHADOW_RAY_BYTES = 32  # ShadowRay record (written by k_shade, read by k_trace_shadow)
+SHADOW_RAY_BYTES = 32  # ShadowRay record (written by k_shadow_gen, read by k_trace_shadow)
 
 
 def parse():
