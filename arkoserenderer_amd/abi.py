@@ -51,8 +51,17 @@ ARK_TEX_RGBA8_UNORM = 0
 ARK_TEX_RGBA8_SRGB = 1
 ARK_TEX_R32F = 2
 ARK_TEX_RGBA32F = 3
+ARK_BRDF_DEFAULT = 0  # MaterialData.h:5-6
+ARK_BRDF_SKIN = 1
 ARK_WRAP_REPEAT = 0
 ARK_WRAP_CLAMP_TO_EDGE = 1
+ARK_WRAP_MIRRORED_REPEAT = 2
+ARK_WRAP_PER_AXIS = 0x100
+
+
+def ark_wrap_axes(s: int, t: int) -> int:
+    """ARK_WRAP_AXES(s, t): separate wrap modes for u (s) and v (t)."""
+    return ARK_WRAP_PER_AXIS | (s & 0xF) | ((t & 0xF) << 4)
 
 
 class ArkDdgiDesc(C.Structure):

@@ -499,7 +499,12 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
             if (t.width <= 0 || t.height <= 0 || !t.data) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "texture %u invalid", i);
             ti.width = t.width;
             ti.height = t.height;
-            ti.wrap = t.wrap;
+            // per-axis wrap, s in bits 0-3 and t in 4-7 (ARK_WRAP_AXES)
+            const int ws = (t.wrap & ARK_WRAP_PER_AXIS) ? (t.wrap & 0xf) : t.wrap, wt = (t.wrap & ARK_WRAP_PER_AXIS) ? ((t.wrap >> 4) & 0xf) : t.wrap;
+            if (ws < ARK_WRAP_REPEAT || ws > ARK_WRAP_MIRRORED_REPEAT || wt < ARK_WRAP_REPEAT || wt > ARK_WRAP_MIRRORED_REPEAT ||
+                ((t.wrap & ARK_WRAP_PER_AXIS) && (t.wrap & ~0x1ff)))
+                return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "texture %u: unknown wrap mode 0x%x", i, t.wrap);
+            ti.wrap = ws | (wt << 4);
             const size_t n = static_cast<size_t>(t.width) * t.height;
             for (size_t p = 0; p < n; ++p)
                 for (int c = 0; c < 4; ++c) {

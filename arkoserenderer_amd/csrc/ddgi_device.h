@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "ark_fmath.h"
+#include "../../include/ark_ddgi.h"
 #include "ddgi_types.h"
 
 namespace ark {
@@ -119,9 +120,17 @@ __device__ __forceinline__ void sphericalUvFromDirection(V3 d, float* u, float* 
     *v = theta / kPi;
 }
 
+// Texel wrap of one axis (GpuTextureInfo.wrap: s in bits 0-3, t in 4-7, normalised
+// by ark_ddgi_set_scene): clamp to edge, mirrored repeat (period 2n, the second
+// half reversed) or repeat.
 __device__ __forceinline__ int wrapCoord(int i, int n, int wrap)
 {
-    if (wrap == 1) return min(max(i, 0), n - 1);
+    if (wrap == ARK_WRAP_CLAMP_TO_EDGE) return min(max(i, 0), n - 1);
+    if (wrap == ARK_WRAP_MIRRORED_REPEAT) {
+        int m = i % (2 * n);
+        m = m < 0 ? m + 2 * n : m;
+        return m < n ? m : 2 * n - 1 - m;
+    }
     int m = i % n;
     return m < 0 ? m + n : m;
 }
@@ -135,8 +144,9 @@ __device__ __forceinline__ float4 sampleTexture(const GpuTextureInfo* __restrict
     float x0f = floorf_(x), y0f = floorf_(y);
     float fx = x - x0f, fy = y - y0f;
     int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
-    int xa = wrapCoord(x0, ti.width, ti.wrap), xb = wrapCoord(x0 + 1, ti.width, ti.wrap);
-    int ya = wrapCoord(y0, ti.height, ti.wrap), yb = wrapCoord(y0 + 1, ti.height, ti.wrap);
+    const int ws = ti.wrap & 0xf, wt = (ti.wrap >> 4) & 0xf;
+    int xa = wrapCoord(x0, ti.width, ws), xb = wrapCoord(x0 + 1, ti.width, ws);
+    int ya = wrapCoord(y0, ti.height, wt), yb = wrapCoord(y0 + 1, ti.height, wt);
     const float4* base = texels + ti.texel_offset;
     float4 t00 = base[static_cast<size_t>(ya) * ti.width + xa];
     float4 t10 = base[static_cast<size_t>(ya) * ti.width + xb];

@@ -2,9 +2,11 @@
 (RT mesh table, u32 index pool, vec3 position pool, RTVertex pool, materials,
 TLAS instances, lights, environment) as numpy arrays, plus loaders:
 
-* ``load_gltf`` — minimal glTF 2.0 (+ .bin) reader following the reference's
+* ``load_gltf`` — glTF 2.0 (+ .bin, images) reader following the reference's
   import rules (arkcore/asset/import/GltfLoader.cpp:372-543 geometry,
-  :918-971 materials) for the in-tree sample models (Cornell box).
+  :817-1035 samplers and materials, GpuScene.cpp:1452-1580 texture formats) for
+  the in-tree sample models (Cornell box, DamagedHelmet); ``merge_scenes`` puts
+  several into one scene (level objects, arkoserenderer_amd/level.py).
 * ``cornell_box`` — BASELINE config C2 (CornellBox.arklvl: +90 deg about X,
   camera f/11 1/125 s ISO 400, no lights, environment = white x brightness).
 * ``soup`` — BASELINE config C4 synthetic triangle-strip soup (C generator in
@@ -48,7 +50,10 @@ def default_material() -> np.ndarray:
     m["mask_cutoff"] = 1.0
     m["metallic_factor"] = 1.0
     m["roughness_factor"] = 1.0
-    m["dielectric_reflectance"] = 0.04
+    # MaterialAsset::calculateDielectricReflectance at the default IOR 1.5 (the shaders
+    # use the DIELECTRIC_REFLECTANCE constant instead, brdf.glsl:6)
+    q = (np.float32(1.5) - np.float32(1.0)) / (np.float32(1.5) + np.float32(1.0))
+    m["dielectric_reflectance"] = q * q
     m["color_tint"] = (1.0, 1.0, 1.0, 1.0)
     return m
 
@@ -214,36 +219,136 @@ def _accessor(g, buffers, idx):
     return arr
 
 
-def load_gltf(path: str, transform: np.ndarray | None = None) -> SceneData:
-    """Loads a .gltf + .bin without textures (factors only): one RT mesh +
-    instance per primitive (mesh segment), CCW winding as stored, material
-    mapping as GltfLoader.cpp:918-971 (alphaMode -> blend mode, alphaCutoff,
-    emissiveFactor, metallic/roughness factors, baseColorFactor -> colorTint)."""
-    with open(path) as fh:
-        g = json.load(fh)
-    base = os.path.dirname(path)
-    buffers = [open(os.path.join(base, b["uri"]), "rb").read() for b in g["buffers"]]
-    materials = []
-    for gm in g.get("materials", []):
-        m = default_material()
-        mode = gm.get("alphaMode", "OPAQUE")
-        if mode == "BLEND":
-            m["blend_mode"] = abi.ARK_BLEND_MODE_TRANSLUCENT
-        elif mode == "MASK":
-            m["blend_mode"] = abi.ARK_BLEND_MODE_MASKED
-            m["mask_cutoff"] = float(gm.get("alphaCutoff", 0.5))
-        m["emissive_factor"] = gm.get("emissiveFactor", [0.0, 0.0, 0.0])
+# glTF sampler wrap -> ImageWrapMode (GltfLoader.cpp:836-849)
+_GLTF_WRAP = {10497: abi.ARK_WRAP_REPEAT, 33071: abi.ARK_WRAP_CLAMP_TO_EDGE, 33648: abi.ARK_WRAP_MIRRORED_REPEAT}
+
+
+def _texture_wrap(g, tex_index: int) -> int:
+    """Wrap of glTF texture `tex_index`: its sampler's wrapS / wrapT; no sampler means
+    repeat in both directions (GltfLoader.cpp:826-832, glTF 2.0 defaults)."""
+    t = g["textures"][tex_index]
+    smp = g["samplers"][t["sampler"]] if t.get("sampler", -1) >= 0 else {}
+    ws = _GLTF_WRAP[smp.get("wrapS", 10497)]
+    wt = _GLTF_WRAP[smp.get("wrapT", 10497)]
+    return ws if ws == wt else abi.ark_wrap_axes(ws, wt)
+
+
+def _decode_image(g, base: str, buffers, image_index: int) -> np.ndarray:
+    """RGBA8 pixels (H, W, 4) of glTF image `image_index`, from its uri or buffer view.
+    PIL decodes (the reference's ImageAsset uses its own decoder: the texel values of
+    lossy JPEGs are therefore not pinned to the reference, only the loading rules are)."""
+    import io
+
+    from PIL import Image
+
+    img = g["images"][image_index]
+    if "uri" in img:
+        src = os.path.join(base, img["uri"])
+    else:
+        view = g["bufferViews"][img["bufferView"]]
+        off = view.get("byteOffset", 0)
+        src = io.BytesIO(buffers[view["buffer"]][off: off + view["byteLength"]])
+    with Image.open(src) as im:
+        return np.ascontiguousarray(np.asarray(im.convert("RGBA"), dtype=np.uint8))
+
+
+def _gltf_material(gm: dict, texture_slot) -> np.ndarray:
+    """GltfLoader::createMaterial (GltfLoader.cpp:915-1035) + GpuScene::registerMaterial
+    (GpuScene.cpp:1452-1517): blend mode from alphaMode (MASK keeps alphaCutoff), the
+    factors, the texture slots (sRGB: base colour, emissive; data: metallic-roughness,
+    normal, occlusion; a missing slot keeps the default texture), the
+    KHR_materials_pbrSpecularGlossiness / _transmission / _ior / _clearcoat extensions
+    and the Arkose BRDF extra. `texture_slot(gltf_texture_index, format)` returns
+    the scene texture index."""
+    m = default_material()
+    mode = gm.get("alphaMode", "OPAQUE")
+    if mode == "BLEND":
+        m["blend_mode"] = abi.ARK_BLEND_MODE_TRANSLUCENT
+    elif mode == "MASK":
+        m["blend_mode"] = abi.ARK_BLEND_MODE_MASKED
+        m["mask_cutoff"] = float(gm.get("alphaCutoff", 0.5))
+    elif mode != "OPAQUE":
+        raise ValueError(f"glTF material alphaMode {mode!r}")  # ASSERT_NOT_REACHED (:925)
+    m["emissive_factor"] = gm.get("emissiveFactor", [0.0, 0.0, 0.0])
+    ext = gm.get("extensions", {})
+
+    def slot(name, info, fmt):
+        if info is not None and info.get("index", -1) >= 0:
+            m[name] = texture_slot(int(info["index"]), fmt)
+
+    slot("emissive", gm.get("emissiveTexture"), abi.ARK_TEX_RGBA8_SRGB)
+    slot("normal_map", gm.get("normalTexture"), abi.ARK_TEX_RGBA8_UNORM)
+    slot("occlusion", gm.get("occlusionTexture"), abi.ARK_TEX_RGBA8_UNORM)
+    sg = ext.get("KHR_materials_pbrSpecularGlossiness")
+    if sg is not None:
+        # unsupported model, approximated as the reference does (:944-961)
+        m["metallic_factor"] = 0.0
+        m["roughness_factor"] = 0.0
+        m["color_tint"] = sg.get("diffuseFactor", [1.0, 1.0, 1.0, 1.0])
+        slot("base_color", sg.get("diffuseTexture"), abi.ARK_TEX_RGBA8_SRGB)
+        slot("metallic_roughness", sg.get("specularGlossinessTexture"), abi.ARK_TEX_RGBA8_UNORM)
+    else:
         pbr = gm.get("pbrMetallicRoughness", {})
         m["metallic_factor"] = float(pbr.get("metallicFactor", 1.0))
         m["roughness_factor"] = float(pbr.get("roughnessFactor", 1.0))
         m["color_tint"] = pbr.get("baseColorFactor", [1.0, 1.0, 1.0, 1.0])
-        materials.append(m)
-    if not materials:
-        materials.append(default_material())
+        slot("base_color", pbr.get("baseColorTexture"), abi.ARK_TEX_RGBA8_SRGB)
+        slot("metallic_roughness", pbr.get("metallicRoughnessTexture"), abi.ARK_TEX_RGBA8_UNORM)
+    if "KHR_materials_transmission" in ext:
+        m["blend_mode"] = abi.ARK_BLEND_MODE_TRANSLUCENT  # (:976-992)
+    ior = np.float32(ext.get("KHR_materials_ior", {}).get("ior", 1.5))
+    # MaterialAsset::calculateDielectricReflectance (MaterialAsset.cpp:115-121), interface IOR 1
+    q = (ior - np.float32(1.0)) / (ior + np.float32(1.0))
+    m["dielectric_reflectance"] = q * q
+    cc = ext.get("KHR_materials_clearcoat", {})
+    m["clearcoat"] = float(cc.get("clearcoatFactor", 0.0))
+    m["clearcoat_roughness"] = float(cc.get("clearcoatRoughnessFactor", 0.0))
+    brdf = gm.get("extras", {}).get("arkose", {}).get("brdf")
+    if brdf is not None:
+        m["brdf"] = {"Default": abi.ARK_BRDF_DEFAULT, "Skin": abi.ARK_BRDF_SKIN}.get(brdf, abi.ARK_BRDF_DEFAULT)
+    return m
+
+
+def load_gltf(path: str, transform: np.ndarray | None = None, textures: bool = True, mesh_name: str | None = None) -> SceneData:
+    """Loads a .gltf + .bin as the reference imports it (GltfLoader.cpp:372-543
+    geometry, :915-1035 materials, :817-913 samplers; GpuScene::registerMaterial for
+    the texture formats): one RT mesh + instance per primitive (mesh segment), CCW
+    winding as stored, node transforms not applied (a MeshAsset holds the raw mesh;
+    the level object's transform places it). `mesh_name` keeps only that glTF mesh
+    (one .arkmsh per glTF mesh). Each (glTF texture, format) pair becomes one scene
+    texture, decoded to RGBA8; `textures=False` keeps the factors only."""
+    with open(path) as fh:
+        g = json.load(fh)
+    base = os.path.dirname(path)
+    buffers = [open(os.path.join(base, b["uri"]), "rb").read() for b in g["buffers"]]
+    tex_list: list = []
+    tex_cache: dict = {}
+    decoded: dict = {}
+
+    def texture_slot(ti: int, fmt: int) -> int:
+        if not textures:
+            return -1
+        key = (ti, fmt)
+        if key not in tex_cache:
+            src = g["textures"][ti]["source"]
+            if src not in decoded:
+                decoded[src] = _decode_image(g, base, buffers, src)
+            px = decoded[src]
+            tex_cache[key] = len(tex_list)
+            tex_list.append(Texture(px.shape[1], px.shape[0], fmt, px, _texture_wrap(g, ti)))
+        return tex_cache[key]
+
+    materials = [_gltf_material(gm, texture_slot) for gm in g.get("materials", [])]
+    default_index = len(materials)
+    materials.append(default_material())  # primitives without a material (GpuScene's default material)
     M = np.eye(3, 4, dtype=np.float32) if transform is None else np.asarray(transform, np.float32).reshape(3, 4)
     pos_l, vtx_l, idx_l, meshes, instances = [], [], [], [], []
     nv = ni = 0
+    found = False
     for mesh in g["meshes"]:
+        if mesh_name is not None and mesh.get("name") != mesh_name:
+            continue
+        found = True
         for prim in mesh["primitives"]:
             attrs = prim["attributes"]
             P = _accessor(g, buffers, attrs["POSITION"]).astype(np.float32)
@@ -259,7 +364,8 @@ def load_gltf(path: str, transform: np.ndarray | None = None) -> SceneData:
             pos_l.append(P)
             vtx_l.append(vx)
             idx_l.append(idx)
-            mat = prim.get("material", 0)
+            mat = prim.get("material", -1)
+            mat = default_index if mat < 0 else mat
             meshes.append((nv, ni, mat))
             inst = np.zeros((), dtype=INSTANCE_DTYPE)
             inst["object_to_world"] = M.reshape(-1)
@@ -271,6 +377,8 @@ def load_gltf(path: str, transform: np.ndarray | None = None) -> SceneData:
             instances.append(inst)
             nv += n
             ni += idx.size
+    if mesh_name is not None and not found:
+        raise KeyError(f"{path}: no glTF mesh named {mesh_name!r}")
     return SceneData(
         positions=np.concatenate(pos_l),
         vertices=np.concatenate(vtx_l),
@@ -278,7 +386,50 @@ def load_gltf(path: str, transform: np.ndarray | None = None) -> SceneData:
         meshes=np.array(meshes, dtype=MESH_DTYPE),
         materials=np.array(materials, dtype=MATERIAL_DTYPE),
         instances=np.array(instances, dtype=INSTANCE_DTYPE),
+        textures=tex_list,
     )
+
+
+def merge_scenes(parts: list) -> SceneData:
+    """One scene of several (GpuScene holds every registered mesh in one set of
+    pools): vertex/index pools concatenated, RT meshes, materials, textures,
+    instances and spot lights re-indexed. Sun and environment come from the first
+    part that has one."""
+    pos, vtx, idx, meshes, mats, insts, tex, spots = [], [], [], [], [], [], [], []
+    sun, env = None, -1
+    nv = ni = nm = nmat = 0
+    for p in parts:
+        nt = len(tex)
+        pos.append(p.positions)
+        vtx.append(p.vertices)
+        idx.append(p.indices)
+        m = p.meshes.copy()
+        m["first_vertex"] += nv
+        m["first_index"] += ni
+        m["material_index"] += nmat
+        meshes.append(m)
+        mt = p.materials.copy()
+        for k in ("base_color", "normal_map", "metallic_roughness", "emissive", "occlusion", "bent_normal_map"):
+            mt[k] = np.where(mt[k] >= 0, mt[k] + nt, mt[k])
+        mats.append(mt)
+        it = p.instances.copy()
+        it["rt_mesh_index"] += nm
+        insts.append(it)
+        tex.extend(p.textures)
+        for sl in p.spots:
+            spots.append(SpotLight(sl.color, sl.direction, sl.right, sl.up, sl.position, sl.outer_cone_half_angle,
+                                   sl.ies_profile_index + nt if sl.ies_profile_index >= 0 else -1))
+        if sun is None:
+            sun = p.sun
+        if env < 0 and p.environment_texture >= 0:
+            env = p.environment_texture + nt
+        nv += p.positions.shape[0]
+        ni += p.indices.size
+        nm += p.meshes.size
+        nmat += p.materials.size
+    return SceneData(positions=np.concatenate(pos), vertices=np.concatenate(vtx), indices=np.concatenate(idx),
+                     meshes=np.concatenate(meshes), materials=np.concatenate(mats), instances=np.concatenate(insts),
+                     textures=tex, sun=sun, spots=spots, environment_texture=env)
 
 
 def manual_exposure(f_number: float, shutter: float, iso: float) -> float:
@@ -314,14 +465,15 @@ def cornell_box() -> tuple[SceneData, dict]:
     return scene, {"light_pre_exposure": pre, "environment_brightness": 3000.0, "z_far": 10000.0}
 
 
-def damaged_helmet() -> SceneData:
+def damaged_helmet(textures: bool = False) -> SceneData:
     """BASELINE config C1 input: DamagedHelmet.gltf (15,452 triangles), baked in
     object space at an identity instance transform, as MeshViewerApp.cpp:845-880 sets
-    up its bake scene (bakeScene->addMesh)."""
+    up its bake scene (bakeScene->addMesh). The bake reads no texture; `textures`
+    decodes the model's five 2048^2 JPEGs for DDGI shading."""
     path = find_asset("DamagedHelmet", "DamagedHelmet.gltf")
     if path is None:
         raise FileNotFoundError("tests/assets/DamagedHelmet/DamagedHelmet.gltf missing")
-    return load_gltf(path)
+    return load_gltf(path, textures=textures)
 
 
 def soup(triangle_count: int = 10_000_000, **overrides) -> SceneData:

@@ -106,10 +106,15 @@ enum {
     ARK_TEX_RGBA32F = 3     /* HDR environment */
 };
 
+/* Texture wrap (ImageWrapModes, GltfLoader.cpp:836-849: glTF wrapS/wrapT). A plain
+ * value applies to both axes; ARK_WRAP_PER_AXIS | s | t << 4 gives each its own. */
 enum {
     ARK_WRAP_REPEAT = 0,
-    ARK_WRAP_CLAMP_TO_EDGE = 1
+    ARK_WRAP_CLAMP_TO_EDGE = 1,
+    ARK_WRAP_MIRRORED_REPEAT = 2,
+    ARK_WRAP_PER_AXIS = 0x100
 };
+#define ARK_WRAP_AXES(s, t) (ARK_WRAP_PER_AXIS | ((s) & 0xf) | (((t) & 0xf) << 4))
 
 /* Grid + resource description (ProbeGrid.h:6-15, DDGIProbeGridData DDGIData.h:11-15). */
 typedef struct ArkDdgiDesc {

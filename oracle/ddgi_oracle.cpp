@@ -270,7 +270,7 @@ inline V3 probePosition(const Grid& g, uint32_t probeIdx)
 // Textures: bilinear, LOD 0, fp32 lerp; sRGB decode per texel before filtering.
 // ---------------------------------------------------------------------------
 struct Tex {
-    int w = 1, h = 1, fmt = ARK_TEX_RGBA8_SRGB, wrap = ARK_WRAP_REPEAT;
+    int w = 1, h = 1, fmt = ARK_TEX_RGBA8_SRGB, wrapS = ARK_WRAP_REPEAT, wrapT = ARK_WRAP_REPEAT;
     std::vector<float> rgba; // decoded texels, 4 floats each
 };
 
@@ -285,7 +285,9 @@ Tex makeTex(const ArkTexture& t)
     r.w = t.width;
     r.h = t.height;
     r.fmt = t.format;
-    r.wrap = t.wrap;
+    // per-axis wrap (ARK_WRAP_AXES): s in bits 0-3, t in bits 4-7
+    r.wrapS = (t.wrap & ARK_WRAP_PER_AXIS) ? (t.wrap & 0xf) : t.wrap;
+    r.wrapT = (t.wrap & ARK_WRAP_PER_AXIS) ? ((t.wrap >> 4) & 0xf) : t.wrap;
     size_t n = static_cast<size_t>(t.width) * t.height;
     r.rgba.resize(n * 4);
     for (size_t i = 0; i < n; ++i) {
@@ -319,9 +321,14 @@ Tex whiteSrgbPixel()
     return r;
 }
 
+// VkSamplerAddressMode per axis: clamp to edge, mirrored repeat, repeat
 inline int wrapCoord(int i, int n, int wrap)
 {
     if (wrap == ARK_WRAP_CLAMP_TO_EDGE) return std::min(std::max(i, 0), n - 1);
+    if (wrap == ARK_WRAP_MIRRORED_REPEAT) {
+        const int p = ((i % (2 * n)) + 2 * n) % (2 * n);
+        return p < n ? p : 2 * n - 1 - p;
+    }
     int m = i % n;
     return m < 0 ? m + n : m;
 }
@@ -334,8 +341,8 @@ void sampleBilinear(const Tex& t, float u, float v, float out[4])
     float x0f = floorf_(x), y0f = floorf_(y);
     float fx = x - x0f, fy = y - y0f;
     int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
-    int xa = wrapCoord(x0, t.w, t.wrap), xb = wrapCoord(x0 + 1, t.w, t.wrap);
-    int ya = wrapCoord(y0, t.h, t.wrap), yb = wrapCoord(y0 + 1, t.h, t.wrap);
+    int xa = wrapCoord(x0, t.w, t.wrapS), xb = wrapCoord(x0 + 1, t.w, t.wrapS);
+    int ya = wrapCoord(y0, t.h, t.wrapT), yb = wrapCoord(y0 + 1, t.h, t.wrapT);
     const float* t00 = &t.rgba[(static_cast<size_t>(ya) * t.w + xa) * 4];
     const float* t10 = &t.rgba[(static_cast<size_t>(ya) * t.w + xb) * 4];
     const float* t01 = &t.rgba[(static_cast<size_t>(yb) * t.w + xa) * 4];

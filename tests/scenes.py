@@ -12,7 +12,7 @@ def _quad(center, u, v):
     return np.stack([c - u - v, c + u - v, c + u + v, c - u + v]).astype(np.float32)
 
 
-def features_scene(seed: int = 7, ies_lut: np.ndarray | None = None) -> S.SceneData:
+def features_scene(seed: int = 7, ies_lut: np.ndarray | None = None, room_wrap: int = abi.ARK_WRAP_REPEAT) -> S.SceneData:
     """Exercises every shading/traversal feature: an opaque room, alpha-masked
     textured quads (any-hit alpha test), a translucent quad (only shadow rays see
     it), a mirrored instance (negative determinant -> flipped facing), sRGB and
@@ -107,7 +107,7 @@ def features_scene(seed: int = 7, ies_lut: np.ndarray | None = None) -> S.SceneD
     # textures
     tex = []
     t0 = (rng.integers(40, 255, size=(8, 8, 4))).astype(np.uint8)  # sRGB room albedo
-    tex.append(S.Texture(8, 8, abi.ARK_TEX_RGBA8_SRGB, t0))
+    tex.append(S.Texture(8, 8, abi.ARK_TEX_RGBA8_SRGB, t0, room_wrap))
     a = np.zeros((16, 16, 4), np.uint8)
     yy, xx = np.mgrid[0:16, 0:16]
     a[..., 0], a[..., 1], a[..., 2] = 200, 180, 90
