@@ -403,6 +403,9 @@ EXPORTS = {
     "ark_ddgi_resource_size": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "ark_ddgi_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "ark_ddgi_write": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
+    "ark_ddgi_state_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "ark_ddgi_save_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "ark_ddgi_load_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "ark_ddgi_get_device_views": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiDeviceViews)]),
     "ark_ddgi_reset_history": (C.c_int, [C.c_void_p]),
     "ark_ddgi_set_counting": (C.c_int, [C.c_void_p, C.c_int]),

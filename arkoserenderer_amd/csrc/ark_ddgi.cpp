@@ -5,6 +5,7 @@
 // working set (slot table, hit records, surfels) and the scene (BVH + RT mesh
 // data + materials + lights). Every update is enqueued on one HIP stream.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -26,6 +27,24 @@
 using namespace ark;
 
 namespace {
+
+// roctx range over a scope (host-side enqueue markers, named after the reference's
+// ScopedDebugZone labels, DDGINode.cpp:152-247); end() closes it early.
+class RoctxRange {
+public:
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { end(); }
+    void end()
+    {
+        if (m_open) roctxRangePop();
+        m_open = false;
+    }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+
+private:
+    bool m_open { true };
+};
 
 struct DeviceBuffer {
     void* ptr = nullptr;
@@ -699,6 +718,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.offsets = ctx->offsets.as<float4>();
     f.slots = ctx->slots.as<GpuProbeSlot>();
     f.fib = ctx->fib.as<float4>();
+    RoctxRange ddgiZone("DDGI");
     ARK_HIP(orderBegin(ctx, s));
     if (ctx->orderR != R) {
         sampleTraversalOrder(R, ctx->orderHost);
@@ -740,6 +760,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         }
     }
     if (f.window_probes > 0) {
+        RoctxRange traceZone("Trace rays");
         ARK_HIP(launch_trace(ctx->scene, f, ctx->traceBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
         if (f.light_count > 0) {
@@ -753,6 +774,9 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
+        traceZone.end();
+        // probeUpdateIrradiance/Visibility + border corners/edges + offsets, fused
+        RoctxRange updateZone("Update probes");
         ARK_HIP(launch_probe_update(f, s));
     } else {
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
@@ -823,6 +847,90 @@ int ark_ddgi_write(ArkDdgiCtx* ctx, int which, const void* src, uint64_t bytes)
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
     ARK_HIP(hipMemcpy(p, src, n, hipMemcpyHostToDevice));
+    return ARK_DDGI_OK;
+}
+
+// --- history checkpoint ------------------------------------------------------
+namespace {
+struct StateHeader {
+    char magic[8];           // "ARKDDGI1"
+    int32_t grid[3];
+    float spacing[3], origin[3];
+    float zFar;
+    int32_t clearMode, shardRank, shardCount;
+    int32_t reserved;        // 0
+    uint64_t irrBytes, visBytes, offBytes;
+};
+static_assert(sizeof(StateHeader) == 88, "state header layout");
+
+StateHeader stateHeaderOf(const ArkDdgiCtx* ctx)
+{
+    StateHeader h {};
+    std::memcpy(h.magic, "ARKDDGI1", 8);
+    h.grid[0] = ctx->X;
+    h.grid[1] = ctx->Y;
+    h.grid[2] = ctx->Z;
+    for (int k = 0; k < 3; ++k) {
+        h.spacing[k] = ctx->desc.probe_spacing[k];
+        h.origin[k] = ctx->desc.offset_to_first[k];
+    }
+    h.zFar = ctx->desc.z_far;
+    h.clearMode = ctx->desc.clear_overflow_mode;
+    h.shardRank = ctx->desc.shard_rank;
+    h.shardCount = ctx->desc.shard_count;
+    h.irrBytes = ctx->irr.bytes;
+    h.visBytes = ctx->vis.bytes;
+    h.offBytes = ctx->offsets.bytes;
+    return h;
+}
+} // namespace
+
+int ark_ddgi_state_size(const ArkDdgiCtx* ctx, uint64_t* outBytes)
+{
+    if (!ctx || !outBytes) return ARK_DDGI_E_INVALID_ARGUMENT;
+    *outBytes = sizeof(StateHeader) + ctx->irr.bytes + ctx->vis.bytes + ctx->offsets.bytes;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_save_state(ArkDdgiCtx* ctx, void* dst, uint64_t bytes)
+{
+    if (!ctx || !dst) return ARK_DDGI_E_INVALID_ARGUMENT;
+    uint64_t need = 0;
+    ark_ddgi_state_size(ctx, &need);
+    if (bytes != need) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "state is %llu bytes, got %llu", (unsigned long long)need, (unsigned long long)bytes);
+    const StateHeader h = stateHeaderOf(ctx);
+    char* o = static_cast<char*>(dst);
+    std::memcpy(o, &h, sizeof(h));
+    o += sizeof(h);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemcpy(o, ctx->irr.ptr, ctx->irr.bytes, hipMemcpyDeviceToHost));
+    o += ctx->irr.bytes;
+    ARK_HIP(hipMemcpy(o, ctx->vis.ptr, ctx->vis.bytes, hipMemcpyDeviceToHost));
+    o += ctx->vis.bytes;
+    ARK_HIP(hipMemcpy(o, ctx->offsets.ptr, ctx->offsets.bytes, hipMemcpyDeviceToHost));
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* src, uint64_t bytes)
+{
+    if (!ctx || !src) return ARK_DDGI_E_INVALID_ARGUMENT;
+    uint64_t need = 0;
+    ark_ddgi_state_size(ctx, &need);
+    if (bytes != need) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "state is %llu bytes, got %llu", (unsigned long long)need, (unsigned long long)bytes);
+    StateHeader h;
+    std::memcpy(&h, src, sizeof(h));
+    const StateHeader mine = stateHeaderOf(ctx);
+    if (std::memcmp(&h, &mine, sizeof(h)) != 0)
+        return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "state blob is of another grid / zFar / clear mode / shard (or not a DDGI state)");
+    const char* i = static_cast<const char*>(src) + sizeof(h);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemcpy(ctx->irr.ptr, i, ctx->irr.bytes, hipMemcpyHostToDevice));
+    i += ctx->irr.bytes;
+    ARK_HIP(hipMemcpy(ctx->vis.ptr, i, ctx->vis.bytes, hipMemcpyHostToDevice));
+    i += ctx->vis.bytes;
+    ARK_HIP(hipMemcpy(ctx->offsets.ptr, i, ctx->offsets.bytes, hipMemcpyHostToDevice));
     return ARK_DDGI_OK;
 }
 

@@ -165,6 +165,19 @@ class DDGIContext:
         data = np.ascontiguousarray(data)
         self.check(self.lib.ark_ddgi_write(self.h, which, data.ctypes.data, data.nbytes), "ark_ddgi_write")
 
+    def save_state(self) -> bytes:
+        """ark_ddgi_save_state: the DDGI history (atlases + offsets) as one blob."""
+        n = C.c_uint64()
+        self.check(self.lib.ark_ddgi_state_size(self.h, C.byref(n)), "ark_ddgi_state_size")
+        buf = (C.c_uint8 * n.value)()
+        self.check(self.lib.ark_ddgi_save_state(self.h, buf, n.value), "ark_ddgi_save_state")
+        return bytes(buf)
+
+    def load_state(self, blob: bytes):
+        """ark_ddgi_load_state: restores a blob of a context with the same grid / zFar / shard."""
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        self.check(self.lib.ark_ddgi_load_state(self.h, buf, len(blob)), "ark_ddgi_load_state")
+
     def device_views(self) -> abi.ArkDdgiDeviceViews:
         v = abi.ArkDdgiDeviceViews()
         self.check(self.lib.ark_ddgi_get_device_views(self.h, C.byref(v)), "ark_ddgi_get_device_views")

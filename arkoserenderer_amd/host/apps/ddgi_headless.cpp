@@ -10,10 +10,19 @@
 //   ddgi_headless --scene s.arkscn | --soup N   --grid X Y Z --spacing sx sy sz --origin ox oy oz
 //                 [--rays R] [--updates K] [--frames F] [--zfar Z] [--exposure E] [--env B]
 //                 [--ambient LX] [--offsets 0|1] [--rebuild-at F] [--device D] --out PREFIX
+//                 [--shards P]                          Z-slab ranks as P contexts in this process,
+//                                                       bands exchanged by device copies (one GPU)
+//                 [--world P --rank r --nccl-id FILE]   rank r of P processes (one per GPU), bands
+//                                                       exchanged by RCCL all-gather; rank 0 writes
+//                                                       the ncclUniqueId to FILE, the others read it
+// Sharded runs dump the (exchanged, therefore complete) atlases of rank 0 / this rank
+// and the probe offsets of this rank's slab ("--shards": merged over the owners).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -22,7 +31,10 @@
 #include "core/Logging.h"
 #include "rendering/GpuScene.h"
 #include "rendering/RenderPipeline.h"
+#include "rendering/backend/hip/SlabExchange.h"
 #include "rendering/nodes/DDGINode.h"
+
+#include <hip/hip_runtime.h>
 
 namespace {
 
@@ -151,6 +163,45 @@ void populate(GpuScene& gs, const ArkDdgiScene& s)
     gs.setEnvironmentMap(s.environment_texture);
 }
 
+std::vector<uint8_t> readResource(ArkDdgiCtx* ctx, int which)
+{
+    uint64_t bytes = 0;
+    if (ark_ddgi_resource_size(ctx, which, &bytes) != 0) return {};
+    std::vector<uint8_t> buf(bytes);
+    if (ark_ddgi_read(ctx, which, buf.data(), bytes) != 0) return {};
+    return buf;
+}
+
+bool writeFile(const std::string& path, const std::vector<uint8_t>& buf)
+{
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    std::fclose(f);
+    return ok;
+}
+
+// rendezvous of the RCCL ranks through a shared file: rank 0 publishes the id
+// (written then renamed, so readers never see a partial file)
+bool shareUniqueId(const std::string& path, int rank, std::vector<uint8_t>& id)
+{
+    if (rank == 0) {
+        if (!RcclSlabExchange::createUniqueId(id)) return false;
+        const std::string tmp = path + ".tmp";
+        return writeFile(tmp, id) && std::rename(tmp.c_str(), path.c_str()) == 0;
+    }
+    for (int tries = 0; tries < 600; ++tries) {
+        if (FILE* f = std::fopen(path.c_str(), "rb")) {
+            id.resize(128);
+            const bool ok = std::fread(id.data(), 1, id.size(), f) == id.size();
+            std::fclose(f);
+            return ok;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    return false;
+}
+
 bool dump(ArkDdgiCtx* ctx, int which, const std::string& path)
 {
     uint64_t bytes = 0;
@@ -172,6 +223,8 @@ int main(int argc, char** argv)
     uint64_t soupTris = 0;
     ProbeGrid grid;
     int rays = 64, updates = 512, frames = 4, device = 0, offsets = 1, rebuildAt = -1;
+    int shards = 1, world = 1, rank = 0;
+    std::string ncclIdPath;
     float zFar = 10000.0f, exposure = 1.0f, env = 1.0f, ambient = 0.0f;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -195,6 +248,10 @@ int main(int argc, char** argv)
         else if (a == "--rebuild-at") rebuildAt = std::atoi(next());
         else if (a == "--device") device = std::atoi(next());
         else if (a == "--out") out = next();
+        else if (a == "--shards") shards = std::atoi(next());
+        else if (a == "--world") world = std::atoi(next());
+        else if (a == "--rank") rank = std::atoi(next());
+        else if (a == "--nccl-id") ncclIdPath = next();
         else ARKOSE_LOG(Fatal, "unknown argument %s", a.c_str());
     }
     SceneFile file;
@@ -221,42 +278,107 @@ int main(int argc, char** argv)
     scene.camera().setFarClipPlane(zFar);
     scene.camera().setExposure(exposure);
 
-    auto makePipeline = [&]() {
+    if (shards < 1 || world < 1 || rank < 0 || rank >= world || (shards > 1 && world > 1) || (world > 1 && ncclIdPath.empty()))
+        ARKOSE_LOG(Fatal, "bad sharding arguments (--shards %d, --world %d --rank %d)", shards, world, rank);
+    const bool rccl = !ncclIdPath.empty();
+    const int ranksHere = shards;                    // contexts in this process
+    const int slabCount = rccl ? world : shards;     // Z-slab ranks in total
+
+    auto makePipeline = [&](int shardRank) {
         auto pipeline = std::make_unique<RenderPipeline>(&scene);
         DDGINode& node = pipeline->addNode<DDGINode>();
         node.setRaysPerProbe(rays);
         node.setProbeUpdatesPerFrame(updates);
         node.setComputeProbeOffsets(offsets != 0);
         node.setMaxProbeUpdates(updates);
+        if (slabCount > 1) node.setShard(shardRank, slabCount);
         return pipeline;
     };
-    auto pipeline = makePipeline();
-    auto registry = std::make_unique<Registry>(backend, nullptr);
-    pipeline->constructAll(*registry);
+    auto nodeOf = [](RenderPipeline& p) {
+        RenderPipelineNode* n = nullptr;
+        p.forEachNodeInResolvedOrder([&](RenderPipelineNode& node, const RenderPipelineNode::ExecuteCallback&) { n = &node; });
+        return static_cast<DDGINode*>(n);
+    };
+    std::vector<std::unique_ptr<RenderPipeline>> pipelines;
+    std::vector<std::unique_ptr<Registry>> registries;
+    for (int r = 0; r < ranksHere; ++r) {
+        pipelines.push_back(makePipeline(rccl ? rank : r));
+        registries.push_back(std::make_unique<Registry>(backend, nullptr));
+        pipelines.back()->constructAll(*registries.back());
+    }
+    // the slab exchange over the constructed contexts
+    std::unique_ptr<SlabExchange> exchange;
+    if (slabCount > 1 || rccl) {
+        std::string err;
+        if (rccl) {
+            SlabBands bands;
+            if (!SlabBands::fromContext(nodeOf(*pipelines[0])->context(), rank, world, bands, err)) ARKOSE_LOG(Fatal, "%s", err.c_str());
+            std::vector<uint8_t> id;
+            if (!shareUniqueId(ncclIdPath, rank, id)) ARKOSE_LOG(Fatal, "cannot share the ncclUniqueId through %s", ncclIdPath.c_str());
+            auto ex = std::make_unique<RcclSlabExchange>(device, rank, world, id.data(), bands);
+            if (!ex->ok()) ARKOSE_LOG(Fatal, "RCCL: %s", ex->error().c_str());
+            exchange = std::move(ex);
+        } else {
+            std::vector<SlabBands> all(ranksHere);
+            for (int r = 0; r < ranksHere; ++r)
+                if (!SlabBands::fromContext(nodeOf(*pipelines[r])->context(), r, ranksHere, all[r], err)) ARKOSE_LOG(Fatal, "%s", err.c_str());
+            exchange = std::make_unique<DeviceCopySlabExchange>(std::move(all));
+        }
+        for (auto& p : pipelines) nodeOf(*p)->setSlabExchange(exchange.get());
+    }
     for (int f = 0; f < frames; ++f) {
         if (f == rebuildAt) {
             // pipeline rebuild (VulkanBackend::reconstructRenderPipelineResources,
             // VulkanBackend.cpp:2327-2347): same nodes, new Registry that adopts the
             // previous one's DDGI history
-            auto nextReg = std::make_unique<Registry>(backend, registry.get());
-            pipeline->constructAll(*nextReg);
-            registry = std::move(nextReg);
+            if (ranksHere != 1 || exchange) ARKOSE_LOG(Fatal, "--rebuild-at is for unsharded runs");
+            auto nextReg = std::make_unique<Registry>(backend, registries[0].get());
+            pipelines[0]->constructAll(*nextReg);
+            registries[0] = std::move(nextReg);
         }
-        pipeline->executeFrame(AppState(1.0f / 60.0f, f / 60.0f, static_cast<uint32_t>(f), f == 0), backend);
+        for (auto& p : pipelines) p->executeFrame(AppState(1.0f / 60.0f, f / 60.0f, static_cast<uint32_t>(f), f == 0), backend);
     }
     backend.synchronize();
-    BindingSet* set = registry->getBindingSet("DDGISamplingSet");
-    if (!set || set->bindings().size() != 4) ARKOSE_LOG(Fatal, "DDGISamplingSet not published");
-    ArkDdgiCtx* ctx = nullptr;
-    // the node of the current pipeline owns the context
-    {
-        RenderPipelineNode* n = nullptr;
-        pipeline->forEachNodeInResolvedOrder([&](RenderPipelineNode& node, const RenderPipelineNode::ExecuteCallback&) { n = &node; });
-        ctx = static_cast<DDGINode*>(n)->context();
+    if (hipDeviceSynchronize() != hipSuccess) ARKOSE_LOG(Error, "device synchronize failed");  // the exchange's side stream
+    for (auto& reg : registries) {
+        BindingSet* set = reg->getBindingSet("DDGISamplingSet");
+        if (!set || set->bindings().size() != 4) ARKOSE_LOG(Fatal, "DDGISamplingSet not published");
     }
+    ArkDdgiCtx* ctx = nodeOf(*pipelines[0])->context();
     bool ok = dump(ctx, ARK_DDGI_ATLAS_IRRADIANCE, out + ".irr") && dump(ctx, ARK_DDGI_ATLAS_VISIBILITY, out + ".vis") &&
-              dump(ctx, ARK_DDGI_PROBE_OFFSETS, out + ".off") && dump(ctx, ARK_DDGI_SURFELS, out + ".surf");
-    registry.reset();
+              dump(ctx, ARK_DDGI_SURFELS, out + ".surf");
+    if (ranksHere > 1) {
+        // every context holds the complete atlases after the exchange
+        const std::vector<uint8_t> irr0 = readResource(ctx, ARK_DDGI_ATLAS_IRRADIANCE), vis0 = readResource(ctx, ARK_DDGI_ATLAS_VISIBILITY);
+        for (int r = 1; r < ranksHere; ++r) {
+            ArkDdgiCtx* c = nodeOf(*pipelines[r])->context();
+            if (readResource(c, ARK_DDGI_ATLAS_IRRADIANCE) != irr0 || readResource(c, ARK_DDGI_ATLAS_VISIBILITY) != vis0) {
+                ARKOSE_LOG(Error, "shard %d: atlases differ from shard 0 after the exchange", r);
+                ok = false;
+            }
+        }
+        // offsets are owner-only: probe i from the rank whose slab holds its z
+        std::vector<float> merged(readResource(ctx, ARK_DDGI_PROBE_OFFSETS).size() / 4, 0.0f);
+        const int X = grid.gridDimensions[0], Z = grid.gridDimensions[2];
+        for (int r = 0; r < ranksHere; ++r) {
+            const std::vector<uint8_t> raw = readResource(nodeOf(*pipelines[r])->context(), ARK_DDGI_PROBE_OFFSETS);
+            const float* o = reinterpret_cast<const float*>(raw.data());
+            for (size_t i = 0; i < merged.size() / 4; ++i) {
+                const int z = static_cast<int>((i % static_cast<size_t>(X * Z)) / static_cast<size_t>(X));
+                if (z * ranksHere / Z == r)
+                    for (int k = 0; k < 4; ++k) merged[i * 4 + k] = o[i * 4 + k];
+            }
+        }
+        std::vector<uint8_t> bytes(merged.size() * 4);
+        std::memcpy(bytes.data(), merged.data(), bytes.size());
+        ok = ok && writeFile(out + ".off", bytes);
+    } else {
+        ok = ok && dump(ctx, ARK_DDGI_PROBE_OFFSETS, out + ".off");
+    }
+    if (exchange) std::printf("ddgi_headless: %d Z-slab ranks, %s exchange\n", slabCount, exchange->name());
+    pipelines.clear();
+    exchange.reset();
+    registries.clear();
     if (soup) ark_soup_free(soup);
     std::printf("ddgi_headless: %d frames, %s\n", frames, ok ? "dumped" : "DUMP FAILED");
     return ok && ark::errorCounter() == 0 ? 0 : 1;

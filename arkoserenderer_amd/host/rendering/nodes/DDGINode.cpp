@@ -1,5 +1,7 @@
 #include "DDGINode.h"
 
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -12,6 +14,11 @@ struct DDGIProbeGridData {
     float probeSpacing[4];
     float offsetToFirst[4];
 };
+
+DDGINode::~DDGINode()
+{
+    if (m_updateDone) (void)hipEventDestroy(static_cast<hipEvent_t>(m_updateDone));
+}
 
 RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registry& reg)
 {
@@ -101,8 +108,21 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
         p.environment_multiplier = scene.preExposedEnvironmentBrightnessFactor();
         p.delta_time = appState.deltaTime();
         p.update_offsets = (m_computeProbeOffsets && m_applyProbeOffsets) ? 1 : 0;
-        if (int rc = ark_ddgi_update(ctx, &p, cmdList.hipStream()); rc != ARK_DDGI_OK)
+        if (m_exchange) {
+            // Z-slab rank: traversal goes ahead, shading waits for the previous exchange;
+            // this update's bands are then exchanged on the exchange's side stream
+            if (!m_updateDone) {
+                hipEvent_t e;
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) ARKOSE_LOG(Fatal, "DDGINode: event creation failed");
+                m_updateDone = e;
+            }
+            if (int rc = ark_ddgi_update_overlapped(ctx, &p, cmdList.hipStream(), m_exchangePending, m_updateDone); rc != ARK_DDGI_OK)
+                ARKOSE_LOG(Error, "DDGINode: ark_ddgi_update_overlapped failed (%d): %s", rc, ark_ddgi_last_error(ctx));
+            m_exchangePending = m_exchange->exchange(m_shardRank, m_updateDone);
+            if (!m_exchangePending) ARKOSE_LOG(Error, "DDGINode: %s slab exchange failed", m_exchange->name());
+        } else if (int rc = ark_ddgi_update(ctx, &p, cmdList.hipStream()); rc != ARK_DDGI_OK) {
             ARKOSE_LOG(Error, "DDGINode: ark_ddgi_update failed (%d): %s", rc, ark_ddgi_last_error(ctx));
+        }
 
         m_probeUpdateIdx = static_cast<int>((m_probeUpdateIdx + probeUpdatesThisFrame) % static_cast<uint32_t>(grid.probeCount()));
     };

@@ -7,6 +7,7 @@
 
 #include "../GpuScene.h"
 #include "../RenderPipelineNode.h"
+#include "../backend/hip/SlabExchange.h"
 
 class DDGINode final : public RenderPipelineNode {
 public:
@@ -24,6 +25,12 @@ public:
     void setApplyProbeOffsets(bool a) { m_applyProbeOffsets = a; }
     void setMaxProbeUpdates(int n) { m_maxProbeUpdates = n; }
     void setShard(int rank, int count) { m_shardRank = rank; m_shardCount = count; }
+    // Z-slab ranks: the atlas exchange after each update (RCCL all-gather, or device
+    // copies for contexts in one process); frame n+1's shading waits for frame n's.
+    void setSlabExchange(SlabExchange* exchange) { m_exchange = exchange; }
+    // the event the last exchange completes (null without an exchange): consumers of
+    // DDGISamplingSet on other ranks' bands wait on it
+    void* pendingExchange() const { return m_exchangePending; }
     ArkDdgiCtx* context() const { return m_ctx; }
     int probeUpdateIdx() const { return m_probeUpdateIdx; }
 
@@ -52,4 +59,9 @@ private:
     int m_shardRank { 0 };
     int m_shardCount { 1 };
     ArkDdgiCtx* m_ctx { nullptr };
+    SlabExchange* m_exchange { nullptr };
+    void* m_updateDone { nullptr };      // hipEvent_t recorded after each update
+    void* m_exchangePending { nullptr }; // hipEvent_t of the last exchange
+public:
+    ~DDGINode() override;
 };

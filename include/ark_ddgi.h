@@ -24,6 +24,16 @@
  *   ark_ddgi_read, ark_ddgi_write <- the published DDGISamplingSet contents
  *                           (DDGINode.cpp:62-66) and the Registry texture reuse that
  *                           carries DDGI history across rebuilds (Registry.cpp:120-150).
+ *   ark_ddgi_save_state, ark_ddgi_load_state <- the DDGI history as one blob (atlases +
+ *                           offsets + grid header): a checkpoint of what the reference
+ *                           keeps only in its Registry textures (no reference
+ *                           counterpart; SURVEY §8(b) suggested ABI).
+ *
+ * Profiling: ark_ddgi_update brackets its launches in roctx ranges named after the
+ * reference's debug zones (DDGINode.cpp:152-247): "DDGI" > "Trace rays" (slot
+ * table, traversal, shadow rays, shading) and "Update probes" (irradiance +
+ * visibility + border copies + probe positions, one fused launch); rocprofv3
+ * --marker-trace records them.
  *
  * Status convention: 0 = OK, negative = error (ARK_DDGI_E_*); the message of the
  * last error is available from ark_ddgi_last_error(ctx). This mirrors the
@@ -298,6 +308,15 @@ int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* out_bytes
 int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);
 int ark_ddgi_write(ArkDdgiCtx* ctx, int which, const void* host_src, uint64_t bytes);
 int ark_ddgi_get_device_views(ArkDdgiCtx* ctx, ArkDdgiDeviceViews* out_views);
+
+/* DDGI history checkpoint: irradiance + visibility atlases and probe offsets
+ * behind a header (magic "ARKDDGI1", grid dims / spacing / origin, zFar, clear mode,
+ * shard rank / count). Blocking. load_state requires a blob of a context with the
+ * same grid, zFar and shard (ARK_DDGI_E_SIZE_MISMATCH / _INVALID_ARGUMENT
+ * otherwise) and leaves the context unchanged on any error. */
+int ark_ddgi_state_size(const ArkDdgiCtx* ctx, uint64_t* out_bytes);
+int ark_ddgi_save_state(ArkDdgiCtx* ctx, void* host_dst, uint64_t bytes);
+int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* host_src, uint64_t bytes);
 
 /* Re-applies the creation-time clears (Registry created the textures anew). */
 int ark_ddgi_reset_history(ArkDdgiCtx* ctx);

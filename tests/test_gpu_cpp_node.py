@@ -49,3 +49,41 @@ def test_cpp_node_matches_python_host(tmp_path, rebuild):
     for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32)):
         got = np.fromfile(out + "." + k, dtype=dt)
         assert np.array_equal(got, py[k]), k
+
+
+def _headless(tmp_path, tag, extra):
+    sc = scenes.features_scene()
+    path = str(tmp_path / "features.arkscn")
+    if not os.path.exists(path):
+        sc.save_binary(path)
+    out = str(tmp_path / tag)
+    cmd = [EXE, "--scene", path, "--grid", "6", "4", "6", "--spacing", "0.7", "0.7", "0.7", "--origin", "-1.75", "0.25", "-1.75",
+           "--rays", "64", "--updates", "100", "--frames", "4", "--zfar", "100", "--exposure", "0.5", "--env", "0.8",
+           "--ambient", "0.1", "--offsets", "1", "--out", out] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return out, r.stdout
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_cpp_zslab_device_copy_exchange_equals_unsharded(tmp_path, shards):
+    """C++ Z-slab ranks (DDGINode::setSlabExchange + ark_ddgi_update_overlapped):
+    P contexts in one process, bands exchanged by device copies on a side stream;
+    every context ends with the unsharded atlases, bit for bit, and the owners'
+    offsets merge to the unsharded offsets."""
+    ref, _ = _headless(tmp_path, "ref", [])
+    got, log = _headless(tmp_path, f"s{shards}", ["--shards", str(shards)])
+    assert f"{shards} Z-slab ranks, device-copy exchange" in log
+    for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32)):
+        assert np.array_equal(np.fromfile(got + "." + k, dtype=dt), np.fromfile(ref + "." + k, dtype=dt)), k
+
+
+def test_cpp_rccl_exchange_one_rank(tmp_path):
+    """The RCCL path of the C++ exchange (ncclCommInitRank from a shared unique id,
+    in-place ncclAllGather of both bands in one group on a side stream) with a
+    1-rank communicator: the run equals the unsharded one."""
+    ref, _ = _headless(tmp_path, "ref", [])
+    got, log = _headless(tmp_path, "rccl", ["--world", "1", "--rank", "0", "--nccl-id", str(tmp_path / "nccl.id")])
+    assert "rccl exchange" in log
+    for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32)):
+        assert np.array_equal(np.fromfile(got + "." + k, dtype=dt), np.fromfile(ref + "." + k, dtype=dt)), k
