@@ -135,7 +135,7 @@ struct ArkDdgiCtx {
     // persistent resources
     DeviceBuffer irr, vis, offsets;
     // working set
-    DeviceBuffer slots, slotOrder, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork;
+    DeviceBuffer slots, slotOrder, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork, reflWork;
     std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
     uint32_t orderR = 0;
     int64_t slotOrderKey = -1; // (first, K) the slot order table was built for
@@ -252,6 +252,18 @@ int ensureShadeWork(ArkDdgiCtx* ctx)
     return ARK_DDGI_OK;
 }
 
+// RT reflections' ray-list work set for `pixels` rays (ark_ddgi_rt_reflections)
+int ensureReflWork(ArkDdgiCtx* ctx, uint64_t pixels)
+{
+    if (pixels >= (1ull << 28) && ctx->lightCount > 0)
+        return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "%llu reflection rays: shadow-ray owners pack (ray << 4) | light in 32 bits", static_cast<unsigned long long>(pixels));
+    auto al = [](uint64_t b) { return (b + 255) & ~static_cast<uint64_t>(255); };
+    const uint64_t bytes = al(pixels * 32) + al(pixels * sizeof(GpuHit)) + al(pixels * 4) + al((kRayCounterWords + kRayCounterStride) * 4) +
+                           al(pixels * ctx->lightCount * sizeof(ShadowRay));
+    if (ctx->reflWork.bytes < bytes) ARK_HIP(ctx->reflWork.alloc(bytes));
+    return ARK_DDGI_OK;
+}
+
 template<typename T>
 int upload(ArkDdgiCtx* ctx, DeviceBuffer& buf, const T* data, size_t count)
 {
@@ -346,6 +358,8 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
+    if (const char* v = std::getenv("ARK_EXP_TRACE_BPC")) ctx->traceBlocks = static_cast<uint32_t>(std::max(1, std::min(occT, std::atoi(v))) * ctx->cuCount);
+    if (const char* v = std::getenv("ARK_EXP_SHADOW_BPC")) ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, std::min(occW, std::atoi(v))) * ctx->cuCount);
     if (clearHistory(ctx) != ARK_DDGI_OK) {
         std::fprintf(stderr, "ark_ddgi_create: %s\n", ctx->lastError.c_str());
         delete ctx;
@@ -360,7 +374,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork, &ctx->reflWork,
                              &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->triNormals, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
                              &ctx->texInfos, &ctx->texels, &ctx->spots })
         b->release();
@@ -1153,8 +1167,33 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.ambient_amount = desc->ambient_amount;
     f.environment_multiplier = desc->environment_multiplier;
     f.spill = ctx->spill.as<uint32_t>();
+    // ray-list work set (ensureReflWork): rays, hit records, light bits, shadow rays, counters
+    const uint64_t pixels = static_cast<uint64_t>(desc->width) * desc->height;
+    if (pixels == 0) return ARK_DDGI_OK;
+    if ((rc = ensureReflWork(ctx, pixels)) != 0) return rc;
+    {
+        char* w = static_cast<char*>(ctx->reflWork.ptr);
+        auto take = [&](uint64_t bytes) {
+            char* q = w;
+            w += (bytes + 255) & ~static_cast<uint64_t>(255);
+            return q;
+        };
+        f.ray_list = reinterpret_cast<const float4*>(take(pixels * 32));
+        f.hits = reinterpret_cast<GpuHit*>(take(pixels * sizeof(GpuHit)));
+        f.shadow_bits = reinterpret_cast<uint32_t*>(take(pixels * 4));
+        f.ray_counter = reinterpret_cast<uint32_t*>(take((kRayCounterWords + kRayCounterStride) * 4));
+        f.shadow_rays = reinterpret_cast<ShadowRay*>(take(pixels * ctx->lightCount * sizeof(ShadowRay)));
+    }
+    f.shadow_count = f.ray_counter + kShadowCountWord;
+    f.shadow_heads = f.ray_counter + kShadowHeadWord;
+    f.list_count = f.ray_counter + kRayCounterWords;
+    f.light_count = ctx->lightCount;
+    f.refill_min = ctx->refillMin;
+    f.grab_chunk = ctx->grabChunk;
+    f.counters = ctx->counters.as<unsigned long long>();
     ARK_HIP(orderBegin(ctx, s));
-    ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, s));
+    ARK_HIP(hipMemsetAsync(f.ray_counter, 0, (kRayCounterWords + kRayCounterStride) * 4, s));
+    ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, ctx->shadowBlocks, s));
     ARK_HIP(orderEnd(ctx, s));
     return ARK_DDGI_OK;
 }

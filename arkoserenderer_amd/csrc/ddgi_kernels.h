@@ -122,6 +122,9 @@ struct FrameArgs {
     uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
+    // ray-list traversals (RT reflections): {origin, tmax}, {direction, pixel} per ray
+    const float4* ray_list;
+    const uint32_t* list_count;
 };
 
 // AO / bent-normal bake of one mesh segment (ark_ddgi_bake_ao; ddgi_kernels.hip §5)
@@ -144,7 +147,10 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 // stage 0: parameterization raster, 1: barycentrics + work list, 2: AO rays
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s);
 hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s);
-hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t blocks, hipStream_t s);
+// RT reflections as a ray-list pipeline: stage 0 setup (G-buffer -> ray list),
+// 1 closest-hit traversal, 2 shadow-ray list, 3 shadow traversal, 4 shading
+hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t traceBlocks, uint32_t shadowBlocks,
+                                 hipStream_t s);
 hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hipStream_t s);
 hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);

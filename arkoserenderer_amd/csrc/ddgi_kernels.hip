@@ -747,7 +747,52 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 #ifdef ARK_TAIL_PROBE
 __device__ unsigned long long g_tail[2][32768][6];
 #endif
-template<bool COUNT, int WPE>
+
+// Ray sources of the closest-hit traversal. ProbeRays: the window's probe rays from
+// the slot table (raygen.rgen:35-92: opaque pass then masked pass, tmin 1e-4, tmax
+// zFar), partitions of whole probes. ListRays: a ray list of {origin, tmax},
+// {direction, id} (rt-reflections/raygen.rgen:111-119: RayFlags_Opaque, cullMask
+// 0x01, tmin 0.01), f.list_count entries, the hit record at the list index.
+struct ProbeRays {
+    static constexpr bool kMaskedPass = true;
+    static constexpr float kTmin = 0.0001f;
+    __device__ static uint32_t total(const FrameArgs& f) { return f.window_rays; }
+    __device__ static void grab(const FrameArgs& f, uint32_t, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+    {
+        grabRays(f, f.ray_counter, home, tried, b, e, f.grab_chunk);
+    }
+    __device__ static void load(const FrameArgs& f, uint32_t r, uint32_t& ray, V3& o, V3& d, float& tmax)
+    {
+        const uint32_t qp = r / f.R;
+        const uint32_t slot = slotAt(f, qp);
+        const float4 fv = f.fib_order[r - qp * f.R]; // (direction, sample index)
+        const GpuProbeSlot ps = f.slots[slot];
+        ray = slot * f.R + __float_as_uint(fv.w); // hit record index
+        o = { ps.pos[0], ps.pos[1], ps.pos[2] };
+        d = rotate(v3(fv.x, fv.y, fv.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+        tmax = f.z_far;
+    }
+};
+
+struct ListRays {
+    static constexpr bool kMaskedPass = false;
+    static constexpr float kTmin = 0.01f;
+    __device__ static uint32_t total(const FrameArgs& f) { return *f.list_count; }
+    __device__ static void grab(const FrameArgs& f, uint32_t total, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+    {
+        grabItems(f.ray_counter, total, home, tried, b, e, f.grab_chunk);
+    }
+    __device__ static void load(const FrameArgs& f, uint32_t r, uint32_t& ray, V3& o, V3& d, float& tmax)
+    {
+        const float4 a = f.ray_list[2u * r], b = f.ray_list[2u * r + 1u];
+        ray = r;
+        o = { a.x, a.y, a.z };
+        tmax = a.w;
+        d = { b.x, b.y, b.z };
+    }
+};
+
+template<bool COUNT, int WPE, class Src = ProbeRays>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
 #ifdef ARK_TAIL_PROBE
@@ -761,7 +806,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t lane = threadIdx.x & 63u;
-    const float tmin = 0.0001f; // raygen.rgen:37
+    const float tmin = Src::kTmin;
+    const uint32_t total = Src::total(f);
     uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
@@ -789,7 +835,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             uint32_t fb = 0, fe = 0; // fresh chunk [fb, fe)
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) grabRays(f, f.ray_counter, home, t, b, e, f.grab_chunk);
+                if (lane == 0) Src::grab(f, total, home, t, b, e);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);
@@ -799,17 +845,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 if (rank < avail) r = poolNext + rank;
                 else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
                 if (r != kNoHit) {
-                    const uint32_t qp = r / f.R;
-                    const uint32_t slot = slotAt(f, qp);
-                    const float4 fv = f.fib_order[r - qp * f.R]; // (direction, sample index)
-                    const GpuProbeSlot ps = f.slots[slot];
-                    ray = slot * f.R + __float_as_uint(fv.w); // hit record index
-                    o = { ps.pos[0], ps.pos[1], ps.pos[2] };
-                    d = rotate(v3(fv.x, fv.y, fv.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+                    float tmax;
+                    Src::load(f, r, ray, o, d, tmax);
                     idir = safeInv(d);
                     oct = rayOctant(idir);
                     active = true;
-                    h = RayHit { f.z_far, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                    h = RayHit { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
                     pass = 0;
                     st.depth = 0;
                     nBits = 0;
@@ -839,7 +880,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
-            if (pass == 0) {
+            if (Src::kMaskedPass && pass == 0) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
                 // cullMask 0x02, tmax = previous hit T (:64-92); a negative tmax
                 // (backface) is an empty interval.
@@ -1615,14 +1656,20 @@ __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
     return x;
 }
 
+// REFL: the reflection ray list (rt-reflections/raygen.rgen:122): queue position =
+// list index, and the closest hit shades back faces too, with the normal flipped
+// (opaque.rchit:121-125): N = -(shading normal), as negation commutes exactly with
+// the normal matrix product and the normalisation.
+template<bool REFL = false>
 __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 {
     __shared__ uint32_t bitsL[kGenSpan];
     __shared__ uint32_t waveOff[kGenSteps][4];
     __shared__ uint32_t blockBase;
-    const uint32_t total = f.window_rays;
+    const uint32_t total = REFL ? *f.list_count : f.window_rays;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t first = blockIdx.x * kGenSpan;
+    if (REFL && first >= total) return; // launched for the largest possible list
     // pass 1 in stages over the thread's kGenSteps rays, so that each stage's
     // dependent loads (slot order -> hit -> triangle normals -> instance) are in
     // flight for all of them at once (the kernel is latency bound)
@@ -1631,19 +1678,25 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         const uint32_t pos = first + k * 256u + threadIdx.x;
-        const uint32_t q = pos / f.R;
-        rays[k] = pos < total ? slotAt(f, q) * f.R + (pos - q * f.R) : kNoHit;
+        if (REFL) {
+            rays[k] = pos < total ? pos : kNoHit;
+        } else {
+            const uint32_t q = pos / f.R;
+            rays[k] = pos < total ? slotAt(f, q) * f.R + (pos - q * f.R) : kNoHit;
+        }
     }
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         hits[k] = rays[k] != kNoHit ? f.hits[rays[k]] : GpuHit { 0.0f, 0.0f, 0.0f, kNoHit };
-        if (hits[k].t < 0.0f) hits[k].tri = kNoHit; // backface: no shading, no shadow ray
+        if (!REFL && hits[k].t < 0.0f) hits[k].tri = kNoHit; // backface: no shading, no shadow ray
     }
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         uint32_t bits = 0;
         if (hits[k].tri != kNoHit) {
-            bits = litLightMask(sc, hitShadingNormal(sc, hits[k].tri, hits[k].u, hits[k].v));
+            V3 N = hitShadingNormal(sc, hits[k].tri, hits[k].u, hits[k].v);
+            if (REFL && hits[k].t < 0.0f) N = -N;
+            bits = litLightMask(sc, N);
             f.shadow_bits[rays[k]] = bits;
         }
         bitsL[k * 256u + threadIdx.x] = bits;
@@ -1671,11 +1724,21 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         uint32_t sj = blockBase + waveOff[k][wave] + waveInclusiveScan(c) - c;
         if (bits == 0) continue;
         const uint32_t pos = first + k * 256u + threadIdx.x;
-        const uint32_t q = pos / f.R;
-        const uint32_t ray = slotAt(f, q) * f.R + (pos - q * f.R);
-        const float t = f.hits[ray].t;
+        uint32_t ray;
         V3 origin, dir;
-        rayOf(f, ray, &origin, &dir);
+        float t;
+        if (REFL) {
+            ray = pos;
+            const float4 a = f.ray_list[2u * pos], b = f.ray_list[2u * pos + 1u];
+            origin = v3(a.x, a.y, a.z);
+            dir = v3(b.x, b.y, b.z);
+            t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
+        } else {
+            const uint32_t q = pos / f.R;
+            ray = slotAt(f, q) * f.R + (pos - q * f.R);
+            t = f.hits[ray].t;
+            rayOf(f, ray, &origin, &dir);
+        }
         const V3 hitPoint = origin + t * dir;
         for (uint32_t b = bits; b; b &= b - 1) {
             const uint32_t l = static_cast<uint32_t>(__builtin_ctz(b));
@@ -2042,7 +2105,7 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
 {
     const uint32_t blocks = (f.window_rays + dev::kGenSpan - 1u) / dev::kGenSpan;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_shadow_gen, dim3(blocks), dim3(256), 0, s, sc, f);
+    hipLaunchKernelGGL(dev::k_shadow_gen<false>, dim3(blocks), dim3(256), 0, s, sc, f);
     return hipGetLastError();
 }
 
@@ -2080,10 +2143,22 @@ hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hi
     return hipGetLastError();
 }
 
-hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t blocks, hipStream_t s)
+hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t traceBlocks, uint32_t shadowBlocks,
+                                 hipStream_t s)
 {
-    if (r.width == 0 || r.height == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_rt_reflections, dim3(blocks), dim3(kTraceBlock), 0, s, sc, f, r);
+    const uint64_t pixels = static_cast<uint64_t>(r.width) * r.height;
+    const uint64_t slots = static_cast<uint64_t>((r.width + 7u) / 8u) * ((r.height + 7u) / 8u) * 64u;
+    hipLaunchKernelGGL(dev::k_refl_setup, dim3(static_cast<uint32_t>((slots + dev::kReflSetupSpan - 1) / dev::kReflSetupSpan)), dim3(256), 0, s, f, r,
+                       const_cast<float4*>(f.ray_list), const_cast<uint32_t*>(f.list_count));
+    void* args[] = { const_cast<SceneArgs*>(&sc), const_cast<FrameArgs*>(&f) };
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(&dev::k_trace<false, 6, dev::ListRays>), dim3(traceBlocks), dim3(kTraceBlock), args, 0, s);
+    if (e != hipSuccess) return e;
+    if (f.light_count > 0) {
+        hipLaunchKernelGGL(dev::k_shadow_gen<true>, dim3(static_cast<uint32_t>((pixels + dev::kGenSpan - 1) / dev::kGenSpan)), dim3(256), 0, s, sc, f);
+        e = launch_trace_shadow(sc, f, shadowBlocks, false, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(dev::k_refl_shade, dim3(static_cast<uint32_t>((pixels + 255) / 256)), dim3(256), 0, s, sc, f, r);
     return hipGetLastError();
 }
 
