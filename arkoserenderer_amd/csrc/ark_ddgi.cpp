@@ -141,7 +141,7 @@ struct ArkDdgiCtx {
     int64_t slotOrderKey = -1; // (first, K) the slot order table was built for
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
-    uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0;
+    uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0, shadowBlocksPerCu = 1;
     // scene
     bool hasScene = false;
     DeviceBuffer nodes, tris, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
@@ -253,6 +253,17 @@ int ensureShadeWork(ArkDdgiCtx* ctx)
 }
 
 // RT reflections' ray-list work set for `pixels` rays (ark_ddgi_rt_reflections)
+// Workgroups of the persistent shadow traversal for `rays` closest-hit rays (~0.25
+// shadow rays each on C4): the launch is a tail of the longest shadow rays when
+// there are few, and fewer co-resident waves shorten each one's iterations
+// (measured on C4: K = 2048 windows 0.228 -> 0.180 ms at 3 workgroups per CU,
+// K = 4096 0.246 -> 0.225, the full grid (8.4 M rays) unchanged from 5 to 6).
+uint32_t shadowBlocksFor(const ArkDdgiCtx* ctx, uint64_t rays)
+{
+    const uint64_t perCu = std::min<uint64_t>(ctx->shadowBlocksPerCu, std::max<uint64_t>(3, rays >> 20));
+    return static_cast<uint32_t>(perCu * ctx->cuCount);
+}
+
 int ensureReflWork(ArkDdgiCtx* ctx, uint64_t pixels)
 {
     if (pixels >= (1ull << 28) && ctx->lightCount > 0)
@@ -358,8 +369,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
-    if (const char* v = std::getenv("ARK_EXP_TRACE_BPC")) ctx->traceBlocks = static_cast<uint32_t>(std::max(1, std::min(occT, std::atoi(v))) * ctx->cuCount);
-    if (const char* v = std::getenv("ARK_EXP_SHADOW_BPC")) ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, std::min(occW, std::atoi(v))) * ctx->cuCount);
+    ctx->shadowBlocksPerCu = static_cast<uint32_t>(std::max(1, occW));
     if (clearHistory(ctx) != ARK_DDGI_OK) {
         std::fprintf(stderr, "ark_ddgi_create: %s\n", ctx->lastError.c_str());
         delete ctx;
@@ -779,7 +789,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
         if (f.light_count > 0) {
             ARK_HIP(launch_shadow_gen(ctx->scene, f, s));
-            ARK_HIP(launch_trace_shadow(ctx->scene, f, ctx->shadowBlocks, count, s));
+            ARK_HIP(launch_trace_shadow(ctx->scene, f, count ? ctx->shadowBlocks : shadowBlocksFor(ctx, f.window_rays), count, s));
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], s));
         // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
@@ -1193,7 +1203,7 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.counters = ctx->counters.as<unsigned long long>();
     ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, (kRayCounterWords + kRayCounterStride) * 4, s));
-    ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, ctx->shadowBlocks, s));
+    ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, shadowBlocksFor(ctx, pixels), s));
     ARK_HIP(orderEnd(ctx, s));
     return ARK_DDGI_OK;
 }

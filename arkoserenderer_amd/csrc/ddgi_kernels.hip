@@ -756,8 +756,7 @@ __device__ unsigned long long g_tail[2][32768][6];
 struct ProbeRays {
     static constexpr bool kMaskedPass = true;
     static constexpr float kTmin = 0.0001f;
-    __device__ static uint32_t total(const FrameArgs& f) { return f.window_rays; }
-    __device__ static void grab(const FrameArgs& f, uint32_t, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+    __device__ static void grab(const FrameArgs& f, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
     {
         grabRays(f, f.ray_counter, home, tried, b, e, f.grab_chunk);
     }
@@ -777,10 +776,9 @@ struct ProbeRays {
 struct ListRays {
     static constexpr bool kMaskedPass = false;
     static constexpr float kTmin = 0.01f;
-    __device__ static uint32_t total(const FrameArgs& f) { return *f.list_count; }
-    __device__ static void grab(const FrameArgs& f, uint32_t total, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
+    __device__ static void grab(const FrameArgs& f, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e)
     {
-        grabItems(f.ray_counter, total, home, tried, b, e, f.grab_chunk);
+        grabItems(f.ray_counter, *f.list_count, home, tried, b, e, f.grab_chunk);
     }
     __device__ static void load(const FrameArgs& f, uint32_t r, uint32_t& ray, V3& o, V3& d, float& tmax)
     {
@@ -807,7 +805,6 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t lane = threadIdx.x & 63u;
     const float tmin = Src::kTmin;
-    const uint32_t total = Src::total(f);
     uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
@@ -835,7 +832,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             uint32_t fb = 0, fe = 0; // fresh chunk [fb, fe)
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) Src::grab(f, total, home, t, b, e);
+                if (lane == 0) Src::grab(f, home, t, b, e);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);

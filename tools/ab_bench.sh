@@ -7,7 +7,7 @@ set -o pipefail
 TAG=${1:-ab}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-BARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-ao-bake --no-compose"
+BARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-ao-bake --no-compose --no-windows"
 if [[ " $* " == *" -- "* ]]; then
   while [[ "$1" != "--" ]]; do BARGS="$BARGS $1"; shift; done
   shift
