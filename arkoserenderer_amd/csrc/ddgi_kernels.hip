@@ -2162,7 +2162,9 @@ hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const 
 hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s)
 {
     if (c.width == 0 || c.height == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_lighting_compose, dim3((c.width + 15u) / 16u, (c.height + 15u) / 16u), dim3(256), 0, s, f, c);
+    const uint64_t tiles = static_cast<uint64_t>((c.width + 15u) / 16u) * ((c.height + 15u) / 16u);
+    if (tiles > (1ull << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dev::k_lighting_compose, dim3(static_cast<uint32_t>((tiles + 7u) / 8u * 8u)), dim3(256), 0, s, f, c);
     return hipGetLastError();
 }
 
