@@ -21,11 +21,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    """ark::dev::k_trace<false, 6>(...) -> k_trace; <true, ...> -> k_trace_counting."""
+    """ark::dev::k_trace<false, 6, ProbeRays>(...) -> k_trace; <true, ...> -> k_trace_counting;
+    the reflections' instantiations -> k_refl_trace / k_refl_shadow_gen."""
     m = re.search(r"\b(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
     if not m:
         return name
     base = m.group(1)
+    if base == "k_trace" and "ListRays" in name:
+        return "k_refl_trace"
+    if base == "k_shadow_gen":
+        return "k_refl_shadow_gen" if m.group(3) == "true" else base
     return base + "_counting" if m.group(3) == "true" else base
 
 
@@ -38,13 +43,27 @@ def main():
             stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                        "pct": float(r["Percentage"])}
     pmc = defaultdict(lambda: defaultdict(list))
+    pmc_ms = defaultdict(list)
     for sub in ("fetch", "write"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         with open(p) as fh:
-            for r in csv.DictReader(fh):
-                pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Dispatch_Id"]))
+        refl = False  # the RT reflections' launches share the shadow traversal kernel
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            refl = refl or k == "k_refl_setup"
+            if refl and k == "k_trace_shadow":
+                k = "k_refl_trace_shadow"
+            pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if sub == "fetch":
+                pmc_ms[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    # kernels the (probe-path-only) trace pass did not run: the consumers of the byte
+    # passes, timed by the PMC pass's own timestamps
+    for k, v in pmc_ms.items():
+        if k not in stats and k.startswith(("k_refl", "k_lighting")):
+            stats[k] = {"calls": len(v), "avg_ms": sum(v) / len(v), "avg_ms_source": "PMC pass dispatch timestamps"}
     kernels = {}
     for k, st in stats.items():
         e = dict(st)
