@@ -115,3 +115,45 @@ def test_c3_substitute_full_grid_probe_subset():
     n = _run(scene, dims, spacing, origin, 256, 10000.0,
              dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), _windows(dims, 8))
     assert n == 2 * 8 * 24
+
+
+def test_c4_full_size_rt_reflections():
+    """RT reflections on the full C4 scene (10 M triangles, 32^3 atlases after a real
+    full-grid frame): the bench's camera and synthetic G-buffer at 160 x 90, the HIP
+    ray-list pipeline (k_refl_setup -> k_trace<ListRays> -> shadow rays -> k_refl_shade)
+    against the oracle given the GPU's atlases, bit for bit."""
+    import torch
+
+    import reflection_inputs as RI
+
+    scene = S.soup(10_000_000)
+    grid = D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    N = grid.probe_count()
+    cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=N, max_rays_per_probe=256, max_probe_updates=N, compute_probe_offsets=True)
+    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
+    ctx.set_scene(scene)
+    ctx.update(D.frame_params(cfg, grid, D.AppState(0), 0, **exposure))
+    ctx.synchronize()
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(scene, threads=16)
+    for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS):
+        orc.write(w, ctx.read(w))
+    W, H = 160, 90
+    cam = RI.camera(W, H, eye=(16.0, 16.0, -6.0), target=(16.0, 14.0, 16.0))
+    g, _ = RI.gbuffer(W, H, cam, seed=5)
+    kw = dict(environment_multiplier=1.0, ambient_amount=0.0)
+    want_rad, want_dir = orc.rt_reflections(W, H, cam, g, threads=16, **kw)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in g.items()}
+    rad = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+    dirs = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+    D.RTReflectionsNode().execute(ctx, cam, {k: dev[k] for k in ("depth", "material", "normal_velocity")}, dev["blue_noise"], rad, dirs, **kw)
+    got_rad, got_dir = rad.cpu().numpy().view(np.uint16), dirs.cpu().numpy().view(np.uint16)
+    for name, got, want in (("radiance", got_rad, want_rad), ("direction", got_dir, want_dir)):
+        bad = np.argwhere(np.any(got != want, axis=-1))
+        assert bad.size == 0, f"{name}: {len(bad)} of {W * H} pixels differ, first {bad[:4].tolist()}"
+    traced = np.any(want_dir != 0, axis=-1)
+    rl = want_rad.view(np.float16)[..., 3].astype(np.float32)[traced]
+    assert traced.sum() > W * H // 2 and (rl < 10000.0).sum() > traced.sum() // 4 and (rl >= 10000.0).any()  # hits and misses
+    ctx.close()
+    orc.close()
