@@ -390,7 +390,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-    uint32_t hitSlots = 0, insideSlots = 0;
+    uint32_t hitSlots = 0, insideLo = 0;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
@@ -402,9 +402,11 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
         const float lim = fmaf(tf, 1.00001f, 1e-7f);
         hitSlots |= (tn <= lim ? 1u : 0u) << s;
-        // origin inside the box: every near-plane distance <= tmin
-        insideSlots |= (tn <= tmin ? 1u : 0u) << (s + 16);
+        // origin inside the box: every near-plane distance <= tmin (bits 0-7 here:
+        // the select constants stay inline, no literal moves; shifted once below)
+        insideLo |= (tn <= tmin ? 1u : 0u) << s;
     }
+    const uint32_t insideSlots = insideLo << 16;
     // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
     // swapping bit pairs / pairs of pairs / nibbles per octant bit
     // (hit and inside masks permuted together: bits 0-7 and 16-23)

@@ -157,3 +157,15 @@ def test_c4_full_size_rt_reflections():
     assert traced.sum() > W * H // 2 and (rl < 10000.0).sum() > traced.sum() // 4 and (rl >= 10000.0).any()  # hits and misses
     ctx.close()
     orc.close()
+
+
+def test_c5_substitute_full_grid_probe_subset():
+    """C5 substitute at full size: the instanced city block (250,000 boxes, ~3 M
+    triangles, 9 meshes, sun + 4 IES spot lights: 5 shadow rays per lit hit), the
+    48x16x48 grid x 512 rays of tools/config_bench.py, offsets on; 8 windows of 32
+    probes over every Z-slab, frames 0 and 1, bit for bit."""
+    scene = S.city_block()
+    dims = (48, 16, 48)
+    n = _run(scene, dims, (5.0, 2.5, 5.0), (2.5, 0.5, 2.5), 512, 1000.0,
+             dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), _windows(dims, 8))
+    assert n == 2 * 8 * 32
