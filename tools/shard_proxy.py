@@ -3,7 +3,10 @@ slab 0 of S (no exchange) runs the C4 workload; prints its ms/step next to the
 unsharded one. A proxy for strong-scaling headroom (the exchange is not included);
 the driver measures real N-GPU runs.
 
-    python tools/shard_proxy.py [--shards 2 4 8] [--steps 10]
+    python tools/shard_proxy.py [--shards 2 4 8] [--steps 10] [--all-ranks]
+
+--all-ranks measures every slab of each S (the strong-scaling step is the slowest
+rank's), not only slab 0.
 """
 import argparse
 import json
@@ -20,6 +23,7 @@ def main():
     ap.add_argument("--shards", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--triangles", type=int, default=10_000_000)
+    ap.add_argument("--all-ranks", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -32,11 +36,11 @@ def main():
     G, R = 32, 256
     grid = D.ProbeGrid((G, G, G), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
     out = {}
-    for s in args.shards:
+    for s, rank in [(s, r) for s in args.shards for r in (range(s) if args.all_ranks else [0])]:
         cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=G ** 3, max_rays_per_probe=R, max_probe_updates=G ** 3,
                            compute_probe_offsets=True)
         node = D.DDGINode(cfg)
-        assert node.construct(scene, grid, 10000.0, device=0, shard_rank=0, shard_count=s,
+        assert node.construct(scene, grid, 10000.0, device=0, shard_rank=rank, shard_count=s,
                               light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
         sptr = torch.cuda.current_stream(dev).cuda_stream
         for f in range(3):
@@ -51,13 +55,16 @@ def main():
             node.execute(D.AppState(4 + f), sptr)
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t0) / args.steps * 1e3
-        out[s] = {"ms_per_step_rank0": round(ms, 4), "kernels_ms": [round(x, 4) for x in kt]}
-        print(json.dumps({"shards": s, **out[s]}), flush=True)
+        rec = {"ms_per_step": round(ms, 4), "kernels_ms": [round(x, 4) for x in kt]}
+        print(json.dumps({"shards": s, "rank": rank, **rec}), flush=True)
+        if s not in out or rec["ms_per_step"] > out[s]["ms_per_step"]:
+            out[s] = dict(rec, slowest_rank=rank)
         node.ctx.close()
         del node
-    base = out.get(1, {}).get("ms_per_step_rank0")
+    base = out.get(1, {}).get("ms_per_step")
     if base:
-        print(json.dumps({"ideal_speedup_without_exchange": {s: round(base / v["ms_per_step_rank0"], 2) for s, v in out.items()}}))
+        print(json.dumps({"slowest_rank_ms": {s: v["ms_per_step"] for s, v in out.items()},
+                          "speedup_without_exchange": {s: round(base / v["ms_per_step"], 2) for s, v in out.items()}}))
 
 
 if __name__ == "__main__":
