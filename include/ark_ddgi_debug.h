@@ -14,7 +14,8 @@ extern "C" {
 
 /* Extra resource id for ark_ddgi_read: the primary-pass hit records of the last
  * update, 16 B each ({float t (negative = backface, +inf = miss), u, v, uint32
- * leaf-order triangle}) in [slot][max_rays_per_probe] order. */
+ * leaf-order triangle}) at slot * rays_per_probe + sample (slot = window slot,
+ * sample = the ray's Fibonacci sample index). */
 #define ARK_DDGI_DEBUG_HITS 100
 
 /* Evaluates op (0 sin, 1 cos, 2 acos, 3 atan2(x,y), 4 log2, 5 exp2, 6 pow(x,y),
