@@ -138,10 +138,27 @@ struct ArkDdgiCtx {
     DeviceBuffer slots, slotOrder, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork, reflWork;
     std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
     uint32_t orderR = 0;
-    int64_t slotOrderKey = -1; // (first, K) the slot order table was built for
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0, shadowBlocksPerCu = 1;
+    // Frames in flight (updateImpl): the per-frame buffers the traversal writes come in
+    // two sets (slot table, slot order, sample directions, hit records, work counters);
+    // frame n uses set n & 1. When frame n's window is independent of frame n - 1's,
+    // its slot table and primary traversal run on traceStream as soon as frame n - 2
+    // (the previous user of the set) is done, overlapping frame n - 1's shadow rays,
+    // shading and probe update on the caller's stream.
+    bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
+    bool pipeReady = false;        // the previous context operation was an update
+    uint32_t parity = 0;           // buffer set of the next update
+    uint32_t prevFirst = 0, prevK = 0, prevR = 0;
+    int prevUpdatedOffsets = 1;
+    hipStream_t traceStream = nullptr;
+    hipEvent_t evTraced = nullptr, evFrameDone[2] = {};
+    bool frameDoneValid[2] = { false, false };
+    uint32_t lastParity = 0;       // buffer set of the last update (debug hit records)
+    int64_t slotOrderKeys[2] = { -1, -1 };
+    uint32_t fibR[2] = { 0, 0 };
+    uint64_t spillRegionWords = 0; // spill region 1 = the primary traversal's
     // scene
     bool hasScene = false;
     DeviceBuffer nodes, tris, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
@@ -211,7 +228,9 @@ int ensureSpill(ArkDdgiCtx* ctx)
     // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
     uint32_t need = std::max<uint32_t>(1u, ctx->bvhMaxDepth + 2u > static_cast<uint32_t>(kStackLds) ? ctx->bvhMaxDepth + 2u - kStackLds : 1u);
     uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the traversal kernels
-    size_t bytes = static_cast<size_t>(need) * 2 * threads * sizeof(uint32_t);
+    const uint64_t words = static_cast<uint64_t>(need) * 2 * threads;
+    const size_t bytes = 2 * words * sizeof(uint32_t); // region 0: all but the primary traversal
+    ctx->spillRegionWords = words;
     if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
     ctx->spillEntries = need;
@@ -345,7 +364,12 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
+        if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
     }
+    if ((e = hipStreamCreateWithFlags(&ctx->traceStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evTraced, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (auto& ev : ctx->evFrameDone)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
@@ -353,13 +377,13 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->vis.alloc(static_cast<size_t>(ctx->Wv) * ctx->Hv * 4)) != hipSuccess) return bad(e, "alloc visibility");
     if ((e = ctx->offsets.alloc(static_cast<size_t>(ctx->N) * 16)) != hipSuccess) return bad(e, "alloc offsets");
     if ((e = ctx->slots.alloc(2 * K * sizeof(GpuProbeSlot))) != hipSuccess) return bad(e, "alloc slots");
-    if ((e = ctx->slotOrder.alloc(K * 4)) != hipSuccess) return bad(e, "alloc slot order");
-    if ((e = ctx->fib.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib");
+    if ((e = ctx->slotOrder.alloc(2 * K * 4)) != hipSuccess) return bad(e, "alloc slot order");
+    if ((e = ctx->fib.alloc(2 * R * 16)) != hipSuccess) return bad(e, "alloc fib");
     if ((e = ctx->order.alloc(R * 4)) != hipSuccess) return bad(e, "alloc order");
-    if ((e = ctx->fibOrder.alloc(R * 16)) != hipSuccess) return bad(e, "alloc fib order");
-    if ((e = ctx->hits.alloc(K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
+    if ((e = ctx->fibOrder.alloc(2 * R * 16)) != hipSuccess) return bad(e, "alloc fib order");
+    if ((e = ctx->hits.alloc(2 * K * R * sizeof(GpuHit))) != hipSuccess) return bad(e, "alloc hits");
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
-    if ((e = ctx->rayCounter.alloc(kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
+    if ((e = ctx->rayCounter.alloc(2 * kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0, occW = 0;
@@ -391,6 +415,10 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->evOrder) (void)hipEventDestroy(ctx->evOrder);
+    if (ctx->evTraced) (void)hipEventDestroy(ctx->evTraced);
+    for (auto& ev : ctx->evFrameDone)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -400,6 +428,7 @@ const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx) { return ctx ? ctx->lastE
 int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
     if (!s || s->struct_size != sizeof(ArkDdgiScene)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiScene");
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
@@ -690,6 +719,15 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
 
+// Do the probe windows [a, a + ka) and [b, b + kb) (indices mod n) share a probe?
+static bool windowsIntersect(uint32_t n, uint32_t a, uint32_t ka, uint32_t b, uint32_t kb)
+{
+    if (ka >= n || kb >= n) return true;
+    const uint32_t ab = (b + n - a) % n; // b relative to a
+    const uint32_t ba = (a + n - b) % n;
+    return ab < ka || ba < kb;
+}
+
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
 {
     return updateImpl(ctx, p, hipStream, nullptr, nullptr);
@@ -740,8 +778,20 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.irr = ctx->irr.as<uint16_t>();
     f.vis = ctx->vis.as<uint16_t>();
     f.offsets = ctx->offsets.as<float4>();
-    f.slots = ctx->slots.as<GpuProbeSlot>();
-    f.fib = ctx->fib.as<float4>();
+    const bool timing = ctx->timing;
+    const bool count = ctx->counting;
+    // Frames in flight: this frame's traversal may start before the previous frame's
+    // shading and probe update are done when it depends on nothing they write: its
+    // probes' offsets were last written two or more frames ago (the windows do not
+    // intersect, or the previous frame did not move probes), the sample order is the
+    // same, and no other context operation came in between. Instrumented updates
+    // (per-kernel events, counters) run serially.
+    const bool pipe = ctx->pipelining && ctx->pipeReady && !timing && !count && R == ctx->prevR &&
+                      (!ctx->prevUpdatedOffsets || !windowsIntersect(N, ctx->prevFirst, ctx->prevK, f.first, K));
+    const uint32_t b = ctx->parity;
+    const uint64_t Kmax = static_cast<uint64_t>(ctx->Kmax), Rmax = static_cast<uint64_t>(ctx->Rmax);
+    f.slots = ctx->slots.as<GpuProbeSlot>() + b * Kmax;
+    f.fib = ctx->fib.as<float4>() + b * Rmax;
     RoctxRange ddgiZone("DDGI");
     ARK_HIP(orderBegin(ctx, s));
     if (ctx->orderR != R) {
@@ -750,59 +800,71 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         ctx->orderR = R;
     }
     f.order = ctx->order.as<uint32_t>();
-    f.fib_order = ctx->fibOrder.as<float4>();
-    f.hits = ctx->hits.as<GpuHit>();
+    f.fib_order = ctx->fibOrder.as<float4>() + b * Rmax;
+    f.hits = ctx->hits.as<GpuHit>() + b * Kmax * Rmax;
     f.surfels = ctx->surfels.as<uint16_t>();
-    f.spill = ctx->spill.as<uint32_t>();
+    f.spill = ctx->spill.as<uint32_t>() + ctx->spillRegionWords; // region 1 (primary traversal)
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
     f.grab_chunk = ctx->grabChunk;
-    f.ray_counter = ctx->rayCounter.as<uint32_t>();
+    f.ray_counter = ctx->rayCounter.as<uint32_t>() + b * kRayCounterWords;
     f.counters = ctx->counters.as<unsigned long long>();
     // shading work set (ensureShadeWork): per-ray light bits | shadow-ray list
     {
-        const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
+        const uint64_t rays = Kmax * Rmax;
         char* w = static_cast<char*>(ctx->shadeWork.ptr);
         f.shadow_bits = reinterpret_cast<uint32_t*>(w);
         f.shadow_rays = reinterpret_cast<ShadowRay*>(w + ((rays * 4 + 255) & ~static_cast<uint64_t>(255)));
     }
     f.shadow_count = f.ray_counter + kShadowCountWord;
     f.shadow_heads = f.ray_counter + kShadowHeadWord;
-    const bool timing = ctx->timing;
-    const bool count = ctx->counting;
+    // the slot table and the primary traversal: on traceStream after frame n - 2 (the
+    // last user of buffer set b) when pipelined, else in line on the caller's stream
+    const hipStream_t ts = pipe ? ctx->traceStream : s;
+    if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
-    ARK_HIP(hipMemsetAsync(ctx->rayCounter.ptr, 0, ctx->rayCounter.bytes, s));
+    ARK_HIP(hipMemsetAsync(f.ray_counter, 0, kRayCounterWords * 4, ts));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
-    ARK_HIP(launch_probe_slots(f, s));
+    ARK_HIP(launch_probe_slots(f, ts));
     {
         // slot traversal order (k_slot_order): rebuilt when the window moves
-        f.slot_order = ctx->slotOrder.as<uint32_t>();
+        f.slot_order = ctx->slotOrder.as<uint32_t>() + b * Kmax;
         const int64_t key = (static_cast<int64_t>(f.first) << 32) | K;
-        if (key != ctx->slotOrderKey) {
-            ARK_HIP(launch_slot_order(f, ctx->slotOrder.as<uint32_t>(), s));
-            ctx->slotOrderKey = key;
+        if (key != ctx->slotOrderKeys[b]) {
+            ARK_HIP(launch_slot_order(f, const_cast<uint32_t*>(f.slot_order), ts));
+            ctx->slotOrderKeys[b] = key;
         }
     }
     if (f.window_probes > 0) {
         RoctxRange traceZone("Trace rays");
-        ARK_HIP(launch_trace(ctx->scene, f, ctx->traceBlocks, count, s));
+        ARK_HIP(launch_trace(ctx->scene, f, ctx->traceBlocks, count, ts));
+        if (pipe) {
+            ARK_HIP(hipEventRecord(ctx->evTraced, ts));
+            ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
+        }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
+        FrameArgs fs = f;
+        fs.spill = ctx->spill.as<uint32_t>(); // region 0
         if (f.light_count > 0) {
-            ARK_HIP(launch_shadow_gen(ctx->scene, f, s));
-            ARK_HIP(launch_trace_shadow(ctx->scene, f, count ? ctx->shadowBlocks : shadowBlocksFor(ctx, f.window_rays), count, s));
+            ARK_HIP(launch_shadow_gen(ctx->scene, fs, s));
+            ARK_HIP(launch_trace_shadow(ctx->scene, fs, count ? ctx->shadowBlocks : shadowBlocksFor(ctx, f.window_rays), count, s));
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[5], s));
         // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
         // rank it waits here for the previous exchange (the traversal above did not)
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-        ARK_HIP(launch_shade(ctx->scene, f, ctx->shadeBlocks, count, s));
+        ARK_HIP(launch_shade(ctx->scene, fs, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
         traceZone.end();
         // probeUpdateIrradiance/Visibility + border corners/edges + offsets, fused
         RoctxRange updateZone("Update probes");
-        ARK_HIP(launch_probe_update(f, s));
+        ARK_HIP(launch_probe_update(fs, s));
     } else {
+        if (pipe) {
+            ARK_HIP(hipEventRecord(ctx->evTraced, ts));
+            ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
+        }
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
@@ -812,8 +874,17 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         }
     }
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
+    ARK_HIP(hipEventRecord(ctx->evFrameDone[b], s));
+    ctx->frameDoneValid[b] = true;
     if (doneEvent) ARK_HIP(hipEventRecord(static_cast<hipEvent_t>(doneEvent), s));
     ARK_HIP(orderEnd(ctx, s));
+    ctx->parity = b ^ 1u;
+    ctx->pipeReady = true;
+    ctx->prevFirst = f.first;
+    ctx->prevK = K;
+    ctx->prevR = R;
+    ctx->prevUpdatedOffsets = p->update_offsets;
+    ctx->lastParity = b;
     ctx->timingValid = timing;
     ctx->countersPending = count;
     ctx->lastRays = f.window_rays;
@@ -836,7 +907,7 @@ static int resourceInfo(const ArkDdgiCtx* ctx, int which, void** ptr, uint64_t* 
     case ARK_DDGI_ATLAS_VISIBILITY: *ptr = ctx->vis.ptr; *bytes = ctx->vis.bytes; return 0;
     case ARK_DDGI_SURFELS: *ptr = ctx->surfels.ptr; *bytes = ctx->surfels.bytes; return 0;
     case ARK_DDGI_PROBE_OFFSETS: *ptr = ctx->offsets.ptr; *bytes = ctx->offsets.bytes; return 0;
-    case ARK_DDGI_DEBUG_HITS: *ptr = ctx->hits.ptr; *bytes = ctx->hits.bytes; return 0;
+    case ARK_DDGI_DEBUG_HITS: *ptr = ctx->hits.as<GpuHit>() + static_cast<uint64_t>(ctx->lastParity) * ctx->Kmax * ctx->Rmax; *bytes = ctx->hits.bytes / 2; return 0;
     default: return ARK_DDGI_E_INVALID_ARGUMENT;
     }
 }
@@ -864,6 +935,7 @@ int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* dst, uint64_t bytes)
 int ark_ddgi_write(ArkDdgiCtx* ctx, int which, const void* src, uint64_t bytes)
 {
     if (!ctx || !src) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
     void* p;
     uint64_t n;
     if (resourceInfo(ctx, which, &p, &n) != 0) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "unknown resource %d", which);
@@ -939,6 +1011,7 @@ int ark_ddgi_save_state(ArkDdgiCtx* ctx, void* dst, uint64_t bytes)
 int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* src, uint64_t bytes)
 {
     if (!ctx || !src) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
     uint64_t need = 0;
     ark_ddgi_state_size(ctx, &need);
     if (bytes != need) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "state is %llu bytes, got %llu", (unsigned long long)need, (unsigned long long)bytes);
@@ -985,6 +1058,7 @@ int ark_ddgi_get_device_views(ArkDdgiCtx* ctx, ArkDdgiDeviceViews* v)
 int ark_ddgi_reset_history(ArkDdgiCtx* ctx)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
     return clearHistory(ctx);

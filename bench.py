@@ -375,7 +375,11 @@ def reference_windows(node, ctx, torch, device, sptr, frame0):
         ctx.set_timing(False)
         torch.cuda.synchronize(device)
         a = [sum(k[i] for k in kt) / len(kt) for i in range(5)]
+        # ms_per_frame: consecutive windows are disjoint, so frame n + 1's traversal
+        # overlaps frame n's shading and update (frames in flight, ark_ddgi.h);
+        # kernels_ms: the instrumented (serial) frames
         out[f"K{K}"] = {"mrays_per_s": round(K * R / ms / 1e3, 1), "probes_updated_per_s": round(K / ms * 1e3, 1), "ms_per_frame": round(ms, 4),
+                        "frames_in_flight": True,
                         "kernels_ms": {"k_trace": round(a[1], 4), "k_shadow": round(a[4], 4), "k_shade": round(a[2], 4),
                                        "k_probe_update": round(a[3], 4)}}
     node.config.probe_updates_per_frame = full
