@@ -148,6 +148,7 @@ struct ArkDdgiCtx {
     // (the previous user of the set) is done, overlapping frame n - 1's shadow rays,
     // shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
+    uint32_t smallTraceBlocks = 0; // primary-traversal grid of a pipelined small window
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
     uint32_t prevFirst = 0, prevK = 0, prevR = 0;
@@ -391,6 +392,11 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occS, kernel_shade_ptr(false), kShadeBlock, 0)) != hipSuccess) return bad(e, "occupancy shade");
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occW, kernel_trace_shadow_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy shadow");
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
+    // a pipelined small window's traversal shares the GPU with the previous frame's
+    // shadow rays, shading and update: 3 workgroups per CU leave them room (K = 2048
+    // windows, 0.5 M rays: 0.55 -> 0.48 ms per frame; K = 4096 unchanged at 3-6, 0.81
+    // at 2, so from 0.75 M rays on the full grid)
+    ctx->smallTraceBlocks = static_cast<uint32_t>(std::min(3, std::max(1, occT)) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
     ctx->shadowBlocksPerCu = static_cast<uint32_t>(std::max(1, occW));
@@ -837,7 +843,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     }
     if (f.window_probes > 0) {
         RoctxRange traceZone("Trace rays");
-        ARK_HIP(launch_trace(ctx->scene, f, ctx->traceBlocks, count, ts));
+        const bool small = pipe && f.window_rays < (3u << 18);
+        ARK_HIP(launch_trace(ctx->scene, f, small ? ctx->smallTraceBlocks : ctx->traceBlocks, count, ts));
         if (pipe) {
             ARK_HIP(hipEventRecord(ctx->evTraced, ts));
             ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
