@@ -143,16 +143,16 @@ struct ArkDdgiCtx {
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0, shadowBlocksPerCu = 1;
     // Frames in flight (updateImpl): the per-frame buffers the traversal writes come in
     // two sets (slot table, slot order, sample directions, hit records, work counters);
-    // frame n uses set n & 1. When frame n's window is independent of frame n - 1's,
-    // its slot table and primary traversal run on traceStream as soon as frame n - 2
-    // (the previous user of the set) is done, overlapping frame n - 1's shadow rays,
-    // shading and probe update on the caller's stream.
+    // frame n uses set n & 1. Frame n's slot table, primary traversal and probe offsets
+    // run on traceStream as soon as frame n - 2 (the previous user of the set) is done,
+    // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
+    // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
     uint32_t smallTraceBlocks = 0; // primary-traversal grid of a pipelined small window
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
-    uint32_t prevFirst = 0, prevK = 0, prevR = 0;
-    int prevUpdatedOffsets = 1;
+    uint32_t prevR = 0;
+    bool prevPipelined = false;    // the previous update's offsets ran on traceStream
     hipStream_t traceStream = nullptr;
     hipEvent_t evTraced = nullptr, evFrameDone[2] = {};
     bool frameDoneValid[2] = { false, false };
@@ -725,14 +725,6 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
 
-// Do the probe windows [a, a + ka) and [b, b + kb) (indices mod n) share a probe?
-static bool windowsIntersect(uint32_t n, uint32_t a, uint32_t ka, uint32_t b, uint32_t kb)
-{
-    if (ka >= n || kb >= n) return true;
-    const uint32_t ab = (b + n - a) % n; // b relative to a
-    const uint32_t ba = (a + n - b) % n;
-    return ab < ka || ba < kb;
-}
 
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
 {
@@ -786,14 +778,13 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.offsets = ctx->offsets.as<float4>();
     const bool timing = ctx->timing;
     const bool count = ctx->counting;
-    // Frames in flight: this frame's traversal may start before the previous frame's
-    // shading and probe update are done when it depends on nothing they write: its
-    // probes' offsets were last written two or more frames ago (the windows do not
-    // intersect, or the previous frame did not move probes), the sample order is the
-    // same, and no other context operation came in between. Instrumented updates
-    // (per-kernel events, counters) run serially.
-    const bool pipe = ctx->pipelining && ctx->pipeReady && !timing && !count && R == ctx->prevR &&
-                      (!ctx->prevUpdatedOffsets || !windowsIntersect(N, ctx->prevFirst, ctx->prevK, f.first, K));
+    // Frames in flight: this frame's slot table, traversal and probe offsets read the
+    // scene, the sample order and the probe offsets only, which nothing of the
+    // previous frame's shadow rays, shading or atlas update writes (its offsets ran
+    // before them). They may start before the previous frame is done when the sample
+    // order is the same and no other writing context operation came in between.
+    // Instrumented updates (per-kernel events, counters) run serially.
+    const bool pipe = ctx->pipelining && ctx->pipeReady && !timing && !count && R == ctx->prevR;
     const uint32_t b = ctx->parity;
     const uint64_t Kmax = static_cast<uint64_t>(ctx->Kmax), Rmax = static_cast<uint64_t>(ctx->Rmax);
     f.slots = ctx->slots.as<GpuProbeSlot>() + b * Kmax;
@@ -828,6 +819,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     // last user of buffer set b) when pipelined, else in line on the caller's stream
     const hipStream_t ts = pipe ? ctx->traceStream : s;
     if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
+    // a serial previous frame wrote its offsets on the caller's stream
+    if (pipe && !ctx->prevPipelined && ctx->frameDoneValid[b ^ 1u]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b ^ 1u], 0));
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, kRayCounterWords * 4, ts));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
@@ -846,6 +839,9 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         const bool small = pipe && f.window_rays < (3u << 18);
         ARK_HIP(launch_trace(ctx->scene, f, small ? ctx->smallTraceBlocks : ctx->traceBlocks, count, ts));
         if (pipe) {
+            // probeUpdateOffset (k_probe_offsets: from the hit records), so that the
+            // next frame's slot table may follow on this stream
+            ARK_HIP(launch_probe_offsets(f, ts));
             ARK_HIP(hipEventRecord(ctx->evTraced, ts));
             ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
         }
@@ -864,8 +860,10 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
         traceZone.end();
-        // probeUpdateIrradiance/Visibility + border corners/edges + offsets, fused
+        // probeUpdateOffset (serial frames), probeUpdateIrradiance/Visibility + border
+        // corners/edges, fused
         RoctxRange updateZone("Update probes");
+        if (!pipe) ARK_HIP(launch_probe_offsets(fs, s));
         ARK_HIP(launch_probe_update(fs, s));
     } else {
         if (pipe) {
@@ -887,10 +885,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     ARK_HIP(orderEnd(ctx, s));
     ctx->parity = b ^ 1u;
     ctx->pipeReady = true;
-    ctx->prevFirst = f.first;
-    ctx->prevK = K;
     ctx->prevR = R;
-    ctx->prevUpdatedOffsets = p->update_offsets;
+    ctx->prevPipelined = pipe;
     ctx->lastParity = b;
     ctx->timingValid = timing;
     ctx->countersPending = count;

@@ -158,6 +158,7 @@ hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
+hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
 const void* kernel_trace_ptr(bool count);
 const void* kernel_shade_ptr(bool count);

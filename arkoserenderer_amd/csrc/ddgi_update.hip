@@ -70,7 +70,8 @@ __device__ __forceinline__ void borderSource(int res, int b, int* dx, int* dy, i
 //
 // Workgroup: 4 probes. Waves 0..3: visibility of probe w (64 orbits = 256 texels);
 // wave 4: irradiance of the 4 probes (16 orbits = 64 texels each, 16 lanes per
-// probe) and their offsets. Rays, surfels and clamped distances are staged in LDS.
+// probe). Rays, surfels and clamped distances are staged in LDS. The probe offsets
+// are k_probe_offsets' (below).
 // ---------------------------------------------------------------------------
 
 // powi_(x, N) for a constant N: the same binary-exponentiation multiply sequence
@@ -105,7 +106,6 @@ struct UpdateLds {
     uint2* rad;     // [P][R + pad]  raw fp16 surfel: radiance rgb + signed distance
     uint32_t* vis;  // [P][18*18]    visibility tile (interior + border)
     uint2* irr;     // [P][10*10]    irradiance tile
-    uint8_t* cls;   // [P][R]        offset ray class
     uint32_t stride; // per-probe stride of ray/d2/rad (elements)
 };
 
@@ -124,15 +124,13 @@ __device__ __forceinline__ UpdateLds updateLds(uint32_t R)
     L.vis = reinterpret_cast<uint32_t*>(p);
     p += sizeof(uint32_t) * kUpdateProbes * 324;
     L.d2 = reinterpret_cast<float*>(p);
-    p += sizeof(float) * kUpdateProbes * L.stride;
-    L.cls = reinterpret_cast<uint8_t*>(p);
     return L;
 }
 
 size_t probe_update_lds_bytes(uint32_t R)
 {
     const size_t stride = R + 4;
-    return kUpdateProbes * (stride * (16 + 8 + 4) + 100 * 8 + 324 * 4 + R); // 38.6 KB at R = 256: 4 workgroups per CU
+    return kUpdateProbes * (stride * (16 + 8 + 4) + 100 * 8 + 324 * 4); // 37.6 KB at R = 256: 4 workgroups per CU
 }
 
 // the orbit of quadrant texel (qx, qy) of a res x res tile: t, x-mirror t', antipode -t, -t'
@@ -324,72 +322,6 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 tile[(ty[k] + 1) * (IR + 2) + tx[k] + 1] = nw;
             }
         }
-        // --- probe offsets (probeUpdateOffset.comp:27-96; full-barrier semantics) ---
-        // rays classified in parallel (counts by ballot), then 6 lanes per probe each
-        // run one component of the two direction sums over the rays in order (adding
-        // +0 for rays of other classes leaves a sum unchanged), one lane finishes.
-        if (f.update_offsets) {
-            const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
-            const float maxOffset = minAxialSpacing / 2.0f;
-            uint32_t backfaceCount[kUpdateProbes], nearFrontfaceCount[kUpdateProbes];
-#pragma unroll
-            for (int q = 0; q < kUpdateProbes; ++q) {
-                backfaceCount[q] = 0;
-                nearFrontfaceCount[q] = 0;
-                for (uint32_t s0 = 0; s0 < R; s0 += 64) {
-                    const uint32_t s = s0 + static_cast<uint32_t>(ln);
-                    uint32_t cls = 0;
-                    if (s < R) {
-                        const float a = f16_to_f32(static_cast<uint16_t>(L.rad[q * L.stride + s].y >> 16));
-                        cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
-                        L.cls[q * R + s] = static_cast<uint8_t>(cls);
-                    }
-                    nearFrontfaceCount[q] += static_cast<uint32_t>(__popcll(__ballot(cls == 1u)));
-                    backfaceCount[q] += static_cast<uint32_t>(__popcll(__ballot(cls == 2u)));
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            float acc = 0.0f;
-            const int q = ln / 6, c = ln % 6;
-            if (ln < 6 * kUpdateProbes) {
-                const float4* ray = L.ray + q * L.stride;
-                const uint8_t* cl = L.cls + q * R;
-                const uint8_t want = c < 3 ? 1u : 2u;
-                const int comp = c % 3;
-                for (uint32_t s = 0; s < R; ++s) {
-                    const float4 r = ray[s];
-                    const float v = comp == 0 ? r.x : (comp == 1 ? r.y : r.z);
-                    acc += cl[s] == want ? v : 0.0f;
-                }
-            }
-            const int b = 6 * (ln < 6 * kUpdateProbes ? q : 0);
-            const V3 accumNearFrontfaceDir = v3(__shfl(acc, b + 0), __shfl(acc, b + 1), __shfl(acc, b + 2));
-            const V3 accumBackfaceDir = v3(__shfl(acc, b + 3), __shfl(acc, b + 4), __shfl(acc, b + 5));
-            if (ln < 6 * kUpdateProbes && c == 0 && slot0 + q < f.window_probes) {
-                uint32_t bc = 0, nc = 0;
-#pragma unroll
-                for (int k = 0; k < kUpdateProbes; ++k) {
-                    if (k == q) { bc = backfaceCount[k]; nc = nearFrontfaceCount[k]; }
-                }
-                const uint32_t probeIdx = f.slots[slot0 + q].probe_index;
-                float4 cur = f.offsets[probeIdx];
-                V3 currentOffset = v3(cur.x, cur.y, cur.z);
-                V3 offset = splat(0.0f);
-                const float stepSize = 0.125f, lerpSpeed = 10.0f;
-                if (static_cast<float>(bc) / static_cast<float>(R) >= 0.25f)
-                    offset = offset + normalize(accumBackfaceDir) * stepSize;
-                else if (nc >= 1)
-                    offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
-                else
-                    offset = offset - currentOffset * stepSize;
-                V3 newOffset = currentOffset + offset;
-                if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-                newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
-                f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
-            }
-        }
     }
     __syncthreads();
     // --- border texels of the updated tiles ------------------------------------
@@ -421,7 +353,98 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Probe offsets (probeUpdateOffset.comp:27-96). Their only reader is a later frame's
+// slot table (raygen.rgen:117-118: the ray origins), and their inputs - the window's
+// ray directions and hit distances, the current offsets - are final once the primary
+// traversal is: the distance the shader reads back from the ray's surfel is the hit
+// record's t (front face), t * 0.2 (back face, t stored negative) or zFar (miss),
+// rounded to fp16 as the surfel stores it (raygen.rgen:108-139). So this kernel runs
+// right after the traversal, and with frames in flight the next frame's slot table
+// and traversal follow it on the traversal stream (ark_ddgi.cpp updateImpl).
+// One wave, 10 probes, 6 lanes per probe: lane c sums component c % 3 of the
+// directions of the rays of class 1 (near front face, c < 3) or 2 (back face) in ray
+// order, as the shader's loop does (adding +0 for the other rays leaves a sum
+// unchanged), and counts them.
+constexpr int kOffsetProbes = 10;
+
+__global__ void __launch_bounds__(64) k_probe_offsets(FrameArgs f)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t R = f.R;
+    float4* fibL = reinterpret_cast<float4*>(smem); // [R]
+    uint8_t* clsL = smem + R * sizeof(float4);       // [kOffsetProbes][R]
+    const uint32_t lane = threadIdx.x;
+    const uint32_t slot0 = blockIdx.x * kOffsetProbes;
+    const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
+    const float maxOffset = minAxialSpacing / 2.0f;
+    for (uint32_t s = lane; s < R; s += 64) fibL[s] = f.fib[s];
+    for (uint32_t i = lane; i < kOffsetProbes * R; i += 64) {
+        const uint32_t p = i / R, s = i - p * R;
+        const uint32_t slot = slot0 + p;
+        uint8_t cls = 0;
+        if (slot < f.window_probes) {
+            const GpuHit h = f.hits[static_cast<size_t>(slot) * R + s];
+            // the surfel's distance (k_shade: miss, back face, front face)
+            const float dist = h.tri == kNoHit ? f.z_far : (h.t < 0.0f ? h.t * 0.2f : h.t);
+            const float a = f16_to_f32(f32_to_f16(dist));
+            cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
+        }
+        clsL[i] = cls;
+    }
+    __syncthreads();
+    const uint32_t q = lane / 6, c = lane % 6;
+    const uint32_t slot = slot0 + q;
+    const bool live = lane < 6 * kOffsetProbes && slot < f.window_probes;
+    float acc = 0.0f;
+    uint32_t cnt = 0;
+    if (live) {
+        const GpuProbeSlot ps = f.slots[slot];
+        const uint8_t want = c < 3 ? 1u : 2u;
+        const uint32_t comp = c % 3;
+        const uint8_t* cl = clsL + q * R;
+        for (uint32_t s = 0; s < R; ++s) {
+            const float4 fb = fibL[s];
+            const V3 d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+            const float v = comp == 0 ? d.x : (comp == 1 ? d.y : d.z);
+            const bool m = cl[s] == want;
+            acc += m ? v : 0.0f;
+            cnt += m ? 1u : 0u;
+        }
+    }
+    const int b = static_cast<int>(6 * (lane < 6 * kOffsetProbes ? q : 0));
+    const V3 accumNearFrontfaceDir = v3(__shfl(acc, b + 0), __shfl(acc, b + 1), __shfl(acc, b + 2));
+    const V3 accumBackfaceDir = v3(__shfl(acc, b + 3), __shfl(acc, b + 4), __shfl(acc, b + 5));
+    const uint32_t nc = __shfl(cnt, b + 0), bc = __shfl(cnt, b + 3);
+    if (live && c == 0) {
+        const uint32_t probeIdx = f.slots[slot].probe_index;
+        float4 cur = f.offsets[probeIdx];
+        V3 currentOffset = v3(cur.x, cur.y, cur.z);
+        V3 offset = splat(0.0f);
+        const float stepSize = 0.125f, lerpSpeed = 10.0f;
+        if (static_cast<float>(bc) / static_cast<float>(R) >= 0.25f)
+            offset = offset + normalize(accumBackfaceDir) * stepSize;
+        else if (nc >= 1)
+            offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
+        else
+            offset = offset - currentOffset * stepSize;
+        V3 newOffset = currentOffset + offset;
+        if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
+        newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
+        f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
+    }
+}
+
 } // namespace dev
+
+hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s)
+{
+    if (f.window_probes == 0 || !f.update_offsets) return hipSuccess;
+    const uint32_t blocks = (f.window_probes + dev::kOffsetProbes - 1) / dev::kOffsetProbes;
+    const size_t lds = static_cast<size_t>(f.R) * (sizeof(float4) + dev::kOffsetProbes);
+    hipLaunchKernelGGL(dev::k_probe_offsets, dim3(blocks), dim3(64), lds, s, f);
+    return hipGetLastError();
+}
 
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s)
 {
