@@ -290,18 +290,18 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
 /* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null
  * stream). Asynchronous: call ark_ddgi_synchronize or synchronize the stream before
  * reading.
- * Frames in flight: when this update's probe window shares no probe with the
- * previous update's (or the previous update did not move probes), uses the same
- * rays per probe, and no other writing operation (set_scene, write, load_state,
- * reset_history) came in between, its slot table and primary-ray traversal run on
- * an internal stream as soon as the update before the previous one is done, i.e.
- * overlapped with the previous update's shadow rays, shading and probe update. They
- * read only the scene, the sample order and this window's probe offsets, which no
- * update in flight writes; every result is the serial one. Everything else of the
- * update (shadow rays, shading, probe update, done_event) stays on `hip_stream`, so
- * the stream's completion still means the update is complete. A caller that writes
- * probe offsets through device pointers between updates should call
- * ark_ddgi_reset_history or ark_ddgi_write instead, or set ARK_DDGI_PIPELINE=0. */
+ * Frames in flight: when this update uses the same rays per probe as the previous
+ * one and no other writing operation (set_scene, write, load_state, reset_history)
+ * came in between, its slot table, primary-ray traversal and probe offsets run on an
+ * internal stream as soon as the update before the previous one is done (and after
+ * the previous update's offsets, on that stream), i.e. overlapped with the previous
+ * update's shadow rays, shading and atlas update. They read only the scene, the
+ * sample order and the probe offsets, which nothing in flight on `hip_stream` writes;
+ * every result is the serial one. Everything else of the update (shadow rays,
+ * shading, atlas update, done_event) stays on `hip_stream`, so the stream's
+ * completion still means the update is complete. A caller that writes probe offsets
+ * through device pointers between updates should use ark_ddgi_write instead, or set
+ * ARK_DDGI_PIPELINE=0. Instrumented updates (timing, counting) run serially. */
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
