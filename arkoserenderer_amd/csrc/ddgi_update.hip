@@ -362,13 +362,15 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
 // rounded to fp16 as the surfel stores it (raygen.rgen:108-139). So this kernel runs
 // right after the traversal, and with frames in flight the next frame's slot table
 // and traversal follow it on the traversal stream (ark_ddgi.cpp updateImpl).
-// One wave, 10 probes, 6 lanes per probe: lane c sums component c % 3 of the
-// directions of the rays of class 1 (near front face, c < 3) or 2 (back face) in ray
-// order, as the shader's loop does (adding +0 for the other rays leaves a sum
-// unchanged), and counts them.
+// 10 probes per workgroup: 256 threads stage the hit distances' classes (each
+// thread's loads in flight together), then one wave sums, 6 lanes per probe: lane c
+// sums component c % 3 of the directions of the rays of class 1 (near front face,
+// c < 3) or 2 (back face) in ray order, as the shader's loop does (adding +0 for the
+// other rays leaves a sum unchanged), and counts them.
 constexpr int kOffsetProbes = 10;
+constexpr int kOffsetBlock = 256;
 
-__global__ void __launch_bounds__(64) k_probe_offsets(FrameArgs f)
+__global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t R = f.R;
@@ -378,21 +380,35 @@ __global__ void __launch_bounds__(64) k_probe_offsets(FrameArgs f)
     const uint32_t slot0 = blockIdx.x * kOffsetProbes;
     const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
     const float maxOffset = minAxialSpacing / 2.0f;
-    for (uint32_t s = lane; s < R; s += 64) fibL[s] = f.fib[s];
-    for (uint32_t i = lane; i < kOffsetProbes * R; i += 64) {
-        const uint32_t p = i / R, s = i - p * R;
-        const uint32_t slot = slot0 + p;
-        uint8_t cls = 0;
-        if (slot < f.window_probes) {
-            const GpuHit h = f.hits[static_cast<size_t>(slot) * R + s];
-            // the surfel's distance (k_shade: miss, back face, front face)
-            const float dist = h.tri == kNoHit ? f.z_far : (h.t < 0.0f ? h.t * 0.2f : h.t);
-            const float a = f16_to_f32(f32_to_f16(dist));
-            cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
+    for (uint32_t s = lane; s < R; s += kOffsetBlock) fibL[s] = f.fib[s];
+    // 4 records per thread in flight at once
+    constexpr uint32_t kBatch = 4;
+    for (uint32_t i0 = 0; i0 < kOffsetProbes * R; i0 += kBatch * kOffsetBlock) {
+        GpuHit h[kBatch];
+        bool ok[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const uint32_t i = i0 + k * kOffsetBlock + lane;
+            const uint32_t p = i / R, s = i - p * R;
+            ok[k] = i < kOffsetProbes * R && slot0 + p < f.window_probes;
+            if (ok[k]) h[k] = f.hits[static_cast<size_t>(slot0 + p) * R + s];
         }
-        clsL[i] = cls;
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const uint32_t i = i0 + k * kOffsetBlock + lane;
+            if (i >= kOffsetProbes * R) continue;
+            uint8_t cls = 0;
+            if (ok[k]) {
+                // the surfel's distance (k_shade: miss, back face, front face)
+                const float dist = h[k].tri == kNoHit ? f.z_far : (h[k].t < 0.0f ? h[k].t * 0.2f : h[k].t);
+                const float a = f16_to_f32(f32_to_f16(dist));
+                cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
+            }
+            clsL[i] = cls;
+        }
     }
     __syncthreads();
+    if (lane >= 64) return;
     const uint32_t q = lane / 6, c = lane % 6;
     const uint32_t slot = slot0 + q;
     const bool live = lane < 6 * kOffsetProbes && slot < f.window_probes;
@@ -442,7 +458,7 @@ hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s)
     if (f.window_probes == 0 || !f.update_offsets) return hipSuccess;
     const uint32_t blocks = (f.window_probes + dev::kOffsetProbes - 1) / dev::kOffsetProbes;
     const size_t lds = static_cast<size_t>(f.R) * (sizeof(float4) + dev::kOffsetProbes);
-    hipLaunchKernelGGL(dev::k_probe_offsets, dim3(blocks), dim3(64), lds, s, f);
+    hipLaunchKernelGGL(dev::k_probe_offsets, dim3(blocks), dim3(dev::kOffsetBlock), lds, s, f);
     return hipGetLastError();
 }
 
