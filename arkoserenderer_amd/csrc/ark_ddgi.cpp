@@ -713,14 +713,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
 static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t K)
 {
     if (ctx->desc.shard_count <= 1) return K;
-    uint32_t n = 0;
-    const uint32_t N = static_cast<uint32_t>(ctx->N), XZ = static_cast<uint32_t>(ctx->X * ctx->Z);
-    for (uint32_t s = 0; s < K; ++s) {
-        uint32_t p = (first + s) % N;
-        int z = static_cast<int>((p % XZ) / static_cast<uint32_t>(ctx->X));
-        if (z >= ctx->slabZ0 && z < ctx->slabZ1) n++;
-    }
-    return n;
+    return slabRankOf(static_cast<uint32_t>(ctx->X), static_cast<uint32_t>(ctx->Y), static_cast<uint32_t>(ctx->Z), static_cast<uint32_t>(ctx->slabZ0),
+                      static_cast<uint32_t>(ctx->slabZ1), first, K);
 }
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);

@@ -28,6 +28,27 @@ constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in
 constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
 
+// Z-slab probes with an index below p (probe order x, then z, then y: a slab is
+// the z rows [z0, z1) of every y sheet, ddgi/common.glsl:53-67).
+__host__ __device__ inline uint32_t slabProbesBelow(uint32_t X, uint32_t Z, uint32_t z0, uint32_t z1, uint32_t p)
+{
+    const uint32_t XZ = X * Z, y = p / XZ, r = p - y * XZ, z = r / X, x = r - z * X;
+    const uint32_t zc = z < z0 ? z0 : (z > z1 ? z1 : z);
+    return y * X * (z1 - z0) + X * (zc - z0) + ((z >= z0 && z < z1) ? x : 0u);
+}
+
+// Slab probes among the first s window positions (probes first, first + 1, ... mod N):
+// the compacted slot of a slab probe at window position s, or the window's slab
+// probe count for s = K.
+__host__ __device__ inline uint32_t slabRankOf(uint32_t X, uint32_t Y, uint32_t Z, uint32_t z0, uint32_t z1, uint32_t first, uint32_t s)
+{
+    const uint32_t N = X * Y * Z;
+    const uint64_t end = static_cast<uint64_t>(first) + s;
+    if (end <= N) return slabProbesBelow(X, Z, z0, z1, static_cast<uint32_t>(end)) - slabProbesBelow(X, Z, z0, z1, first);
+    return slabProbesBelow(X, Z, z0, z1, N) - slabProbesBelow(X, Z, z0, z1, first) +
+           slabProbesBelow(X, Z, z0, z1, static_cast<uint32_t>(end - N));
+}
+
 // One shadow ray: origin + tmax, direction + owner ((probe ray << 4) | light).
 struct alignas(16) ShadowRay {
     float4 origin_tmax;

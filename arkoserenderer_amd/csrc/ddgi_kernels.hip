@@ -106,7 +106,8 @@ __device__ __forceinline__ bool inSlab(const FrameArgs& f, uint32_t probeIdx)
 }
 
 // Unsharded: slot s <-> probe (first + s) % N (raygen.rgen:113). Sharded (Z-slab):
-// a single workgroup compacts the window in order, so slots are deterministic.
+// the window's slab probes in window order, each slot from the closed-form count of
+// slab probes before it (slabRankOf), so slots are deterministic and one thread each.
 __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
 {
     const uint32_t N = static_cast<uint32_t>(f.X * f.Y * f.Z);
@@ -119,36 +120,14 @@ __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
         V3 e = sphericalFibonacciSample(sample, f.R);
         f.fib_order[tid] = make_float4(e.x, e.y, e.z, __uint_as_float(sample));
     }
-    if (f.sharded) return;
-    if (tid < f.window) writeSlot(f, tid, (tid + f.first) % N);
-}
-
-__global__ void __launch_bounds__(1024) k_probe_slots_sharded(FrameArgs f)
-{
-    __shared__ uint32_t waveCount[16];
-    __shared__ uint32_t base;
-    const uint32_t N = static_cast<uint32_t>(f.X * f.Y * f.Z);
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) base = 0;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < f.window; c0 += 1024u) {
-        uint32_t s = c0 + threadIdx.x;
-        uint32_t probeIdx = (s + f.first) % N;
-        bool keep = s < f.window && inSlab(f, probeIdx);
-        uint64_t m = __ballot(keep);
-        if (lane == 0) waveCount[wave] = static_cast<uint32_t>(__popcll(m));
-        __syncthreads();
-        uint32_t before = base;
-        for (uint32_t w = 0; w < wave; ++w) before += waveCount[w];
-        uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-        if (keep) writeSlot(f, before + rank, probeIdx);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t tot = 0;
-            for (uint32_t w = 0; w < 16; ++w) tot += waveCount[w];
-            base += tot;
-        }
-        __syncthreads();
+    if (tid >= f.window) return;
+    const uint32_t probeIdx = (tid + f.first) % N;
+    if (!f.sharded) {
+        writeSlot(f, tid, probeIdx);
+    } else if (inSlab(f, probeIdx)) {
+        writeSlot(f, slabRankOf(static_cast<uint32_t>(f.X), static_cast<uint32_t>(f.Y), static_cast<uint32_t>(f.Z), static_cast<uint32_t>(f.slab_z0),
+                                static_cast<uint32_t>(f.slab_z1), f.first, tid),
+                  probeIdx);
     }
 }
 
@@ -2036,10 +2015,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 // ---------------------------------------------------------------------------
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
 {
-    uint32_t n = f.sharded ? f.R : (f.window > f.R ? f.window : f.R);
-    uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(dev::k_probe_slots, dim3(blocks), dim3(256), 0, s, f);
-    if (f.sharded) hipLaunchKernelGGL(dev::k_probe_slots_sharded, dim3(1), dim3(1024), 0, s, f);
+    const uint32_t n = f.window > f.R ? f.window : f.R;
+    hipLaunchKernelGGL(dev::k_probe_slots, dim3((n + 255u) / 256u), dim3(256), 0, s, f);
     return hipGetLastError();
 }
 
