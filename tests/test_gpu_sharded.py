@@ -174,3 +174,44 @@ def test_overlapped_update_two_slabs_one_gpu():
         for c in ctxs:
             r = diff_report("atlas", c.read(which), o)
             assert r["mismatch"] == 0, (which, r)
+
+
+def test_bench_frame_loop_over_one_rank_rccl():
+    """bench.py's N > 1 frame loop as it runs on every rank: DDGINode.execute_overlapped
+    driven by OverlappedSlabExchange (torch events, a side stream, the in-place RCCL
+    all-gather of SlabExchange), here over a 1-rank communicator, several frames
+    enqueued without host synchronisation: the atlases and offsets equal a plain
+    node's (the exchange of one rank moves nothing, so only the event plumbing and
+    stream order are under test)."""
+    import torch
+    import torch.distributed as dist
+
+    from arkoserenderer_amd.collective import OverlappedSlabExchange, SlabExchange
+
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=512)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    plain, ranked = D.DDGINode(cfg), D.DDGINode(cfg)
+    assert plain.construct(sc, grid, ex["z_far"], device=0, **exposure)
+    assert ranked.construct(sc, grid, ex["z_far"], device=0, shard_rank=0, shard_count=1, **exposure)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29541"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        exch = OverlappedSlabExchange(ranked, SlabExchange.from_views(ranked.ctx.device_views(), 0, 1, dev).exchange, dev)
+        sptr = torch.cuda.current_stream(dev).cuda_stream
+        for f in range(6):
+            plain.execute(D.AppState(f), sptr)
+            exch.step(D.AppState(f), sptr)
+        torch.cuda.synchronize(dev)
+        for which in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS):
+            a, b = plain.ctx.read(which), ranked.ctx.read(which)
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), which
+    finally:
+        dist.destroy_process_group()
+        plain.ctx.close()
+        ranked.ctx.close()
