@@ -148,7 +148,7 @@ struct ArkDdgiCtx {
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
-    uint32_t smallTraceBlocks = 0; // primary-traversal grid of a pipelined small window
+    uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined update (frames in flight)
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
     uint32_t prevR = 0;
@@ -157,7 +157,6 @@ struct ArkDdgiCtx {
     hipEvent_t evTraced = nullptr, evFrameDone[2] = {};
     bool frameDoneValid[2] = { false, false };
     uint32_t lastParity = 0;       // buffer set of the last update (debug hit records)
-    int64_t slotOrderKeys[2] = { -1, -1 };
     uint32_t fibR[2] = { 0, 0 };
     uint64_t spillRegionWords = 0; // spill region 1 = the primary traversal's
     // scene
@@ -392,11 +391,13 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occS, kernel_shade_ptr(false), kShadeBlock, 0)) != hipSuccess) return bad(e, "occupancy shade");
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occW, kernel_trace_shadow_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy shadow");
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
-    // a pipelined small window's traversal shares the GPU with the previous frame's
-    // shadow rays, shading and update: 3 workgroups per CU leave them room (K = 2048
-    // windows, 0.5 M rays: 0.55 -> 0.48 ms per frame; K = 4096 unchanged at 3-6, 0.81
-    // at 2, so from 0.75 M rays on the full grid)
-    ctx->smallTraceBlocks = static_cast<uint32_t>(std::min(3, std::max(1, occT)) * ctx->cuCount);
+    // a pipelined update's traversal shares the GPU with the previous frame's shadow
+    // rays, shading and probe update: 3 workgroups per CU (half the occupancy) leave
+    // them room, whatever the window (tools/shard_proxy.py, tools/window_proxy.py,
+    // profiles/r02_m13-15: Z-slab steps P = 8 0.705 -> 0.640 ms, P = 4 1.21 -> 1.11,
+    // P = 2 2.22 -> 2.10; K = 4096 windows 0.72 -> 0.65, K = 2048 0.43 unchanged; the
+    // whole grid 4.11 -> 4.09; 2 per CU: P = 8 0.72, 4 per CU: 0.69)
+    ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(3, std::max(1, occT)) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
     ctx->shadowBlocksPerCu = static_cast<uint32_t>(std::max(1, occW));
@@ -818,20 +819,11 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, kRayCounterWords * 4, ts));
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
+    f.slot_order = ctx->slotOrder.as<uint32_t>() + b * Kmax; // written by k_probe_slots
     ARK_HIP(launch_probe_slots(f, ts));
-    {
-        // slot traversal order (k_slot_order): rebuilt when the window moves
-        f.slot_order = ctx->slotOrder.as<uint32_t>() + b * Kmax;
-        const int64_t key = (static_cast<int64_t>(f.first) << 32) | K;
-        if (key != ctx->slotOrderKeys[b]) {
-            ARK_HIP(launch_slot_order(f, const_cast<uint32_t*>(f.slot_order), ts));
-            ctx->slotOrderKeys[b] = key;
-        }
-    }
     if (f.window_probes > 0) {
         RoctxRange traceZone("Trace rays");
-        const bool small = pipe && f.window_rays < (3u << 18);
-        ARK_HIP(launch_trace(ctx->scene, f, small ? ctx->smallTraceBlocks : ctx->traceBlocks, count, ts));
+        ARK_HIP(launch_trace(ctx->scene, f, pipe ? ctx->pipeTraceBlocks : ctx->traceBlocks, count, ts));
         if (pipe) {
             // probeUpdateOffset (k_probe_offsets: from the hit records), so that the
             // next frame's slot table may follow on this stream

@@ -28,25 +28,86 @@ constexpr int kShadeChunk = 1024;  // probe rays per shading block iteration (in
 constexpr int kMaxLights = 11;     // 1 directional + 10 spot lights (GpuScene.cpp:430)
 constexpr uint32_t kNoHit = 0xffffffffu;
 
-// Z-slab probes with an index below p (probe order x, then z, then y: a slab is
-// the z rows [z0, z1) of every y sheet, ddgi/common.glsl:53-67).
-__host__ __device__ inline uint32_t slabProbesBelow(uint32_t X, uint32_t Z, uint32_t z0, uint32_t z1, uint32_t p)
+// Probe index p as (y, z, x) of the probe order x, then z, then y (ddgi/common.glsl:53-67).
+struct ProbeXZY {
+    uint32_t y, z, x;
+};
+
+__host__ __device__ inline ProbeXZY probeXZY(uint32_t X, uint32_t Z, uint32_t p)
 {
-    const uint32_t XZ = X * Z, y = p / XZ, r = p - y * XZ, z = r / X, x = r - z * X;
-    const uint32_t zc = z < z0 ? z0 : (z > z1 ? z1 : z);
-    return y * X * (z1 - z0) + X * (zc - z0) + ((z >= z0 && z < z1) ? x : 0u);
+    const uint32_t XZ = X * Z, y = p / XZ, r = p - y * XZ, z = r / X;
+    return { y, z, r - z * X };
 }
 
-// Slab probes among the first s window positions (probes first, first + 1, ... mod N):
+// Probes with an index below q's that lie in the box x in [xa, xb), z in [za, zb)
+// (every y).
+__host__ __device__ inline uint32_t boxProbesBelow(ProbeXZY q, uint32_t xa, uint32_t xb, uint32_t za, uint32_t zb)
+{
+    const uint32_t zc = q.z < za ? za : (q.z > zb ? zb : q.z);
+    const uint32_t xc = q.x < xa ? xa : (q.x > xb ? xb : q.x);
+    return q.y * (xb - xa) * (zb - za) + (xb - xa) * (zc - za) + ((q.z >= za && q.z < zb) ? xc - xa : 0u);
+}
+
+// Box probes among the first s window positions (probes first, first + 1, ... mod N).
+__host__ __device__ inline uint32_t windowBoxCount(uint32_t X, uint32_t Y, uint32_t Z, uint32_t first, uint32_t s, uint32_t xa, uint32_t xb, uint32_t za,
+                                                   uint32_t zb)
+{
+    const uint32_t N = X * Y * Z;
+    const uint64_t end = static_cast<uint64_t>(first) + s;
+    const uint32_t below = boxProbesBelow(probeXZY(X, Z, first), xa, xb, za, zb);
+    if (end <= N) return boxProbesBelow(probeXZY(X, Z, static_cast<uint32_t>(end)), xa, xb, za, zb) - below;
+    return Y * (xb - xa) * (zb - za) - below + boxProbesBelow(probeXZY(X, Z, static_cast<uint32_t>(end - N)), xa, xb, za, zb);
+}
+
+// Slab probes (z rows [z0, z1) of every y sheet) among the first s window positions:
 // the compacted slot of a slab probe at window position s, or the window's slab
 // probe count for s = K.
 __host__ __device__ inline uint32_t slabRankOf(uint32_t X, uint32_t Y, uint32_t Z, uint32_t z0, uint32_t z1, uint32_t first, uint32_t s)
 {
-    const uint32_t N = X * Y * Z;
-    const uint64_t end = static_cast<uint64_t>(first) + s;
-    if (end <= N) return slabProbesBelow(X, Z, z0, z1, static_cast<uint32_t>(end)) - slabProbesBelow(X, Z, z0, z1, first);
-    return slabProbesBelow(X, Z, z0, z1, N) - slabProbesBelow(X, Z, z0, z1, first) +
-           slabProbesBelow(X, Z, z0, z1, static_cast<uint32_t>(end - N));
+    return windowBoxCount(X, Y, Z, first, s, 0u, X, z0, z1);
+}
+
+// Traversal-order bucket of a window probe (kRayParts = 8 blocks of the x-z plane:
+// 4 along x and 2 along z of the slab [zlo, zlo + zext), or 8 along x for a one-layer
+// slab) and the bucket's box.
+__host__ __device__ inline uint32_t slotBucketOf(uint32_t X, uint32_t zlo, uint32_t zext, uint32_t x, uint32_t z)
+{
+    if (zext >= 2) return x * 4u / X + 4u * ((z - zlo) * 2u / zext < 1u ? 0u : 1u);
+    return x * 8u / X;
+}
+
+__host__ __device__ inline void slotBucketBox(uint32_t X, uint32_t zlo, uint32_t zext, uint32_t b, uint32_t& xa, uint32_t& xb, uint32_t& za, uint32_t& zb)
+{
+    if (zext >= 2) {
+        const uint32_t bx = b & 3u, zm = (zext + 1u) / 2u;
+        xa = (bx * X + 3u) / 4u;
+        xb = ((bx + 1u) * X + 3u) / 4u;
+        za = zlo + ((b >> 2) ? zm : 0u);
+        zb = zlo + ((b >> 2) ? zext : zm);
+    } else {
+        xa = (b * X + 7u) / 8u;
+        xb = ((b + 1u) * X + 7u) / 8u;
+        za = zlo;
+        zb = zlo + zext;
+    }
+}
+
+// Queue position of the window probe at window position s (probe p = (first + s) % N,
+// inside the slab [zlo, zlo + zext)): the stable bucket sort of the window's slots by
+// slotBucketOf, in closed form - the window probes of lower buckets, then those of its
+// own bucket at earlier window positions.
+__host__ __device__ inline uint32_t slotQueuePos(uint32_t X, uint32_t Y, uint32_t Z, uint32_t zlo, uint32_t zext, uint32_t first, uint32_t K, uint32_t s,
+                                                 uint32_t p)
+{
+    const ProbeXZY q = probeXZY(X, Z, p);
+    const uint32_t b = slotBucketOf(X, zlo, zext, q.x, q.z);
+    uint32_t xa, xb, za, zb, pos = 0;
+    for (uint32_t k = 0; k < b; ++k) {
+        slotBucketBox(X, zlo, zext, k, xa, xb, za, zb);
+        pos += windowBoxCount(X, Y, Z, first, K, xa, xb, za, zb);
+    }
+    slotBucketBox(X, zlo, zext, b, xa, xb, za, zb);
+    return pos + windowBoxCount(X, Y, Z, first, s, xa, xb, za, zb);
 }
 
 // One shadow ray: origin + tmax, direction + owner ((probe ray << 4) | light).
@@ -173,7 +234,6 @@ hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, 
 hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const ArkReflectionsDesc& r, uint32_t traceBlocks, uint32_t shadowBlocks,
                                  hipStream_t s);
 hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hipStream_t s);
-hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s);
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);

@@ -2,8 +2,8 @@
 //
 // One update (DDGINode.cpp:132-259) is these launches on one stream:
 //   1. k_probe_slots    window -> slot table (probe position + offset, per-probe
-//                       ray rotation) and the spherical-Fibonacci table
-//                       (+ k_slot_order when the window moves).
+//                       ray rotation), the slots' traversal order and the
+//                       spherical-Fibonacci table.
 //   2. k_trace          persistent traversal of all K*R probe rays: opaque pass
 //                       (closest hit) then masked pass (alpha-tested any-hit),
 //                       software 8-wide quantized BVH (80 B nodes) with a per-lane
@@ -108,9 +108,19 @@ __device__ __forceinline__ bool inSlab(const FrameArgs& f, uint32_t probeIdx)
 // Unsharded: slot s <-> probe (first + s) % N (raygen.rgen:113). Sharded (Z-slab):
 // the window's slab probes in window order, each slot from the closed-form count of
 // slab probes before it (slabRankOf), so slots are deterministic and one thread each.
+// Traversal order of the slots (f.slot_order: queue position -> slot), in the same
+// pass: the probes are cut into 8 blocks of the x-z plane (4 along x, 2 along z, or
+// 8 along x for a one-layer slab) and each block's slots keep their window order,
+// whose slowest coordinate is y (a stable bucket sort, in closed form: slotQueuePos).
+// The trace and shade queues hand the 8 per-XCD partitions out in this order, so
+// partition p sweeps block p bottom to top and all XCDs work on the same few y-layers
+// at any time: the chip-wide working set of BVH nodes and triangles is one slice of
+// the scene (Infinity Cache sized) instead of eight. Only the order of work changes,
+// never a result.
 __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
 {
-    const uint32_t N = static_cast<uint32_t>(f.X * f.Y * f.Z);
+    const uint32_t X = static_cast<uint32_t>(f.X), Y = static_cast<uint32_t>(f.Y), Z = static_cast<uint32_t>(f.Z);
+    const uint32_t N = X * Y * Z;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid < f.R) {
         V3 d = sphericalFibonacciSample(tid, f.R);
@@ -122,76 +132,12 @@ __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
     }
     if (tid >= f.window) return;
     const uint32_t probeIdx = (tid + f.first) % N;
-    if (!f.sharded) {
-        writeSlot(f, tid, probeIdx);
-    } else if (inSlab(f, probeIdx)) {
-        writeSlot(f, slabRankOf(static_cast<uint32_t>(f.X), static_cast<uint32_t>(f.Y), static_cast<uint32_t>(f.Z), static_cast<uint32_t>(f.slab_z0),
-                                static_cast<uint32_t>(f.slab_z1), f.first, tid),
-                  probeIdx);
-    }
-}
-
-// Traversal order of the window's slots (one workgroup; a stable bucket sort).
-// The probes are cut into 8 blocks of the x-z plane (4 along x, 2 along z, or 8
-// along x for a one-layer slab) and each block's slots keep their window order,
-// whose slowest coordinate is y. The trace and shade queues hand the 8 per-XCD
-// partitions out in this order, so partition p sweeps block p bottom to top and
-// all XCDs work on the same few y-layers at any time: the chip-wide working set
-// of BVH nodes and triangles is one slice of the scene (Infinity Cache sized)
-// instead of eight. Only the order of work changes, never a result.
-__global__ void __launch_bounds__(1024) k_slot_order(FrameArgs f, uint32_t* __restrict__ order)
-{
-    __shared__ uint32_t waveCount[16][8];
-    __shared__ uint32_t bucketBase[8];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t n = f.window_probes;
-    const int zlo = f.sharded ? f.slab_z0 : 0, zhi = f.sharded ? f.slab_z1 : f.Z;
-    const int zext = max(1, zhi - zlo);
-    auto bucketOf = [&](uint32_t slot) -> uint32_t {
-        const uint32_t probeIdx = f.slots[slot].probe_index;
-        const uint32_t sheetProbeIdx = probeIdx % static_cast<uint32_t>(f.X * f.Z);
-        const int x = static_cast<int>(sheetProbeIdx % static_cast<uint32_t>(f.X));
-        const int z = static_cast<int>(sheetProbeIdx / static_cast<uint32_t>(f.X)) - zlo;
-        if (zext >= 2) return static_cast<uint32_t>(x * 4 / f.X + 4 * min(1, z * 2 / zext));
-        return static_cast<uint32_t>(x * 8 / f.X);
-    };
-    if (threadIdx.x < 8) bucketBase[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint32_t s = threadIdx.x; s < n; s += 1024u) atomicAdd(&bucketBase[bucketOf(s)], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < 8; ++b) {
-            const uint32_t c = bucketBase[b];
-            bucketBase[b] = acc;
-            acc += c;
-        }
-    }
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < n; c0 += 1024u) {
-        const uint32_t s = c0 + threadIdx.x;
-        const bool valid = s < n;
-        const uint32_t b = valid ? bucketOf(s) : 8u;
-        uint32_t rank = 0;
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint64_t m = __ballot(b == k);
-            if (b == k) rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-            if (lane == 0) waveCount[wave][k] = static_cast<uint32_t>(__popcll(m));
-        }
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = bucketBase[b] + rank;
-            for (uint32_t w = 0; w < wave; ++w) pos += waveCount[w][b];
-            order[pos] = s;
-        }
-        __syncthreads();
-        if (threadIdx.x < 8) {
-            uint32_t tot = 0;
-            for (uint32_t w = 0; w < 16; ++w) tot += waveCount[w][threadIdx.x];
-            bucketBase[threadIdx.x] += tot;
-        }
-        __syncthreads();
-    }
+    const uint32_t z0 = f.sharded ? static_cast<uint32_t>(f.slab_z0) : 0u, z1 = f.sharded ? static_cast<uint32_t>(f.slab_z1) : Z;
+    if (f.sharded && !inSlab(f, probeIdx)) return;
+    const uint32_t slot = f.sharded ? slabRankOf(X, Y, Z, z0, z1, f.first, tid) : tid;
+    writeSlot(f, slot, probeIdx);
+    if (f.slot_order)
+        const_cast<uint32_t*>(f.slot_order)[slotQueuePos(X, Y, Z, z0, max(1u, z1 - z0), f.first, f.window, tid, probeIdx)] = slot;
 }
 
 // queue position -> slot (identity without an order table)
@@ -2017,13 +1963,6 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
 {
     const uint32_t n = f.window > f.R ? f.window : f.R;
     hipLaunchKernelGGL(dev::k_probe_slots, dim3((n + 255u) / 256u), dim3(256), 0, s, f);
-    return hipGetLastError();
-}
-
-hipError_t launch_slot_order(const FrameArgs& f, uint32_t* order, hipStream_t s)
-{
-    if (f.window_probes == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_slot_order, dim3(1), dim3(1024), 0, s, f, order);
     return hipGetLastError();
 }
 

@@ -40,7 +40,7 @@ def _tile_mask(dims, probes, res):
 
 def _windows(dims, count):
     """`count` windows of 32 consecutive probes (one x run at fixed y, z; x spans all
-    four x blocks of k_slot_order) with z covering every Z-slab of 8 and y spread."""
+    four x blocks of the slot traversal order) with z covering every Z-slab of 8 and y spread."""
     X, Y, Z = dims
     n = min(32, X)
     out = []
