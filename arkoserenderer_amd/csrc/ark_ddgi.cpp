@@ -28,6 +28,9 @@ using namespace ark;
 
 namespace {
 
+// pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
+constexpr uint32_t kPipeHalfRays = 5u << 20;
+
 // roctx range over a scope (host-side enqueue markers, named after the reference's
 // ScopedDebugZone labels, DDGINode.cpp:152-247); end() closes it early.
 class RoctxRange {
@@ -148,7 +151,7 @@ struct ArkDdgiCtx {
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
-    uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined update (frames in flight)
+    uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined window below kPipeHalfRays rays
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
     uint32_t prevR = 0;
@@ -392,11 +395,12 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occW, kernel_trace_shadow_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy shadow");
     ctx->traceBlocks = static_cast<uint32_t>(std::max(1, occT) * ctx->cuCount);
     // a pipelined update's traversal shares the GPU with the previous frame's shadow
-    // rays, shading and probe update: 3 workgroups per CU (half the occupancy) leave
-    // them room, whatever the window (tools/shard_proxy.py, tools/window_proxy.py,
-    // profiles/r02_m13-15: Z-slab steps P = 8 0.705 -> 0.640 ms, P = 4 1.21 -> 1.11,
-    // P = 2 2.22 -> 2.10; K = 4096 windows 0.72 -> 0.65, K = 2048 0.43 unchanged; the
-    // whole grid 4.11 -> 4.09; 2 per CU: P = 8 0.72, 4 per CU: 0.69)
+    // rays, shading and probe update: below kPipeHalfRays rays, 3 workgroups per CU
+    // (half the occupancy) leave them room (tools/shard_proxy.py,
+    // tools/window_proxy.py, profiles/r02_m13-15: Z-slab steps P = 8 0.705 -> 0.640 ms,
+    // P = 4 1.21 -> 1.11, P = 2 2.22 -> 2.10; K = 4096 windows 0.72 -> 0.65, K = 2048
+    // 0.43 unchanged; 2 per CU: P = 8 0.72, 4 per CU: 0.69). The whole C4 grid (8.4 M
+    // rays) keeps the full grid: 4.059 vs 4.067 ms per step at 3 (profiles/r02_m17_ab).
     ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(3, std::max(1, occT)) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
@@ -823,7 +827,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     ARK_HIP(launch_probe_slots(f, ts));
     if (f.window_probes > 0) {
         RoctxRange traceZone("Trace rays");
-        ARK_HIP(launch_trace(ctx->scene, f, pipe ? ctx->pipeTraceBlocks : ctx->traceBlocks, count, ts));
+        const bool half = pipe && f.window_rays < kPipeHalfRays;
+        ARK_HIP(launch_trace(ctx->scene, f, half ? ctx->pipeTraceBlocks : ctx->traceBlocks, count, ts));
         if (pipe) {
             // probeUpdateOffset (k_probe_offsets: from the hit records), so that the
             // next frame's slot table may follow on this stream

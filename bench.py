@@ -52,8 +52,8 @@ SHADOW_RAY_BYTES = 32  # ShadowRay record (written by k_shadow_gen, read by k_tr
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--triangles", type=int, default=10_000_000)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--rays", type=int, default=256)
