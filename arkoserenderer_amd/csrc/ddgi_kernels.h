@@ -14,7 +14,11 @@ namespace ark {
 #define ARK_STACK_LDS 8
 #endif
 #ifndef ARK_LDS_NODES
-#define ARK_LDS_NODES 128
+// 64 top nodes (5 KB of LDS per traversal workgroup instead of 10): the traversal itself
+// is unchanged (2.29-2.35 ms serially), but with frames in flight the previous frame's
+// kernels find LDS beside it: C4 step 4.06 -> 4.00 ms (128 -> 64; 32: 3.98 ms but the
+// reference windows 1 % slower; stack entries 4 instead of 8 spill: +6 %), profiles/r02_m22-23
+#define ARK_LDS_NODES 64
 #endif
 constexpr int kStackLds = ARK_STACK_LDS; // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
 constexpr int kTraceBlock = 256;
