@@ -12,9 +12,12 @@ Besides `value`, rank 0 at N = 1 reports: the reference's own windows (K = 4096,
 the node's cap, DDGINode.h:23; K = 2048, its default, DDGINode.h:31) with per-kernel
 times; config C2 (Cornell 8^3 x 64) on the GPU; the CPU baseline (the oracle on the
 box's host cores, one warm-up then the median of >= 5 frames, C4 and C2); the C1 AO
-bake; the DDGI consumers. The roofline object carries the algorithmic-bytes
-fraction (SURVEY §8d model) and, from a rocprofv3 PMC pass of this same library
-build (matched by its sha256), the measured HBM traffic and its fraction.
+bake; the DDGI consumers. The roofline object's `achieved` / `frac` are the
+measured HBM traffic of the dominant kernel (a rocprofv3 PMC pass of this same
+library build, matched by its sha256) over its HIP-event launch time; the SURVEY
+§8d algorithmic model is kept beside it as `cache_inclusive_frac` (most of its
+node fetches hit L2 / Infinity Cache), with the VALU issue fractions and the
+whole-update figures (roofline()).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -177,23 +180,8 @@ def main():
     kernel_bytes = algorithmic_bytes(cnt, R)
     kernel_ms = {"k_trace": avg[1], "k_shade": avg[2], "k_shadow": avg[4], "k_probe_update": avg[3]}
     dom = max(kernel_ms, key=kernel_ms.get)
-    achieved = kernel_bytes[dom] / (kernel_ms[dom] * 1e-3) / 1e9
-    roof = {
-        # the roofline the kernel is priced against is HBM (no dense contraction: no
-        # MFMA); what limits it is instruction issue and dependent-fetch latency (SQ
-        # counters below): 83 % of its algorithmic bytes are L2/MALL hits
-        "bound": "latency",
-        "roofline": "hbm",
-        "kernel": dom,
-        "achieved": round(achieved, 2),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "algorithmic_bytes_per_launch": int(kernel_bytes[dom]),
-        "avg_launch_ms": round(kernel_ms[dom], 4),
-    }
-    roof.update(measured_traffic(args.pmc, dom, lib_sha, args, G, kernel_ms[dom]))
-    roof.update(sq_limiter(args.sq, dom, lib_sha))
+    ms_per_step = dt / args.steps * 1e3
+    roof = roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G)
 
     result = {
         "metric": "Mrays/s + probes-updated/s, DDGI 32^3 grid x 256 rays, at 1/2/4/8 MI355X",
@@ -203,7 +191,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -290,55 +278,102 @@ def per_ray(cnt):
 PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow"], "k_probe_update": ["k_probe_update"]}
 
 
-def measured_traffic(path, dom, lib_sha, args, G, launch_ms):
-    """HBM bytes per launch from the PMC summary of THIS library build
-    (tools/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction of
-    MI355X_MICROARCH.md), on the same workload; null otherwise."""
-    out = {"traffic": None, "traffic_frac": None, "traffic_source": None}
+# every kernel of one probe-path update (the whole-update counter figure)
+PMC_PATH_KERNELS = ("k_probe_slots", "k_trace", "k_probe_offsets", "k_shadow_gen", "k_trace_shadow", "k_shade", "k_probe_update")
+CLOCK_GHZ = 2.4      # MI355X max engine clock (MI355X_MICROARCH.md); the VALU fractions below use it
+SIMDS = 256 * 4      # 256 CUs x 4 SIMDs
+WAVE64_VALU_CYCLES = 2  # a wave64 VALU instruction issues over 2 cycles on the 32-wide CDNA4 SIMD
+
+
+def _load_summary(path, lib_sha, what):
+    """A profiles/ summary of THIS library build (matched by sha256), or (None, why).
+    PMC summaries keep the hash under config, SQ summaries at the top."""
     if not os.path.exists(path):
-        out["traffic_source"] = "no PMC summary"
-        return out
+        return None, f"no {what} summary"
     try:
         with open(path) as fh:
-            pm = json.load(fh)
+            j = json.load(fh)
     except (OSError, ValueError) as e:
-        out["traffic_source"] = f"unreadable PMC summary: {e}"
-        return out
-    cfg = pm.get("config", {})
-    if cfg.get("lib_sha16") != lib_sha:
-        out["traffic_source"] = f"PMC summary {pm.get('tag')} is of another build ({cfg.get('lib_sha16')}): not used"
-        return out
-    if cfg.get("triangles") != args.triangles or cfg.get("grid") != G:
-        out["traffic_source"] = f"PMC summary {pm.get('tag')} is of another workload: not used"
-        return out
-    ks = [pm["kernels"].get(k) for k in PMC_KERNELS[dom]]
-    if any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
-        out["traffic_source"] = f"PMC summary {pm.get('tag')} lacks {dom}"
-        return out
-    traffic = sum(k["hbm_bytes_per_launch"] for k in ks)
-    out["traffic"] = int(traffic)
-    out["traffic_frac"] = round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    out["traffic_source"] = pm.get("source")
-    return out
+        return None, f"unreadable {what} summary: {e}"
+    sha = j.get("config", {}).get("lib_sha16") if "config" in j else j.get("lib_sha16")
+    if sha != lib_sha:
+        return None, f"{what} summary {j.get('tag')} is of another build ({sha}): not used"
+    return j, None
 
 
-def sq_limiter(path, dom, lib_sha):
-    """SQ counter evidence for the limiter (tools/sq_summary.py --json) of this build."""
-    if not os.path.exists(path):
-        return {"limiter_evidence": None}
-    try:
-        with open(path) as fh:
-            sq = json.load(fh)
-    except (OSError, ValueError):
-        return {"limiter_evidence": None}
-    if sq.get("lib_sha16") != lib_sha:
-        return {"limiter_evidence": f"SQ summary {sq.get('tag')} is of another build: not used"}
-    k = sq.get("kernels", {}).get(PMC_KERNELS[dom][0] if dom != "k_shadow" else "k_trace_shadow")
-    if k is None:
-        return {"limiter_evidence": None}
-    return {"limiter_evidence": {key: k[key] for key in ("valu_active_per_wave", "wait_inst_any_per_wave", "wait_any_per_wave",
-                                                          "valu_insts_per_launch", "l2_hit") if key in k}
-            | {"source": sq.get("source")}}
+def roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G):
+    """The roofline object of the dominant kernel plus the whole update.
+
+    `achieved` / `frac` are MEASURED HBM bytes: (2 FETCH_SIZE + WRITE_SIZE) x 1024 per
+    launch (tools/pmc_summary.py; the gfx950 FETCH_SIZE halving of MI355X_MICROARCH.md
+    §HBM) from a rocprofv3 PMC pass of this same library build, divided by this run's
+    HIP-event launch time. The SURVEY §8(d) algorithmic model (80-B nodes and 48-B
+    triangles per visit, counter-instrumented visit counts) is kept beside it as
+    `cache_inclusive_*`: it counts every node fetch, and most of them are L2 / Infinity
+    Cache hits (LDS-cached top nodes included), so it is a cache-inclusive request
+    rate, not HBM traffic. `valu_issue_frac` = VALU wave-instructions / (1024 SIMDs x
+    2.4 GHz x t); `valu_simd_busy_frac` counts the 2 cycles a wave64 VALU instruction
+    occupies a 32-wide SIMD."""
+    t = kernel_ms[dom] * 1e-3
+    alg = kernel_bytes[dom]
+    roof = {
+        # priced against HBM (no dense contraction, no MFMA); limited by instruction
+        # issue and dependent-fetch latency (SQ counters below)
+        "bound": "latency",
+        "roofline": "hbm",
+        "kernel": dom,
+        "achieved": None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": None,
+        "traffic": None,
+        "avg_launch_ms": round(kernel_ms[dom], 4),
+        "algorithmic_bytes_per_launch": int(alg),
+        "cache_inclusive_achieved": round(alg / t / 1e9, 2),
+        "cache_inclusive_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    pm, why = _load_summary(args.pmc, lib_sha, "PMC")
+    if pm is not None:
+        cfg = pm.get("config", {})
+        if cfg.get("triangles") != args.triangles or cfg.get("grid") != G:
+            pm, why = None, f"PMC summary {pm.get('tag')} is of another workload: not used"
+    if pm is not None:
+        ks = [pm["kernels"].get(k) for k in PMC_KERNELS[dom]]
+        if any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
+            pm, why = None, f"PMC summary {pm.get('tag')} lacks {dom}"
+    if pm is not None:
+        traffic = sum(k["hbm_bytes_per_launch"] for k in ks)
+        roof["traffic"] = int(traffic)
+        roof["achieved"] = round(traffic / t / 1e9, 2)
+        roof["frac"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 4)
+        roof["traffic_source"] = pm.get("source")
+        roof["traffic_profile_avg_launch_ms"] = round(sum(k["avg_ms"] for k in ks), 4)
+    else:
+        roof["traffic_source"] = why
+    sq, why_sq = _load_summary(args.sq, lib_sha, "SQ")
+    sq_kernel = PMC_KERNELS[dom][0] if dom != "k_shadow" else "k_trace_shadow"
+    k = sq.get("kernels", {}).get(sq_kernel) if sq else None
+    if k is not None:
+        valu = k.get("valu_insts_per_launch", 0)
+        roof["valu_issue_frac"] = round(valu / (SIMDS * CLOCK_GHZ * 1e9 * t), 4)
+        roof["valu_simd_busy_frac"] = round(valu * WAVE64_VALU_CYCLES / (SIMDS * CLOCK_GHZ * 1e9 * t), 4)
+        roof["limiter_evidence"] = {key: k[key] for key in ("valu_active_per_wave", "wait_inst_any_per_wave", "wait_any_per_wave",
+                                                             "valu_insts_per_launch", "salu_insts_per_launch", "l2_hit",
+                                                             "clock_ghz_effective") if key in k} | {"source": sq.get("source")}
+    else:
+        roof["limiter_evidence"] = why_sq
+    # the whole update (SURVEY §8(d): (sum B_ray + sum B_probe) / wall time of the update)
+    step_alg = sum(kernel_bytes.values())
+    whole = {"ms_per_step": round(ms_per_step, 4), "algorithmic_bytes_per_step": int(step_alg),
+             "cache_inclusive_achieved": round(step_alg / (ms_per_step * 1e-3) / 1e9, 2),
+             "cache_inclusive_frac": round(step_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+             "hbm_bytes_per_step": None, "achieved": None, "frac": None}
+    if pm is not None and all(k in pm["kernels"] and "hbm_bytes_per_launch" in pm["kernels"][k] for k in PMC_PATH_KERNELS):
+        hbm = sum(pm["kernels"][k]["hbm_bytes_per_launch"] for k in PMC_PATH_KERNELS)
+        whole.update(hbm_bytes_per_step=int(hbm), achieved=round(hbm / (ms_per_step * 1e-3) / 1e9, 2),
+                     frac=round(hbm / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    roof["whole_update"] = whole
+    return roof
 
 
 def reference_windows(node, ctx, torch, device, sptr, frame0):
@@ -536,7 +571,11 @@ def rt_reflections_line(args, torch, ctx):
     e1.record(side)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    traced = int(((g["depth"] < 1.0 - 1e-6) & (g["material"][..., 0] / 255.0 < 0.7)).sum())
+    # the pixels k_refl_setup traces, in its fp32 arithmetic: depth < 1 - 1e-6 and
+    # roughness = material.r / 255 below the descriptor's no-tracing roughness
+    depth_ok = g["depth"].astype(np.float32) < np.float32(1.0) - np.float32(1e-6)
+    rough = g["material"][..., 0].astype(np.float32) / np.float32(255.0)
+    traced = int((depth_ok & (rough < np.float32(d.no_tracing_roughness))).sum())
     return {
         "workload": f"{W}x{H} pixels ({traced} traced), synthetic G-buffer, C4 scene + atlases",
         "gpu_ms": round(ms, 4),

@@ -1324,10 +1324,27 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
     const uint32_t first = p->first_probe_index % N;
     const uint32_t frameIdx = p->frame_index;
     std::vector<Stats> tstats(std::max(threads, 1));
+    // The window's probes by slot (raygen.rgen:113: slot s <-> probe (first + s) % N).
+    // A Z-slab shard (desc.shard_rank of desc.shard_count) updates only the
+    // window probes whose z lies in its slab [r Z/P, (r+1) Z/P), in window order, at
+    // compacted slots - the slot assignment of k_probe_slots, restated plainly.
+    std::vector<uint32_t> window;
+    window.reserve(K);
+    {
+        const int P = std::max(1, static_cast<int>(o.desc.shard_count));
+        const int z0 = o.desc.shard_rank * (g.Z / P), z1 = z0 + g.Z / P;
+        for (uint32_t s = 0; s < K; ++s) {
+            const uint32_t probeIdx = (s + first) % N;
+            int x, y, z;
+            probeCoord(g, probeIdx, &x, &y, &z);
+            if (P == 1 || (z >= z0 && z < z1)) window.push_back(probeIdx);
+        }
+    }
+    const int W = static_cast<int>(window.size());
 
     // 1. trace rays (raygen.rgen main, launch (K, R))
-    parallelFor(static_cast<int>(K), threads, [&](int slot, int tid) {
-        uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+    parallelFor(W, threads, [&](int slot, int tid) {
+        uint32_t probeIdx = window[slot];
         V3 pos = probePosition(g, probeIdx);
         const float* off = &o.offsets[static_cast<size_t>(probeIdx) * 4];
         pos = pos + v3(off[0], off[1], off[2]);
@@ -1342,8 +1359,8 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
 
     // 2+3. irradiance & visibility update (probeUpdateIrradiance.comp / probeUpdateVisibility.comp)
     const float gridMaxSpacing = fmaxf_(g.spacing.x, fmaxf_(g.spacing.y, g.spacing.z)); // DDGINode.cpp:148
-    parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
-        uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+    parallelFor(W, threads, [&](int slot, int) {
+        uint32_t probeIdx = window[slot];
         std::vector<V3> dirs(R);
         for (uint32_t s = 0; s < R; ++s) dirs[s] = calculateRotatedSphericalFibonacciSample(probeIdx, s, R, frameIdx);
         const uint16_t* sf = &o.surfels[static_cast<size_t>(slot) * o.Rmax * 4];
@@ -1444,8 +1461,8 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
     if (p->update_offsets) {
         const float minAxialSpacing = fminf_(g.spacing.x, fminf_(g.spacing.y, g.spacing.z));
         const float maxOffset = minAxialSpacing / 2.0f; // DDGINode.cpp:248-250
-        parallelFor(static_cast<int>(K), threads, [&](int slot, int) {
-            uint32_t probeIdx = (static_cast<uint32_t>(slot) + first) % N;
+        parallelFor(W, threads, [&](int slot, int) {
+            uint32_t probeIdx = window[slot];
             const uint16_t* sf = &o.surfels[static_cast<size_t>(slot) * o.Rmax * 4];
             float* cur = &o.offsets[static_cast<size_t>(probeIdx) * 4];
             V3 currentOffset = v3(cur[0], cur[1], cur[2]);

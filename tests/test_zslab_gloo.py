@@ -1,7 +1,13 @@
-"""Z-slab sharding over 2 ranks with the gloo backend on CPU: each rank updates
-only its slab (here: the oracle's full update with the other band discarded),
-then SlabExchange's in-place all-gather must rebuild exactly the unsharded
-atlases. Exercises the same exchange code bench.py runs over RCCL."""
+"""Z-slab sharding over 2 and 4 ranks with the gloo backend on CPU, for real: each
+rank runs a SHARDED oracle (desc shard_rank / shard_count: it traces, shades and
+updates only the window probes of its own slab, at compacted slots, as
+k_probe_slots does), then SlabExchange's in-place all-gather of the atlas row bands
+(the code bench.py runs over RCCL) hands every rank the other slabs' tiles, which
+are written back into its oracle before the next frame - the next frame's indirect
+bounce samples them at arbitrary hit points (raygen.rgen:127 ->
+probeSampling.glsl:64-163). After every frame each rank's gathered atlases, and
+its own probes' offsets, must equal an unsharded oracle's bit for bit; the full
+grid, a ragged window and a window that wraps are run."""
 import os
 import socket
 
@@ -20,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, result_q):
+def _worker(rank, world, port, window, frames, result_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -37,49 +43,69 @@ def _worker(rank, world, port, result_q):
     from parity import make_desc
 
     sc, ex = S.cornell_box()
-    grid = D.ProbeGrid((4, 4, 4), (0.5, 0.5, 0.5), (-0.75, 0.25, -0.75))
-    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=64, max_rays_per_probe=32, max_probe_updates=64)
-    orc = O.Oracle(make_desc(grid, ex["z_far"], cfg))
-    orc.set_scene(sc, 2)
+    grid = D.ProbeGrid((4, 4, 8), (0.5, 0.5, 0.25), (-0.75, 0.25, -0.9))
+    N = grid.probe_count()
     X, Y, Z = grid.grid_dimensions
-    ok = True
-    for f in range(3):
-        p = D.frame_params(cfg, grid, D.AppState(f), 0, light_pre_exposure=ex["light_pre_exposure"],
-                           environment_brightness=ex["environment_brightness"])
-        orc.update(p, 2)
-        full = {w: orc.read(w).copy() for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY)}
-        bufs = []
-        tensors = {}
-        for w, tile in ((abi.ARK_DDGI_ATLAS_IRRADIANCE, 10), (abi.ARK_DDGI_ATLAS_VISIBILITY, 18)):
-            a = full[w].view(np.uint8).copy()
-            total = a.size
-            slab = total // world
-            # this rank only "computed" its own band: scramble the rest
-            mine = a[rank * slab:(rank + 1) * slab].copy()
-            a[:] = 0xAB
-            a[rank * slab:(rank + 1) * slab] = mine
+    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=window, compute_probe_offsets=True,
+                       max_rays_per_probe=32, max_probe_updates=N)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    mine_orc = O.Oracle(make_desc(grid, ex["z_far"], cfg, shard_rank=rank, shard_count=world))
+    full_orc = O.Oracle(make_desc(grid, ex["z_far"], cfg))
+    mine_orc.set_scene(sc, 2)
+    full_orc.set_scene(sc, 2)
+    z = (np.arange(N) % (X * Z)) // X
+    owned = (z >= rank * (Z // world)) & (z < (rank + 1) * (Z // world))
+    report = []
+    first = 0
+    for f in range(frames):
+        p = D.frame_params(cfg, grid, D.AppState(f), first, **exposure)
+        mine_orc.update(p, 2)
+        full_orc.update(p, 2)
+        first = (first + p.probe_updates) % N
+        bufs, tensors = [], {}
+        for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY):
+            # negative control: before the exchange the other slabs' tiles are stale
+            report.append((f, "stale", int(np.count_nonzero(mine_orc.read(w) != full_orc.read(w)))))
+            a = mine_orc.read(w).view(np.uint8).copy()
+            slab = a.size // world  # a Z-slab is a contiguous texel-row band
             t = torch.from_numpy(a)
             tensors[w] = t
-            # a Z-slab is a contiguous row band: rows [z0*tile, z1*tile) of the atlas
-            assert slab == (Z // world) * tile * (X * tile * Y) * (8 if tile == 10 else 4)
             bufs.append((t, rank * slab, slab))
         SlabExchange(bufs, rank, world).exchange()
         for w, t in tensors.items():
-            ok &= np.array_equal(t.numpy(), full[w].view(np.uint8))
-    result_q.put((rank, bool(ok)))
+            gathered = t.numpy().view(np.uint16)
+            mine_orc.write(w, gathered)  # the next frame reads the other slabs' tiles
+            want = full_orc.read(w)
+            report.append((f, w, int(np.count_nonzero(gathered != want))))
+        off_m = mine_orc.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[owned]
+        off_f = full_orc.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[owned]
+        report.append((f, "offsets", int(np.count_nonzero(off_m.view(np.uint32) != off_f.view(np.uint32)))))
+        report.append((f, "moved", int(np.count_nonzero(off_f))))
+    mine_orc.close()
+    full_orc.close()
+    result_q.put((rank, report))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_zslab_allgather_two_ranks_gloo():
-    world = 2
+@pytest.mark.parametrize("world,window,frames", [(2, 128, 3), (4, 128, 3), (2, 45, 4)])
+def test_zslab_sharded_oracles_two_and_four_ranks_gloo(world, window, frames):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, window, frames, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    assert sorted(res) == list(range(world))
+    for rank, report in res.items():
+        for f, what, n in report:
+            if what in ("moved", "stale"):
+                continue
+            assert n == 0, (rank, f, what, n)
+    # the offsets moved somewhere (the comparison is not of zeros), and each rank's own
+    # update left the other slabs' tiles stale until the exchange
+    assert any(n > 0 for rep in res.values() for f, what, n in rep if what == "moved")
+    assert all(any(n > 0 for f, what, n in rep if what == "stale") for rep in res.values())

@@ -66,6 +66,15 @@ def main():
         for r in csv.DictReader(open(glob.glob(f"{d}/sq1/run_counter_collection.csv")[0])):
             if r["Counter_Name"] == "SQ_WAVES":
                 calls[short(r["Kernel_Name"])] += 1
+        # effective clock per kernel (MI355X_MICROARCH.md, DVFS give-back): GRBM_GUI_ACTIVE
+        # summed over the 8 XCDs / 8 / the dispatch's wall time, from the tcc pass
+        grbm, wall = collections.defaultdict(float), collections.defaultdict(float)
+        for f in glob.glob(f"{d}/tcc/run_counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                    k = short(r["Kernel_Name"])
+                    grbm[k] += float(r["Counter_Value"])
+                    wall[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
         kernels = {}
         for k, v in agg.items():
             b = base_name(k)
@@ -80,7 +89,8 @@ def main():
                           "valu_insts_per_launch": round(v.get("SQ_INSTS_VALU", 0) / n),
                           "salu_insts_per_launch": round(v.get("SQ_INSTS_SALU", 0) / n),
                           "vmem_rd_insts_per_launch": round(v.get("SQ_INSTS_VMEM_RD", 0) / n),
-                          "l2_hit": round(hit / (hit + miss), 3) if hit + miss else None}
+                          "l2_hit": round(hit / (hit + miss), 3) if hit + miss else None,
+                          "clock_ghz_effective": round(grbm[k] / 8 / wall[k] / 1e9, 3) if wall[k] > 0 else None}
         out = {"tag": tag, "lib_sha16": lib_sha, "source": f"rocprofv3 --pmc SQ_*/TCC_* passes (tools/prof_sq.sh), profiles/{tag}_sq.*",
                "kernels": kernels}
         with open(os.path.join(ROOT, "profiles", f"{tag}_sq.json"), "w") as fh:
