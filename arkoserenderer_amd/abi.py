@@ -397,6 +397,9 @@ EXPORTS = {
     "ark_ddgi_destroy": (None, [C.c_void_p]),
     "ark_ddgi_last_error": (C.c_char_p, [C.c_void_p]),
     "ark_ddgi_set_scene": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiScene)]),
+    "ark_ddgi_share_scene": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ark_ddgi_mark_external_write": (C.c_int, [C.c_void_p]),
+    "ark_ddgi_get_next_probe_index": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ark_ddgi_update": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
     "ark_ddgi_synchronize": (C.c_int, [C.c_void_p]),
     "ark_ddgi_update_overlapped": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -61,37 +61,139 @@ class SlabExchange:
             dist.all_gather_into_tensor(full, mine, group=self.group)
 
 
+EXCHANGE_FAILURE_EXIT_CODE = 14  # as the C++ ExchangeWatchdog (SlabExchange.h)
+
+
+def _rccl_async_error(group) -> int:
+    """ncclCommGetAsyncError of the RCCL communicator behind a torch process group
+    (ProcessGroupNCCL._comm_ptr), 0 = ncclSuccess; 0 when there is none to ask
+    (gloo, or a communicator not created yet)."""
+    import ctypes as C
+
+    import torch.distributed as dist
+
+    try:
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        backend = pg._get_backend(__import__("torch").device("cuda"))
+        comm = int(backend._comm_ptr())
+    except (RuntimeError, AttributeError, ValueError):
+        return 0
+    if not comm:
+        return 0
+    global _RCCL
+    if _RCCL is None:
+        _RCCL = C.CDLL("librccl.so")
+        _RCCL.ncclCommGetAsyncError.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        _RCCL.ncclCommGetAsyncError.restype = C.c_int
+    err = C.c_int(0)
+    rc = _RCCL.ncclCommGetAsyncError(C.c_void_p(comm), C.byref(err))
+    # ncclInProgress (7) is a non-blocking communicator still initialising: not an error
+    return rc if rc != 0 else (err.value if err.value != 7 else 0)
+
+
+_RCCL = None
+
+
+class ExchangeWatchdog:
+    """Failure detection of the Z-slab exchange (ncclCommGetAsyncError
+    polling in multi-GPU mode), the Python twin of the C++ ExchangeWatchdog
+    (SlabExchange.h). wait(event) polls the exchange's completion event and the
+    communicator's asynchronous error until a deadline (ARK_EXCHANGE_TIMEOUT_S,
+    default 120 s); on an error or at the deadline it calls on_failure(why), whose
+    default aborts the process group (the communicator's pending work is cancelled and
+    peers see an error), logs an Error and ends the process with exit code 14. No
+    re-exec. A dead peer would otherwise hang every rank: the next frame's shading
+    waits for the all-gather on the device and the host blocks at its next sync."""
+
+    def __init__(self, timeout_s: float | None = None, group=None, on_failure=None):
+        import os
+
+        if timeout_s is None or timeout_s <= 0:
+            timeout_s = float(os.environ.get("ARK_EXCHANGE_TIMEOUT_S", "0") or 0) or 120.0
+        self.timeout_s, self.group = float(timeout_s), group
+        self.on_failure = on_failure or self.abort_and_exit
+
+    def wait(self, event, what: str) -> bool:
+        import time
+
+        t0 = time.monotonic()
+        pause = 2e-5
+        while not event.query():
+            err = _rccl_async_error(self.group)
+            if err:
+                self.on_failure(f"{what}: communicator error {err}")
+                return False
+            waited = time.monotonic() - t0
+            if waited > self.timeout_s:
+                self.on_failure(f"{what}: not complete after {waited:.3f} s (deadline {self.timeout_s:.3f} s)")
+                return False
+            time.sleep(pause)
+            pause = min(2 * pause, 2e-3)
+        return True
+
+    def abort_and_exit(self, why: str):
+        import os
+        import sys
+
+        import torch.distributed as dist
+
+        try:
+            if dist.is_initialized():
+                dist.distributed_c10d._abort_process_group(self.group)
+        finally:
+            print(f"[Error] Z-slab exchange failed, exiting: {why}", file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(EXCHANGE_FAILURE_EXIT_CODE)
+
+
 class OverlappedSlabExchange:
     """One rank's frame loop with the atlas all-gather of frame N on a side stream,
     overlapped with frame N+1's probe-ray traversal (which reads only the scene,
     the slot table and this rank's own probe offsets). Frame N+1's shading waits
     for the all-gather (it samples the previous atlases at any probe); the
-    all-gather waits for frame N's probe update (ark_ddgi_update_overlapped)."""
+    all-gather waits for frame N's probe update (ark_ddgi_update_overlapped).
 
-    def __init__(self, node, exchange, device):
+    Bounded: before frame N's all-gather is enqueued, frame N-2's must have completed
+    (ExchangeWatchdog.wait on its event, polled against a deadline): the host runs at
+    most two exchanges ahead of the device, and a peer that stops answering ends the
+    process at the deadline instead of hanging it. drain() waits (bounded) for the last."""
+
+    def __init__(self, node, exchange, device, watchdog: ExchangeWatchdog | None = None):
         import torch
 
         self.node, self.exchange = node, exchange
+        self.watchdog = watchdog or ExchangeWatchdog()
         self.comm = torch.cuda.Stream(device)
         self.updated = torch.cuda.Event()
-        self.gathered = torch.cuda.Event()
+        # completion of frame n's all-gather in slot n & 1
+        self.gathered = [torch.cuda.Event(), torch.cuda.Event()]
         # torch creates events lazily: record once so the raw handles exist
         cur = torch.cuda.current_stream(device)
         self.updated.record(cur)
-        self.gathered.record(cur)
-        self.pending = False
+        for e in self.gathered:
+            e.record(cur)
+        self.frames = 0
 
     def step(self, app, stream_ptr: int):
         import torch
 
-        wait = self.gathered.cuda_event if self.pending else None
+        prev = self.gathered[(self.frames - 1) & 1]
+        wait = prev.cuda_event if self.frames > 0 else None
+        slot = self.gathered[self.frames & 1]
+        if self.frames >= 2 and not self.watchdog.wait(slot, "slab exchange frame n-2"):
+            return None
         p = self.node.execute_overlapped(app, stream_ptr, wait, self.updated.cuda_event)
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(self.updated)
             self.exchange()
-            self.gathered.record(self.comm)
-        self.pending = True
+            slot.record(self.comm)
+        self.frames += 1
         return p
+
+    def drain(self) -> bool:
+        if self.frames == 0:
+            return True
+        return self.watchdog.wait(self.gathered[(self.frames - 1) & 1], "slab exchange drain")
 
 
 def slab_bands(total_bytes: int, world: int):

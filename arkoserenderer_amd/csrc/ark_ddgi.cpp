@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -118,6 +119,29 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 
 } // namespace
 
+// The scene of a context on the device (ark_ddgi_set_scene): BVH nodes + triangles,
+// shading records, RT mesh data, materials, textures, lights. Reference-counted:
+// ark_ddgi_share_scene lets the Z-slab contexts of one GPU use one copy.
+struct SceneStore {
+    int device = 0;
+    DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
+    std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
+    std::vector<ArkRTTriangleMesh> meshHost;
+    SceneArgs args {};
+    ArkDdgiBvhStats bvhStats {};
+    uint32_t bvhMaxDepth = 0;
+    uint32_t lightCount = 0;
+    SceneStore() = default;
+    SceneStore(const SceneStore&) = delete;
+    SceneStore& operator=(const SceneStore&) = delete;
+    ~SceneStore()
+    {
+        (void)hipSetDevice(device);
+        for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &spots })
+            b->release();
+    }
+};
+
 struct ArkDdgiCtx {
     ArkDdgiDesc desc {};
     std::string lastError;
@@ -164,15 +188,13 @@ struct ArkDdgiCtx {
     uint64_t spillRegionWords = 0; // spill region 1 = the primary traversal's
     // scene
     bool hasScene = false;
-    DeviceBuffer nodes, tris, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
-    std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
-    std::vector<ArkRTTriangleMesh> meshHost;
+    std::shared_ptr<SceneStore> sceneStore; // device scene (possibly shared with other contexts)
     // AO bake results (ark_ddgi_bake_ao)
     DeviceBuffer bakeTri, bakeBary, bakeOut, bakePixels, bakeCounters;
     uint32_t bakeW = 0, bakeH = 0;
     int bakeBent = 0;
-    SceneArgs scene {};
-    ArkDdgiBvhStats bvhStats {};
+    SceneArgs scene {};          // = sceneStore->args
+    ArkDdgiBvhStats bvhStats {}; // = sceneStore->bvhStats
     uint32_t bvhMaxDepth = 0;
     // instrumentation
     bool counting = false;
@@ -183,6 +205,7 @@ struct ArkDdgiCtx {
     ArkDdgiCounters lastCounters {};
     bool countersPending = false;
     uint64_t lastRays = 0, lastProbes = 0;
+    uint32_t nextProbeIndex = 0; // (first + K) % N of the last update, or of a loaded state
 
     int fail(int code, const char* fmt, ...)
     {
@@ -312,6 +335,22 @@ float srgbToLinear(float c)
     return c <= 0.04045f ? c / 12.92f : powf_((c + 0.055f) / 1.055f, 2.4f);
 }
 
+// Makes `st` the context's scene: the per-context work sets follow its light count
+// and BVH depth.
+int adoptScene(ArkDdgiCtx* ctx, std::shared_ptr<SceneStore> st)
+{
+    ctx->scene = st->args;
+    ctx->bvhStats = st->bvhStats;
+    ctx->bvhMaxDepth = st->bvhMaxDepth;
+    ctx->lightCount = st->lightCount;
+    ctx->sceneStore = std::move(st);
+    int rc;
+    if ((rc = ensureShadeWork(ctx)) != 0) return rc;
+    if ((rc = ensureSpill(ctx)) != 0) return rc;
+    ctx->hasScene = true;
+    return ARK_DDGI_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -420,9 +459,9 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork, &ctx->reflWork,
-                             &ctx->counters, &ctx->nodes, &ctx->tris, &ctx->triNormals, &ctx->indices, &ctx->vertices, &ctx->positions, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters, &ctx->meshes, &ctx->materials, &ctx->instances,
-                             &ctx->texInfos, &ctx->texels, &ctx->spots })
+                             &ctx->counters, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
         b->release();
+    ctx->sceneStore.reset();
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->evOrder) (void)hipEventDestroy(ctx->evOrder);
@@ -443,6 +482,12 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (!s || s->struct_size != sizeof(ArkDdgiScene)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiScene");
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
+    // the previous scene goes first (its memory is reused), unless another context
+    // shares it; a failure below leaves the context without a scene
+    ctx->hasScene = false;
+    ctx->sceneStore.reset();
+    auto st = std::make_shared<SceneStore>();
+    st->device = ctx->device;
     const auto t0 = std::chrono::steady_clock::now();
     // validate
     for (uint32_t i = 0; i < s->instance_count; ++i) {
@@ -630,23 +675,22 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     const size_t triOffset = (nodeBytes + 255) & ~static_cast<size_t>(255);
     const size_t triBytes = (allTris.size() + 1) * sizeof(GpuTriangle); // + padding record
     if (triOffset + triBytes >= (1ull << 32)) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "BVH nodes + triangles exceed 4 GiB");
-    ARK_HIP(ctx->nodes.alloc(triOffset + triBytes));
-    ARK_HIP(hipMemcpy(ctx->nodes.ptr, allNodes.data(), nodeBytes, hipMemcpyHostToDevice));
+    ARK_HIP(st->nodes.alloc(triOffset + triBytes));
+    ARK_HIP(hipMemcpy(st->nodes.ptr, allNodes.data(), nodeBytes, hipMemcpyHostToDevice));
     allTris.push_back(GpuTriangle {}); // padding: a five-load fetch of the last triangle stays in bounds (ARK_FETCH5)
-    ARK_HIP(hipMemcpy(static_cast<char*>(ctx->nodes.ptr) + triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
+    ARK_HIP(hipMemcpy(static_cast<char*>(st->nodes.ptr) + triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
     allTris.pop_back();
-    ctx->tris.release();
-    if ((rc = upload(ctx, ctx->indices, s->indices, s->index_count)) != 0) return rc;
-    if ((rc = upload(ctx, ctx->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
-    if ((rc = upload(ctx, ctx->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
-    ctx->instHost.assign(s->instances, s->instances + s->instance_count);
-    ctx->meshHost.assign(s->meshes, s->meshes + s->mesh_count);
-    if ((rc = upload(ctx, ctx->meshes, s->meshes, s->mesh_count)) != 0) return rc;
-    if ((rc = upload(ctx, ctx->materials, s->materials, s->material_count)) != 0) return rc;
-    if ((rc = upload(ctx, ctx->instances, ginst.data(), ginst.size())) != 0) return rc;
-    if ((rc = upload(ctx, ctx->texInfos, infos.data(), infos.size())) != 0) return rc;
-    if ((rc = upload(ctx, ctx->texels, texels.data(), texels.size())) != 0) return rc;
-    if ((rc = upload(ctx, ctx->spots, gspots.data(), gspots.size())) != 0) return rc;
+    if ((rc = upload(ctx, st->indices, s->indices, s->index_count)) != 0) return rc;
+    if ((rc = upload(ctx, st->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
+    if ((rc = upload(ctx, st->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
+    st->instHost.assign(s->instances, s->instances + s->instance_count);
+    st->meshHost.assign(s->meshes, s->meshes + s->mesh_count);
+    if ((rc = upload(ctx, st->meshes, s->meshes, s->mesh_count)) != 0) return rc;
+    if ((rc = upload(ctx, st->materials, s->materials, s->material_count)) != 0) return rc;
+    if ((rc = upload(ctx, st->instances, ginst.data(), ginst.size())) != 0) return rc;
+    if ((rc = upload(ctx, st->texInfos, infos.data(), infos.size())) != 0) return rc;
+    if ((rc = upload(ctx, st->texels, texels.data(), texels.size())) != 0) return rc;
+    if ((rc = upload(ctx, st->spots, gspots.data(), gspots.size())) != 0) return rc;
     {
         // per-triangle shading records (GpuTriangle order, 64 B): the three vertex
         // normals, the instance and the three UVs, copied from the vertex pool, so
@@ -669,25 +713,25 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
             std::memcpy(o + 9, &inst, 4);
         }
         if (tn.empty()) tn.assign(16, 0.0f);
-        if ((rc = upload(ctx, ctx->triNormals, tn.data(), tn.size())) != 0) return rc;
+        if ((rc = upload(ctx, st->triNormals, tn.data(), tn.size())) != 0) return rc;
     }
-    SceneArgs& sc = ctx->scene;
-    sc.nodes = ctx->nodes.as<GpuBvh8Node>();
-    sc.tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(ctx->nodes.ptr) + triOffset);
+    SceneArgs& sc = st->args;
+    sc.nodes = st->nodes.as<GpuBvh8Node>();
+    sc.tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st->nodes.ptr) + triOffset);
     sc.tri_byte_offset = static_cast<uint32_t>(triOffset);
-    sc.tri_normals = ctx->triNormals.as<float4>();
+    sc.tri_normals = st->triNormals.as<float4>();
     sc.root_opaque = roots[0];
     sc.root_masked = roots[1];
     sc.root_blend = roots[2];
     sc.opaque_nodes = opaqueNodes;
     sc.texture_count = static_cast<int32_t>(s->texture_count);
-    sc.indices = ctx->indices.as<uint32_t>();
-    sc.vertices = ctx->vertices.as<float>();
-    sc.meshes = ctx->meshes.as<ArkRTTriangleMesh>();
-    sc.materials = ctx->materials.as<ArkShaderMaterial>();
-    sc.instances = ctx->instances.as<GpuInstance>();
-    sc.tex_infos = ctx->texInfos.as<GpuTextureInfo>();
-    sc.texels = ctx->texels.as<float4>();
+    sc.indices = st->indices.as<uint32_t>();
+    sc.vertices = st->vertices.as<float>();
+    sc.meshes = st->meshes.as<ArkRTTriangleMesh>();
+    sc.materials = st->materials.as<ArkShaderMaterial>();
+    sc.instances = st->instances.as<GpuInstance>();
+    sc.tex_infos = st->texInfos.as<GpuTextureInfo>();
+    sc.texels = st->texels.as<float4>();
     sc.white_texture = static_cast<int32_t>(s->texture_count);
     sc.env_texture = (s->environment_texture >= 0 && static_cast<uint32_t>(s->environment_texture) < s->texture_count) ? s->environment_texture : sc.white_texture;
     sc.has_sun = s->has_directional_light ? 1 : 0;
@@ -696,24 +740,36 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         sc.sun_dir[k] = s->directional_light.world_space_direction[k];
     }
     sc.spot_count = static_cast<int32_t>(s->spot_light_count);
-    sc.spots = ctx->spots.as<GpuSpotLight>();
-    ctx->bvhMaxDepth = maxDepth;
+    sc.spots = st->spots.as<GpuSpotLight>();
+    st->bvhMaxDepth = maxDepth;
     if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
-    ctx->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
-    if ((rc = ensureShadeWork(ctx)) != 0) return rc;
-    if ((rc = ensureSpill(ctx)) != 0) return rc;
-    ctx->hasScene = true;
+    st->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
     const auto t1 = std::chrono::steady_clock::now();
-    ctx->bvhStats.node_count = allNodes.size();
-    ctx->bvhStats.triangle_count = allTris.size();
-    ctx->bvhStats.max_depth = maxDepth;
-    ctx->bvhStats.max_leaf_size = maxLeaf;
-    ctx->bvhStats.sah_cost = sah;
-    ctx->bvhStats.build_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    ctx->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvh8Node);
-    ctx->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
-    return ARK_DDGI_OK;
+    st->bvhStats.node_count = allNodes.size();
+    st->bvhStats.triangle_count = allTris.size();
+    st->bvhStats.max_depth = maxDepth;
+    st->bvhStats.max_leaf_size = maxLeaf;
+    st->bvhStats.sah_cost = sah;
+    st->bvhStats.build_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    st->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvh8Node);
+    st->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
+    return adoptScene(ctx, std::move(st));
 }
+
+int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
+    if (!src || src == ctx || !src->hasScene || !src->sceneStore) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "share_scene: the source context has no scene");
+    if (src->device != ctx->device) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "share_scene: contexts on devices %d and %d", src->device, ctx->device);
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    std::shared_ptr<SceneStore> st = src->sceneStore;
+    ctx->hasScene = false;
+    ctx->sceneStore.reset();
+    return adoptScene(ctx, std::move(st));
+}
+
 
 static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t K)
 {
@@ -886,6 +942,14 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     ctx->countersPending = count;
     ctx->lastRays = f.window_rays;
     ctx->lastProbes = f.window_probes;
+    ctx->nextProbeIndex = (f.first + K) % N;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_mark_external_write(ArkDdgiCtx* ctx)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ctx->pipeReady = false; // the next update's traversal waits for this
     return ARK_DDGI_OK;
 }
 
@@ -951,7 +1015,7 @@ struct StateHeader {
     float spacing[3], origin[3];
     float zFar;
     int32_t clearMode, shardRank, shardCount;
-    int32_t reserved;        // 0
+    uint32_t nextProbeIndex; // the rolling window's next first probe (m_probeUpdateIdx, DDGINode.h:32)
     uint64_t irrBytes, visBytes, offBytes;
 };
 static_assert(sizeof(StateHeader) == 88, "state header layout");
@@ -971,6 +1035,7 @@ StateHeader stateHeaderOf(const ArkDdgiCtx* ctx)
     h.clearMode = ctx->desc.clear_overflow_mode;
     h.shardRank = ctx->desc.shard_rank;
     h.shardCount = ctx->desc.shard_count;
+    h.nextProbeIndex = ctx->nextProbeIndex;
     h.irrBytes = ctx->irr.bytes;
     h.visBytes = ctx->vis.bytes;
     h.offBytes = ctx->offsets.bytes;
@@ -1014,8 +1079,9 @@ int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* src, uint64_t bytes)
     if (bytes != need) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "state is %llu bytes, got %llu", (unsigned long long)need, (unsigned long long)bytes);
     StateHeader h;
     std::memcpy(&h, src, sizeof(h));
-    const StateHeader mine = stateHeaderOf(ctx);
-    if (std::memcmp(&h, &mine, sizeof(h)) != 0)
+    StateHeader mine = stateHeaderOf(ctx);
+    mine.nextProbeIndex = h.nextProbeIndex; // the window position is state, not geometry
+    if (std::memcmp(&h, &mine, sizeof(h)) != 0 || h.nextProbeIndex >= static_cast<uint32_t>(ctx->N))
         return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "state blob is of another grid / zFar / clear mode / shard (or not a DDGI state)");
     const char* i = static_cast<const char*>(src) + sizeof(h);
     ARK_HIP(hipSetDevice(ctx->device));
@@ -1025,6 +1091,14 @@ int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* src, uint64_t bytes)
     ARK_HIP(hipMemcpy(ctx->vis.ptr, i, ctx->vis.bytes, hipMemcpyHostToDevice));
     i += ctx->vis.bytes;
     ARK_HIP(hipMemcpy(ctx->offsets.ptr, i, ctx->offsets.bytes, hipMemcpyHostToDevice));
+    ctx->nextProbeIndex = h.nextProbeIndex;
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_next_probe_index(const ArkDdgiCtx* ctx, uint32_t* out)
+{
+    if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    *out = ctx->nextProbeIndex;
     return ARK_DDGI_OK;
 }
 
@@ -1133,11 +1207,11 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!d || d->struct_size != sizeof(ArkBakeAoDesc)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkBakeAoDesc");
     if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: no scene");
-    if (d->instance_index >= ctx->instHost.size()) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: instance %u out of range", d->instance_index);
+    if (d->instance_index >= ctx->sceneStore->instHost.size()) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: instance %u out of range", d->instance_index);
     if (d->width == 0 || d->height == 0 || d->width > 16384 || d->height > 16384 || d->sample_count == 0)
         return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bake: extent %ux%u / %u samples", d->width, d->height, d->sample_count);
-    const ArkRTInstance& inst = ctx->instHost[d->instance_index];
-    const ArkRTTriangleMesh& mesh = ctx->meshHost[inst.rt_mesh_index];
+    const ArkRTInstance& inst = ctx->sceneStore->instHost[d->instance_index];
+    const ArkRTTriangleMesh& mesh = ctx->sceneStore->meshHost[inst.rt_mesh_index];
     const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(orderBegin(ctx, s));
@@ -1158,9 +1232,9 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
     b.bent = d->bent_normals ? 1 : 0;
     b.first_index = static_cast<uint32_t>(mesh.first_index);
     b.first_vertex = static_cast<uint32_t>(mesh.first_vertex);
-    b.indices = ctx->indices.as<uint32_t>();
-    b.positions = ctx->positions.as<float>();
-    b.vertices = ctx->vertices.as<float>();
+    b.indices = ctx->sceneStore->indices.as<uint32_t>();
+    b.positions = ctx->sceneStore->positions.as<float>();
+    b.vertices = ctx->sceneStore->vertices.as<float>();
     b.tri_idx = ctx->bakeTri.as<uint32_t>();
     b.bary = ctx->bakeBary.as<uint16_t>();
     b.out = ctx->bakeOut.as<uint8_t>();

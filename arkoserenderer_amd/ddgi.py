@@ -136,6 +136,16 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_set_scene(self.h, C.byref(s)), "ark_ddgi_set_scene")
         self._scene = scene
 
+    def share_scene(self, src: "DDGIContext"):
+        """ark_ddgi_share_scene: use src's device scene and BVH (same GPU), no copy."""
+        self.check(self.lib.ark_ddgi_share_scene(self.h, src.h), "ark_ddgi_share_scene")
+        self._scene = src._scene
+
+    def mark_external_write(self):
+        """ark_ddgi_mark_external_write: offsets / atlases were written through the
+        device views on the next update's stream; that update then runs after it."""
+        self.check(self.lib.ark_ddgi_mark_external_write(self.h), "ark_ddgi_mark_external_write")
+
     def update(self, params: abi.ArkDdgiFrameParams, stream: int | None = None):
         self.check(self.lib.ark_ddgi_update(self.h, C.byref(params), C.c_void_p(stream) if stream else None), "ark_ddgi_update")
 
@@ -177,6 +187,12 @@ class DDGIContext:
         """ark_ddgi_load_state: restores a blob of a context with the same grid / zFar / shard."""
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         self.check(self.lib.ark_ddgi_load_state(self.h, buf, len(blob)), "ark_ddgi_load_state")
+
+    def next_probe_index(self) -> int:
+        """ark_ddgi_get_next_probe_index: the rolling window's next first probe."""
+        v = C.c_uint32()
+        self.check(self.lib.ark_ddgi_get_next_probe_index(self.h, C.byref(v)), "ark_ddgi_get_next_probe_index")
+        return int(v.value)
 
     def device_views(self) -> abi.ArkDdgiDeviceViews:
         v = abi.ArkDdgiDeviceViews()
@@ -325,6 +341,15 @@ class DDGINode:
         self.ctx.update(p, stream)
         self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
         return p
+
+    def save_state(self) -> bytes:
+        """The node's DDGI history: atlases, offsets and the window position."""
+        return self.ctx.save_state()
+
+    def load_state(self, blob: bytes):
+        """Restores save_state()'s blob and resumes the rolling window where it was."""
+        self.ctx.load_state(blob)
+        self.probe_update_idx = self.ctx.next_probe_index()
 
 
 class BakeAmbientOcclusionNode:

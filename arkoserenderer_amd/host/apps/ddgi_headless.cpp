@@ -13,14 +13,28 @@
 //                 [--shards P]                          Z-slab ranks as P contexts in this process,
 //                                                       bands exchanged by device copies (one GPU)
 //                 [--world P --rank r --nccl-id FILE]   rank r of P processes (one per GPU), bands
-//                                                       exchanged by RCCL all-gather; rank 0 writes
-//                                                       the ncclUniqueId to FILE, the others read it
+//                 [--nccl-nonce S]                      exchanged by RCCL all-gather; rank 0 writes
+//                                                       the ncclUniqueId (+ nonce S) to FILE, the
+//                                                       others read it (a file without S, or older
+//                                                       than their own start, is stale: they wait)
+//                 [--save-state FILE] [--load-state FILE] [--first-frame F]
+//                                                       checkpoint of the (unsharded) node after the
+//                                                       last frame / before the first; frame indices
+//                                                       start at F (DDGINode::saveState/loadState)
+//                 [--exchange-timeout SEC]              deadline of the exchange watchdog
+//                 [--exchange-deadline-test]            1-rank RCCL: stalls the exchange stream for
+//                                                       1.5 s under a 0.2 s deadline; the watchdog
+//                                                       must end the process with exit code 14
 // Sharded runs dump the (exchanged, therefore complete) atlases of rank 0 / this rank
 // and the probe offsets of this rank's slab ("--shards": merged over the owners).
+#include <sys/stat.h>
+
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <memory>
 #include <thread>
 #include <string>
@@ -181,25 +195,45 @@ bool writeFile(const std::string& path, const std::vector<uint8_t>& buf)
     return ok;
 }
 
-// rendezvous of the RCCL ranks through a shared file: rank 0 publishes the id
-// (written then renamed, so readers never see a partial file)
-bool shareUniqueId(const std::string& path, int rank, std::vector<uint8_t>& id)
+// rendezvous of the RCCL ranks through a shared file: rank 0 removes any old file,
+// then publishes the 128-byte id followed by the launch nonce (written then renamed,
+// so readers never see a partial file). A reader takes only a file with this
+// launch's nonce; without a nonce, only a file written after its own start (a file
+// left by an earlier run holds a dead id, and ncclCommInitRank on it would hang).
+bool shareUniqueId(const std::string& path, int rank, const std::string& nonce, std::time_t startedAt, std::vector<uint8_t>& id)
 {
     if (rank == 0) {
+        std::remove(path.c_str());
         if (!RcclSlabExchange::createUniqueId(id)) return false;
+        std::vector<uint8_t> blob(id);
+        blob.insert(blob.end(), nonce.begin(), nonce.end());
         const std::string tmp = path + ".tmp";
-        return writeFile(tmp, id) && std::rename(tmp.c_str(), path.c_str()) == 0;
+        return writeFile(tmp, blob) && std::rename(tmp.c_str(), path.c_str()) == 0;
     }
     for (int tries = 0; tries < 600; ++tries) {
-        if (FILE* f = std::fopen(path.c_str(), "rb")) {
-            id.resize(128);
-            const bool ok = std::fread(id.data(), 1, id.size(), f) == id.size();
-            std::fclose(f);
-            return ok;
+        struct stat st {};
+        if (stat(path.c_str(), &st) == 0 && (!nonce.empty() || st.st_mtime + 1 >= startedAt)) {
+            if (FILE* f = std::fopen(path.c_str(), "rb")) {
+                std::vector<uint8_t> blob(128 + nonce.size() + 1);
+                const size_t n = std::fread(blob.data(), 1, blob.size(), f);
+                std::fclose(f);
+                if (n == 128 + nonce.size() && std::equal(nonce.begin(), nonce.end(), blob.begin() + 128)) {
+                    id.assign(blob.begin(), blob.begin() + 128);
+                    return true;
+                }
+            }
         }
         std::this_thread::sleep_for(std::chrono::milliseconds(100));
     }
     return false;
+}
+
+// A bounded stall of a stream (the exchange deadline test): one lane sleeps until
+// `ticks` of the constant wall clock have passed, then the kernel ends.
+__global__ void k_stall(uint64_t ticks)
+{
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 bool dump(ArkDdgiCtx* ctx, int which, const std::string& path)
@@ -224,7 +258,12 @@ int main(int argc, char** argv)
     ProbeGrid grid;
     int rays = 64, updates = 512, frames = 4, device = 0, offsets = 1, rebuildAt = -1;
     int shards = 1, world = 1, rank = 0;
-    std::string ncclIdPath;
+    std::string ncclIdPath, ncclNonce;
+    double exchangeTimeout = 0.0;
+    std::string saveStatePath, loadStatePath;
+    int firstFrame = 0;
+    bool deadlineTest = false;
+    const std::time_t startedAt = std::time(nullptr);
     float zFar = 10000.0f, exposure = 1.0f, env = 1.0f, ambient = 0.0f;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -252,6 +291,12 @@ int main(int argc, char** argv)
         else if (a == "--world") world = std::atoi(next());
         else if (a == "--rank") rank = std::atoi(next());
         else if (a == "--nccl-id") ncclIdPath = next();
+        else if (a == "--nccl-nonce") ncclNonce = next();
+        else if (a == "--exchange-timeout") exchangeTimeout = std::strtod(next(), nullptr);
+        else if (a == "--exchange-deadline-test") deadlineTest = true;
+        else if (a == "--save-state") saveStatePath = next();
+        else if (a == "--load-state") loadStatePath = next();
+        else if (a == "--first-frame") firstFrame = std::atoi(next());
         else ARKOSE_LOG(Fatal, "unknown argument %s", a.c_str());
     }
     SceneFile file;
@@ -314,9 +359,25 @@ int main(int argc, char** argv)
             SlabBands bands;
             if (!SlabBands::fromContext(nodeOf(*pipelines[0])->context(), rank, world, bands, err)) ARKOSE_LOG(Fatal, "%s", err.c_str());
             std::vector<uint8_t> id;
-            if (!shareUniqueId(ncclIdPath, rank, id)) ARKOSE_LOG(Fatal, "cannot share the ncclUniqueId through %s", ncclIdPath.c_str());
-            auto ex = std::make_unique<RcclSlabExchange>(device, rank, world, id.data(), bands);
+            if (!shareUniqueId(ncclIdPath, rank, ncclNonce, startedAt, id)) ARKOSE_LOG(Fatal, "cannot share the ncclUniqueId through %s", ncclIdPath.c_str());
+            auto ex = std::make_unique<RcclSlabExchange>(device, rank, world, id.data(), bands, deadlineTest ? 0.2 : exchangeTimeout);
             if (!ex->ok()) ARKOSE_LOG(Fatal, "RCCL: %s", ex->error().c_str());
+            if (deadlineTest) {
+                if (world != 1) ARKOSE_LOG(Fatal, "--exchange-deadline-test runs with --world 1");
+                // frame 0's all-gather queues behind a 1.5 s stall; frame 2's exchange waits
+                // for it with a 0.2 s deadline. The handler lets the bounded stall finish
+                // (so no kernel is left running), then takes the default failure path.
+                RcclSlabExchange* rx = ex.get();
+                rx->watchdog().setFailureHandler([rx](const std::string& why) {
+                    std::printf("ddgi_headless: watchdog fired: %s\n", why.c_str());
+                    (void)hipDeviceSynchronize();
+                    ExchangeWatchdog::abortAndExit(rx->comm(), why);
+                });
+                int khz = 0;
+                if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+                hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, static_cast<hipStream_t>(rx->stream()), static_cast<uint64_t>(khz) * 1500u);
+                if (hipGetLastError() != hipSuccess) ARKOSE_LOG(Fatal, "stall kernel launch failed");
+            }
             exchange = std::move(ex);
         } else {
             std::vector<SlabBands> all(ranksHere);
@@ -326,7 +387,18 @@ int main(int argc, char** argv)
         }
         for (auto& p : pipelines) nodeOf(*p)->setSlabExchange(exchange.get());
     }
-    for (int f = 0; f < frames; ++f) {
+    if (!loadStatePath.empty()) {
+        if (ranksHere != 1 || exchange) ARKOSE_LOG(Fatal, "--load-state is for unsharded runs");
+        FILE* fh = std::fopen(loadStatePath.c_str(), "rb");
+        if (!fh) ARKOSE_LOG(Fatal, "cannot read %s", loadStatePath.c_str());
+        std::vector<uint8_t> blob;
+        uint8_t buf[1 << 16];
+        for (size_t n; (n = std::fread(buf, 1, sizeof(buf), fh)) > 0;) blob.insert(blob.end(), buf, buf + n);
+        std::fclose(fh);
+        if (!nodeOf(*pipelines[0])->loadState(blob)) ARKOSE_LOG(Fatal, "DDGINode::loadState failed");
+        std::printf("ddgi_headless: resumed at probe %d\n", nodeOf(*pipelines[0])->probeUpdateIdx());
+    }
+    for (int f = firstFrame; f < firstFrame + frames; ++f) {
         if (f == rebuildAt) {
             // pipeline rebuild (VulkanBackend::reconstructRenderPipelineResources,
             // VulkanBackend.cpp:2327-2347): same nodes, new Registry that adopts the
@@ -339,12 +411,17 @@ int main(int argc, char** argv)
         for (auto& p : pipelines) p->executeFrame(AppState(1.0f / 60.0f, f / 60.0f, static_cast<uint32_t>(f), f == 0), backend);
     }
     backend.synchronize();
+    if (exchange && !exchange->drain()) ARKOSE_LOG(Error, "slab exchange did not complete");
     if (hipDeviceSynchronize() != hipSuccess) ARKOSE_LOG(Error, "device synchronize failed");  // the exchange's side stream
     for (auto& reg : registries) {
         BindingSet* set = reg->getBindingSet("DDGISamplingSet");
         if (!set || set->bindings().size() != 4) ARKOSE_LOG(Fatal, "DDGISamplingSet not published");
     }
     ArkDdgiCtx* ctx = nodeOf(*pipelines[0])->context();
+    if (!saveStatePath.empty()) {
+        std::vector<uint8_t> blob;
+        if (!nodeOf(*pipelines[0])->saveState(blob) || !writeFile(saveStatePath, blob)) ARKOSE_LOG(Fatal, "cannot save the DDGI state");
+    }
     bool ok = dump(ctx, ARK_DDGI_ATLAS_IRRADIANCE, out + ".irr") && dump(ctx, ARK_DDGI_ATLAS_VISIBILITY, out + ".vis") &&
               dump(ctx, ARK_DDGI_SURFELS, out + ".surf");
     if (ranksHere > 1) {

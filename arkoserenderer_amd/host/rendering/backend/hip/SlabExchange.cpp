@@ -3,9 +3,76 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "core/Logging.h"
+
+// --- failure detection -----------------------------------------------------------
+
+ExchangeWatchdog::ExchangeWatchdog(double timeoutSeconds)
+    : m_timeout(timeoutSeconds)
+{
+    if (m_timeout <= 0.0) {
+        const char* e = std::getenv("ARK_EXCHANGE_TIMEOUT_S");
+        m_timeout = e ? std::atof(e) : 0.0;
+        if (m_timeout <= 0.0) m_timeout = 120.0;
+    }
+}
+
+bool ExchangeWatchdog::wait(void* hipEvent, void* ncclComm, const char* what)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    auto sleepFor = std::chrono::microseconds(20);
+    for (;;) {
+        const hipError_t q = hipEventQuery(static_cast<hipEvent_t>(hipEvent));
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) {
+            fail(ncclComm, std::string(what) + ": hipEventQuery: " + hipGetErrorString(q));
+            return false;
+        }
+        if (ncclComm) {
+            ncclResult_t async = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(static_cast<ncclComm_t>(ncclComm), &async);
+            if (r != ncclSuccess || (async != ncclSuccess && async != ncclInProgress)) {
+                fail(ncclComm, std::string(what) + ": communicator error: " + ncclGetErrorString(r != ncclSuccess ? r : async));
+                return false;
+            }
+        }
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (waited > m_timeout) {
+            char buf[96];
+            std::snprintf(buf, sizeof(buf), ": not complete after %.3f s (deadline %.3f s)", waited, m_timeout);
+            fail(ncclComm, std::string(what) + buf);
+            return false;
+        }
+        std::this_thread::sleep_for(sleepFor);
+        sleepFor = std::min(sleepFor * 2, std::chrono::microseconds(2000));
+    }
+}
+
+void ExchangeWatchdog::fail(void* ncclComm, const std::string& why)
+{
+    if (m_onFailure) {
+        m_onFailure(why);
+        return;
+    }
+    abortAndExit(ncclComm, why);
+}
+
+void ExchangeWatchdog::abortAndExit(void* ncclComm, const std::string& why)
+{
+    // abort first: the communicator's pending operations are cancelled and peers
+    // blocked on this rank see an error instead of waiting forever
+    if (ncclComm) (void)ncclCommAbort(static_cast<ncclComm_t>(ncclComm));
+    ARKOSE_LOG(Error, "Z-slab exchange failed, exiting: %s", why.c_str());
+    std::fflush(stderr);
+    std::fflush(stdout);
+    std::_Exit(kExchangeFailureExitCode);
+}
 
 bool SlabBands::fromContext(ArkDdgiCtx* ctx, int rank, int world, SlabBands& out, std::string& error)
 {
@@ -38,8 +105,8 @@ bool RcclSlabExchange::createUniqueId(std::vector<uint8_t>& out)
     return true;
 }
 
-RcclSlabExchange::RcclSlabExchange(int device, int rank, int world, const void* uniqueId, const SlabBands& bands)
-    : m_rank(rank), m_bands(bands)
+RcclSlabExchange::RcclSlabExchange(int device, int rank, int world, const void* uniqueId, const SlabBands& bands, double timeoutSeconds)
+    : m_rank(rank), m_bands(bands), m_watchdog(timeoutSeconds)
 {
     if (hipSetDevice(device) != hipSuccess) {
         m_error = "hipSetDevice failed";
@@ -54,22 +121,33 @@ RcclSlabExchange::RcclSlabExchange(int device, int rank, int world, const void* 
     }
     m_comm = comm;
     hipStream_t s;
-    hipEvent_t e;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    hipEvent_t e0, e1;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
         m_error = "side stream / event creation failed";
         return;
     }
     m_stream = s;
-    m_done = e;
+    m_done[0] = e0;
+    m_done[1] = e1;
     m_ok = true;
 }
 
 RcclSlabExchange::~RcclSlabExchange()
 {
+    // bounded: a stuck exchange ends the process through the watchdog
+    if (m_ok) (void)drain();
     if (m_stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(m_stream));
     if (m_comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(m_comm));
-    if (m_done) (void)hipEventDestroy(static_cast<hipEvent_t>(m_done));
+    for (void* e : m_done)
+        if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
     if (m_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(m_stream));
+}
+
+bool RcclSlabExchange::drain()
+{
+    if (!m_ok || m_frames == 0) return m_ok;
+    return m_watchdog.wait(m_done[(m_frames - 1) & 1u], m_comm, "RcclSlabExchange drain");
 }
 
 void* RcclSlabExchange::exchange(int rank, void* updateDone)
@@ -80,6 +158,9 @@ void* RcclSlabExchange::exchange(int rank, void* updateDone)
     }
     const hipStream_t s = static_cast<hipStream_t>(m_stream);
     const ncclComm_t comm = static_cast<ncclComm_t>(m_comm);
+    void* const slot = m_done[m_frames & 1u];
+    // frame n - 2's all-gather (the last record of this slot) must be complete
+    if (m_frames >= 2 && !m_watchdog.wait(slot, m_comm, "RcclSlabExchange frame n-2")) return nullptr;
     if (updateDone) (void)hipStreamWaitEvent(s, static_cast<hipEvent_t>(updateDone), 0);
     // in place: this rank's band already sits at recvbuff + rank * count
     ncclResult_t r = ncclGroupStart();
@@ -92,14 +173,15 @@ void* RcclSlabExchange::exchange(int rank, void* updateDone)
         ARKOSE_LOG(Error, "RcclSlabExchange: all-gather failed: %s", ncclGetErrorString(r != ncclSuccess ? r : g));
         return nullptr;
     }
-    (void)hipEventRecord(static_cast<hipEvent_t>(m_done), s);
-    return m_done;
+    (void)hipEventRecord(static_cast<hipEvent_t>(slot), s);
+    ++m_frames;
+    return slot;
 }
 
 // --- device copies (one process, one GPU) ----------------------------------------
 
 DeviceCopySlabExchange::DeviceCopySlabExchange(std::vector<SlabBands> ranks)
-    : m_ranks(std::move(ranks)), m_ready(m_ranks.size(), nullptr)
+    : m_ranks(std::move(ranks)), m_ready(m_ranks.size(), nullptr), m_hasArrived(m_ranks.size(), false)
 {
     hipStream_t s;
     hipEvent_t e;
@@ -116,11 +198,19 @@ DeviceCopySlabExchange::~DeviceCopySlabExchange()
     (void)hipStreamDestroy(static_cast<hipStream_t>(m_stream));
 }
 
+bool DeviceCopySlabExchange::drain()
+{
+    return m_watchdog.wait(m_done, nullptr, "DeviceCopySlabExchange drain");
+}
+
 void* DeviceCopySlabExchange::exchange(int rank, void* updateDone)
 {
+    if (m_hasArrived[rank]) ARKOSE_LOG(Fatal, "DeviceCopySlabExchange: rank %d exchanged twice in one frame", rank);
     m_ready[rank] = updateDone;
+    m_hasArrived[rank] = true;
     if (++m_arrived < static_cast<int>(m_ranks.size())) return m_done; // recorded when the last rank arrives
     m_arrived = 0;
+    std::fill(m_hasArrived.begin(), m_hasArrived.end(), false);
     const hipStream_t s = static_cast<hipStream_t>(m_stream);
     for (void* e : m_ready)
         if (e) (void)hipStreamWaitEvent(s, static_cast<hipEvent_t>(e), 0);

@@ -11,6 +11,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -33,7 +34,42 @@ public:
     // Enqueues this rank's share of the exchange of the update that `updateDone`
     // completes. Returns the event the next update's shading waits on.
     virtual void* exchange(int rank, void* updateDone) = 0;
+    // false while the event exchange() returned to `rank` for the current frame is not
+    // recorded yet: an update of the next frame must not be enqueued until it is
+    virtual bool readyForNextUpdate(int rank) const { (void)rank; return true; }
+    // Waits (bounded) until every exchange enqueued so far has completed.
+    virtual bool drain() { return true; }
     virtual const char* name() const = 0;
+};
+
+// Failure detection of the exchange (ncclCommGetAsyncError polling in
+// multi-GPU mode). A dead or stuck peer would otherwise hang every rank forever: the
+// shading of the next frame waits on the all-gather's event on the device, and the
+// host blocks at the next synchronisation. wait() polls the exchange's completion
+// event and the communicator's asynchronous error until a deadline; on an error or
+// at the deadline it calls the failure handler, whose default aborts the
+// communicator (ncclCommAbort), logs an Error and ends the process with
+// kExchangeFailureExitCode (the reference's ARKOSE_LOG(Fatal) -> exit convention,
+// arkcore/core/Logging.h:87; no re-exec).
+class ExchangeWatchdog {
+public:
+    static constexpr int kExchangeFailureExitCode = 14;
+    // (what failed) -> the handler; after it returns, wait() returns false
+    using FailureHandler = std::function<void(const std::string&)>;
+    // timeout from ARK_EXCHANGE_TIMEOUT_S (seconds, default 120) unless given (> 0)
+    explicit ExchangeWatchdog(double timeoutSeconds = 0.0);
+    double timeoutSeconds() const { return m_timeout; }
+    void setFailureHandler(FailureHandler h) { m_onFailure = std::move(h); }
+    // true when `hipEvent` completed; polls ncclCommGetAsyncError(`ncclComm`) meanwhile
+    // (null comm: event only). `what` names the wait in the log.
+    bool wait(void* hipEvent, void* ncclComm, const char* what);
+    // the default failure: ncclCommAbort (if a comm), an Error log, process exit
+    [[noreturn]] static void abortAndExit(void* ncclComm, const std::string& why);
+
+private:
+    void fail(void* ncclComm, const std::string& why);
+    double m_timeout;
+    FailureHandler m_onFailure;
 };
 
 // One process per GPU: ncclAllGather (RCCL over xGMI) of each band in place, on a
@@ -42,12 +78,20 @@ class RcclSlabExchange final : public SlabExchange {
 public:
     // `uniqueId` = the 128-byte ncclUniqueId all ranks share (rank 0 creates it,
     // createUniqueId); the communicator is created here (ncclCommInitRank).
-    RcclSlabExchange(int device, int rank, int world, const void* uniqueId, const SlabBands& bands);
+    RcclSlabExchange(int device, int rank, int world, const void* uniqueId, const SlabBands& bands, double timeoutSeconds = 0.0);
     ~RcclSlabExchange() override;
     bool ok() const { return m_ok; }
     const std::string& error() const { return m_error; }
+    // Frame n's all-gather first waits (bounded, on the host) for frame n - 2's: the
+    // host runs at most two exchanges ahead of the device, and a peer that stops
+    // answering ends the process at the deadline instead of hanging it.
     void* exchange(int rank, void* updateDone) override;
+    bool drain() override;
     const char* name() const override { return "rccl"; }
+    ExchangeWatchdog& watchdog() { return m_watchdog; }
+    // the side stream the all-gathers run on (hipStream_t) and the communicator
+    void* stream() const { return m_stream; }
+    void* comm() const { return m_comm; }
     static bool createUniqueId(std::vector<uint8_t>& out);
 
 private:
@@ -55,9 +99,11 @@ private:
     SlabBands m_bands;
     void* m_comm { nullptr };
     void* m_stream { nullptr };
-    void* m_done { nullptr };
+    void* m_done[2] { nullptr, nullptr }; // completion of frame n in slot n & 1
+    uint64_t m_frames { 0 };
     bool m_ok { false };
     std::string m_error;
+    ExchangeWatchdog m_watchdog;
 };
 
 // P contexts in one process (the one-GPU test harness): the same band exchange as
@@ -69,12 +115,18 @@ public:
     explicit DeviceCopySlabExchange(std::vector<SlabBands> ranks);
     ~DeviceCopySlabExchange() override;
     void* exchange(int rank, void* updateDone) override;
+    // a rank that already arrived at a frame the others have not finished may not
+    // update again: its next shading would wait on the previous frame's record
+    bool readyForNextUpdate(int rank) const override { return !m_hasArrived[rank]; }
+    bool drain() override;
     const char* name() const override { return "device-copy"; }
 
 private:
     std::vector<SlabBands> m_ranks;
     std::vector<void*> m_ready;
+    std::vector<bool> m_hasArrived;
     int m_arrived { 0 };
+    ExchangeWatchdog m_watchdog;
     void* m_stream { nullptr };
     void* m_done { nullptr };
 };

@@ -20,6 +20,31 @@ DDGINode::~DDGINode()
     if (m_updateDone) (void)hipEventDestroy(static_cast<hipEvent_t>(m_updateDone));
 }
 
+bool DDGINode::saveState(std::vector<uint8_t>& out) const
+{
+    uint64_t bytes = 0;
+    if (!m_ctx || ark_ddgi_state_size(m_ctx, &bytes) != ARK_DDGI_OK) return false;
+    out.resize(bytes);
+    if (int rc = ark_ddgi_save_state(m_ctx, out.data(), bytes); rc != ARK_DDGI_OK) {
+        ARKOSE_LOG(Error, "DDGINode: ark_ddgi_save_state failed (%d): %s", rc, ark_ddgi_last_error(m_ctx));
+        return false;
+    }
+    return true;
+}
+
+bool DDGINode::loadState(const std::vector<uint8_t>& blob)
+{
+    if (!m_ctx) return false;
+    if (int rc = ark_ddgi_load_state(m_ctx, blob.data(), blob.size()); rc != ARK_DDGI_OK) {
+        ARKOSE_LOG(Error, "DDGINode: ark_ddgi_load_state failed (%d): %s", rc, ark_ddgi_last_error(m_ctx));
+        return false;
+    }
+    uint32_t next = 0;
+    if (ark_ddgi_get_next_probe_index(m_ctx, &next) != ARK_DDGI_OK) return false;
+    m_probeUpdateIdx = static_cast<int>(next);
+    return true;
+}
+
 RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registry& reg)
 {
     // DDGINode.cpp:39-42
@@ -111,6 +136,8 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
         if (m_exchange) {
             // Z-slab rank: traversal goes ahead, shading waits for the previous exchange;
             // this update's bands are then exchanged on the exchange's side stream
+            if (!m_exchange->readyForNextUpdate(m_shardRank))
+                ARKOSE_LOG(Fatal, "DDGINode: rank %d updates again before every rank's %s exchange of its previous frame", m_shardRank, m_exchange->name());
             if (!m_updateDone) {
                 hipEvent_t e;
                 if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) ARKOSE_LOG(Fatal, "DDGINode: event creation failed");

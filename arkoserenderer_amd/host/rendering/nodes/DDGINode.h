@@ -9,6 +9,9 @@
 #include "../RenderPipelineNode.h"
 #include "../backend/hip/SlabExchange.h"
 
+#include <cstdint>
+#include <vector>
+
 class DDGINode final : public RenderPipelineNode {
 public:
     std::string name() const override { return "DDGI"; }
@@ -33,6 +36,11 @@ public:
     void* pendingExchange() const { return m_exchangePending; }
     ArkDdgiCtx* context() const { return m_ctx; }
     int probeUpdateIdx() const { return m_probeUpdateIdx; }
+    void setProbeUpdateIdx(int idx) { m_probeUpdateIdx = idx; }
+    // DDGI history checkpoint (ark_ddgi_save_state / _load_state): atlases, offsets and
+    // the rolling window position, so a resumed node continues where it stopped
+    bool saveState(std::vector<uint8_t>& out) const;
+    bool loadState(const std::vector<uint8_t>& blob);
 
     // we can dynamically choose to do fewer samples or probes, but not more since it defines the fixed image size
     static constexpr int MaxNumProbeSamples { ARK_DDGI_MAX_RAYS_PER_PROBE };

@@ -161,6 +161,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if exch is not None:
+        exch.drain()  # bounded (collective.ExchangeWatchdog): a dead peer ends the run
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()

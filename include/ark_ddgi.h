@@ -18,6 +18,8 @@
  *                           (material.glsl:9-14), SceneLightSet (lighting.glsl:8-17),
  *                           environment map (GpuScene.cpp:1041-1048). The BVH that the
  *                           Vulkan driver builds is built here instead.
+ *   ark_ddgi_share_scene <- one scene (TLAS + buffers) bound by several nodes of one
+ *                           device: the Z-slab contexts of a GPU share it.
  *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:132-259):
  *                           traceRays -> irradiance update -> visibility update ->
  *                           border copies -> probe offsets.
@@ -284,8 +286,16 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** out_ctx);
 void ark_ddgi_destroy(ArkDdgiCtx* ctx);
 const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx);
 
-/* Copies the scene arrays to HBM and builds the BVH (host arrays are not retained). */
+/* Copies the scene arrays to HBM and builds the BVH (host arrays are not retained).
+ * On error the context is left without a scene (ARK_DDGI_E_NO_SCENE on update). */
 int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
+
+/* Makes `ctx` use the scene of `src` (same device): the device arrays and BVH that
+ * src's last set_scene built are shared, not copied, and stay alive while any context
+ * uses them. For the Z-slab contexts of one GPU (the reference binds one TLAS and one
+ * set of scene buffers per device, GpuScene.cpp:872-1010); a later set_scene on
+ * either context gives it a scene of its own. */
+int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src);
 
 /* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null
  * stream). Asynchronous: call ark_ddgi_synchronize or synchronize the stream before
@@ -300,9 +310,14 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
  * every result is the serial one. Everything else of the update (shadow rays,
  * shading, atlas update, done_event) stays on `hip_stream`, so the stream's
  * completion still means the update is complete. A caller that writes probe offsets
- * through device pointers between updates should use ark_ddgi_write instead, or set
- * ARK_DDGI_PIPELINE=0. Instrumented updates (timing, counting) run serially. */
+ * through device pointers (ark_ddgi_get_device_views) between updates calls
+ * ark_ddgi_mark_external_write after enqueueing that write: the next update then runs
+ * serially, after it. Instrumented updates (timing, counting) run serially. */
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
+/* The caller wrote context resources through device pointers (probe offsets, atlases)
+ * on the stream of the next update: that update waits for the write instead of
+ * starting its traversal on the internal stream (see Frames in flight above). */
+int ark_ddgi_mark_external_write(ArkDdgiCtx* ctx);
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
 /* ark_ddgi_update for a Z-slab rank that overlaps the atlas exchange with the next
@@ -323,12 +338,17 @@ int ark_ddgi_get_device_views(ArkDdgiCtx* ctx, ArkDdgiDeviceViews* out_views);
 
 /* DDGI history checkpoint: irradiance + visibility atlases and probe offsets
  * behind a header (magic "ARKDDGI1", grid dims / spacing / origin, zFar, clear mode,
- * shard rank / count). Blocking. load_state requires a blob of a context with the
- * same grid, zFar and shard (ARK_DDGI_E_SIZE_MISMATCH / _INVALID_ARGUMENT
- * otherwise) and leaves the context unchanged on any error. */
+ * shard rank / count, the rolling window's next first probe). Blocking. load_state
+ * requires a blob of a context with the same grid, zFar and shard
+ * (ARK_DDGI_E_SIZE_MISMATCH / _INVALID_ARGUMENT otherwise) and leaves the context
+ * unchanged on any error. */
 int ark_ddgi_state_size(const ArkDdgiCtx* ctx, uint64_t* out_bytes);
 int ark_ddgi_save_state(ArkDdgiCtx* ctx, void* host_dst, uint64_t bytes);
 int ark_ddgi_load_state(ArkDdgiCtx* ctx, const void* host_src, uint64_t bytes);
+/* The rolling window's next first probe: (first_probe_index + K) % N of the last
+ * update, or the value a loaded state carried (0 for a new context). The node resumes
+ * its m_probeUpdateIdx (DDGINode.h:32, advanced at DDGINode.cpp:258) from it. */
+int ark_ddgi_get_next_probe_index(const ArkDdgiCtx* ctx, uint32_t* out_index);
 
 /* Re-applies the creation-time clears (Registry created the textures anew). */
 int ark_ddgi_reset_history(ArkDdgiCtx* ctx);

@@ -87,3 +87,36 @@ def test_cpp_rccl_exchange_one_rank(tmp_path):
     assert "rccl exchange" in log
     for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32)):
         assert np.array_equal(np.fromfile(got + "." + k, dtype=dt), np.fromfile(ref + "." + k, dtype=dt)), k
+
+
+def test_cpp_rccl_exchange_watchdog_deadline(tmp_path):
+    """Failure detection of the C++ exchange: a 1-rank communicator whose
+    side stream is stalled for 1.5 s (a bounded kernel) under a 0.2 s deadline. Frame
+    2's exchange waits for frame 0's all-gather, the watchdog polls the event and
+    ncclCommGetAsyncError, fires at the deadline, and the default failure path aborts
+    the communicator, logs an Error and ends the process with exit code 14 (the stall
+    kernel is allowed to finish first, so nothing is left running on the GPU)."""
+    sc = scenes.features_scene()
+    path = str(tmp_path / "features.arkscn")
+    sc.save_binary(path)
+    cmd = [EXE, "--scene", path, "--grid", "6", "4", "6", "--spacing", "0.7", "0.7", "0.7", "--origin", "-1.75", "0.25", "-1.75",
+           "--rays", "64", "--updates", "100", "--frames", "4", "--zfar", "100", "--out", str(tmp_path / "dl"),
+           "--world", "1", "--rank", "0", "--nccl-id", str(tmp_path / "nccl.id"), "--exchange-deadline-test"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 14, (r.returncode, r.stdout, r.stderr)
+    assert "watchdog fired: RcclSlabExchange frame n-2: not complete after" in r.stdout, r.stdout
+    assert "[Error] Z-slab exchange failed, exiting" in r.stderr, r.stderr
+
+
+def test_cpp_rccl_rendezvous_ignores_stale_id(tmp_path):
+    """Rank 0 replaces an id file left by an earlier run: a stale file
+    holding garbage sits at the path before the 1-rank run starts; the run must still
+    initialise its communicator and equal the unsharded run."""
+    ref, _ = _headless(tmp_path, "ref", [])
+    stale = tmp_path / "nccl.id"
+    stale.write_bytes(b"\xab" * 128)
+    got, log = _headless(tmp_path, "rccl", ["--world", "1", "--rank", "0", "--nccl-id", str(stale), "--nccl-nonce", "run-2"])
+    assert "rccl exchange" in log
+    assert stale.read_bytes().endswith(b"run-2")
+    for k, dt in (("irr", np.uint16), ("vis", np.uint16)):
+        assert np.array_equal(np.fromfile(got + "." + k, dtype=dt), np.fromfile(ref + "." + k, dtype=dt)), k

@@ -215,3 +215,99 @@ def test_bench_frame_loop_over_one_rank_rccl():
         dist.destroy_process_group()
         plain.ctx.close()
         ranked.ctx.close()
+
+
+def _stalled_exchange_run(timeout_s, on_failure, port):
+    """bench.py's N > 1 frame loop over a 1-rank RCCL communicator whose first
+    all-gather queues behind a bounded ~1.5 s kernel on the exchange stream
+    (torch.cuda._sleep): frame 2's step must wait for frame 0's all-gather."""
+    import torch
+    import torch.distributed as dist
+
+    from arkoserenderer_amd.collective import ExchangeWatchdog, OverlappedSlabExchange, SlabExchange
+
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((4, 4, 4), (0.5, 0.5, 0.5), (-0.75, 0.25, -0.75))
+    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=64, max_rays_per_probe=32, max_probe_updates=64)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    node = D.DDGINode(cfg)
+    assert node.construct(sc, grid, ex["z_far"], device=0, shard_rank=0, shard_count=1,
+                          light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    gather = SlabExchange.from_views(node.ctx.device_views(), 0, 1, dev).exchange
+    calls = []
+
+    def exchange():
+        if not calls:
+            torch.cuda._sleep(int(3.5e9))  # bounded: ends by itself after ~1.5 s
+        calls.append(1)
+        gather()
+
+    wd = ExchangeWatchdog(timeout_s=timeout_s, on_failure=on_failure)
+    exch = OverlappedSlabExchange(node, exchange, dev, wd)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    results = [exch.step(D.AppState(f), sptr) for f in range(3)]
+    return node, exch, results
+
+
+def test_python_exchange_watchdog_fires_at_deadline():
+    """collective.ExchangeWatchdog (SURVEY §5 failure detection): with the exchange
+    stream stalled and a 0.2 s deadline, frame 2's step does not enqueue anything and
+    reports the timeout to the failure handler; a generous deadline lets the same
+    stall pass."""
+    import torch
+    import torch.distributed as dist
+
+    fired = []
+    node, exch, res = _stalled_exchange_run(0.2, fired.append, 29547)
+    try:
+        assert res[0] is not None and res[1] is not None and res[2] is None
+        assert len(fired) == 1 and "slab exchange frame n-2: not complete after" in fired[0], fired
+    finally:
+        torch.cuda.synchronize()  # the stall kernel finishes by itself
+        dist.destroy_process_group()
+        node.ctx.close()
+    fired = []
+    node, exch, res = _stalled_exchange_run(30.0, fired.append, 29548)
+    try:
+        assert all(r is not None for r in res) and not fired
+        assert exch.drain()
+    finally:
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+        node.ctx.close()
+
+
+def test_python_exchange_watchdog_exits_process(tmp_path):
+    """The default failure path in its own process: the process group is aborted, an
+    Error is logged and the process ends with exit code 14 (the handler lets the
+    bounded stall kernel finish first)."""
+    import subprocess
+    import sys
+
+    tests = os.path.dirname(os.path.abspath(__file__))
+    script = tmp_path / "wd.py"
+    script.write_text(
+        "import sys, torch\n"
+        f"sys.path.insert(0, {os.path.dirname(tests)!r}); sys.path.insert(0, {tests!r})\n"
+        "import test_gpu_sharded as T\n"
+        "box = {}\n"
+        "def fail(why):\n"
+        "    torch.cuda.synchronize()\n"
+        "    box['exch'].watchdog.abort_and_exit(why)\n"
+        "class Lazy:\n"
+        "    def __call__(self, why): fail(why)\n"
+        "import arkoserenderer_amd.collective as Cl\n"
+        "orig = Cl.OverlappedSlabExchange.__init__\n"
+        "def init(self, *a, **k):\n"
+        "    orig(self, *a, **k); box['exch'] = self\n"
+        "Cl.OverlappedSlabExchange.__init__ = init\n"
+        "T._stalled_exchange_run(0.2, Lazy(), 29549)\n"
+        "print('not reached')\n")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 14, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "not reached" not in r.stdout
+    assert "[Error] Z-slab exchange failed, exiting: slab exchange frame n-2: not complete after" in r.stderr

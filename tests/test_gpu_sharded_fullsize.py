@@ -1,0 +1,143 @@
+"""The Z-slab path at full C4 size (BASELINE config "Synthetic
+10M-triangle soup, 32x32x32 probes x 256 rays, 8xMI355X Z-slab shard"): P = 8 slab
+contexts on one GPU (one scene shared by ark_ddgi_share_scene), each updating only
+its slab of the whole-grid window (K = N), exchanging the atlas bands by device
+copies on a side stream in the order OverlappedSlabExchange issues the RCCL
+all-gather (frame n+1's traversal goes ahead, its shading waits for frame n's
+exchange), for 2 frames. Checked:
+
+  * every slab context's gathered atlases equal an unsharded context's (same
+    scene, same frames) over the WHOLE atlas, bit for bit, after each frame, and
+    every slab's offsets equal the unsharded offsets on the probes it owns;
+  * oracle windows in every slab (one x-row of 32 probes per slab, frames 0 and 1,
+    frame 1 from the GPU's gathered frame-0 atlases): the slab context's surfels at
+    their compacted slots (k_probe_slots' closed-form rank), atlas tiles (interior +
+    border) and owner offsets, bit for bit, as test_gpu_fullsize.py does unsharded.
+
+P = 8 slabs are 4 probe layers deep (a 4,096-probe, 1 M-ray window per rank): the
+half-occupancy pipelined traversal (below 5 M rays) and 4-layer slot compaction run."""
+import numpy as np
+import pytest
+
+from arkoserenderer_amd import abi
+from arkoserenderer_amd import ddgi as D
+from arkoserenderer_amd import scene as S
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+ATLASES = (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY)
+
+
+def _tile_mask(dims, probes, res):
+    X, Y, Z = dims
+    t = res + 2
+    m = np.zeros((Z * t, X * Y * t), bool)
+    for p in probes:
+        y, rem = divmod(int(p), X * Z)
+        z, x = divmod(rem, X)
+        m[z * t:(z + 1) * t, (x + y * X) * t:(x + y * X + 1) * t] = True
+    return m
+
+
+@pytest.mark.parametrize("P", [8])
+def test_c4_eight_zslabs_one_gpu_full_size(P):
+    import torch
+
+    from arkoserenderer_amd.collective import device_bytes
+
+    scene = S.soup(10_000_000)
+    dims = (32, 32, 32)
+    X, Y, Z = dims
+    grid = D.ProbeGrid(dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    N, R, Zs = grid.probe_count(), 256, Z // P
+    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    full = D.DDGIContext(grid, 10000.0, cfg)
+    full.set_scene(scene)
+    slabs = [D.DDGIContext(grid, 10000.0, cfg, 0, r, P) for r in range(P)]
+    for c in slabs:
+        c.share_scene(full)
+    views = [c.device_views() for c in slabs]
+    atl = [[(device_bytes(v.irradiance_atlas, v.irradiance_bytes, dev), int(v.irradiance_slab_offset), int(v.irradiance_slab_bytes)),
+            (device_bytes(v.visibility_atlas, v.visibility_bytes, dev), int(v.visibility_slab_offset), int(v.visibility_slab_bytes))] for v in views]
+    streams = [torch.cuda.Stream(dev) for _ in slabs]
+    comm = torch.cuda.Stream(dev)
+    done = [torch.cuda.Event() for _ in slabs]
+    gathered = torch.cuda.Event()
+    for e in done + [gathered]:
+        e.record(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize(dev)
+
+    zof = (np.arange(N) % (X * Z)) // X
+    owner = zof // Zs
+    ocfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=X, max_rays_per_probe=R, max_probe_updates=X, compute_probe_offsets=True)
+    orc = O.Oracle(D.desc_for(grid, 10000.0, ocfg))
+    orc.set_scene(scene, threads=16)
+    # one x-row of X probes per slab: z = the slab's 2nd layer (or its 1st), y spread
+    windows = [(r, X * (r * Zs + (r % 2) * (Zs // 2)) + X * Z * ((5 * r + 3) % Y)) for r in range(P)]
+    start = None
+    for frame in range(2):
+        p = D.frame_params(cfg, grid, D.AppState(frame), 0, **exposure)
+        for c, s, e in zip(slabs, streams, done):
+            c.update_overlapped(p, s.cuda_stream, gathered.cuda_event if frame > 0 else None, e.cuda_event)
+        with torch.cuda.stream(comm):
+            for e in done:
+                comm.wait_event(e)
+            for k in range(2):  # each owner's band into every other context
+                for src in range(P):
+                    t, off, n = atl[src][k]
+                    for dst in range(P):
+                        if dst != src:
+                            atl[dst][k][0][off:off + n].copy_(t[off:off + n])
+            gathered.record(comm)
+        full.update(p)
+        torch.cuda.synchronize(dev)
+        # 1. the gathered atlases of every slab context = the unsharded context's, whole
+        want = {w: full.read(w) for w in ATLASES}
+        for r, c in enumerate(slabs):
+            for w in ATLASES:
+                got = c.read(w)
+                assert np.array_equal(got, want[w]), f"frame {frame} slab {r}: {int(np.count_nonzero(got != want[w]))} atlas values of {w} differ"
+        full_off = full.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)
+        merged_off = np.zeros_like(full_off)
+        for r, c in enumerate(slabs):
+            mine = owner == r
+            o = c.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)
+            assert np.array_equal(o[mine].view(np.uint32), full_off[mine].view(np.uint32)), f"frame {frame} slab {r}: offsets differ"
+            merged_off[mine] = o[mine]
+        assert np.count_nonzero(full_off) > 0
+        # 2. oracle windows in every slab
+        for r, first in windows:
+            if frame == 0:
+                orc.reset_history()
+            else:
+                for w in ATLASES:
+                    orc.write(w, start[w])
+                orc.write(abi.ARK_DDGI_PROBE_OFFSETS, start["off"])
+            orc.update(D.frame_params(ocfg, grid, D.AppState(frame), first, **exposure), threads=16)
+            probes = np.arange(first, first + X)
+            assert np.all(owner[probes] == r)
+            y, z = probes[0] // (X * Z), (probes[0] % (X * Z)) // X
+            slot0 = y * X * Zs + (z - r * Zs) * X  # rank of the probe among the slab's window probes
+            gs = slabs[r].read(abi.ARK_DDGI_SURFELS).reshape(N, R, 4)[slot0:slot0 + X]
+            os_ = orc.read(abi.ARK_DDGI_SURFELS).reshape(X, R, 4)
+            bad = np.argwhere(np.any(gs != os_, axis=-1))
+            assert bad.size == 0, f"frame {frame} slab {r}: {len(bad)} surfels differ, first (slot, ray) {bad[:4].tolist()}"
+            assert np.count_nonzero(os_) > 0
+            for w, res, ch in ((abi.ARK_DDGI_ATLAS_IRRADIANCE, 8, 4), (abi.ARK_DDGI_ATLAS_VISIBILITY, 16, 2)):
+                m = _tile_mask(dims, probes, res)
+                ga = slabs[r].read(w).reshape(m.shape[0], m.shape[1], ch)[m]
+                oa = orc.read(w).reshape(m.shape[0], m.shape[1], ch)[m]
+                same = (ga == oa) | (np.isnan(O.f16_to_f32(ga)) & np.isnan(O.f16_to_f32(oa)))
+                assert same.all(), f"frame {frame} slab {r}: {int((~same).sum())} tile values of {w} differ from the oracle"
+            go = slabs[r].read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[probes]
+            oo = orc.read(abi.ARK_DDGI_PROBE_OFFSETS).reshape(N, 4)[probes]
+            assert np.array_equal(go.view(np.uint32), oo.view(np.uint32)), f"frame {frame} slab {r}: offsets differ from the oracle"
+        start = {w: slabs[0].read(w) for w in ATLASES}
+        start["off"] = merged_off.reshape(-1)
+    for c in slabs + [full]:
+        c.close()
+    orc.close()

@@ -1,7 +1,9 @@
 """DDGI history checkpoint through the C-ABI (ark_ddgi_save_state / _load_state):
-frames 0..4 straight equal frames 0..2, a save, a fresh context that loads the
-blob, and frames 3..4 — bit for bit (atlases, offsets, surfels). A blob of another
-grid or a truncated one is refused and leaves the context unchanged."""
+frames 0..4 straight equal frames 0..2, a save, a fresh node that loads the blob
+(atlases, offsets and the rolling window position), and frames 3..4 — bit for bit
+(atlases, offsets, surfels), through the Python node and through the C++ DDGINode
+(DDGINode::saveState / loadState, driven by ddgi_headless). A blob of another grid
+or a truncated one is refused and leaves the context unchanged."""
 import numpy as np
 import pytest
 
@@ -34,13 +36,14 @@ def test_save_load_resumes_bit_exactly():
     b = _node(sc)
     for f in range(3):
         b.execute(D.AppState(f))
-    blob = b.ctx.save_state()
+    blob = b.save_state()
     idx = b.probe_update_idx
+    assert idx == 300 % GRID.probe_count()
     b.ctx.close()
 
     c = _node(sc)
-    c.ctx.load_state(blob)
-    c.probe_update_idx = idx
+    c.load_state(blob)  # the window position travels in the blob's header
+    assert c.probe_update_idx == idx
     for f in range(3, 5):
         c.execute(D.AppState(f))
     c.ctx.synchronize()
@@ -74,3 +77,33 @@ def test_load_state_refuses_foreign_and_truncated_blobs():
     for w in WHICH[:3]:
         assert np.array_equal(a.ctx.read(w), before[w]), w
     a.ctx.close()
+
+
+def test_cpp_node_save_load_resumes_window(tmp_path):
+    """The C++ DDGINode resumes from a checkpoint: a run of frames 0..4 equals frames
+    0..2 saved by one process and frames 3..4 of another process that loads the
+    blob - the node's window index (100 probes per frame of 144: it wraps) comes back
+    from the blob, not from a hand-set member."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "arkoserenderer_amd", "bin", "ddgi_headless")
+    sc = scenes.features_scene()
+    path = str(tmp_path / "features.arkscn")
+    sc.save_binary(path)
+    base = [exe, "--scene", path, "--grid", "6", "4", "6", "--spacing", "0.7", "0.7", "0.7", "--origin", "-1.75", "0.25", "-1.75",
+            "--rays", "64", "--updates", "100", "--zfar", "100", "--exposure", "0.5", "--env", "0.8", "--ambient", "0.1", "--offsets", "1"]
+
+    def run(*extra):
+        r = subprocess.run(base + list(extra), capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+
+    run("--frames", "5", "--out", str(tmp_path / "straight"))
+    run("--frames", "3", "--out", str(tmp_path / "first"), "--save-state", str(tmp_path / "state.bin"))
+    log = run("--frames", "2", "--first-frame", "3", "--load-state", str(tmp_path / "state.bin"), "--out", str(tmp_path / "resumed"))
+    assert "resumed at probe 12" in log  # 300 % 144
+    for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32), ("surf", np.uint16)):
+        a = np.fromfile(str(tmp_path / f"straight.{k}"), dtype=dt)
+        b = np.fromfile(str(tmp_path / f"resumed.{k}"), dtype=dt)
+        assert np.array_equal(a, b), k
