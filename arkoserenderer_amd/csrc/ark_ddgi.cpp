@@ -31,6 +31,8 @@ namespace {
 
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
 constexpr uint32_t kPipeHalfRays = 5u << 20;
+// u32 words per shadow-ray bin counter (ddgi_kernels.hip kBinStride)
+constexpr uint64_t kShadowBinStride = 32;
 
 // roctx range over a scope (host-side enqueue markers, named after the reference's
 // ScopedDebugZone labels, DDGINode.cpp:152-247); end() closes it early.
@@ -131,6 +133,7 @@ struct SceneStore {
     ArkDdgiBvhStats bvhStats {};
     uint32_t bvhMaxDepth = 0;
     uint32_t lightCount = 0;
+    float boundsLo[3] { 0, 0, 0 }, boundsHi[3] { 0, 0, 0 }; // world AABB of all triangles
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
     SceneStore& operator=(const SceneStore&) = delete;
@@ -168,6 +171,11 @@ struct ArkDdgiCtx {
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0, shadowBlocksPerCu = 1;
+    // light-space binning of the shadow-ray list (FrameArgs::shadow_bin_grid); the sun's
+    // cell axes follow from the scene (adoptScene)
+    uint32_t shadowBinGrid = 0; // ARK_SHADOW_BIN_GRID (off: measured slower)
+    uint32_t shadowBinMinRays = 1u << 16; // windows below this many probe rays keep the queue order
+    float sunBinAxes[2][4] = {};
     // Frames in flight (updateImpl): the per-frame buffers the traversal writes come in
     // two sets (slot table, slot order, sample directions, hit records, work counters);
     // frame n uses set n & 1. Frame n's slot table, primary traversal and probe offsets
@@ -287,13 +295,44 @@ hipError_t orderEnd(ArkDdgiCtx* ctx, hipStream_t s)
 
 // Shading work set for the largest window: per-ray light bits, then k_shadow_gen's
 // shadow-ray list (at most one ray per probe ray and light).
+// With binning (shadowBinGrid > 0) also the generator's unsorted list, the per-entry
+// bin key and rank, and the bin counts / starts.
+struct ShadeWorkLayout {
+    uint64_t bits, list, gen, key, rank, count, start, total;
+};
+
+ShadeWorkLayout shadeWorkLayout(const ArkDdgiCtx* ctx)
+{
+    auto al = [](uint64_t b) { return (b + 255) & ~static_cast<uint64_t>(255); };
+    const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
+    const uint64_t entries = rays * ctx->lightCount;
+    const uint64_t bins = ctx->shadowBinGrid ? static_cast<uint64_t>(ctx->lightCount) * ctx->shadowBinGrid * ctx->shadowBinGrid : 0;
+    ShadeWorkLayout w {};
+    w.bits = 0;
+    w.list = al(rays * 4);
+    w.gen = w.list + al(entries * sizeof(ShadowRay));
+    const uint64_t binned = bins ? 1 : 0;
+    w.key = w.gen + binned * al(entries * sizeof(ShadowRay));
+    w.rank = w.key + binned * al(entries * 4);
+    w.count = w.rank + binned * al(entries * 4);
+    w.start = w.count + al(bins * 4 * kShadowBinStride);
+    w.total = w.start + al(bins * 4);
+    return w;
+}
+
 int ensureShadeWork(ArkDdgiCtx* ctx)
 {
     const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
     if (rays >= (1ull << 28) && ctx->lightCount > 0)
         return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "%llu rays per update: shadow-ray owners pack (ray << 4) | light in 32 bits", static_cast<unsigned long long>(rays));
-    const uint64_t bytes = ((rays * 4 + 255) & ~static_cast<uint64_t>(255)) + rays * ctx->lightCount * sizeof(ShadowRay);
-    if (ctx->shadeWork.bytes < bytes) ARK_HIP(ctx->shadeWork.alloc(bytes));
+    const ShadeWorkLayout w = shadeWorkLayout(ctx);
+    if (ctx->shadeWork.bytes < w.total) {
+        ARK_HIP(ctx->shadeWork.alloc(w.total));
+        // the bin counts start at zero; the bin scan zeroes them again after each frame
+        if (w.start > w.count) ARK_HIP(hipMemset(static_cast<char*>(ctx->shadeWork.ptr) + w.count, 0, w.start - w.count));
+    } else if (w.start > w.count) {
+        ARK_HIP(hipMemset(static_cast<char*>(ctx->shadeWork.ptr) + w.count, 0, w.start - w.count));
+    }
     return ARK_DDGI_OK;
 }
 
@@ -343,6 +382,34 @@ int adoptScene(ArkDdgiCtx* ctx, std::shared_ptr<SceneStore> st)
     ctx->bvhStats = st->bvhStats;
     ctx->bvhMaxDepth = st->bvhMaxDepth;
     ctx->lightCount = st->lightCount;
+    // Sun cells: an orthonormal pair (e1, e2) perpendicular to the sun direction, the
+    // scene AABB's projection onto it mapped to [0, G) (shadowBinKey)
+    if (st->args.has_sun && ctx->shadowBinGrid) {
+        const float* d = st->args.sun_dir;
+        const double n = std::sqrt(double(d[0]) * d[0] + double(d[1]) * d[1] + double(d[2]) * d[2]);
+        const double L[3] = { n > 0 ? d[0] / n : 0.0, n > 0 ? d[1] / n : 1.0, n > 0 ? d[2] / n : 0.0 };
+        const int least = std::fabs(L[0]) <= std::fabs(L[1]) && std::fabs(L[0]) <= std::fabs(L[2]) ? 0 : (std::fabs(L[1]) <= std::fabs(L[2]) ? 1 : 2);
+        double a[3] = { 0, 0, 0 };
+        a[least] = 1.0;
+        double e1[3] = { L[1] * a[2] - L[2] * a[1], L[2] * a[0] - L[0] * a[2], L[0] * a[1] - L[1] * a[0] };
+        const double n1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        for (double& c : e1) c /= n1;
+        const double e2[3] = { L[1] * e1[2] - L[2] * e1[1], L[2] * e1[0] - L[0] * e1[2], L[0] * e1[1] - L[1] * e1[0] };
+        const double* E[2] = { e1, e2 };
+        for (int k = 0; k < 2; ++k) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int c = 0; c < 8; ++c) {
+                const double P[3] = { (c & 1) ? st->boundsHi[0] : st->boundsLo[0], (c & 2) ? st->boundsHi[1] : st->boundsLo[1],
+                                      (c & 4) ? st->boundsHi[2] : st->boundsLo[2] };
+                const double u = P[0] * E[k][0] + P[1] * E[k][1] + P[2] * E[k][2];
+                lo = std::min(lo, u);
+                hi = std::max(hi, u);
+            }
+            const double scale = ctx->shadowBinGrid / std::max(hi - lo, 1e-6);
+            for (int c = 0; c < 3; ++c) ctx->sunBinAxes[k][c] = static_cast<float>(E[k][c] * scale);
+            ctx->sunBinAxes[k][3] = static_cast<float>(-lo * scale);
+        }
+    }
     ctx->sceneStore = std::move(st);
     int rc;
     if ((rc = ensureShadeWork(ctx)) != 0) return rc;
@@ -407,6 +474,13 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
+        // ARK_SHADOW_BIN_GRID: light-space cells per axis of the shadow-ray binning
+        // (a power of 2 up to 256), 0 = the list in queue order
+        if (const char* g = std::getenv("ARK_SHADOW_BIN_GRID")) {
+            const int v = std::atoi(g);
+            ctx->shadowBinGrid = v <= 0 ? 0u : static_cast<uint32_t>(std::min(256, 1 << static_cast<int>(std::ceil(std::log2(std::max(1, v))))));
+        }
+        if (const char* m = std::getenv("ARK_SHADOW_BIN_MIN_RAYS")) ctx->shadowBinMinRays = static_cast<uint32_t>(std::max(0, std::atoi(m)));
     }
     if ((e = hipStreamCreateWithFlags(&ctx->traceStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evTraced, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
@@ -547,6 +621,10 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
                         hi[a] = std::max(hi[a], v[a]);
                     }
         opt.inflate_abs = bvh8_inflation_box(lo, hi); // one inflation for all classes (shadow rays test all)
+        for (int a = 0; a < 3; ++a) {
+            st->boundsLo[a] = lo[a] <= hi[a] ? lo[a] : 0.0f;
+            st->boundsHi[a] = lo[a] <= hi[a] ? hi[a] : 0.0f;
+        }
     }
     // host threads for the build: the box's CPU share per GPU is 16 cores
     opt.threads = 16;
@@ -866,10 +944,23 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.counters = ctx->counters.as<unsigned long long>();
     // shading work set (ensureShadeWork): per-ray light bits | shadow-ray list
     {
-        const uint64_t rays = Kmax * Rmax;
+        const ShadeWorkLayout l = shadeWorkLayout(ctx);
         char* w = static_cast<char*>(ctx->shadeWork.ptr);
-        f.shadow_bits = reinterpret_cast<uint32_t*>(w);
-        f.shadow_rays = reinterpret_cast<ShadowRay*>(w + ((rays * 4 + 255) & ~static_cast<uint64_t>(255)));
+        f.shadow_bits = reinterpret_cast<uint32_t*>(w + l.bits);
+        f.shadow_rays = reinterpret_cast<ShadowRay*>(w + l.list);
+        f.shadow_rays_gen = f.shadow_rays;
+        f.shadow_bin_grid = 0;
+        // binning pays for itself on large lists only (a window of a few probes is
+        // one wave's work either way)
+        if (ctx->shadowBinGrid && f.window_rays >= ctx->shadowBinMinRays) {
+            f.shadow_bin_grid = ctx->shadowBinGrid;
+            f.shadow_rays_gen = reinterpret_cast<ShadowRay*>(w + l.gen);
+            f.shadow_bin_key = reinterpret_cast<uint32_t*>(w + l.key);
+            f.shadow_bin_rank = reinterpret_cast<uint32_t*>(w + l.rank);
+            f.shadow_bin_count = reinterpret_cast<uint32_t*>(w + l.count);
+            f.shadow_bin_start = reinterpret_cast<uint32_t*>(w + l.start);
+            std::memcpy(f.sun_bin_axes, ctx->sunBinAxes, sizeof(f.sun_bin_axes));
+        }
     }
     f.shadow_count = f.ray_counter + kShadowCountWord;
     f.shadow_heads = f.ray_counter + kShadowHeadWord;

@@ -206,6 +206,21 @@ struct FrameArgs {
     ShadowRay* shadow_rays;  // k_shadow_gen's list: [window_rays * light_count] worst case
     uint32_t* shadow_count;  // = ray_counter + kShadowCountWord
     uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
+    // Light-space binning of the shadow-ray list (shadow_bin_grid = G > 0): k_shadow_gen
+    // writes shadow_rays_gen with a bin key (light, Morton cell of the G x G light-space
+    // grid) and its rank in the bin, k_shadow_bin_scan turns the bin counts into bin
+    // starts, k_shadow_scatter writes shadow_rays in bin order. Sun rays: the cell of
+    // the origin projected on the plane perpendicular to the sun (parallel rays of one
+    // cell walk one column of the scene); spot rays: the octahedral cell of the
+    // direction from the spot. Only the order of the list changes (any-hit results do
+    // not depend on it).
+    ShadowRay* shadow_rays_gen;
+    uint32_t* shadow_bin_key;   // [list entry] light * G^2 + Morton(cell)
+    uint32_t* shadow_bin_rank;  // [list entry] rank in its bin (atomic order)
+    uint32_t* shadow_bin_count; // [light_count * G^2] (zeroed again by the scan)
+    uint32_t* shadow_bin_start; // [light_count * G^2]
+    uint32_t shadow_bin_grid;   // G (power of 2, <= 256); 0 = list in queue order
+    float sun_bin_axes[2][4];   // cell coordinate = dot(X, axis.xyz) + axis.w, in [0, G)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
     // ray-list traversals (RT reflections): {origin, tmax}, {direction, pixel} per ray
@@ -241,6 +256,7 @@ hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hi
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
+// k_shadow_gen, then (f.shadow_bin_grid > 0) the bin scan and the scatter into bin order
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s);

@@ -22,6 +22,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -301,12 +302,40 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // operands (measured 3.02 vs 2.72 ms traversal at C4 in round 1).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
+#ifndef ARK_NODE_LDEXP
+#define ARK_NODE_LDEXP 0 // per-axis step * idir as v_ldexp_f32 of the exponent byte instead of a float build + multiply
+#endif
+#ifndef ARK_MASK_ADDC
+#define ARK_MASK_ADDC 0 // hit / inside masks as m = 2m + bit (v_addc with the compare as carry) over slots 7..0
+#endif
+#ifndef ARK_NODE_INSIDE
+#define ARK_NODE_INSIDE 1 // origin-containing children first (0: plain octant order)
+#endif
+#if ARK_MASK_ADDC
+// m << 1 | (a <= b) in two VALU: the compare writes VCC and v_addc adds it in as the
+// carry (m + m + carry); an unordered compare (NaN) shifts in 0, as `<=` does
+__device__ __forceinline__ uint32_t shiftInLe(uint32_t m, float a, float b)
+{
+    uint32_t r;
+    asm("v_cmp_le_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc" : "=v"(r) : "v"(a), "v"(b), "v"(m) : "vcc");
+    return r;
+}
+#endif
+
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
+#if ARK_NODE_LDEXP
+    // exponent byte e: the step is 2^(e - 127) (e = 0 never occurs for a used axis:
+    // the builder's steps are normal numbers)
+    const float ax = __builtin_amdgcn_ldexpf(idir.x, static_cast<int>(w0.w & 0xffu) - 127);
+    const float ay = __builtin_amdgcn_ldexpf(idir.y, static_cast<int>((w0.w >> 8) & 0xffu) - 127);
+    const float az = __builtin_amdgcn_ldexpf(idir.z, static_cast<int>((w0.w >> 16) & 0xffu) - 127);
+#else
     const float ax = __uint_as_float((w0.w & 0xffu) << 23) * idir.x;
     const float ay = __uint_as_float(((w0.w >> 8) & 0xffu) << 23) * idir.y;
     const float az = __uint_as_float(((w0.w >> 16) & 0xffu) << 23) * idir.z;
+#endif
     const float bx = (__uint_as_float(w0.x) - o.x) * idir.x;
     const float by = (__uint_as_float(w0.y) - o.y) * idir.y;
     const float bz = (__uint_as_float(w0.z) - o.z) * idir.z;
@@ -317,7 +346,8 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
     uint32_t hitSlots = 0, insideLo = 0;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int k = 0; k < 8; ++k) {
+        const int s = ARK_MASK_ADDC ? 7 - k : k;
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
         const bool hiWord = s >= 4;
         auto q = [&](uint32_t w0_, uint32_t w1_) { return static_cast<float>(((hiWord ? w1_ : w0_) >> sh) & 0xffu); };
@@ -326,10 +356,15 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
         const float lim = fmaf(tf, 1.00001f, 1e-7f);
+#if ARK_MASK_ADDC
+        hitSlots = shiftInLe(hitSlots, tn, lim);
+        if (ARK_NODE_INSIDE) insideLo = shiftInLe(insideLo, tn, tmin);
+#else
         hitSlots |= (tn <= lim ? 1u : 0u) << s;
         // origin inside the box: every near-plane distance <= tmin (bits 0-7 here:
         // the select constants stay inline, no literal moves; shifted once below)
-        insideLo |= (tn <= tmin ? 1u : 0u) << s;
+        if (ARK_NODE_INSIDE) insideLo |= (tn <= tmin ? 1u : 0u) << s;
+#endif
     }
     const uint32_t insideSlots = insideLo << 16;
     // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
@@ -1584,6 +1619,46 @@ __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 // list index, and the closest hit shades back faces too, with the normal flipped
 // (opaque.rchit:121-125): N = -(shading normal), as negation commutes exactly with
 // the normal matrix product and the normalisation.
+#ifndef ARK_BIN_STRIDE
+#define ARK_BIN_STRIDE 32
+#endif
+// u32 words between two bin counters: each counter on its own 128-B line, so the
+// device-scope atomics of k_shadow_gen (which bypass the per-XCD L2s) do not queue
+// on a few shared lines (C4, G = 64, counters packed: shadow phase 0.75 -> 1.74 ms)
+constexpr uint32_t kBinStride = ARK_BIN_STRIDE;
+
+// 2-D Morton code of a cell (x, y < 256)
+__device__ __forceinline__ uint32_t morton2(uint32_t x, uint32_t y)
+{
+    auto spread = [](uint32_t v) {
+        v = (v | (v << 4)) & 0x0f0fu;
+        v = (v | (v << 2)) & 0x3333u;
+        return (v | (v << 1)) & 0x5555u;
+    };
+    return spread(x) | (spread(y) << 1);
+}
+
+// Light-space bin of shadow ray (light l, origin X): see FrameArgs::shadow_bin_grid.
+__device__ __forceinline__ uint32_t shadowBinKey(const SceneArgs& sc, const FrameArgs& f, uint32_t l, V3 X)
+{
+    const uint32_t G = f.shadow_bin_grid;
+    const float gmax = static_cast<float>(G) - 0.5f;
+    float cu, cv;
+    if (sc.has_sun && l == 0) {
+        cu = X.x * f.sun_bin_axes[0][0] + X.y * f.sun_bin_axes[0][1] + X.z * f.sun_bin_axes[0][2] + f.sun_bin_axes[0][3];
+        cv = X.x * f.sun_bin_axes[1][0] + X.y * f.sun_bin_axes[1][1] + X.z * f.sun_bin_axes[1][2] + f.sun_bin_axes[1][3];
+    } else {
+        const GpuSpotLight& sl = sc.spots[l - (sc.has_sun ? 1u : 0u)];
+        float ox, oy;
+        octahedralEncode(normalize(X - v3(sl.position[0], sl.position[1], sl.position[2])), &ox, &oy);
+        cu = (ox * 0.5f + 0.5f) * static_cast<float>(G);
+        cv = (oy * 0.5f + 0.5f) * static_cast<float>(G);
+    }
+    // NaN (a degenerate origin) lands in cell 0
+    const uint32_t x = static_cast<uint32_t>(fminf(fmaxf(cu, 0.0f), gmax)), y = static_cast<uint32_t>(fminf(fmaxf(cv, 0.0f), gmax));
+    return l * G * G + morton2(x, y);
+}
+
 template<bool REFL = false>
 __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 {
@@ -1664,15 +1739,58 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             rayOf(f, ray, &origin, &dir);
         }
         const V3 hitPoint = origin + t * dir;
+        const bool binned = !REFL && f.shadow_bin_grid != 0;
         for (uint32_t b = bits; b; b &= b - 1) {
             const uint32_t l = static_cast<uint32_t>(__builtin_ctz(b));
             V3 ld;
             float tmax;
             shadowRayOf(sc, f.z_far, l, hitPoint, &ld, &tmax);
-            f.shadow_rays[sj++] = ShadowRay { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax),
-                                              make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
+            const ShadowRay sr { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax), make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
+            if (binned) {
+                const uint32_t key = shadowBinKey(sc, f, l, hitPoint);
+                f.shadow_bin_key[sj] = key;
+                f.shadow_bin_rank[sj] = atomicAdd(f.shadow_bin_count + key * kBinStride, 1u);
+                f.shadow_rays_gen[sj++] = sr;
+            } else {
+                f.shadow_rays[sj++] = sr;
+            }
         }
     }
+}
+
+// Exclusive scan of the shadow-ray bin counts into bin starts, one workgroup of 1,024
+// threads (each a contiguous run of bins); the counts are zeroed for the next frame.
+constexpr uint32_t kBinScanBlock = 1024;
+__global__ void __launch_bounds__(kBinScanBlock) k_shadow_bin_scan(FrameArgs f)
+{
+    __shared__ uint32_t waveSum[kBinScanBlock / 64];
+    const uint32_t bins = f.light_count * f.shadow_bin_grid * f.shadow_bin_grid;
+    const uint32_t per = (bins + kBinScanBlock - 1u) / kBinScanBlock;
+    const uint32_t b0 = min(bins, threadIdx.x * per), b1 = min(bins, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += f.shadow_bin_count[b * kBinStride];
+    const uint32_t inc = waveInclusiveScan(sum);
+    const uint32_t wave = threadIdx.x >> 6;
+    if (__lane_id() == 63u) waveSum[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; ++w) base += waveSum[w];
+    uint32_t run = base + inc - sum;
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t c = f.shadow_bin_count[b * kBinStride];
+        f.shadow_bin_start[b] = run;
+        f.shadow_bin_count[b * kBinStride] = 0u;
+        run += c;
+    }
+}
+
+// The shadow-ray list in bin order: entry i of k_shadow_gen's list goes to its bin's
+// start + its rank (grid-stride over the device-side count).
+__global__ void __launch_bounds__(256) k_shadow_scatter(FrameArgs f)
+{
+    const uint32_t total = *f.shadow_count;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u)
+        f.shadow_rays[f.shadow_bin_start[f.shadow_bin_key[i]] + f.shadow_bin_rank[i]] = f.shadow_rays_gen[i];
 }
 
 // Atlas clears (DDGINode.cpp:50-55) as 32-bit fills.
@@ -2021,6 +2139,13 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
     const uint32_t blocks = (f.window_rays + dev::kGenSpan - 1u) / dev::kGenSpan;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(dev::k_shadow_gen<false>, dim3(blocks), dim3(256), 0, s, sc, f);
+    if (f.shadow_bin_grid != 0) {
+        hipLaunchKernelGGL(dev::k_shadow_bin_scan, dim3(1), dim3(dev::kBinScanBlock), 0, s, f);
+        // at most one shadow ray per window ray and light; a few waves per CU
+        const uint64_t worst = static_cast<uint64_t>(f.window_rays) * f.light_count;
+        const uint32_t sblocks = static_cast<uint32_t>(std::min<uint64_t>((worst + 255u) / 256u, 2048u));
+        hipLaunchKernelGGL(dev::k_shadow_scatter, dim3(sblocks), dim3(256), 0, s, f);
+    }
     return hipGetLastError();
 }
 

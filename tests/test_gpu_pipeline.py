@@ -1,8 +1,11 @@
 """Frames in flight (ark_ddgi.h, ark_ddgi_update): a rolling window's slot table and
 primary traversal overlap the previous frame's shadow rays, shading and update. The
 dependence rule must leave every result equal to the serial run (ARK_DDGI_PIPELINE=0):
-disjoint windows with probes moving, windows that intersect (serial fallback), and an
-offsets write between two updates (the next traversal must see it)."""
+disjoint windows with probes moving, windows that intersect (they pipeline too: the
+offsets of update n run on the traversal stream before update n+1's slot table, so
+the next traversal reads them in order), an offsets write through ark_ddgi_write
+between two updates, and one through the device views on the update stream flagged
+with ark_ddgi_mark_external_write (the next traversal must see either)."""
 import os
 
 import numpy as np
@@ -52,8 +55,9 @@ def _run(n, frames, poke=None):
 
 @pytest.mark.parametrize("K", [48, 36, 100])
 def test_pipelined_equals_serial(K):
-    """K = 48 / 36: consecutive windows are disjoint (pipelined); K = 100: they
-    intersect while probes move (serial fallback)."""
+    """K = 48 / 36: consecutive windows are disjoint; K = 100: they intersect while
+    probes move. All pipeline (no serial fallback exists or is needed: the offsets run
+    in order on the traversal stream)."""
     sc = scenes.features_scene()
     a = _run(_node(sc, K, True), 8)
     b = _run(_node(sc, K, False), 8)
@@ -69,3 +73,35 @@ def test_offsets_write_between_updates():
     for fa, fb in zip(a, b):
         for w in WHICH:
             assert np.array_equal(fa[w], fb[w]), w
+
+
+def test_device_view_offsets_write_marked_external():
+    """A torch kernel writes every probe's offset through ark_ddgi_get_device_views on
+    the stream of the next update, then ark_ddgi_mark_external_write: the pipelined
+    node (whose traversal would otherwise start on the internal stream before the
+    write) equals the serial one bit for bit."""
+    import torch
+
+    from arkoserenderer_amd.collective import device_bytes
+
+    sc = scenes.features_scene()
+    dev = torch.device("cuda", 0)
+    outs = []
+    for pipelined in (True, False):
+        n = _node(sc, 48, pipelined)
+        v = n.ctx.device_views()
+        off = device_bytes(v.probe_offsets, v.probe_offsets_bytes, dev).view(torch.float32).view(-1, 4)
+        stream = torch.cuda.Stream(dev)
+        out = []
+        for f in range(7):
+            if f == 4:
+                with torch.cuda.stream(stream):
+                    off[:, :3] += 0.03
+                n.ctx.mark_external_write()
+            n.execute(D.AppState(f), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        out = {w: n.ctx.read(w).copy() for w in WHICH}
+        n.ctx.close()
+        outs.append(out)
+    for w in WHICH:
+        assert np.array_equal(outs[0][w], outs[1][w]), w
