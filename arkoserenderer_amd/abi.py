@@ -43,6 +43,7 @@ ARK_DDGI_ATLAS_VISIBILITY = 1
 ARK_DDGI_SURFELS = 2
 ARK_DDGI_PROBE_OFFSETS = 3
 ARK_DDGI_DEBUG_HITS = 100
+ARK_DDGI_DEBUG_RAY_STEPS = 101
 
 ARK_DDGI_CLEAR_OVERFLOW_INF = 0
 ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE = 1

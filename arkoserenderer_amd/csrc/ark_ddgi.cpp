@@ -31,6 +31,8 @@ namespace {
 
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
 constexpr uint32_t kPipeHalfRays = 5u << 20;
+// BVH8 child selection default (ARK_BVH8_COLLAPSE overrides)
+constexpr bool kBvh8SahCollapseDefault = false;
 // u32 words per shadow-ray bin counter (ddgi_kernels.hip kBinStride)
 constexpr uint64_t kShadowBinStride = 32;
 
@@ -166,6 +168,7 @@ struct ArkDdgiCtx {
     DeviceBuffer irr, vis, offsets;
     // working set
     DeviceBuffer slots, slotOrder, fib, fibOrder, order, hits, surfels, spill, rayCounter, counters, shadeWork, reflWork;
+    DeviceBuffer raySteps; // counting updates: u16 traversal iterations per probe ray (ARK_DDGI_DEBUG_RAY_STEPS)
     std::vector<uint32_t> orderHost; // traversal order of the samples for orderR
     uint32_t orderR = 0;
     uint32_t lightCount = 0;
@@ -533,7 +536,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork, &ctx->reflWork,
-                             &ctx->counters, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
+                             &ctx->raySteps, &ctx->counters, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
         b->release();
     ctx->sceneStore.reset();
     for (auto& ev : ctx->ev)
@@ -631,6 +634,13 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
     // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
+    // BVH2 -> BVH8 child selection: ARK_BVH8_COLLAPSE=sah (Ylitie et al. 2017 DP) or
+    // greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's SAH terms
+    Bvh8CollapseOptions copt;
+    copt.sah_optimal = kBvh8SahCollapseDefault;
+    if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
+    if (const char* e = std::getenv("ARK_BVH8_NODE_COST")) copt.node_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
+    if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     std::vector<GpuBvh8Node> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
@@ -644,7 +654,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH2 leaf of %u triangles", r2.max_leaf);
         if (c == 0) sah = r2.sah_cost;
         maxLeaf = std::max(maxLeaf, r2.max_leaf);
-        Bvh8BuildResult r = collapse_bvh8(r2, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()));
+        Bvh8BuildResult r = collapse_bvh8(r2, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()), copt);
         roots[c] = static_cast<int32_t>(allNodes.size());
         if (c == 0) opaqueNodes = static_cast<uint32_t>(r.nodes.size());
         maxDepth = std::max(maxDepth, r.max_depth);
@@ -942,6 +952,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.grab_chunk = (pipe && f.window_rays < kPipeHalfRays) ? std::min<uint32_t>(ctx->grabChunk, 32u) : ctx->grabChunk;
     f.ray_counter = ctx->rayCounter.as<uint32_t>() + b * kRayCounterWords;
     f.counters = ctx->counters.as<unsigned long long>();
+    f.ray_steps = count ? ctx->raySteps.as<uint16_t>() : nullptr;
     // shading work set (ensureShadeWork): per-ray light bits | shadow-ray list
     {
         const ShadeWorkLayout l = shadeWorkLayout(ctx);
@@ -1060,6 +1071,7 @@ static int resourceInfo(const ArkDdgiCtx* ctx, int which, void** ptr, uint64_t* 
     case ARK_DDGI_SURFELS: *ptr = ctx->surfels.ptr; *bytes = ctx->surfels.bytes; return 0;
     case ARK_DDGI_PROBE_OFFSETS: *ptr = ctx->offsets.ptr; *bytes = ctx->offsets.bytes; return 0;
     case ARK_DDGI_DEBUG_HITS: *ptr = ctx->hits.as<GpuHit>() + static_cast<uint64_t>(ctx->lastParity) * ctx->Kmax * ctx->Rmax; *bytes = ctx->hits.bytes / 2; return 0;
+    case ARK_DDGI_DEBUG_RAY_STEPS: *ptr = ctx->raySteps.ptr; *bytes = ctx->raySteps.bytes; return ctx->raySteps.ptr ? 0 : ARK_DDGI_E_INVALID_ARGUMENT;
     default: return ARK_DDGI_E_INVALID_ARGUMENT;
     }
 }
@@ -1230,6 +1242,11 @@ int ark_ddgi_set_counting(ArkDdgiCtx* ctx, int enabled)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ctx->counting = enabled != 0;
+    if (ctx->counting && !ctx->raySteps.ptr) {
+        ARK_HIP(hipSetDevice(ctx->device));
+        ARK_HIP(ctx->raySteps.alloc(static_cast<size_t>(ctx->Kmax) * ctx->Rmax * 2));
+        ARK_HIP(hipMemset(ctx->raySteps.ptr, 0, ctx->raySteps.bytes));
+    }
     return ARK_DDGI_OK;
 }
 

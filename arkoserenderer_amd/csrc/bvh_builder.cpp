@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -356,10 +358,130 @@ float bvh8_inflation_box(const float lo[3], const float hi[3])
     return static_cast<float>(1e-6 * std::sqrt(d2));
 }
 
-Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base)
+// SAH-optimal collapse plan (Ylitie, Karras, Laine 2017, "Efficient incoherent ray
+// traversal on GPUs through compressed wide BVHs", §3.1). For every BVH2 internal
+// node n and i = 1..8: cost[n][i] = the least SAH cost of the subtree below n when it
+// is represented by at most i children of a BVH8 node - n itself as one BVH8 node
+// (A(n) Cnode + its best 8-way distribution) or one leaf slot (A(n) Ctri T(n), when its
+// T(n) <= kBvh8MaxLeafSize triangles, contiguous in leaf order), or its two subtrees
+// sharing the i slots. Leaf children of the BVH2 stay leaves (A Ctri count).
+struct CollapsePlan {
+    std::vector<float> cost;    // [node][8]
+    std::vector<uint8_t> pick;  // [node][8]: i = 1: 0 node, 1 leaf; i >= 2: 0 = as i - 1, else k slots to the left child
+    std::vector<uint32_t> first, count; // triangle range of the subtree (leaf order)
+    float cNode = 1.0f, cTri = 1.0f;
+};
+
+float childCost(const CollapsePlan& P, const Child8& c, int i)
+{
+    if (c.code >= 0) return P.cost[8u * static_cast<uint32_t>(c.code) + (i - 1)];
+    return P.cTri * c.box.area() * static_cast<float>((static_cast<uint32_t>(~c.code) & (kMaxLeafSize - 1)) + 1);
+}
+
+CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri)
+{
+    CollapsePlan P;
+    P.cNode = cNode;
+    P.cTri = cTri;
+    const size_t N = bvh2.nodes.size();
+    P.cost.assign(8 * N, 0.0f);
+    P.pick.assign(8 * N, 0);
+    P.first.assign(N, 0);
+    P.count.assign(N, 0);
+    // children have larger indices than their parent (allocated at the parent's split)
+    for (size_t k = N; k-- > 0;) {
+        Child8 ch[2];
+        int m = 0;
+        childrenOf(bvh2.nodes[k], ch, m);
+        uint32_t lo = UINT32_MAX, tot = 0;
+        for (int c = 0; c < m; ++c) {
+            if (ch[c].code >= 0) {
+                lo = std::min(lo, P.first[ch[c].code]);
+                tot += P.count[ch[c].code];
+            } else {
+                const uint32_t code = static_cast<uint32_t>(~ch[c].code);
+                lo = std::min(lo, code >> kLeafCountBits);
+                tot += (code & (kMaxLeafSize - 1)) + 1u;
+            }
+        }
+        P.first[k] = lo;
+        P.count[k] = tot;
+        Aabb box;
+        for (int c = 0; c < m; ++c) box.grow(ch[c].box);
+        const float area = box.area();
+        float* C = &P.cost[8 * k];
+        uint8_t* pk = &P.pick[8 * k];
+        // distributions of j slots over the two subtrees
+        auto dist = [&](int j, int& bestK) {
+            float best = INFINITY;
+            bestK = 0;
+            if (m == 1) {
+                bestK = j;
+                return childCost(P, ch[0], j);
+            }
+            for (int kk = 1; kk < j; ++kk) {
+                const float v = childCost(P, ch[0], kk) + childCost(P, ch[1], j - kk);
+                if (v < best) {
+                    best = v;
+                    bestK = kk;
+                }
+            }
+            return best;
+        };
+        int k8;
+        const float asNode = cNode * area + dist(8, k8);
+        const float asLeaf = tot <= static_cast<uint32_t>(kBvh8MaxLeafSize) ? cTri * area * static_cast<float>(tot) : INFINITY;
+        C[0] = std::min(asNode, asLeaf);
+        pk[0] = asLeaf < asNode ? 1 : 0;
+        for (int i = 2; i <= 8; ++i) {
+            int kk;
+            const float d = dist(i, kk);
+            if (d < C[i - 2]) {
+                C[i - 1] = d;
+                pk[i - 1] = static_cast<uint8_t>(kk);
+            } else {
+                C[i - 1] = C[i - 2];
+                pk[i - 1] = 0;
+            }
+        }
+    }
+    return P;
+}
+
+// The children the plan gives a subtree (BVH2 item `c`) when it gets `i` slots.
+void emitChildren(const BvhBuildResult& bvh2, const CollapsePlan& P, const Child8& c, int i, Child8* out, int& n)
+{
+    if (c.code < 0) {
+        out[n++] = c;
+        return;
+    }
+    const uint32_t k = static_cast<uint32_t>(c.code);
+    while (i > 1 && P.pick[8 * k + (i - 1)] == 0) --i;
+    if (i == 1) {
+        Child8 x = c;
+        if (P.pick[8 * k] == 1) // the whole subtree as one leaf slot
+            x.code = ~static_cast<int32_t>((P.first[k] << kLeafCountBits) | (P.count[k] - 1u));
+        out[n++] = x;
+        return;
+    }
+    Child8 two[2];
+    int m = 0;
+    childrenOf(bvh2.nodes[k], two, m);
+    const int kk = P.pick[8 * k + (i - 1)];
+    if (m == 1) {
+        emitChildren(bvh2, P, two[0], i, out, n);
+        return;
+    }
+    emitChildren(bvh2, P, two[0], kk, out, n);
+    emitChildren(bvh2, P, two[1], i - kk, out, n);
+}
+
+Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& copt)
 {
     Bvh8BuildResult res;
     if (bvh2.nodes.empty()) return res;
+    CollapsePlan plan;
+    if (copt.sah_optimal) plan = planCollapse(bvh2, copt.node_cost, copt.tri_cost);
     struct Item {
         uint32_t src;
         uint32_t dst;
@@ -369,38 +491,72 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
     queue.push_back({ 0u, 0u, 1u });
     res.nodes.resize(1);
     res.tris.reserve(bvh2.tris.size());
+    double sah = 0.0, rootArea = 0.0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const Item it = queue[qi];
         res.max_depth = std::max(res.max_depth, it.depth);
-        // gather up to 8 children: open the largest-area internal child first
         Child8 ch[8];
         int n = 0;
-        {
+        if (copt.sah_optimal) {
+            // the plan's best 8-way distribution below this node
             Child8 two[2];
             int m = 0;
             childrenOf(bvh2.nodes[it.src], two, m);
-            for (int c = 0; c < m; ++c) ch[n++] = two[c];
-        }
-        for (;;) {
-            int best = -1;
-            float bestArea = -1.0f;
-            for (int c = 0; c < n; ++c)
-                if (ch[c].code >= 0 && ch[c].box.area() > bestArea) {
-                    bestArea = ch[c].box.area();
-                    best = c;
+            if (m == 1) {
+                emitChildren(bvh2, plan, two[0], 8, ch, n);
+            } else {
+                const uint32_t src = it.src;
+                int kk = 1;
+                float best = INFINITY;
+                for (int k = 1; k < 8; ++k) {
+                    const float v = childCost(plan, two[0], k) + childCost(plan, two[1], 8 - k);
+                    if (v < best) {
+                        best = v;
+                        kk = k;
+                    }
                 }
-            if (best < 0) break;
-            Child8 two[2];
-            int m = 0;
-            childrenOf(bvh2.nodes[ch[best].code], two, m);
-            if (n - 1 + m > 8) break;
-            ch[best] = two[0];
-            for (int c = 1; c < m; ++c) ch[n++] = two[c];
-            if (m == 0) ch[best] = ch[--n];
+                (void)src;
+                emitChildren(bvh2, plan, two[0], kk, ch, n);
+                emitChildren(bvh2, plan, two[1], 8 - kk, ch, n);
+            }
+        } else {
+            // gather up to 8 children: open the largest-area internal child first
+            {
+                Child8 two[2];
+                int m = 0;
+                childrenOf(bvh2.nodes[it.src], two, m);
+                for (int c = 0; c < m; ++c) ch[n++] = two[c];
+            }
+            for (;;) {
+                int best = -1;
+                float bestArea = -1.0f;
+                for (int c = 0; c < n; ++c)
+                    if (ch[c].code >= 0 && ch[c].box.area() > bestArea) {
+                        bestArea = ch[c].box.area();
+                        best = c;
+                    }
+                if (best < 0) break;
+                Child8 two[2];
+                int m = 0;
+                childrenOf(bvh2.nodes[ch[best].code], two, m);
+                if (n - 1 + m > 8) break;
+                ch[best] = two[0];
+                for (int c = 1; c < m; ++c) ch[n++] = two[c];
+                if (m == 0) ch[best] = ch[--n];
+            }
         }
         // octant slots: greedy on the alignment of child centre offsets with slot signs
         Aabb box;
         for (int c = 0; c < n; ++c) box.grow(ch[c].box);
+        // SAH cost of the result (node cost 1, the plan's triangle cost), for reports
+        if (qi == 0) {
+            rootArea = std::max(1e-30, static_cast<double>(box.area()));
+            sah += 1.0;
+        }
+        for (int c = 0; c < n; ++c) {
+            const double a = ch[c].box.area() / rootArea;
+            sah += ch[c].code >= 0 ? a : a * copt.tri_cost * static_cast<double>((static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1);
+        }
         float pc[3];
         for (int a = 0; a < 3; ++a) pc[a] = 0.5f * (box.lo[a] + box.hi[a]);
         struct Cand {
@@ -475,6 +631,7 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
         res.nodes.resize(res.nodes.size() + nInternal);
         res.nodes[it.dst] = nd;
     }
+    res.sah_cost = static_cast<float>(sah);
     return res;
 }
 
@@ -506,7 +663,10 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
     opt.max_leaf_size = kBvh8MaxLeafSize;
     opt.inflate_abs = bvh8_inflation(triangles, n);
     const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
-    const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u);
+    Bvh8CollapseOptions copt;
+    if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
+    if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
+    const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u, copt);
     uint64_t violations = 0, internalChildren = 0;
     std::vector<uint32_t> seen(n, 0);
     struct Box {
@@ -579,7 +739,7 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
         out[4] = r8.tris.size();
         out[5] = r2.nodes.size();
         out[6] = internalChildren;
-        out[7] = 0;
+        out[7] = static_cast<uint64_t>(static_cast<double>(r8.sah_cost) * 1e6); // BVH8 SAH cost x 1e6
     }
     return violations == 0 ? 0 : 1;
 }

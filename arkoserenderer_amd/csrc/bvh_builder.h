@@ -46,14 +46,24 @@ struct Bvh8BuildResult {
     std::vector<GpuTriangle> tris;  // in BVH8 leaf order
     uint32_t max_depth = 0;
     uint32_t leaf_children = 0;
+    float sah_cost = 0.0f; // SAH cost (node 1, triangle Bvh8CollapseOptions::tri_cost) relative to the root
 };
 
 // Collapses a BVH2 (built with max_leaf_size <= kBvh8MaxLeafSize, node_base 0,
 // tri_base 0) into the 8-wide quantized layout: every node adopts the largest-area
-// internal descendants of its BVH2 node until it has 8 children, children are
+// internal descendants of its BVH2 node until it has 8 children (or the SAH-optimal
+// set, Bvh8CollapseOptions::sah_optimal), children are
 // placed in octant slots, and the triangles of each node's leaf children are
 // stored contiguously. Node/triangle indices are offset by node_base/tri_base.
-Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base);
+struct Bvh8CollapseOptions {
+    // true: the SAH-optimal child selection of Ylitie et al. 2017 (dynamic programming
+    // over BVH2 subtrees, also merging subtrees of <= kBvh8MaxLeafSize triangles into
+    // one leaf slot); false: greedy largest-area opening
+    bool sah_optimal = false;
+    float node_cost = 1.0f; // SAH cost of visiting a BVH8 node (8 box tests)
+    float tri_cost = 1.0f;  // SAH cost of one triangle test
+};
+Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& opt);
 
 // Absolute box inflation for the BVH8 slab test: 1e-6 of the diagonal of the
 // bounding box of nTriangles world-space triangles (9 floats each). It bounds

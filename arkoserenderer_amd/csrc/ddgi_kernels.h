@@ -223,6 +223,7 @@ struct FrameArgs {
     float sun_bin_axes[2][4];   // cell coordinate = dot(X, axis.xyz) + axis.w, in [0, G)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
+    uint16_t* ray_steps;     // counting updates: traversal iterations of each probe ray (both passes) at its hit-record index
     // ray-list traversals (RT reflections): {origin, tmax}, {direction, pixel} per ray
     const float4* ray_list;
     const uint32_t* list_count;

@@ -767,7 +767,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
     const uint32_t lane = threadIdx.x & 63u;
     const float tmin = Src::kTmin;
-    uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0;
+    uint32_t cNodes = 0, cTris = 0, cHits = 0, cIter = 0, rSteps = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
     const uint32_t home = xccId();
@@ -829,7 +829,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
         if (__ballot(active) == 0) break;
-        if (COUNT) cIter++;
+        if (COUNT) {
+            cIter++;
+            rSteps += active ? 1u : 0u;
+        }
 #ifdef ARK_TAIL_PROBE
         itAll++;
         if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
@@ -874,6 +877,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     }
                     f.hits[ray] = out;
                 }
+                if (COUNT && f.ray_steps) f.ray_steps[ray] = static_cast<uint16_t>(min(rSteps, 65535u));
+                if (COUNT) rSteps = 0;
                 active = false;
             }
         }

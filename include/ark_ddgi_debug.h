@@ -18,6 +18,13 @@ extern "C" {
  * sample = the ray's Fibonacci sample index). */
 #define ARK_DDGI_DEBUG_HITS 100
 
+/* Extra resource id for ark_ddgi_read: the traversal iterations (both passes) of
+ * every probe ray of the last counting update (ark_ddgi_set_counting), uint16 at
+ * the ray's hit-record index (slot * rays_per_probe + sample), saturating at 65535;
+ * sized max_probe_updates x max_rays_per_probe. For the launch-tail analysis
+ * (tools/ray_cost.py); counting is enabled first. */
+#define ARK_DDGI_DEBUG_RAY_STEPS 101
+
 /* Evaluates op (0 sin, 1 cos, 2 acos, 3 atan2(x,y), 4 log2, 5 exp2, 6 pow(x,y),
  * 7 fp32->fp16->fp32 round trip, 8 powf_pos_(x,y)) on `device` for n inputs (host arrays). */
 int ark_ddgi_debug_fmath(int device, int op, const float* x, const float* y, float* out, uint64_t n);
@@ -36,7 +43,9 @@ int ark_ddgi_debug_struct_sizes(uint32_t* out, int n);
  * (9 floats each) on the host and checks it: every triangle in exactly one leaf,
  * every quantized plane exactly representable, every triangle vertex inside the
  * decoded boxes of its leaf and of all its ancestors. out[8] = {nodes, leaf
- * children, max depth, violations, triangles, bvh2 nodes, internal children, 0}.
+ * children, max depth, violations, triangles, bvh2 nodes, internal children, BVH8
+ * SAH cost x 1e6 (node cost 1)}. The BVH8 child selection follows ARK_BVH8_COLLAPSE
+ * ("sah" = SAH-optimal, else greedy) and ARK_BVH8_TRI_COST, as set_scene does.
  * Returns 0 when the check passes, 1 when it found violations. No GPU. */
 int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out);
 

@@ -1,12 +1,16 @@
 """Per-rank cost of an S-way Z-slab run, measured on ONE GPU: a context that owns
-slab 0 of S (no exchange) runs the C4 workload; prints its ms/step next to the
-unsharded one. A proxy for strong-scaling headroom (the exchange is not included);
-the driver measures real N-GPU runs.
+slab 0 of S runs the C4 workload; prints its ms/step next to the unsharded one. A
+proxy for strong-scaling headroom; the driver measures real N-GPU runs.
 
-    python tools/shard_proxy.py [--shards 2 4 8] [--steps 10] [--all-ranks]
+    python tools/shard_proxy.py [--shards 2 4 8] [--steps 10] [--all-ranks] [--exchange]
 
 --all-ranks measures every slab of each S (the strong-scaling step is the slowest
-rank's), not only slab 0.
+rank's), not only slab 0. --exchange adds an exchange stand-in: the frame loop of
+bench.py's ranks (collective.OverlappedSlabExchange: the next frame's traversal goes
+ahead, its shading waits for the exchange) with a device copy of the (S-1)/S of both
+atlases a rank receives per step (60 MB at S = 8) on the side stream in place of the
+RCCL all-gather, so the copy's HBM traffic and CU time contend with the traversal as
+RCCL's copy kernels would (the xGMI transfer time itself is not modelled).
 """
 import argparse
 import json
@@ -24,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--triangles", type=int, default=10_000_000)
     ap.add_argument("--all-ranks", action="store_true")
+    ap.add_argument("--exchange", action="store_true", help="exchange stand-in (device copy of the received bands)")
     args = ap.parse_args()
     import torch
 
@@ -43,8 +48,29 @@ def main():
         assert node.construct(scene, grid, 10000.0, device=0, shard_rank=rank, shard_count=s,
                               light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
         sptr = torch.cuda.current_stream(dev).cuda_stream
+        run = node.execute
+        if args.exchange and s > 1:
+            from arkoserenderer_amd.collective import OverlappedSlabExchange, device_bytes
+
+            v = node.ctx.device_views()
+            bands = []
+            for ptr, total, off, n in ((v.irradiance_atlas, v.irradiance_bytes, v.irradiance_slab_offset, v.irradiance_slab_bytes),
+                                       (v.visibility_atlas, v.visibility_bytes, v.visibility_slab_offset, v.visibility_slab_bytes)):
+                atlas = device_bytes(ptr, total, dev)
+                bands.append((atlas, atlas.clone(), int(off), int(n)))  # the clone stands for the other ranks' bands
+
+            def exchange():
+                for atlas, other, off, n in bands:  # everything but this rank's own band
+                    if off > 0:
+                        atlas[:off].copy_(other[:off])
+                    if off + n < atlas.numel():
+                        atlas[off + n:].copy_(other[off + n:])
+
+            loop = OverlappedSlabExchange(node, exchange, dev)
+            run = loop.step
         for f in range(3):
-            node.execute(D.AppState(f), sptr)
+            run(D.AppState(f), sptr)
+        torch.cuda.synchronize(dev)
         node.ctx.set_timing(True)
         node.execute(D.AppState(3), sptr)
         kt = node.ctx.last_timings()
@@ -52,11 +78,12 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for f in range(args.steps):
-            node.execute(D.AppState(4 + f), sptr)
+            run(D.AppState(4 + f), sptr)
         t_host = time.perf_counter() - t0  # enqueue time: the host keeps ahead of the GPU when this is below ms_per_step
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t0) / args.steps * 1e3
-        rec = {"ms_per_step": round(ms, 4), "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4), "kernels_ms": [round(x, 4) for x in kt]}
+        rec = {"ms_per_step": round(ms, 4), "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4), "kernels_ms": [round(x, 4) for x in kt],
+               "exchange_stand_in": bool(args.exchange and s > 1)}
         print(json.dumps({"shards": s, "rank": rank, **rec}), flush=True)
         if s not in out or rec["ms_per_step"] > out[s]["ms_per_step"]:
             out[s] = dict(rec, slowest_rank=rank)
