@@ -52,9 +52,9 @@ def main():
         ctx.synchronize()
         steps = ctx.read(abi.ARK_DDGI_DEBUG_RAY_STEPS)[: N * R].reshape(N, R).astype(np.float64)
         hits = ctx.read(abi.ARK_DDGI_DEBUG_HITS).view(np.float32).reshape(-1, 4)[: N * R, 0].reshape(N, R)
-        frames.append((steps, np.isinf(hits)))
+        frames.append((steps, np.isinf(hits), np.abs(hits)))
     out = {}
-    for f, (st, miss) in enumerate(frames):
+    for f, (st, miss, dist) in enumerate(frames):
         flat = st.ravel()
         srt = np.sort(flat)[::-1]
         tot = flat.sum()
@@ -68,6 +68,16 @@ def main():
             "p99_hit": float(np.percentile(st[~miss], 99)), "p99_miss": float(np.percentile(st[miss], 99)) if miss.any() else None,
         }
     p0, p1 = frames[0][0].sum(1), frames[1][0].sum(1)
+    # a cost proxy k_probe_offsets could compute from the hit records it reads anyway:
+    # the summed hit distance, misses (and long hits) capped
+    caps = {}
+    for cap in (2.0, 4.0, 8.0, 32.0):
+        proxy0 = np.minimum(frames[0][2], cap).sum(1)
+        caps[str(cap)] = {"rank_corr_with_steps_same_frame": round(spearman(proxy0, p0), 4),
+                          "rank_corr_with_steps_next_frame": round(spearman(proxy0, p1), 4)}
+    # per ray: how well distance predicts the ray's iterations
+    d0 = np.minimum(frames[0][2], 64.0).ravel()
+    ray_corr = round(spearman(d0[::7], frames[0][0].ravel()[::7]), 4)
     m0, m1 = frames[0][0].max(1), frames[1][0].max(1)
     idx = np.arange(N)
     x, z, y = idx % G, (idx % (G * G)) // G, idx // (G * G)
@@ -79,6 +89,8 @@ def main():
         "edge_probe_mean_sum_over_interior": round(float(p0[edge].mean() / p0[~edge].mean()), 3),
         "top1pct_probes_frac_edge": round(float(edge[np.argsort(p0)[::-1][: N // 100]].mean()), 3),
         "per_probe_max_p50_p99": [float(np.percentile(m0, 50)), float(np.percentile(m0, 99))],
+        "distance_proxy": caps,
+        "ray_rank_corr_distance_steps": ray_corr,
     }
     print(json.dumps(out, indent=1))
     if args.json:
