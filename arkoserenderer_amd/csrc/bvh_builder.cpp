@@ -743,3 +743,139 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
     }
     return violations == 0 ? 0 : 1;
 }
+
+// ark_ddgi_debug.h: traversal statistics of the BVH8 that set_scene would upload
+// (host simulation of k_trace's closest-hit order: per node the hit children,
+// those whose box holds the origin first, then octant order; a node's leaf
+// triangles are tested right after it). For comparing BVH builds without a GPU.
+extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const float* rays, uint64_t nRays, int threads, uint64_t* out)
+{
+    using namespace ark;
+    std::vector<BuildTriangle> tris(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            tris[i].v0[a] = triangles[9 * i + a];
+            tris[i].v1[a] = triangles[9 * i + 3 + a];
+            tris[i].v2[a] = triangles[9 * i + 6 + a];
+        }
+        tris[i].instance = 0;
+        tris[i].primitive = static_cast<uint32_t>(i);
+        tris[i].flip_facing = 0;
+    }
+    BvhBuildOptions opt;
+    opt.max_leaf_size = kBvh8MaxLeafSize;
+    opt.inflate_abs = bvh8_inflation(triangles, n);
+    opt.threads = threads > 0 ? threads : 8;
+    if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
+    const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
+    Bvh8CollapseOptions copt;
+    if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
+    if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
+    const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u, copt);
+    std::atomic<uint64_t> nodes { 0 }, triTests { 0 }, hits { 0 }, maxSteps { 0 };
+    // ARK_SIM_ORDER=distance: exact front-to-back child order (what octant order approximates)
+    const bool sortByDistance = std::getenv("ARK_SIM_ORDER") && std::strcmp(std::getenv("ARK_SIM_ORDER"), "distance") == 0;
+    auto worker = [&](uint64_t r0, uint64_t r1) {
+        uint64_t cn = 0, ct = 0, ch = 0, ms = 0;
+        for (uint64_t r = r0; r < r1; ++r) {
+            const float* ry = rays + 7 * r;
+            const float o[3] = { ry[0], ry[1], ry[2] }, d[3] = { ry[3], ry[4], ry[5] };
+            float tmax = ry[6];
+            const float tmin = 1e-4f;
+            float idir[3];
+            for (int a = 0; a < 3; ++a) idir[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? (d[a] < 0.0f ? -1e-20f : 1e-20f) : d[a]);
+            const uint32_t oct = (idir[0] < 0 ? 1u : 0u) | (idir[1] < 0 ? 2u : 0u) | (idir[2] < 0 ? 4u : 0u);
+            std::vector<uint32_t> stack { 0u };
+            bool hit = false;
+            uint64_t steps = 0;
+            while (!stack.empty()) {
+                const uint32_t ni = stack.back();
+                stack.pop_back();
+                const GpuBvh8Node& nd = r8.nodes[ni];
+                cn++;
+                steps++;
+                struct C { float tn; uint32_t k; bool inside; int s; };
+                C hitc[8];
+                int nh = 0;
+                for (int s = 0; s < 8; ++s) {
+                    const bool internal = (nd.imask >> s) & 1u;
+                    if (!internal && nd.meta[s] == 0) continue;
+                    float tn = tmin, tf = tmax;
+                    for (int a = 0; a < 3; ++a) {
+                        const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
+                        const float lo = std::fma(static_cast<float>(nd.qlo[a][s]), step, nd.p[a]);
+                        const float hi = std::fma(static_cast<float>(nd.qhi[a][s]), step, nd.p[a]);
+                        float t0 = (lo - o[a]) * idir[a], t1 = (hi - o[a]) * idir[a];
+                        if (t0 > t1) std::swap(t0, t1);
+                        tn = std::max(tn, t0);
+                        tf = std::min(tf, t1);
+                    }
+                    if (tn <= tf * 1.00001f + 1e-7f) hitc[nh++] = { tn, static_cast<uint32_t>(s) ^ oct, tn <= tmin, s };
+                }
+                // leaf triangles of this node now, internal children by (inside first, k order)
+                uint32_t internalBefore[8];
+                uint32_t cntInt = 0;
+                for (int s = 0; s < 8; ++s) {
+                    internalBefore[s] = cntInt;
+                    if ((nd.imask >> s) & 1u) cntInt++;
+                }
+                for (int i = 0; i < nh; ++i) {
+                    const int s = hitc[i].s;
+                    if ((nd.imask >> s) & 1u) continue;
+                    const uint32_t unary = nd.meta[s] >> 5, off = nd.meta[s] & 31u;
+                    const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : 3u);
+                    for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
+                        ct++;
+                        steps++;
+                        const GpuTriangle& g = r8.tris[t];
+                        const float v0[3] = { g.t0[0], g.t0[1], g.t0[2] }, e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+                        const float pv[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
+                        const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+                        if (det == 0.0f) continue;
+                        const float inv = 1.0f / det;
+                        const float sv[3] = { o[0] - v0[0], o[1] - v0[1], o[2] - v0[2] };
+                        const float u = (sv[0] * pv[0] + sv[1] * pv[1] + sv[2] * pv[2]) * inv;
+                        if (!(u >= 0.0f && u <= 1.0f)) continue;
+                        const float q[3] = { sv[1] * e1[2] - sv[2] * e1[1], sv[2] * e1[0] - sv[0] * e1[2], sv[0] * e1[1] - sv[1] * e1[0] };
+                        const float v = (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]) * inv;
+                        if (!(v >= 0.0f && u + v <= 1.0f)) continue;
+                        const float tt = (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]) * inv;
+                        if (tt >= tmin && tt <= tmax) {
+                            tmax = tt;
+                            hit = true;
+                        }
+                    }
+                }
+                // push internal children so that the first to visit is on top
+                if (sortByDistance) std::sort(hitc, hitc + nh, [](const C& a, const C& b) { return a.tn < b.tn; });
+                else std::sort(hitc, hitc + nh, [](const C& a, const C& b) { return a.inside != b.inside ? a.inside : a.k < b.k; });
+                for (int i = nh - 1; i >= 0; --i) {
+                    const int s = hitc[i].s;
+                    if (((nd.imask >> s) & 1u) && hitc[i].tn <= tmax * 1.00001f + 1e-7f) stack.push_back(nd.child_base + internalBefore[s]);
+                }
+            }
+            ch += hit ? 1 : 0;
+            ms = std::max(ms, steps);
+        }
+        nodes += cn;
+        triTests += ct;
+        hits += ch;
+        uint64_t m = maxSteps.load();
+        while (ms > m && !maxSteps.compare_exchange_weak(m, ms)) {}
+    };
+    const int T = std::max(1, threads);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(worker, nRays * t / T, nRays * (t + 1) / T);
+    for (auto& th : pool) th.join();
+    if (out) {
+        out[0] = nodes.load();
+        out[1] = triTests.load();
+        out[2] = hits.load();
+        out[3] = r8.nodes.size();
+        out[4] = static_cast<uint64_t>(static_cast<double>(r8.sah_cost) * 1e6);
+        out[5] = maxSteps.load();
+        out[6] = r8.max_depth;
+        out[7] = 0;
+    }
+    return 0;
+}

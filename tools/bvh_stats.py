@@ -1,0 +1,82 @@
+"""BVH build comparison without a GPU: node visits, triangle tests and SAH cost per
+probe ray of the C4 workload (or a scaled soup) under the BVH8 builds selected by
+environment (ARK_BVH8_COLLAPSE=sah|greedy, ARK_BVH8_TRI_COST, ARK_BVH_INTERSECTION_COST),
+through ark_ddgi_debug_bvh8_trace_stats (a host simulation of k_trace's visiting order).
+Rays: the frame-0 probe rays (rotated spherical Fibonacci, ddgi/common.glsl:12-25) of
+a sample of probes spread over the grid.
+
+    python tools/bvh_stats.py [--triangles N] [--probes P] [--rays R] [--threads T] [--variants "greedy" "sah 1.0" ...]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def world_triangles(sc):
+    ws = []
+    for inst in sc.instances:
+        mesh = sc.meshes[inst["rt_mesh_index"]]
+        idx = sc.indices[mesh["first_index"]: mesh["first_index"] + 3 * inst["triangle_count"]]
+        p = sc.positions[mesh["first_vertex"] + idx.astype(np.int64)]
+        M = inst["object_to_world"].reshape(3, 4)
+        ws.append((p @ M[:, :3].T + M[:, 3]).reshape(-1, 9))
+    return np.ascontiguousarray(np.concatenate(ws), np.float32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--triangles", type=int, default=10_000_000)
+    ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--probes", type=int, default=256)
+    ap.add_argument("--rays", type=int, default=256)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--variants", nargs="+", default=["greedy", "sah 1.0", "sah 0.5", "sah 0.3"])
+    args = ap.parse_args()
+    import oracle_lib as O
+    from arkoserenderer_amd import abi
+    from arkoserenderer_amd import scene as S
+
+    G, R = args.grid, args.rays
+    sc = S.soup(args.triangles)
+    tris = world_triangles(sc)
+    rng = np.random.default_rng(5)
+    probes = rng.choice(G ** 3, args.probes, replace=False)
+    rays = np.zeros((args.probes * R, 7), np.float32)
+    k = 0
+    for p in probes:
+        y, rem = divmod(int(p), G * G)
+        z, x = divmod(rem, G)
+        for s in range(R):
+            d = np.zeros(3, np.float32)
+            O.load().oracle_rotated_fib(int(p), s, R, 0, d.ctypes.data)
+            rays[k] = [x, y, z, d[0], d[1], d[2], 10000.0]
+            k += 1
+    lib = abi.load_library()
+    res = {}
+    for v in args.variants:
+        parts = v.split()
+        os.environ["ARK_BVH8_COLLAPSE"] = parts[0]
+        if len(parts) > 1:
+            os.environ["ARK_BVH8_TRI_COST"] = parts[1]
+        else:
+            os.environ.pop("ARK_BVH8_TRI_COST", None)
+        out = (C.c_uint64 * 8)()
+        t = time.time()
+        lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out)
+        n = rays.shape[0]
+        res[v] = {"nodes_per_ray": round(out[0] / n, 3), "tris_per_ray": round(out[1] / n, 3), "hit_frac": round(out[2] / n, 4),
+                  "bvh8_nodes": out[3], "sah": out[4] / 1e6, "max_steps": out[5], "depth": out[6], "s": round(time.time() - t, 1)}
+        print(v, json.dumps(res[v]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
