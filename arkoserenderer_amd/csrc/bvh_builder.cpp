@@ -748,7 +748,8 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
 // (host simulation of k_trace's closest-hit order: per node the hit children,
 // those whose box holds the origin first, then octant order; a node's leaf
 // triangles are tested right after it). For comparing BVH builds without a GPU.
-extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const float* rays, uint64_t nRays, int threads, uint64_t* out)
+extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const float* rays, uint64_t nRays, int threads, uint64_t* out,
+                                                uint32_t* perRay)
 {
     using namespace ark;
     std::vector<BuildTriangle> tris(n);
@@ -856,6 +857,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
             }
             ch += hit ? 1 : 0;
             ms = std::max(ms, steps);
+            if (perRay) perRay[r] = static_cast<uint32_t>(steps);
         }
         nodes += cn;
         triTests += ct;

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--rays", type=int, default=256)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--variants", nargs="+", default=["greedy", "sah 1.0", "sah 0.5", "sah 0.3"])
+    ap.add_argument("--save-steps", default=None, help="save per-ray steps, probes and rays (npz per variant) with this prefix")
+    ap.add_argument("--all-probes-of", type=int, default=0, help="use every probe of this many consecutive z layers at y = G/2 instead of a random sample")
     args = ap.parse_args()
     import oracle_lib as O
     from arkoserenderer_amd import abi
@@ -50,6 +52,10 @@ def main():
     tris = world_triangles(sc)
     rng = np.random.default_rng(5)
     probes = rng.choice(G ** 3, args.probes, replace=False)
+    if args.all_probes_of:
+        y = G // 2
+        probes = np.array([x + G * z + G * G * y for z in range(args.all_probes_of) for x in range(G)])
+        args.probes = len(probes)
     rays = np.zeros((args.probes * R, 7), np.float32)
     k = 0
     for p in probes:
@@ -71,7 +77,10 @@ def main():
             os.environ.pop("ARK_BVH8_TRI_COST", None)
         out = (C.c_uint64 * 8)()
         t = time.time()
-        lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out)
+        steps = np.zeros(rays.shape[0], np.uint32)
+        lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out, steps.ctypes.data)
+        if args.save_steps:
+            np.savez_compressed(f"{args.save_steps}_{v.replace(' ', '_')}.npz", steps=steps, probes=probes, rays=rays)
         n = rays.shape[0]
         res[v] = {"nodes_per_ray": round(out[0] / n, 3), "tris_per_ray": round(out[1] / n, 3), "hit_frac": round(out[2] / n, 4),
                   "bvh8_nodes": out[3], "sah": out[4] / 1e6, "max_steps": out[5], "depth": out[6], "s": round(time.time() - t, 1)}
