@@ -207,23 +207,32 @@ __device__ __forceinline__ V3 safeInv(V3 d)
     return { f(d.x), f(d.y), f(d.z) };
 }
 
-// Möller–Trumbore, identical op order to the oracle's intersectTri.
+// Möller–Trumbore, identical op order to the oracle's intersectTri. The cross and dot
+// products are fused explicitly (crossFma / dotFma: 6 and 3 VALU instead of 9 and 5;
+// the ray-triangle test is the traversal step's second largest block), in the same
+// places as the oracle, so results stay bit-exact under -ffp-contract=off.
+__device__ __forceinline__ V3 crossFma(V3 a, V3 b)
+{
+    return { fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)) };
+}
+__device__ __forceinline__ float dotFma3(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+
 __device__ __forceinline__ bool intersectTri(V3 o, V3 d, float tmin, float tmax, const GpuTriangle& tr, float* outT, float* outU, float* outV, bool* backfaceDet)
 {
     V3 v0 = { tr.t0[0], tr.t0[1], tr.t0[2] };
     V3 e1 = { tr.t0[3], tr.t1[0], tr.t1[1] };
     V3 e2 = { tr.t1[2], tr.t1[3], tr.t2[0] };
-    V3 p = cross(d, e2);
-    float det = dot(e1, p);
+    V3 p = crossFma(d, e2);
+    float det = dotFma3(e1, p);
     if (det == 0.0f) return false;
     float inv = 1.0f / det;
     V3 s = o - v0;
-    float u = dot(s, p) * inv;
+    float u = dotFma3(s, p) * inv;
     if (!(u >= 0.0f && u <= 1.0f)) return false;
-    V3 q = cross(s, e1);
-    float v = dot(d, q) * inv;
+    V3 q = crossFma(s, e1);
+    float v = dotFma3(d, q) * inv;
     if (!(v >= 0.0f && u + v <= 1.0f)) return false;
-    float tt = dot(e2, q) * inv;
+    float tt = dotFma3(e2, q) * inv;
     if (!(tt >= tmin && tt <= tmax)) return false;
     *outT = tt;
     *outU = u;
@@ -302,14 +311,16 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // operands (measured 3.02 vs 2.72 ms traversal at C4 in round 1).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24).
+// Node-visit instruction budget (tools/isa_budget.py): the defaults cut
+// k_trace's node block from 269 to 223 VALU (gfx950 ISA of this file)
 #ifndef ARK_NODE_LDEXP
-#define ARK_NODE_LDEXP 0 // per-axis step * idir as v_ldexp_f32 of the exponent byte instead of a float build + multiply
+#define ARK_NODE_LDEXP 1 // per-axis step * idir as v_ldexp_f32 of the exponent byte instead of a float build + multiply
 #endif
 #ifndef ARK_MASK_ADDC
-#define ARK_MASK_ADDC 0 // hit / inside masks as m = 2m + bit (v_addc with the compare as carry) over slots 7..0
+#define ARK_MASK_ADDC 1 // hit / inside masks as m = 2m + bit (v_cmp to VCC + v_addc) over slots 7..0
 #endif
 #ifndef ARK_NODE_INSIDE
-#define ARK_NODE_INSIDE 1 // origin-containing children first (0: plain octant order)
+#define ARK_NODE_INSIDE 0 // 1: origin-containing children first, else plain octant order (40 VALU per node for +0.8 % node visits)
 #endif
 #if ARK_MASK_ADDC
 // m << 1 | (a <= b) in two VALU: the compare writes VCC and v_addc adds it in as the

@@ -542,22 +542,32 @@ struct Ray {
     float tmin, tmax;
 };
 
-// Möller–Trumbore (shared exact op order with the HIP kernel ddgi_trace.hip).
+// Möller–Trumbore (shared exact op order with the HIP kernel, ddgi_kernels.hip
+// intersectTri): cross and dot products fused explicitly, one fma per cross
+// component (a.y b.z - a.z b.y = fma(a.y, b.z, -(a.z b.y))) and two per dot
+// product (fma(a.x, b.x, fma(a.y, b.y, a.z b.z))). The Vulkan driver's intersection
+// arithmetic is unspecified, so the restatement fixes one.
 // Front face iff det > 0 (i.e. dot(cross(e1,e2), d) < 0: CCW seen from the ray
 // origin, Vulkan/DXR algebraic convention).
+inline V3 crossFma(V3 a, V3 b)
+{
+    return { std::fma(a.y, b.z, -(a.z * b.y)), std::fma(a.z, b.x, -(a.x * b.z)), std::fma(a.x, b.y, -(a.y * b.x)) };
+}
+inline float dotFma3(V3 a, V3 b) { return std::fma(a.x, b.x, std::fma(a.y, b.y, a.z * b.z)); }
+
 inline bool intersectTri(const Ray& r, const WTri& t, float tmax, float* outT, float* outU, float* outV, bool* backface)
 {
-    V3 p = cross(r.d, t.e2);
-    float det = dot(t.e1, p);
+    V3 p = crossFma(r.d, t.e2);
+    float det = dotFma3(t.e1, p);
     if (det == 0.0f) return false;
     float inv = 1.0f / det;
     V3 s = r.o - t.v0;
-    float u = dot(s, p) * inv;
+    float u = dotFma3(s, p) * inv;
     if (!(u >= 0.0f && u <= 1.0f)) return false;
-    V3 q = cross(s, t.e1);
-    float v = dot(r.d, q) * inv;
+    V3 q = crossFma(s, t.e1);
+    float v = dotFma3(r.d, q) * inv;
     if (!(v >= 0.0f && u + v <= 1.0f)) return false;
-    float tt = dot(t.e2, q) * inv;
+    float tt = dotFma3(t.e2, q) * inv;
     if (!(tt >= r.tmin && tt <= tmax)) return false;
     *outT = tt;
     *outU = u;
