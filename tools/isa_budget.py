@@ -36,7 +36,7 @@ def parse(path, key):
     if not starts:
         raise SystemExit(f"no kernel matching {key}")
     i0 = starts[0]
-    name = lines[i0][:-1]
+    name = lines[i0].split(":")[0]
     i1 = next(i for i in range(i0, len(lines)) if lines[i].startswith(".Lfunc_end"))
     blocks = OrderedDict()
     cur = "entry"
@@ -52,10 +52,13 @@ def parse(path, key):
             blocks[cur].append(s.split()[0])
     meta = {}
     text = "\n".join(lines)
-    m = re.search(r"\.name:\s+" + re.escape(name) + r"(.*?)(\n    - |\Z)", text, re.S)
+    m = re.search(r"\.name:\s+" + re.escape(name) + r"\n", text)
     if m:
+        # the entry's scalar fields follow its .name up to .wavefront_size
+        tail = text[m.end():m.end() + 4000]
+        tail = tail[:tail.find(".wavefront_size")] if ".wavefront_size" in tail else tail
         for k in ("sgpr_count", "vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "group_segment_fixed_size", "private_segment_fixed_size"):
-            mm = re.search(r"\." + k + r":\s+(\d+)", m.group(1))
+            mm = re.search(r"\." + k + r":\s+(\d+)", tail)
             if mm:
                 meta[k] = int(mm.group(1))
     return name, blocks, meta
