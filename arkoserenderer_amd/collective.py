@@ -117,7 +117,7 @@ class ExchangeWatchdog:
         import time
 
         t0 = time.monotonic()
-        pause = 2e-5
+        pause = 1e-5
         while not event.query():
             err = _rccl_async_error(self.group)
             if err:
@@ -128,7 +128,9 @@ class ExchangeWatchdog:
                 self.on_failure(f"{what}: not complete after {waited:.3f} s (deadline {self.timeout_s:.3f} s)")
                 return False
             time.sleep(pause)
-            pause = min(2 * pause, 2e-3)
+            # capped at 0.1 ms: a longer sleep overshoots the event by up to its own
+            # length, and the host would then enqueue the next frame late
+            pause = min(2 * pause, 1e-4)
         return True
 
     def abort_and_exit(self, why: str):
@@ -153,10 +155,15 @@ class OverlappedSlabExchange:
     for the all-gather (it samples the previous atlases at any probe); the
     all-gather waits for frame N's probe update (ark_ddgi_update_overlapped).
 
-    Bounded: before frame N's all-gather is enqueued, frame N-2's must have completed
+    Bounded: before frame N is enqueued, frame N-RING's all-gather must have completed
     (ExchangeWatchdog.wait on its event, polled against a deadline): the host runs at
-    most two exchanges ahead of the device, and a peer that stops answering ends the
-    process at the deadline instead of hanging it. drain() waits (bounded) for the last."""
+    most RING exchanges ahead of the device, and a peer that stops answering ends the
+    process at the deadline instead of hanging it. drain() waits (bounded) for the last.
+    RING = 3: with 2 the host waits for frame N-2's exchange, which ends only after
+    frame N-2's update, and enqueues frame N's traversal after the traversal stream
+    has already gone idle (Z-slab proxy at P = 8 with an exchange stand-in, round 3)."""
+
+    RING = 3
 
     def __init__(self, node, exchange, device, watchdog: ExchangeWatchdog | None = None):
         import torch
@@ -165,8 +172,8 @@ class OverlappedSlabExchange:
         self.watchdog = watchdog or ExchangeWatchdog()
         self.comm = torch.cuda.Stream(device)
         self.updated = torch.cuda.Event()
-        # completion of frame n's all-gather in slot n & 1
-        self.gathered = [torch.cuda.Event(), torch.cuda.Event()]
+        # completion of frame n's all-gather in slot n % RING
+        self.gathered = [torch.cuda.Event() for _ in range(self.RING)]
         # torch creates events lazily: record once so the raw handles exist
         cur = torch.cuda.current_stream(device)
         self.updated.record(cur)
@@ -177,10 +184,10 @@ class OverlappedSlabExchange:
     def step(self, app, stream_ptr: int):
         import torch
 
-        prev = self.gathered[(self.frames - 1) & 1]
+        prev = self.gathered[(self.frames - 1) % self.RING]
         wait = prev.cuda_event if self.frames > 0 else None
-        slot = self.gathered[self.frames & 1]
-        if self.frames >= 2 and not self.watchdog.wait(slot, "slab exchange frame n-2"):
+        slot = self.gathered[self.frames % self.RING]
+        if self.frames >= self.RING and not self.watchdog.wait(slot, f"slab exchange frame n-{self.RING}"):
             return None
         p = self.node.execute_overlapped(app, stream_ptr, wait, self.updated.cuda_event)
         with torch.cuda.stream(self.comm):
@@ -193,7 +200,7 @@ class OverlappedSlabExchange:
     def drain(self) -> bool:
         if self.frames == 0:
             return True
-        return self.watchdog.wait(self.gathered[(self.frames - 1) & 1], "slab exchange drain")
+        return self.watchdog.wait(self.gathered[(self.frames - 1) % self.RING], "slab exchange drain")
 
 
 def slab_bands(total_bytes: int, world: int):

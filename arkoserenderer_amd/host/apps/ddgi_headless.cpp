@@ -364,7 +364,7 @@ int main(int argc, char** argv)
             if (!ex->ok()) ARKOSE_LOG(Fatal, "RCCL: %s", ex->error().c_str());
             if (deadlineTest) {
                 if (world != 1) ARKOSE_LOG(Fatal, "--exchange-deadline-test runs with --world 1");
-                // frame 0's all-gather queues behind a 1.5 s stall; frame 2's exchange waits
+                // frame 0's all-gather queues behind a 1.5 s stall; frame 3's exchange waits
                 // for it with a 0.2 s deadline. The handler lets the bounded stall finish
                 // (so no kernel is left running), then takes the default failure path.
                 RcclSlabExchange* rx = ex.get();

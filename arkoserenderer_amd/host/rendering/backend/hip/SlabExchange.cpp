@@ -26,7 +26,7 @@ ExchangeWatchdog::ExchangeWatchdog(double timeoutSeconds)
 bool ExchangeWatchdog::wait(void* hipEvent, void* ncclComm, const char* what)
 {
     const auto t0 = std::chrono::steady_clock::now();
-    auto sleepFor = std::chrono::microseconds(20);
+    auto sleepFor = std::chrono::microseconds(10);
     for (;;) {
         const hipError_t q = hipEventQuery(static_cast<hipEvent_t>(hipEvent));
         if (q == hipSuccess) return true;
@@ -50,7 +50,8 @@ bool ExchangeWatchdog::wait(void* hipEvent, void* ncclComm, const char* what)
             return false;
         }
         std::this_thread::sleep_for(sleepFor);
-        sleepFor = std::min(sleepFor * 2, std::chrono::microseconds(2000));
+        // capped at 0.1 ms: a longer sleep overshoots the event by up to its own length
+        sleepFor = std::min(sleepFor * 2, std::chrono::microseconds(100));
     }
 }
 
@@ -121,15 +122,19 @@ RcclSlabExchange::RcclSlabExchange(int device, int rank, int world, const void* 
     }
     m_comm = comm;
     hipStream_t s;
-    hipEvent_t e0, e1;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
-        m_error = "side stream / event creation failed";
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        m_error = "side stream creation failed";
         return;
     }
     m_stream = s;
-    m_done[0] = e0;
-    m_done[1] = e1;
+    for (void*& slot : m_done) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            m_error = "event creation failed";
+            return;
+        }
+        slot = e;
+    }
     m_ok = true;
 }
 
@@ -147,7 +152,7 @@ RcclSlabExchange::~RcclSlabExchange()
 bool RcclSlabExchange::drain()
 {
     if (!m_ok || m_frames == 0) return m_ok;
-    return m_watchdog.wait(m_done[(m_frames - 1) & 1u], m_comm, "RcclSlabExchange drain");
+    return m_watchdog.wait(m_done[(m_frames - 1) % kRing], m_comm, "RcclSlabExchange drain");
 }
 
 void* RcclSlabExchange::exchange(int rank, void* updateDone)
@@ -158,9 +163,9 @@ void* RcclSlabExchange::exchange(int rank, void* updateDone)
     }
     const hipStream_t s = static_cast<hipStream_t>(m_stream);
     const ncclComm_t comm = static_cast<ncclComm_t>(m_comm);
-    void* const slot = m_done[m_frames & 1u];
-    // frame n - 2's all-gather (the last record of this slot) must be complete
-    if (m_frames >= 2 && !m_watchdog.wait(slot, m_comm, "RcclSlabExchange frame n-2")) return nullptr;
+    void* const slot = m_done[m_frames % kRing];
+    // frame n - kRing's all-gather (the last record of this slot) must be complete
+    if (m_frames >= kRing && !m_watchdog.wait(slot, m_comm, "RcclSlabExchange frame n-3")) return nullptr;
     if (updateDone) (void)hipStreamWaitEvent(s, static_cast<hipEvent_t>(updateDone), 0);
     // in place: this rank's band already sits at recvbuff + rank * count
     ncclResult_t r = ncclGroupStart();

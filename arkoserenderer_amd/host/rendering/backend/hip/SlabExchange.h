@@ -82,9 +82,11 @@ public:
     ~RcclSlabExchange() override;
     bool ok() const { return m_ok; }
     const std::string& error() const { return m_error; }
-    // Frame n's all-gather first waits (bounded, on the host) for frame n - 2's: the
-    // host runs at most two exchanges ahead of the device, and a peer that stops
-    // answering ends the process at the deadline instead of hanging it.
+    // Frame n's all-gather first waits (bounded, on the host) for frame n - kRing's:
+    // the host runs at most kRing exchanges ahead of the device, and a peer that stops
+    // answering ends the process at the deadline instead of hanging it. kRing = 3:
+    // with 2, frame n - 2's exchange ends only after frame n - 2's update, and the host
+    // enqueued frame n's traversal after the traversal stream had gone idle.
     void* exchange(int rank, void* updateDone) override;
     bool drain() override;
     const char* name() const override { return "rccl"; }
@@ -99,7 +101,8 @@ private:
     SlabBands m_bands;
     void* m_comm { nullptr };
     void* m_stream { nullptr };
-    void* m_done[2] { nullptr, nullptr }; // completion of frame n in slot n & 1
+    static constexpr uint32_t kRing = 3;
+    void* m_done[kRing] {}; // completion of frame n in slot n % kRing
     uint64_t m_frames { 0 };
     bool m_ok { false };
     std::string m_error;

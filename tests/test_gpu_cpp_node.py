@@ -92,7 +92,7 @@ def test_cpp_rccl_exchange_one_rank(tmp_path):
 def test_cpp_rccl_exchange_watchdog_deadline(tmp_path):
     """Failure detection of the C++ exchange: a 1-rank communicator whose
     side stream is stalled for 1.5 s (a bounded kernel) under a 0.2 s deadline. Frame
-    2's exchange waits for frame 0's all-gather, the watchdog polls the event and
+    3's exchange waits for frame 0's all-gather, the watchdog polls the event and
     ncclCommGetAsyncError, fires at the deadline, and the default failure path aborts
     the communicator, logs an Error and ends the process with exit code 14 (the stall
     kernel is allowed to finish first, so nothing is left running on the GPU)."""
@@ -104,7 +104,7 @@ def test_cpp_rccl_exchange_watchdog_deadline(tmp_path):
            "--world", "1", "--rank", "0", "--nccl-id", str(tmp_path / "nccl.id"), "--exchange-deadline-test"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert r.returncode == 14, (r.returncode, r.stdout, r.stderr)
-    assert "watchdog fired: RcclSlabExchange frame n-2: not complete after" in r.stdout, r.stdout
+    assert "watchdog fired: RcclSlabExchange frame n-3: not complete after" in r.stdout, r.stdout
     assert "[error] z-slab exchange failed, exiting" in r.stderr.lower(), r.stderr
 
 

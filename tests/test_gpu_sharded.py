@@ -249,13 +249,13 @@ def _stalled_exchange_run(timeout_s, on_failure, port):
     wd = ExchangeWatchdog(timeout_s=timeout_s, on_failure=on_failure)
     exch = OverlappedSlabExchange(node, exchange, dev, wd)
     sptr = torch.cuda.current_stream(dev).cuda_stream
-    results = [exch.step(D.AppState(f), sptr) for f in range(3)]
+    results = [exch.step(D.AppState(f), sptr) for f in range(OverlappedSlabExchange.RING + 1)]
     return node, exch, results
 
 
 def test_python_exchange_watchdog_fires_at_deadline():
     """collective.ExchangeWatchdog (SURVEY §5 failure detection): with the exchange
-    stream stalled and a 0.2 s deadline, frame 2's step does not enqueue anything and
+    stream stalled and a 0.2 s deadline, frame RING's step does not enqueue anything and
     reports the timeout to the failure handler; a generous deadline lets the same
     stall pass."""
     import torch
@@ -264,8 +264,8 @@ def test_python_exchange_watchdog_fires_at_deadline():
     fired = []
     node, exch, res = _stalled_exchange_run(0.2, fired.append, 29547)
     try:
-        assert res[0] is not None and res[1] is not None and res[2] is None
-        assert len(fired) == 1 and "slab exchange frame n-2: not complete after" in fired[0], fired
+        assert all(r is not None for r in res[:-1]) and res[-1] is None
+        assert len(fired) == 1 and "slab exchange frame n-3: not complete after" in fired[0], fired
     finally:
         torch.cuda.synchronize()  # the stall kernel finishes by itself
         dist.destroy_process_group()
@@ -310,4 +310,4 @@ def test_python_exchange_watchdog_exits_process(tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 14, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "not reached" not in r.stdout
-    assert "[Error] Z-slab exchange failed, exiting: slab exchange frame n-2: not complete after" in r.stderr
+    assert "[Error] Z-slab exchange failed, exiting: slab exchange frame n-3: not complete after" in r.stderr
