@@ -31,8 +31,6 @@ namespace {
 
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
 constexpr uint32_t kPipeHalfRays = 5u << 20;
-// BVH8 child selection default (ARK_BVH8_COLLAPSE overrides)
-constexpr bool kBvh8SahCollapseDefault = false;
 // u32 words per shadow-ray bin counter (ddgi_kernels.hip kBinStride)
 constexpr uint64_t kShadowBinStride = 32;
 
@@ -634,10 +632,10 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
     // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
-    // BVH2 -> BVH8 child selection: ARK_BVH8_COLLAPSE=sah (Ylitie et al. 2017 DP) or
-    // greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's SAH terms
+    // BVH2 -> BVH8 child selection: SAH-optimal (Ylitie et al. 2017 DP; the default) or
+    // ARK_BVH8_COLLAPSE=greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's
+    // SAH terms
     Bvh8CollapseOptions copt;
-    copt.sah_optimal = kBvh8SahCollapseDefault;
     if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
     if (const char* e = std::getenv("ARK_BVH8_NODE_COST")) copt.node_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
@@ -646,6 +644,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     int32_t roots[3] = { -1, -1, -1 };
     uint32_t opaqueNodes = 0;
     uint32_t maxDepth = 0, maxLeaf = 0;
+    uint64_t triangles = 0;
     float sah = 0.0f;
     for (int c = 0; c < 3; ++c) {
         if (cls[c].empty()) continue;
@@ -658,13 +657,15 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         roots[c] = static_cast<int32_t>(allNodes.size());
         if (c == 0) opaqueNodes = static_cast<uint32_t>(r.nodes.size());
         maxDepth = std::max(maxDepth, r.max_depth);
+        triangles += r.triangles;
         allNodes.insert(allNodes.end(), r.nodes.begin(), r.nodes.end());
         allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
     }
     if (allNodes.size() >= (1ull << 31) || allTris.size() >= (1ull << 31)) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "scene too large for 31-bit BVH indices");
     // Structural check before anything reaches the GPU: every node is referenced
     // once from a root-reachable parent (no cycles, no sharing), every leaf's
-    // triangles lie inside the triangle array and every triangle is covered once.
+    // triangles lie inside the triangle array and every triangle (every record but
+    // the holes of the rows) is covered once.
     {
         std::vector<uint8_t> seenNode(allNodes.size(), 0);
         std::vector<uint8_t> seenTri(allTris.size(), 0);
@@ -678,27 +679,25 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
             seenNode[n] = 1;
             const GpuBvh8Node& nd = allNodes[n];
             uint32_t internal = 0;
+            if (nd.leaf_tris >> 24) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
             for (int sl = 0; sl < 8; ++sl) {
                 const bool isInternal = (nd.imask >> sl) & 1u;
-                if (isInternal) {
-                    if (nd.meta[sl] != 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
-                    work.push_back(nd.child_base + internal++);
-                } else if (nd.meta[sl] != 0) {
-                    const uint32_t unary = nd.meta[sl] >> 5, off = nd.meta[sl] & 31u;
-                    if (unary != 1u && unary != 3u && unary != 7u) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf code");
-                    const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : 3u);
-                    if (off + cnt > 24u || static_cast<uint64_t>(nd.tri_base) + off + cnt > allTris.size()) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
-                    for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
-                        if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
-                        seenTri[t] = 1;
-                    }
+                uint32_t slotTris[kBvh8MaxLeafSize];
+                const int cnt = bvh8SlotTriangles(nd, sl, slotTris);
+                if (cnt < 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
+                if (isInternal) work.push_back(nd.child_base + internal++);
+                for (int i = 0; i < cnt; ++i) {
+                    const uint32_t t = slotTris[i];
+                    if (t >= allTris.size() || isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
+                    if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
+                    seenTri[t] = 1;
                 }
                 for (int a = 0; a < 3; ++a)
-                    if ((isInternal || nd.meta[sl] != 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
+                    if ((isInternal || cnt > 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
             }
         }
         for (size_t t = 0; t < seenTri.size(); ++t)
-            if (!seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
+            if (!seenTri[t] && !isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
     }
     // textures: decoded to float4 texels (sRGB EOTF per texel), + trailing 1x1 white
     std::vector<GpuTextureInfo> infos;
@@ -786,6 +785,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         // instead of instance -> mesh -> indices -> vertices
         std::vector<float> tn(allTris.size() * 16, 0.0f);
         for (size_t t = 0; t < allTris.size(); ++t) {
+            if (isHoleTriangle(allTris[t])) continue; // never hit: no record
             uint32_t inst, prim;
             std::memcpy(&inst, &allTris[t].t2[1], 4);
             std::memcpy(&prim, &allTris[t].t2[2], 4);
@@ -834,7 +834,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     st->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
     const auto t1 = std::chrono::steady_clock::now();
     st->bvhStats.node_count = allNodes.size();
-    st->bvhStats.triangle_count = allTris.size();
+    st->bvhStats.triangle_count = triangles;
     st->bvhStats.max_depth = maxDepth;
     st->bvhStats.max_leaf_size = maxLeaf;
     st->bvhStats.sah_cost = sah;

@@ -337,7 +337,70 @@ void quantGrid(float L, float H, int& e, double& p)
     }
 }
 
+// First-fit placement of a node's leaf-triangle rows (a 24-bit pattern over
+// positions base + 0..23) into the triangle array: the lowest base, at most
+// kRowWindow below the end of the array, whose positions are all free. The search
+// is bounded, so the collapse stays linear; rows of neighbouring nodes interleave.
+class RowPlacer {
+public:
+    uint32_t place(uint32_t pattern)
+    {
+        const uint32_t lo = m_end > kRowWindow ? m_end - kRowWindow : 0u;
+        for (uint32_t b = lo;; ++b)
+            if ((window(b) & pattern) == 0) {
+                mark(b, pattern);
+                return b;
+            }
+    }
+
+private:
+    static constexpr uint32_t kRowWindow = 512;
+    uint64_t window(uint32_t b) const // occupancy of positions b .. b + 23
+    {
+        const size_t i = b >> 6;
+        const uint32_t sh = b & 63u;
+        uint64_t w = i < m_bits.size() ? m_bits[i] >> sh : 0u;
+        if (sh && i + 1 < m_bits.size()) w |= m_bits[i + 1] << (64u - sh);
+        return w & 0xffffffu;
+    }
+    void mark(uint32_t b, uint32_t pattern)
+    {
+        const size_t i = b >> 6;
+        const uint32_t sh = b & 63u;
+        if (m_bits.size() < i + 2) m_bits.resize(i + 2, 0u);
+        m_bits[i] |= static_cast<uint64_t>(pattern) << sh;
+        if (sh > 40u) m_bits[i + 1] |= static_cast<uint64_t>(pattern) >> (64u - sh);
+        m_end = std::max(m_end, b + 32u - static_cast<uint32_t>(__builtin_clz(pattern)));
+    }
+    std::vector<uint64_t> m_bits;
+    uint32_t m_end = 0;
+};
+
 } // namespace
+
+GpuTriangle holeTriangle()
+{
+    GpuTriangle t;
+    std::memset(&t, 0, sizeof(t));
+    std::memcpy(&t.t2[1], &kHoleInstance, 4);
+    return t;
+}
+
+bool isHoleTriangle(const GpuTriangle& t)
+{
+    uint32_t inst;
+    std::memcpy(&inst, &t.t2[1], 4);
+    return inst == kHoleInstance;
+}
+
+int bvh8SlotTriangles(const GpuBvh8Node& nd, int s, uint32_t out[kBvh8MaxLeafSize])
+{
+    const uint32_t bits = bvh8SlotTris(nd.leaf_tris, s) >> s;
+    if ((nd.imask >> s) & 1u) return bits ? -1 : 0;
+    const int n = bits == 0x010101u ? 3 : (bits == 0x0101u ? 2 : (bits == 1u ? 1 : (bits == 0u ? 0 : -1)));
+    for (int i = 0; i < n; ++i) out[i] = nd.tri_base + 8u * static_cast<uint32_t>(i) + static_cast<uint32_t>(s);
+    return n;
+}
 
 float bvh8_inflation(const float* xyz, uint64_t nTriangles)
 {
@@ -490,7 +553,8 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
     std::vector<Item> queue;
     queue.push_back({ 0u, 0u, 1u });
     res.nodes.resize(1);
-    res.tris.reserve(bvh2.tris.size());
+    res.tris.reserve(bvh2.tris.size() + bvh2.tris.size() / 8);
+    RowPlacer rowPlacer;
     double sah = 0.0, rootArea = 0.0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const Item it = queue[qi];
@@ -593,12 +657,23 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             nd.p[a] = static_cast<float>(p[a]);
             nd.e[a] = static_cast<uint8_t>(e + 127);
         }
-        // children in slot order: internal ones get consecutive node indices, leaf
-        // triangles are appended contiguously
+        // children in slot order: internal ones get consecutive node indices; leaf
+        // triangle i of slot s goes to row position 8 i + s (GpuBvh8Node), the rows
+        // placed at the first base in the tail of the array where all of their
+        // positions are free
         const uint32_t childBase = static_cast<uint32_t>(res.nodes.size());
-        const uint32_t triStart = static_cast<uint32_t>(res.tris.size());
+        uint32_t rows = 0;
+        for (int s = 0; s < 8; ++s) {
+            const int c = childIn[s];
+            if (c < 0 || ch[c].code >= 0) continue;
+            const uint32_t cnt = (static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1u;
+            for (uint32_t i = 0; i < cnt; ++i) rows |= 1u << (8u * i + static_cast<uint32_t>(s));
+        }
+        const uint32_t triStart = rows ? rowPlacer.place(rows) : 0u;
+        if (rows && res.tris.size() < triStart + 24u) res.tris.resize(triStart + 24u, holeTriangle());
         nd.child_base = node_base + childBase;
         nd.tri_base = tri_base + triStart;
+        nd.leaf_tris = rows;
         uint32_t nInternal = 0;
         for (int s = 0; s < 8; ++s) {
             const int c = childIn[s];
@@ -622,15 +697,17 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             } else {
                 const uint32_t code = static_cast<uint32_t>(~k.code);
                 const uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
-                const uint32_t off = static_cast<uint32_t>(res.tris.size()) - triStart;
-                for (uint32_t t = first; t < first + cnt; ++t) res.tris.push_back(bvh2.tris[t]);
-                nd.meta[s] = static_cast<uint8_t>((((1u << cnt) - 1u) << 5) | off);
+                for (uint32_t i = 0; i < cnt; ++i) res.tris[triStart + 8u * i + static_cast<uint32_t>(s)] = bvh2.tris[first + i];
                 res.leaf_children++;
+                res.triangles += cnt;
             }
         }
         res.nodes.resize(res.nodes.size() + nInternal);
         res.nodes[it.dst] = nd;
     }
+    // drop trailing holes (the array keeps one padding record for the five-load fetch
+    // in the uploader)
+    while (!res.tris.empty() && isHoleTriangle(res.tris.back())) res.tris.pop_back();
     res.sah_cost = static_cast<float>(sah);
     return res;
 }
@@ -689,7 +766,13 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
         uint32_t internal = 0;
         for (int s = 0; s < 8; ++s) {
             const bool in = (nd.imask >> s) & 1u;
-            if (!in && nd.meta[s] == 0) continue;
+            uint32_t slotTris[kBvh8MaxLeafSize];
+            const int cnt = bvh8SlotTriangles(nd, s, slotTris);
+            if (cnt < 0) {
+                violations++;
+                continue;
+            }
+            if (!in && cnt == 0) continue;
             Box b;
             for (int a = 0; a < 3; ++a) {
                 const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
@@ -705,14 +788,9 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
                 work.push_back({ nd.child_base + internal++, std::move(anc) });
                 continue;
             }
-            const uint32_t unary = nd.meta[s] >> 5, off = nd.meta[s] & 31u;
-            const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : (unary == 7u ? 3u : 0u));
-            if (cnt == 0 || off + cnt > 24u) {
-                violations++;
-                continue;
-            }
-            for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
-                if (t >= r8.tris.size()) {
+            for (int ti = 0; ti < cnt; ++ti) {
+                const uint32_t t = slotTris[ti];
+                if (t >= r8.tris.size() || isHoleTriangle(r8.tris[t])) {
                     violations++;
                     continue;
                 }
@@ -736,7 +814,7 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
         out[1] = r8.leaf_children;
         out[2] = r8.max_depth;
         out[3] = violations;
-        out[4] = r8.tris.size();
+        out[4] = r8.triangles;
         out[5] = r2.nodes.size();
         out[6] = internalChildren;
         out[7] = static_cast<uint64_t>(static_cast<double>(r8.sah_cost) * 1e6); // BVH8 SAH cost x 1e6
@@ -800,7 +878,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                 int nh = 0;
                 for (int s = 0; s < 8; ++s) {
                     const bool internal = (nd.imask >> s) & 1u;
-                    if (!internal && nd.meta[s] == 0) continue;
+                    if (!internal && bvh8SlotTris(nd.leaf_tris, s) == 0) continue;
                     float tn = tmin, tf = tmax;
                     for (int a = 0; a < 3; ++a) {
                         const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
@@ -823,9 +901,10 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                 for (int i = 0; i < nh; ++i) {
                     const int s = hitc[i].s;
                     if ((nd.imask >> s) & 1u) continue;
-                    const uint32_t unary = nd.meta[s] >> 5, off = nd.meta[s] & 31u;
-                    const uint32_t cnt = unary == 1u ? 1u : (unary == 3u ? 2u : 3u);
-                    for (uint32_t t = nd.tri_base + off; t < nd.tri_base + off + cnt; ++t) {
+                    uint32_t slotTris[kBvh8MaxLeafSize];
+                    const int cnt = bvh8SlotTriangles(nd, s, slotTris);
+                    for (int ti = 0; ti < cnt; ++ti) {
+                        const uint32_t t = slotTris[ti];
                         ct++;
                         steps++;
                         const GpuTriangle& g = r8.tris[t];
@@ -877,7 +956,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
         out[4] = static_cast<uint64_t>(static_cast<double>(r8.sah_cost) * 1e6);
         out[5] = maxSteps.load();
         out[6] = r8.max_depth;
-        out[7] = 0;
+        out[7] = r8.tris.size();
     }
     return 0;
 }

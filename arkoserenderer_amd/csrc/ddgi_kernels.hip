@@ -310,7 +310,7 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // v_pk_fma_f32 pair issues in two slots on gfx950 and needs moves to pair its
 // operands (measured 3.02 vs 2.72 ms traversal at C4 in round 1).
 // Returns the hit internal children as a node group and the hit leaf children's
-// triangles as a bit mask over [tBase, tBase + 24).
+// triangles as a bit mask over [tBase, tBase + 24) (2 VALU: triangle rows).
 // Node-visit instruction budget (tools/isa_budget.py): the defaults cut
 // k_trace's node block from 269 to 223 VALU (gfx950 ISA of this file)
 #ifndef ARK_NODE_LDEXP
@@ -385,20 +385,12 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     m = fx ? (((m & 0x00550055u) << 1) | ((m >> 1) & 0x00550055u)) : m;
     m = fy ? (((m & 0x00330033u) << 2) | ((m >> 2) & 0x00330033u)) : m;
     m = fz ? (((m & 0x000f000fu) << 4) | ((m >> 4) & 0x000f000fu)) : m;
-    // leaf children: their triangle ranges (meta: unary count << 5 | offset)
-    uint32_t tb = 0;
-    const uint32_t leafHits = hitSlots & ~imask;
-    if (leafHits) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const uint32_t meta = ((s < 4 ? w1.z : w1.w) >> ((s & 3) * 8)) & 0xffu;
-            tb |= ((leafHits >> s) & 1u) ? ((meta >> 5) << (meta & 31u)) : 0u;
-        }
-    }
+    // leaf children: their triangle rows (GpuBvh8Node: bit 8 i + s = triangle i of
+    // slot s), the hit slots replicated into the three rows and masked
     gBase = w1.x;
     gBits = (m & 0x00ff00ffu) | (imask << 8);
     tBase = w1.y;
-    tBits = tb;
+    tBits = ((hitSlots & ~imask & 0xffu) * 0x010101u) & w1.z;
 }
 
 __device__ __forceinline__ GpuTriangle triFromWords(uint4 a, uint4 b, uint4 c)

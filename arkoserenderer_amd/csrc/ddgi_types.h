@@ -32,27 +32,36 @@ constexpr int kMaxLeafSize = 1 << kLeafCountBits;
 // plane decodes EXACTLY in fp32 (one fma), and q is rounded outward, so a decoded
 // child box contains the (already inflated) BVH2 child box it replaces.
 //   w0..2  p.xyz            w3  e.x | e.y << 8 | e.z << 16 | imask << 24
-//   w4     child_base       w5  tri_base          w6,7  meta[8]
+//   w4     child_base       w5  tri_base          w6  leaf_tris   w7  reserved (0)
 //   w8,9   qlo.x[8]         w10,11 qlo.y[8]       w12,13 qlo.z[8]
 //   w14,15 qhi.x[8]         w16,17 qhi.y[8]       w18,19 qhi.z[8]
 // Slot s of a node holds its child whose centre lies on the (s & 1 ? + : -) x,
 // (s & 2 ? + : -) y, (s & 4 ? + : -) z side of the node centre, as far as the
 // children allow, so visiting hit slots in increasing (s ^ rayOctant) order is
 // roughly front to back. imask bit s: internal child, stored at
-// child_base + popcount(imask & ((1 << s) - 1)). meta[s] != 0: leaf child whose
-// (meta >> 5) unary-coded 1..3 triangles start at tri_base + (meta & 31).
+// child_base + popcount(imask & ((1 << s) - 1)). Leaf triangles in rows of 8:
+// bit 8 i + s of leaf_tris is the i-th triangle (i < kBvh8MaxLeafSize) of leaf
+// slot s, stored at tri_base + 8 i + s, so the triangles of a set H of hit leaf
+// slots are (H * 0x010101) & leaf_tris (two VALU; a per-slot offset/count code
+// cost ~40). Slot s is a leaf iff bit s is set. Rows of neighbouring nodes are
+// interleaved in the triangle array (first fit), so the positions an internal
+// slot leaves free are mostly used by other nodes' triangles; any position still
+// free is a hole record (kHoleInstance) that no leaf references.
 struct alignas(16) GpuBvh8Node {
     float p[3];
     uint8_t e[3];
     uint8_t imask;
     uint32_t child_base;
     uint32_t tri_base;
-    uint8_t meta[8];
+    uint32_t leaf_tris;
+    uint32_t reserved;
     uint8_t qlo[3][8];
     uint8_t qhi[3][8];
 };
 static_assert(sizeof(GpuBvh8Node) == 80, "BVH8 node is 80 B");
 constexpr int kBvh8MaxLeafSize = 3;
+// triangles of leaf slot s within leaf_tris (bits s, s + 8, s + 16)
+inline constexpr uint32_t bvh8SlotTris(uint32_t leafTris, int s) { return leafTris & (0x010101u << s); }
 
 // World-space triangle record, 48 B = 3 x 16 B, in leaf order:
 //   t0 = (v0.x, v0.y, v0.z, e1.x)   t1 = (e1.y, e1.z, e2.x, e2.y)
@@ -60,6 +69,9 @@ constexpr int kBvh8MaxLeafSize = 3;
 //        when the instance's det(ObjectToWorld) < 0, i.e. its facing is mirrored)
 // Closest-hit ties are broken on (instance, primitive), i.e. the global triangle
 // id, so the hit does not depend on the BVH shape (same rule in the oracle).
+// A hole of the BVH8 triangle rows (GpuBvh8Node) is all zero but instance =
+// kHoleInstance.
+constexpr uint32_t kHoleInstance = 0xffffffffu;
 struct alignas(16) GpuTriangle {
     float t0[4];
     float t1[4];

@@ -45,7 +45,8 @@ int ark_ddgi_debug_struct_sizes(uint32_t* out, int n);
  * decoded boxes of its leaf and of all its ancestors. out[8] = {nodes, leaf
  * children, max depth, violations, triangles, bvh2 nodes, internal children, BVH8
  * SAH cost x 1e6 (node cost 1)}. The BVH8 child selection follows ARK_BVH8_COLLAPSE
- * ("sah" = SAH-optimal, else greedy) and ARK_BVH8_TRI_COST, as set_scene does.
+ * (unset or "sah" = SAH-optimal, any other value = greedy) and ARK_BVH8_TRI_COST, as
+ * set_scene does.
  * Returns 0 when the check passes, 1 when it found violations. No GPU. */
 int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out);
 
@@ -53,7 +54,8 @@ int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out)
  * closest-hit order: hit children, origin-containing first, then octant order; the
  * leaf triangles of a node right after it): nRays rays of 7 floats (origin,
  * direction, tmax) over `threads` host threads. out[8] = {node visits, triangle
- * tests, hits, BVH8 nodes, SAH cost x 1e6, max steps of one ray, max depth, 0};
+ * tests, hits, BVH8 nodes, SAH cost x 1e6, max steps of one ray, max depth,
+ * triangle records (leaf triangle rows, holes included)};
  * per_ray_steps (if not NULL) gets each ray's node visits + triangle tests.
  * For comparing BVH builds (ARK_BVH8_COLLAPSE, ARK_BVH8_TRI_COST,
  * ARK_BVH_INTERSECTION_COST) without a GPU: tools/bvh_stats.py. */

@@ -83,7 +83,8 @@ def main():
             np.savez_compressed(f"{args.save_steps}_{v.replace(' ', '_')}.npz", steps=steps, probes=probes, rays=rays)
         n = rays.shape[0]
         res[v] = {"nodes_per_ray": round(out[0] / n, 3), "tris_per_ray": round(out[1] / n, 3), "hit_frac": round(out[2] / n, 4),
-                  "bvh8_nodes": out[3], "sah": out[4] / 1e6, "max_steps": out[5], "depth": out[6], "s": round(time.time() - t, 1)}
+                  "bvh8_nodes": out[3], "sah": out[4] / 1e6, "max_steps": out[5], "depth": out[6],
+                  "triangle_records_per_triangle": round(out[7] / tris.shape[0], 4), "s": round(time.time() - t, 1)}
         print(v, json.dumps(res[v]), flush=True)
 
 
