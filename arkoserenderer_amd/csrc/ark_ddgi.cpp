@@ -679,7 +679,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
             seenNode[n] = 1;
             const GpuBvh8Node& nd = allNodes[n];
             uint32_t internal = 0;
-            if (nd.leaf_tris >> 24) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
+            if ((nd.leaf_tris >> 24) || (nd.leaf_mask & nd.imask)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
             for (int sl = 0; sl < 8; ++sl) {
                 const bool isInternal = (nd.imask >> sl) & 1u;
                 uint32_t slotTris[kBvh8MaxLeafSize];

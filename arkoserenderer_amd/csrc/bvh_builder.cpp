@@ -376,6 +376,33 @@ private:
     uint32_t m_end = 0;
 };
 
+// The smallest row stride (GpuBvh8Node) under which every position s + stride * i
+// (i < 3) of a leaf slot s is free or s's own triangle i, so a hit leaf slot's
+// spread never reaches another slot's triangle, and the rows fit in 24 positions.
+uint32_t leafRowStride(const uint32_t cnt[8])
+{
+    static const bool fixed8 = std::getenv("ARK_BVH8_ROW_STRIDE8") != nullptr; // A/B: rows of 8 for every node
+    for (uint32_t st = fixed8 ? 8u : 1u; st < 8; ++st) {
+        int owner[24];
+        for (int& o : owner) o = -1;
+        bool ok = true;
+        for (uint32_t s = 0; s < 8 && ok; ++s)
+            for (uint32_t i = 0; i < cnt[s] && ok; ++i) {
+                const uint32_t p = s + st * i;
+                ok = p < 24u && owner[p] < 0;
+                if (ok) owner[p] = static_cast<int>(s);
+            }
+        for (uint32_t s = 0; s < 8 && ok; ++s)
+            if (cnt[s])
+                for (uint32_t i = 0; i < 3u && ok; ++i) {
+                    const uint32_t p = s + st * i;
+                    ok = p >= 24u || owner[p] < 0 || owner[p] == static_cast<int>(s);
+                }
+        if (ok) return st;
+    }
+    return 8u;
+}
+
 } // namespace
 
 GpuTriangle holeTriangle()
@@ -395,11 +422,19 @@ bool isHoleTriangle(const GpuTriangle& t)
 
 int bvh8SlotTriangles(const GpuBvh8Node& nd, int s, uint32_t out[kBvh8MaxLeafSize])
 {
-    const uint32_t bits = bvh8SlotTris(nd.leaf_tris, s) >> s;
-    if ((nd.imask >> s) & 1u) return bits ? -1 : 0;
-    const int n = bits == 0x010101u ? 3 : (bits == 0x0101u ? 2 : (bits == 1u ? 1 : (bits == 0u ? 0 : -1)));
-    for (int i = 0; i < n; ++i) out[i] = nd.tri_base + 8u * static_cast<uint32_t>(i) + static_cast<uint32_t>(s);
-    return n;
+    const bool leaf = (nd.leaf_mask >> s) & 1u;
+    if (!leaf) return 0;
+    if (((nd.imask >> s) & 1u) || nd.tri_stride < 1u || nd.tri_stride > 8u) return -1;
+    int n = 0;
+    bool ended = false;
+    for (uint32_t i = 0; i < static_cast<uint32_t>(kBvh8MaxLeafSize); ++i) {
+        const uint32_t pos = static_cast<uint32_t>(s) + nd.tri_stride * i;
+        const bool set = pos < 24u && ((nd.leaf_tris >> pos) & 1u);
+        if (set && ended) return -1; // the slot's spread reaches another slot's triangle
+        if (!set) ended = true;
+        else out[n++] = nd.tri_base + pos;
+    }
+    return n > 0 ? n : -1;
 }
 
 float bvh8_inflation(const float* xyz, uint64_t nTriangles)
@@ -658,22 +693,28 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             nd.e[a] = static_cast<uint8_t>(e + 127);
         }
         // children in slot order: internal ones get consecutive node indices; leaf
-        // triangle i of slot s goes to row position 8 i + s (GpuBvh8Node), the rows
-        // placed at the first base in the tail of the array where all of their
+        // triangle i of slot s goes to position s + stride * i (GpuBvh8Node), the
+        // rows placed at the first base in the tail of the array where all of their
         // positions are free
         const uint32_t childBase = static_cast<uint32_t>(res.nodes.size());
-        uint32_t rows = 0;
+        uint32_t leafCnt[8] = {}, leafMask = 0;
         for (int s = 0; s < 8; ++s) {
             const int c = childIn[s];
             if (c < 0 || ch[c].code >= 0) continue;
-            const uint32_t cnt = (static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1u;
-            for (uint32_t i = 0; i < cnt; ++i) rows |= 1u << (8u * i + static_cast<uint32_t>(s));
+            leafCnt[s] = (static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1u;
+            leafMask |= 1u << s;
         }
+        const uint32_t stride = leafRowStride(leafCnt);
+        uint32_t rows = 0;
+        for (uint32_t s = 0; s < 8; ++s)
+            for (uint32_t i = 0; i < leafCnt[s]; ++i) rows |= 1u << (s + stride * i);
         const uint32_t triStart = rows ? rowPlacer.place(rows) : 0u;
         if (rows && res.tris.size() < triStart + 24u) res.tris.resize(triStart + 24u, holeTriangle());
         nd.child_base = node_base + childBase;
         nd.tri_base = tri_base + triStart;
         nd.leaf_tris = rows;
+        nd.tri_stride = static_cast<uint8_t>(stride);
+        nd.leaf_mask = static_cast<uint8_t>(leafMask);
         uint32_t nInternal = 0;
         for (int s = 0; s < 8; ++s) {
             const int c = childIn[s];
@@ -697,7 +738,7 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             } else {
                 const uint32_t code = static_cast<uint32_t>(~k.code);
                 const uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
-                for (uint32_t i = 0; i < cnt; ++i) res.tris[triStart + 8u * i + static_cast<uint32_t>(s)] = bvh2.tris[first + i];
+                for (uint32_t i = 0; i < cnt; ++i) res.tris[triStart + static_cast<uint32_t>(s) + stride * i] = bvh2.tris[first + i];
                 res.leaf_children++;
                 res.triangles += cnt;
             }
@@ -878,7 +919,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                 int nh = 0;
                 for (int s = 0; s < 8; ++s) {
                     const bool internal = (nd.imask >> s) & 1u;
-                    if (!internal && bvh8SlotTris(nd.leaf_tris, s) == 0) continue;
+                    if (!internal && !((nd.leaf_mask >> s) & 1u)) continue;
                     float tn = tmin, tf = tmax;
                     for (int a = 0; a < 3; ++a) {
                         const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);

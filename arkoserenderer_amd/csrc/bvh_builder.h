@@ -70,9 +70,10 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
 // Hole records of the triangle rows (kHoleInstance)
 GpuTriangle holeTriangle();
 bool isHoleTriangle(const GpuTriangle& t);
-// Triangle indices of leaf slot s of a node (tri_base + 8 i + s for the set bits of
-// its rows, in row order); -1 when the slot's bits are not rows 0..n-1 of s, or an
-// internal slot has any
+// Triangle indices of leaf slot s of a node (tri_base + s + stride * i for the
+// consecutive set bits of its row from i = 0); 0 for a slot that is not a leaf, -1
+// when a leaf slot has no triangle, an internal slot is marked leaf, or the slot's
+// spread reaches another slot's triangle (GpuBvh8Node)
 int bvh8SlotTriangles(const GpuBvh8Node& nd, int s, uint32_t out[kBvh8MaxLeafSize]);
 
 // Absolute box inflation for the BVH8 slab test: 1e-6 of the diagonal of the

@@ -217,6 +217,13 @@ __device__ __forceinline__ V3 crossFma(V3 a, V3 b)
 }
 __device__ __forceinline__ float dotFma3(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
 
+// Branch free: in a wave some lane passes each early-out test on almost every
+// step, so the early returns saved no VALU and cost an exec-mask branch each
+// (~14 SALU per traversal step). The accepted set is the oracle's: u <= 1 follows
+// from v >= 0 and RN(u + v) <= 1 (rounding is monotonic), and det == 0 gives
+// inv = +-inf, so u or v is NaN or infinite and one of u >= 0, v >= 0, u + v <= 1
+// fails, as the oracle's early return rejects it; the values of an accepted hit
+// are computed exactly as the oracle computes them.
 __device__ __forceinline__ bool intersectTri(V3 o, V3 d, float tmin, float tmax, const GpuTriangle& tr, float* outT, float* outU, float* outV, bool* backfaceDet)
 {
     V3 v0 = { tr.t0[0], tr.t0[1], tr.t0[2] };
@@ -224,21 +231,17 @@ __device__ __forceinline__ bool intersectTri(V3 o, V3 d, float tmin, float tmax,
     V3 e2 = { tr.t1[2], tr.t1[3], tr.t2[0] };
     V3 p = crossFma(d, e2);
     float det = dotFma3(e1, p);
-    if (det == 0.0f) return false;
     float inv = 1.0f / det;
     V3 s = o - v0;
     float u = dotFma3(s, p) * inv;
-    if (!(u >= 0.0f && u <= 1.0f)) return false;
     V3 q = crossFma(s, e1);
     float v = dotFma3(d, q) * inv;
-    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
     float tt = dotFma3(e2, q) * inv;
-    if (!(tt >= tmin && tt <= tmax)) return false;
     *outT = tt;
     *outU = u;
     *outV = v;
     *backfaceDet = det < 0.0f;
-    return true;
+    return (u >= 0.0f) & (v >= 0.0f) & (u + v <= 1.0f) & (tt >= tmin) & (tt <= tmax);
 }
 
 __device__ __forceinline__ GpuTriangle loadTri(const GpuTriangle* __restrict__ tris, uint32_t i)
@@ -385,12 +388,14 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     m = fx ? (((m & 0x00550055u) << 1) | ((m >> 1) & 0x00550055u)) : m;
     m = fy ? (((m & 0x00330033u) << 2) | ((m >> 2) & 0x00330033u)) : m;
     m = fz ? (((m & 0x000f000fu) << 4) | ((m >> 4) & 0x000f000fu)) : m;
-    // leaf children: their triangle rows (GpuBvh8Node: bit 8 i + s = triangle i of
-    // slot s), the hit slots replicated into the three rows and masked
+    // leaf children: their triangle rows (GpuBvh8Node: bit s + stride i = triangle
+    // i of leaf slot s), the hit leaf slots spread over the three rows and masked
     gBase = w1.x;
     gBits = (m & 0x00ff00ffu) | (imask << 8);
     tBase = w1.y;
-    tBits = ((hitSlots & ~imask & 0xffu) * 0x010101u) & w1.z;
+    const uint32_t stride = w1.w & 31u, leafHits = hitSlots & (w1.w >> 8) & 0xffu;
+    const uint32_t x = (leafHits << stride) | leafHits;
+    tBits = ((x << stride) | x) & w1.z;
 }
 
 __device__ __forceinline__ GpuTriangle triFromWords(uint4 a, uint4 b, uint4 c)
@@ -841,7 +846,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
 #endif
         // ---- one step: a pending leaf triangle and the next node -------------------
-        if (active && !done()) travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
+        // (an active lane is never done here: the check after the step retires or
+        // restarts it, and a step of a done lane would change nothing anyway)
+        if (active) travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
@@ -1547,11 +1554,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
         if (active) {
-            bool occluded = false;
-            if (!done()) {
-                RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-                occluded = travStepDual<kTraceBlock, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
-            }
+            // (a done lane - a root waiting for its helpers - steps as a no-op)
+            RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+            const bool occluded = travStepDual<kTraceBlock, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
             const bool helper = pass >= 256;
             const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
             if (occluded) {

@@ -32,21 +32,25 @@ constexpr int kMaxLeafSize = 1 << kLeafCountBits;
 // plane decodes EXACTLY in fp32 (one fma), and q is rounded outward, so a decoded
 // child box contains the (already inflated) BVH2 child box it replaces.
 //   w0..2  p.xyz            w3  e.x | e.y << 8 | e.z << 16 | imask << 24
-//   w4     child_base       w5  tri_base          w6  leaf_tris   w7  reserved (0)
+//   w4     child_base       w5  tri_base          w6  leaf_tris   w7  stride | leaf_mask << 8
 //   w8,9   qlo.x[8]         w10,11 qlo.y[8]       w12,13 qlo.z[8]
 //   w14,15 qhi.x[8]         w16,17 qhi.y[8]       w18,19 qhi.z[8]
 // Slot s of a node holds its child whose centre lies on the (s & 1 ? + : -) x,
 // (s & 2 ? + : -) y, (s & 4 ? + : -) z side of the node centre, as far as the
 // children allow, so visiting hit slots in increasing (s ^ rayOctant) order is
 // roughly front to back. imask bit s: internal child, stored at
-// child_base + popcount(imask & ((1 << s) - 1)). Leaf triangles in rows of 8:
-// bit 8 i + s of leaf_tris is the i-th triangle (i < kBvh8MaxLeafSize) of leaf
-// slot s, stored at tri_base + 8 i + s, so the triangles of a set H of hit leaf
-// slots are (H * 0x010101) & leaf_tris (two VALU; a per-slot offset/count code
-// cost ~40). Slot s is a leaf iff bit s is set. Rows of neighbouring nodes are
-// interleaved in the triangle array (first fit), so the positions an internal
-// slot leaves free are mostly used by other nodes' triangles; any position still
-// free is a hole record (kHoleInstance) that no leaf references.
+// child_base + popcount(imask & ((1 << s) - 1)). leaf_mask bit s: leaf child.
+// Leaf triangles in strided rows: triangle i (< kBvh8MaxLeafSize) of leaf slot s is
+// at tri_base + s + stride * i, and bit s + stride * i of leaf_tris marks it, so the
+// triangles of a set H of hit leaf slots are
+//     (H | H << stride | H << 2 stride) & leaf_tris
+// (three VALU; a per-slot offset/count code cost ~40). The builder picks the
+// smallest stride (1..8; 8 always works) for which no position s' + stride * i'
+// (i' < 3) of a leaf s' belongs to another slot's triangle, which keeps a node's
+// triangles close together (stride 8 for all nodes spread them over 24 records:
+// +42 % HBM traffic, profiles/r03_k). Nodes' rows interleave in the triangle array
+// (first fit), and a position nothing uses is a hole record (kHoleInstance) that no
+// leaf references.
 struct alignas(16) GpuBvh8Node {
     float p[3];
     uint8_t e[3];
@@ -54,14 +58,16 @@ struct alignas(16) GpuBvh8Node {
     uint32_t child_base;
     uint32_t tri_base;
     uint32_t leaf_tris;
-    uint32_t reserved;
+    uint8_t tri_stride;
+    uint8_t leaf_mask;
+    uint8_t pad[2];
     uint8_t qlo[3][8];
     uint8_t qhi[3][8];
 };
 static_assert(sizeof(GpuBvh8Node) == 80, "BVH8 node is 80 B");
 constexpr int kBvh8MaxLeafSize = 3;
-// triangles of leaf slot s within leaf_tris (bits s, s + 8, s + 16)
-inline constexpr uint32_t bvh8SlotTris(uint32_t leafTris, int s) { return leafTris & (0x010101u << s); }
+// the positions of leaf slot s's row (bits s, s + stride, s + 2 stride), unmasked
+inline constexpr uint32_t bvh8SlotRow(uint32_t stride, int s) { return (1u | 1u << stride | 1u << (2u * stride)) << s; }
 
 // World-space triangle record, 48 B = 3 x 16 B, in leaf order:
 //   t0 = (v0.x, v0.y, v0.z, e1.x)   t1 = (e1.y, e1.z, e2.x, e2.y)
