@@ -345,7 +345,8 @@ class RowPlacer {
 public:
     uint32_t place(uint32_t pattern)
     {
-        const uint32_t lo = m_end > kRowWindow ? m_end - kRowWindow : 0u;
+        static const uint32_t back = std::getenv("ARK_BVH8_ROW_WINDOW") ? static_cast<uint32_t>(std::atoi(std::getenv("ARK_BVH8_ROW_WINDOW"))) : kRowWindow;
+        const uint32_t lo = m_end > back ? m_end - back : 0u;
         for (uint32_t b = lo;; ++b)
             if ((window(b) & pattern) == 0) {
                 mark(b, pattern);

@@ -325,6 +325,10 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_NODE_INSIDE
 #define ARK_NODE_INSIDE 0 // 1: origin-containing children first, else plain octant order (40 VALU per node for +0.8 % node visits)
 #endif
+// LDS octant permutation table of the node visit (loadNodeCache fills it; every
+// kernel that visits nodes calls loadNodeCache first)
+__shared__ uint8_t g_octPerm[8 * 256];
+
 #if ARK_MASK_ADDC
 // m << 1 | (a <= b) in two VALU: the compare writes VCC and v_addc adds it in as the
 // carry (m + m + carry); an unordered compare (NaN) shifts in 0, as `<=` does
@@ -380,14 +384,21 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         if (ARK_NODE_INSIDE) insideLo |= (tn <= tmin ? 1u : 0u) << s;
 #endif
     }
+    // internal children: slot bits -> visiting order bits (k = slot ^ oct)
+#if ARK_NODE_INSIDE
+    // by swapping bit pairs / pairs of pairs / nibbles per octant bit (hit and
+    // inside masks permuted together: bits 0-7 and 16-23)
     const uint32_t insideSlots = insideLo << 16;
-    // internal children: slot bits -> visiting order bits (k = slot ^ oct), by
-    // swapping bit pairs / pairs of pairs / nibbles per octant bit
-    // (hit and inside masks permuted together: bits 0-7 and 16-23)
     uint32_t m = (hitSlots & imask) | (insideSlots & (hitSlots << 16) & (imask << 16));
     m = fx ? (((m & 0x00550055u) << 1) | ((m >> 1) & 0x00550055u)) : m;
     m = fy ? (((m & 0x00330033u) << 2) | ((m >> 2) & 0x00330033u)) : m;
     m = fz ? (((m & 0x000f000fu) << 4) | ((m >> 4) & 0x000f000fu)) : m;
+#else
+    // one LDS byte (g_octPerm, filled by loadNodeCache) instead of the three
+    // conditional swap stages (15 VALU)
+    (void)insideLo;
+    const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
+#endif
     // leaf children: their triangle rows (GpuBvh8Node: bit s + stride i = triangle
     // i of leaf slot s), the hit leaf slots spread over the three rows and masked
     gBase = w1.x;
@@ -450,6 +461,14 @@ __device__ __forceinline__ NodeCache loadNodeCache(const SceneArgs& sc, uint4* l
         nc.count = min(static_cast<uint32_t>(NODES), sc.opaque_nodes);
         const uint4* src = reinterpret_cast<const uint4*>(sc.nodes + nc.base);
         for (uint32_t i = threadIdx.x; i < nc.count * 5u; i += BLOCK) lds[i] = src[i];
+    }
+    // octant permutation table of visitNode8: entry (oct << 8 | m) has bit k set iff
+    // bit k ^ oct of m is set
+    for (uint32_t i = threadIdx.x; i < 8u * 256u; i += BLOCK) {
+        const uint32_t oct = i >> 8, m = i & 0xffu;
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < 8u; ++k) r |= ((m >> (k ^ oct)) & 1u) << k;
+        g_octPerm[i] = static_cast<uint8_t>(r);
     }
     __syncthreads();
     return nc;
