@@ -663,10 +663,17 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             float score;
             int c, s;
         };
+        // Internal children take their octant slots first; leaf children only decide
+        // which triangles a hit slot adds (their order does not matter), so they fill
+        // the remaining slots in ascending order, most triangles first, which keeps a
+        // node's triangle rows compact (leafRowStride). ARK_BVH8_LEAF_SLOTS=octant:
+        // leaves compete for octant slots like internal children (A/B).
+        static const bool leafOctant = std::getenv("ARK_BVH8_LEAF_SLOTS") && std::strcmp(std::getenv("ARK_BVH8_LEAF_SLOTS"), "octant") == 0;
         Cand cand[64];
         int nc = 0;
         for (int c = 0; c < n; ++c)
             for (int s = 0; s < 8; ++s) {
+                if (!leafOctant && ch[c].code < 0) break;
                 float sc = 0.0f;
                 for (int a = 0; a < 3; ++a) {
                     const float off = 0.5f * (ch[c].box.lo[a] + ch[c].box.hi[a]) - pc[a];
@@ -682,6 +689,19 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
                 slotOf[cand[k].c] = cand[k].s;
                 childIn[cand[k].s] = cand[k].c;
             }
+        if (!leafOctant) {
+            int leaves[8], nl = 0;
+            for (int c = 0; c < n; ++c)
+                if (ch[c].code < 0) leaves[nl++] = c;
+            auto cnt = [&](int c) { return (static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1u; };
+            std::stable_sort(leaves, leaves + nl, [&](int a, int b) { return cnt(a) > cnt(b); });
+            int sl = 0;
+            for (int i = 0; i < nl; ++i) {
+                while (childIn[sl] >= 0) ++sl;
+                slotOf[leaves[i]] = sl;
+                childIn[sl] = leaves[i];
+            }
+        }
         // quantization grid of this node
         GpuBvh8Node nd;
         std::memset(&nd, 0, sizeof(nd));
