@@ -17,8 +17,13 @@ namespace ark {
 // 64 top nodes (5 KB of LDS per traversal workgroup instead of 10): the traversal itself
 // is unchanged (2.29-2.35 ms serially), but with frames in flight the previous frame's
 // kernels find LDS beside it: C4 step 4.06 -> 4.00 ms (128 -> 64; 32: 3.98 ms but the
-// reference windows 1 % slower; stack entries 4 instead of 8 spill: +6 %), profiles/r02_m22-23
-#define ARK_LDS_NODES 64
+// reference windows 1 % slower; stack entries 4 instead of 8 spill: +6 %), profiles/r02_m22-23.
+// Round 3 added the 2 KB octant table (g_octPerm) to every traversal workgroup; 48 nodes
+// bring the workgroup back to about round 2's 21 KB: C4 2,277 -> 2,312 Mrays/s in two
+// 10-step A/B runs (32 / 40 / 56 nodes alike, 7 waves/SIMD at 72 VGPRs spills and loses
+// 5 %), 2,224 -> 2,246 at the bench's 20 steps; windows and Z-slab proxy within noise
+// (profiles/r03_q, r03_r, r03_s)
+#define ARK_LDS_NODES 48
 #endif
 constexpr int kStackLds = ARK_STACK_LDS; // traversal stack entries (node groups, 2 words) per lane kept in LDS (power of 2)
 constexpr int kTraceBlock = 256;

@@ -2122,9 +2122,15 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
 // Dual-step traversal at 6 waves/SIMD (80 VGPRs): the only spills (4 VGPRs) sit in
 // the masked pass's alpha test. C4: 2.39 ms, against 2.51 at 5 waves (96 VGPRs, no
 // spill) and 2.65 for one step per iteration at 6 waves.
+#ifndef ARK_TRACE_WPE
+#define ARK_TRACE_WPE 6
+#endif
+#ifndef ARK_SHADOW_WPE
+#define ARK_SHADOW_WPE 6
+#endif
 const void* kernel_trace_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, 6>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, ARK_TRACE_WPE>);
 }
 
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
@@ -2197,7 +2203,7 @@ const void* kernel_shade_ptr(bool count)
 
 const void* kernel_trace_shadow_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, 6>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE>);
 }
 
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s)
