@@ -192,6 +192,21 @@ struct ArkDdgiCtx {
     hipStream_t traceStream = nullptr;
     hipEvent_t evTraced = nullptr, evFrameDone[2] = {};
     bool frameDoneValid[2] = { false, false };
+    // Device-side frame sequencing of pipelined frames (k_seq_signal / k_seq_wait
+    // instead of cross-queue event waits): seqWords [0] = the last frame whose
+    // traversal-stream part (slot table, traversal, offsets) is done, [32] = the last
+    // frame whose caller-stream part is done, [64] = a wait timed out (a signal folded
+    // into the last kernel - its last workgroup storing the word after a device-scope
+    // fence per workgroup - measured slower: the fences write back L2, K = 2048 frames
+    // 0.371 -> 0.387 ms, profiles/r03_y). setSeq[b] = the
+    // frame that last used buffer set b, when that frame was sequenced this way
+    // (else its evFrameDone[b] is recorded). ARK_DDGI_SEQ_SYNC=0: events throughout.
+    bool seqSync = true;
+    DeviceBuffer seqWords;
+    uint32_t frameSeq = 0;
+    uint32_t setSeq[2] = { 0, 0 };
+    bool setSeqValid[2] = { false, false };
+    uint64_t seqTimeoutTicks = 0;
     uint32_t lastParity = 0;       // buffer set of the last update (debug hit records)
     uint32_t fibR[2] = { 0, 0 };
     uint64_t spillRegionWords = 0; // spill region 1 = the primary traversal's
@@ -475,6 +490,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
+        if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
         // ARK_SHADOW_BIN_GRID: light-space cells per axis of the shadow-ray binning
         // (a power of 2 up to 256), 0 = the list in queue order
         if (const char* g = std::getenv("ARK_SHADOW_BIN_GRID")) {
@@ -484,9 +500,13 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* m = std::getenv("ARK_SHADOW_BIN_MIN_RAYS")) ctx->shadowBinMinRays = static_cast<uint32_t>(std::max(0, std::atoi(m)));
     }
     if ((e = hipStreamCreateWithFlags(&ctx->traceStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-    if ((e = hipEventCreateWithFlags(&ctx->evTraced, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    // stream-order events of the frames in flight (ARK_SYNC_EVENT_FLAGS: extra
+    // hipEventCreateWithFlags flags, for A/B runs of the release scope)
+    unsigned syncFlags = hipEventDisableTiming;
+    if (const char* ef = std::getenv("ARK_SYNC_EVENT_FLAGS")) syncFlags |= static_cast<unsigned>(std::strtoul(ef, nullptr, 0));
+    if ((e = hipEventCreateWithFlags(&ctx->evTraced, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->evFrameDone)
-        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+        if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t K = static_cast<size_t>(ctx->Kmax), R = static_cast<size_t>(ctx->Rmax);
@@ -502,6 +522,14 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
     if ((e = ctx->rayCounter.alloc(2 * kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
+    if ((e = ctx->seqWords.alloc(96 * 4)) != hipSuccess) return bad(e, "alloc sequence words");
+    if ((e = hipMemset(ctx->seqWords.ptr, 0, ctx->seqWords.bytes)) != hipSuccess) return bad(e, "clear sequence words");
+    {
+        // k_seq_wait's bound: 10 s of the device wall clock (kHz attribute)
+        int rateKhz = 0;
+        if (hipDeviceGetAttribute(&rateKhz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || rateKhz <= 0) rateKhz = 100000;
+        ctx->seqTimeoutTicks = static_cast<uint64_t>(rateKhz) * 1000ull * 10ull;
+    }
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0, occW = 0;
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
@@ -533,7 +561,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->shadeWork, &ctx->reflWork,
+    for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->seqWords, &ctx->shadeWork, &ctx->reflWork,
                              &ctx->raySteps, &ctx->counters, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
         b->release();
     ctx->sceneStore.reset();
@@ -879,6 +907,19 @@ int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, voi
     return updateImpl(ctx, p, hipStream, shadeWaitEvent, doneEvent);
 }
 
+// The caller's stream s waits for the traversal stream's part of a pipelined frame
+// (slot table, traversal, offsets): device-side sequencing, or an event.
+static hipError_t tracedSync(ArkDdgiCtx* ctx, bool seq, uint32_t seqN, hipStream_t ts, hipStream_t s)
+{
+    if (seq) {
+        uint32_t* w = ctx->seqWords.as<uint32_t>();
+        hipError_t e = launch_seq_signal(w, seqN, ts);
+        return e != hipSuccess ? e : launch_seq_wait(w, seqN, w + 64, ctx->seqTimeoutTicks, s);
+    }
+    hipError_t e = hipEventRecord(ctx->evTraced, ts);
+    return e != hipSuccess ? e : hipStreamWaitEvent(s, ctx->evTraced, 0);
+}
+
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
@@ -978,11 +1019,17 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     // the slot table and the primary traversal: on traceStream after frame n - 2 (the
     // last user of buffer set b) when pipelined, else in line on the caller's stream
     const hipStream_t ts = pipe ? ctx->traceStream : s;
-    if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
+    uint32_t* seqTrace = ctx->seqWords.as<uint32_t>();
+    uint32_t* seqMain = seqTrace + 32;
+    uint32_t* seqTimedOut = seqTrace + 64;
+    const bool seq = pipe && ctx->seqSync;
+    const uint32_t seqN = seq ? ++ctx->frameSeq : 0u;
+    if (pipe && ctx->setSeqValid[b]) ARK_HIP(launch_seq_wait(seqMain, ctx->setSeq[b], seqTimedOut, ctx->seqTimeoutTicks, ts));
+    else if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
     // a serial previous frame wrote its offsets on the caller's stream
     if (pipe && !ctx->prevPipelined && ctx->frameDoneValid[b ^ 1u]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b ^ 1u], 0));
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
-    ARK_HIP(hipMemsetAsync(f.ray_counter, 0, kRayCounterWords * 4, ts));
+    // (k_probe_slots zeroes f.ray_counter)
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
     f.slot_order = ctx->slotOrder.as<uint32_t>() + b * Kmax; // written by k_probe_slots
     ARK_HIP(launch_probe_slots(f, ts));
@@ -992,10 +1039,12 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         ARK_HIP(launch_trace(ctx->scene, f, half ? ctx->pipeTraceBlocks : ctx->traceBlocks, count, ts));
         if (pipe) {
             // probeUpdateOffset (k_probe_offsets: from the hit records), so that the
-            // next frame's slot table may follow on this stream
+            // next frame's slot table may follow on this stream. The rest of the frame
+            // needs only the hit records, but waiting for the offsets too costs less
+            // (7 us) than a second cross-stream wait for them at the end of the frame
+            // (each wait ~11 us of queue latency, satisfied or not: profiles/r03_v)
             ARK_HIP(launch_probe_offsets(f, ts));
-            ARK_HIP(hipEventRecord(ctx->evTraced, ts));
-            ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
+            ARK_HIP(tracedSync(ctx, seq, seqN, ts, s));
         }
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[1], s));
         FrameArgs fs = f;
@@ -1018,10 +1067,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         if (!pipe) ARK_HIP(launch_probe_offsets(fs, s));
         ARK_HIP(launch_probe_update(fs, s));
     } else {
-        if (pipe) {
-            ARK_HIP(hipEventRecord(ctx->evTraced, ts));
-            ARK_HIP(hipStreamWaitEvent(s, ctx->evTraced, 0));
-        }
+        if (pipe) ARK_HIP(tracedSync(ctx, seq, seqN, ts, s));
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
@@ -1031,7 +1077,14 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         }
     }
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[3], s));
-    ARK_HIP(hipEventRecord(ctx->evFrameDone[b], s));
+    if (seq) {
+        ARK_HIP(launch_seq_signal(seqMain, seqN, s));
+        ctx->setSeq[b] = seqN;
+        ctx->setSeqValid[b] = true;
+    } else {
+        ARK_HIP(hipEventRecord(ctx->evFrameDone[b], s));
+        ctx->setSeqValid[b] = false;
+    }
     ctx->frameDoneValid[b] = true;
     if (doneEvent) ARK_HIP(hipEventRecord(static_cast<hipEvent_t>(doneEvent), s));
     ARK_HIP(orderEnd(ctx, s));
@@ -1060,6 +1113,9 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
+    uint32_t timedOut = 0;
+    ARK_HIP(hipMemcpy(&timedOut, ctx->seqWords.as<uint32_t>() + 64, 4, hipMemcpyDeviceToHost));
+    if (timedOut) return ctx->fail(ARK_DDGI_E_DEVICE, "a frame-sequencing wait between the context's streams timed out (10 s)");
     return ARK_DDGI_OK;
 }
 

@@ -267,6 +267,9 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
+// frame sequencing between two streams of one context (k_seq_signal / k_seq_wait)
+hipError_t launch_seq_signal(uint32_t* word, uint32_t value, hipStream_t s);
+hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint64_t timeoutTicks, hipStream_t s);
 const void* kernel_trace_ptr(bool count);
 const void* kernel_shade_ptr(bool count);
 const void* kernel_trace_shadow_ptr(bool count);

@@ -123,6 +123,9 @@ __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
     const uint32_t X = static_cast<uint32_t>(f.X), Y = static_cast<uint32_t>(f.Y), Z = static_cast<uint32_t>(f.Z);
     const uint32_t N = X * Y * Z;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    // this frame's work counters (trace / shadow heads, shadow-list count): zeroed here
+    // rather than by a separate fill ahead of this kernel on the traversal stream
+    for (uint32_t i = tid; i < kRayCounterWords; i += gridDim.x * blockDim.x) f.ray_counter[i] = 0u;
     if (tid < f.R) {
         V3 d = sphericalFibonacciSample(tid, f.R);
         f.fib[tid] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -1825,6 +1828,33 @@ __global__ void __launch_bounds__(256) k_shadow_scatter(FrameArgs f)
         f.shadow_rays[f.shadow_bin_start[f.shadow_bin_key[i]] + f.shadow_bin_rank[i]] = f.shadow_rays_gen[i];
 }
 
+// Frame sequencing between a context's two streams (ark_ddgi.cpp updateImpl): the
+// producer stream ends its part of frame n with k_seq_signal (word = n, a release
+// store after the kernels before it on that stream), the consumer stream starts with
+// k_seq_wait (one wave polls the word with acquire loads until it reaches n). A
+// cross-queue event wait costs 12-16 us of queue latency per frame, satisfied or not
+// (profiles/r03_v, r03_w); this pair costs two one-wave launches. Every wait ends:
+// the word is written by work enqueued earlier on the other stream, which nothing
+// blocks; after timeout_ticks of the wall clock the wave sets *timed_out and returns
+// (ark_ddgi_synchronize reports it).
+__global__ void __launch_bounds__(64) k_seq_signal(uint32_t* word, uint32_t value)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(64) k_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timed_out, uint64_t timeout_ticks)
+{
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    while (static_cast<int32_t>(__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - value) < 0) {
+        if (wall_clock64() - t0 > timeout_ticks) {
+            atomicOr(timed_out, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // Atlas clears (DDGINode.cpp:50-55) as 32-bit fills.
 __global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t value)
 {
@@ -2184,6 +2214,18 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
         const uint32_t sblocks = static_cast<uint32_t>(std::min<uint64_t>((worst + 255u) / 256u, 2048u));
         hipLaunchKernelGGL(dev::k_shadow_scatter, dim3(sblocks), dim3(256), 0, s, f);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_signal(uint32_t* word, uint32_t value, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_seq_signal, dim3(1), dim3(64), 0, s, word, value);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint64_t timeoutTicks, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_seq_wait, dim3(1), dim3(64), 0, s, word, value, timedOut, timeoutTicks);
     return hipGetLastError();
 }
 

@@ -362,77 +362,90 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
 // rounded to fp16 as the surfel stores it (raygen.rgen:108-139). So this kernel runs
 // right after the traversal, and with frames in flight the next frame's slot table
 // and traversal follow it on the traversal stream (ark_ddgi.cpp updateImpl).
-// 10 probes per workgroup: 256 threads stage the hit distances' classes (each
-// thread's loads in flight together), then one wave sums, 6 lanes per probe: lane c
-// sums component c % 3 of the directions of the rays of class 1 (near front face,
-// c < 3) or 2 (back face) in ray order, as the shader's loop does (adding +0 for the
-// other rays leaves a sum unchanged), and counts them.
-constexpr int kOffsetProbes = 10;
+// P probes per workgroup (P * R = 1,024 summands per kind). Phase 1, all 256 threads
+// (their hit loads in flight together): each ray's class and rotated direction give
+// the six summands of its probe's sums - direction component c % 3 of a class-1 ray
+// (near front face, c < 3) or a class-2 ray (back face), +0 for the others, exactly the
+// `m ? v : 0` the sum adds - staged in LDS, and the class counts (LDS atomics). Phase 2:
+// lane 6q + c adds its summands in ray order, as the shader's loop does, one LDS read and
+// one add per ray. (Until round 3 the summing lanes also rotated every direction
+// themselves: 256 dependent iterations of ~35 VALU on one wave, 31 us per launch even
+// for 2,048 probes, on the traversal stream's critical path.)
 constexpr int kOffsetBlock = 256;
+
+__host__ __device__ __forceinline__ uint32_t offsetProbesPerBlock(uint32_t R)
+{
+    const uint32_t p = R ? 1024u / R : 1u;
+    return p < 1u ? 1u : (p > 32u ? 32u : p);
+}
 
 __global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t R = f.R;
-    float4* fibL = reinterpret_cast<float4*>(smem); // [R]
-    uint8_t* clsL = smem + R * sizeof(float4);       // [kOffsetProbes][R]
-    const uint32_t lane = threadIdx.x;
-    const uint32_t slot0 = blockIdx.x * kOffsetProbes;
+    const uint32_t P = offsetProbesPerBlock(R);
+    const uint32_t stride = 6u * R + 8u; // floats per probe: +8 puts the probes' rows on different LDS banks
+    float* valL = reinterpret_cast<float*>(smem);               // [P][R][6] summands
+    float* sumL = valL + P * stride;                              // [P][6] sums
+    uint32_t* cntL = reinterpret_cast<uint32_t*>(sumL + 6u * P);  // [P][2] class-1 / class-2 counts
+    const uint32_t tid = threadIdx.x;
+    const uint32_t slot0 = blockIdx.x * P;
     const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
     const float maxOffset = minAxialSpacing / 2.0f;
-    for (uint32_t s = lane; s < R; s += kOffsetBlock) fibL[s] = f.fib[s];
+    for (uint32_t i = tid; i < 2u * P; i += kOffsetBlock) cntL[i] = 0u;
+    __syncthreads();
     // 4 records per thread in flight at once
     constexpr uint32_t kBatch = 4;
-    for (uint32_t i0 = 0; i0 < kOffsetProbes * R; i0 += kBatch * kOffsetBlock) {
+    for (uint32_t i0 = 0; i0 < P * R; i0 += kBatch * kOffsetBlock) {
         GpuHit h[kBatch];
+        float4 fb[kBatch];
         bool ok[kBatch];
 #pragma unroll
         for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t i = i0 + k * kOffsetBlock + lane;
+            const uint32_t i = i0 + k * kOffsetBlock + tid;
             const uint32_t p = i / R, s = i - p * R;
-            ok[k] = i < kOffsetProbes * R && slot0 + p < f.window_probes;
-            if (ok[k]) h[k] = f.hits[static_cast<size_t>(slot0 + p) * R + s];
+            ok[k] = i < P * R && slot0 + p < f.window_probes;
+            if (ok[k]) {
+                h[k] = f.hits[static_cast<size_t>(slot0 + p) * R + s];
+                fb[k] = f.fib[s];
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t i = i0 + k * kOffsetBlock + lane;
-            if (i >= kOffsetProbes * R) continue;
-            uint8_t cls = 0;
-            if (ok[k]) {
-                // the surfel's distance (k_shade: miss, back face, front face)
-                const float dist = h[k].tri == kNoHit ? f.z_far : (h[k].t < 0.0f ? h[k].t * 0.2f : h[k].t);
-                const float a = f16_to_f32(f32_to_f16(dist));
-                cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
-            }
-            clsL[i] = cls;
+            if (!ok[k]) continue;
+            const uint32_t i = i0 + k * kOffsetBlock + tid;
+            const uint32_t p = i / R, s = i - p * R;
+            // the surfel's distance (k_shade: miss, back face, front face)
+            const float dist = h[k].tri == kNoHit ? f.z_far : (h[k].t < 0.0f ? h[k].t * 0.2f : h[k].t);
+            const float a = f16_to_f32(f32_to_f16(dist));
+            const uint32_t cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
+            const GpuProbeSlot& ps = f.slots[slot0 + p];
+            const V3 d = rotate(v3(fb[k].x, fb[k].y, fb[k].z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
+            float* v = valL + p * stride + 6u * s;
+            v[0] = cls == 1u ? d.x : 0.0f;
+            v[1] = cls == 1u ? d.y : 0.0f;
+            v[2] = cls == 1u ? d.z : 0.0f;
+            v[3] = cls == 2u ? d.x : 0.0f;
+            v[4] = cls == 2u ? d.y : 0.0f;
+            v[5] = cls == 2u ? d.z : 0.0f;
+            if (cls) atomicAdd(cntL + 2u * p + (cls - 1u), 1u);
         }
     }
     __syncthreads();
-    if (lane >= 64) return;
-    const uint32_t q = lane / 6, c = lane % 6;
-    const uint32_t slot = slot0 + q;
-    const bool live = lane < 6 * kOffsetProbes && slot < f.window_probes;
-    float acc = 0.0f;
-    uint32_t cnt = 0;
-    if (live) {
-        const GpuProbeSlot ps = f.slots[slot];
-        const uint8_t want = c < 3 ? 1u : 2u;
-        const uint32_t comp = c % 3;
-        const uint8_t* cl = clsL + q * R;
-        for (uint32_t s = 0; s < R; ++s) {
-            const float4 fb = fibL[s];
-            const V3 d = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
-            const float v = comp == 0 ? d.x : (comp == 1 ? d.y : d.z);
-            const bool m = cl[s] == want;
-            acc += m ? v : 0.0f;
-            cnt += m ? 1u : 0u;
-        }
+    if (tid < 6u * P && slot0 + tid / 6u < f.window_probes) {
+        const float* v = valL + (tid / 6u) * stride + tid % 6u;
+        float acc = 0.0f;
+#pragma unroll 8
+        for (uint32_t s = 0; s < R; ++s) acc += v[6u * s];
+        sumL[tid] = acc;
     }
-    const int b = static_cast<int>(6 * (lane < 6 * kOffsetProbes ? q : 0));
-    const V3 accumNearFrontfaceDir = v3(__shfl(acc, b + 0), __shfl(acc, b + 1), __shfl(acc, b + 2));
-    const V3 accumBackfaceDir = v3(__shfl(acc, b + 3), __shfl(acc, b + 4), __shfl(acc, b + 5));
-    const uint32_t nc = __shfl(cnt, b + 0), bc = __shfl(cnt, b + 3);
-    if (live && c == 0) {
+    __syncthreads();
+    const uint32_t slot = slot0 + tid;
+    if (tid < P && slot < f.window_probes) {
+        const float* sm = sumL + 6u * tid;
+        const V3 accumNearFrontfaceDir = v3(sm[0], sm[1], sm[2]);
+        const V3 accumBackfaceDir = v3(sm[3], sm[4], sm[5]);
+        const uint32_t nc = cntL[2u * tid], bc = cntL[2u * tid + 1u];
         const uint32_t probeIdx = f.slots[slot].probe_index;
         float4 cur = f.offsets[probeIdx];
         V3 currentOffset = v3(cur.x, cur.y, cur.z);
@@ -456,8 +469,15 @@ __global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
 hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s)
 {
     if (f.window_probes == 0 || !f.update_offsets) return hipSuccess;
-    const uint32_t blocks = (f.window_probes + dev::kOffsetProbes - 1) / dev::kOffsetProbes;
-    const size_t lds = static_cast<size_t>(f.R) * (sizeof(float4) + dev::kOffsetProbes);
+    const uint32_t P = dev::offsetProbesPerBlock(f.R);
+    const uint32_t blocks = (f.window_probes + P - 1) / P;
+    const size_t lds = sizeof(float) * (static_cast<size_t>(P) * (6u * f.R + 8u) + 6u * P) + sizeof(uint32_t) * 2u * P;
+    static size_t lds_set = 0;
+    if (lds > 65536 && lds > lds_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::k_probe_offsets), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        if (e != hipSuccess) return e;
+        lds_set = lds;
+    }
     hipLaunchKernelGGL(dev::k_probe_offsets, dim3(blocks), dim3(dev::kOffsetBlock), lds, s, f);
     return hipGetLastError();
 }

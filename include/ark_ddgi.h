@@ -312,12 +312,17 @@ int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src);
  * completion still means the update is complete. A caller that writes probe offsets
  * through device pointers (ark_ddgi_get_device_views) between updates calls
  * ark_ddgi_mark_external_write after enqueueing that write: the next update then runs
- * serially, after it. Instrumented updates (timing, counting) run serially. */
+ * serially, after it. Instrumented updates (timing, counting) run serially. The two
+ * streams hand a pipelined frame over by device-side sequence words (a one-wave
+ * signal and a one-wave bounded wait per direction) instead of cross-queue events. */
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
 /* The caller wrote context resources through device pointers (probe offsets, atlases)
  * on the stream of the next update: that update waits for the write instead of
  * starting its traversal on the internal stream (see Frames in flight above). */
 int ark_ddgi_mark_external_write(ArkDdgiCtx* ctx);
+/* Waits for all work of the device; ARK_DDGI_E_DEVICE if a frame-sequencing wait
+ * between the context's streams gave up after 10 s (its frame's results are then
+ * unspecified). */
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 
 /* ark_ddgi_update for a Z-slab rank that overlaps the atlas exchange with the next
