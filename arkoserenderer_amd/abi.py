@@ -404,6 +404,9 @@ EXPORTS = {
     "ark_ddgi_update": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
     "ark_ddgi_synchronize": (C.c_int, [C.c_void_p]),
     "ark_ddgi_update_overlapped": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "ark_ddgi_update_exchanged": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
+    "ark_ddgi_exchange_begin": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ark_ddgi_exchange_end": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ark_ddgi_resource_size": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "ark_ddgi_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "ark_ddgi_write": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),

@@ -61,6 +61,110 @@ class SlabExchange:
             dist.all_gather_into_tensor(full, mine, group=self.group)
 
 
+class RcclBandExchange:
+    """The same in-place all-gather of the two atlas bands, issued straight to RCCL
+    (ncclGroupStart; ncclAllGather x 2; ncclGroupEnd) on the caller's current stream,
+    through a communicator of its own (ncclCommInitRank; the ncclUniqueId travels over
+    the torch.distributed group). torch's ProcessGroupNCCL runs a collective on its
+    internal stream behind an event wait each way; on MI355X every cross-queue wait
+    costs 12-16 us of queue latency, and both bands in one group halve the launches.
+    The C++ node's RcclSlabExchange (SlabExchange.cpp) issues the same group."""
+
+    NCCL_UINT8 = 1  # ncclDataType_t
+
+    def __init__(self, buffers, rank: int, world: int, group=None):
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        self.rank, self.world = rank, world
+        self.bufs = []
+        for full, off, slab in buffers:
+            assert slab * world == full.numel() and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
+            self.bufs.append((full.data_ptr(), full.data_ptr() + off, slab))
+        lib = _rccl()
+        uid = _NcclUniqueId()
+        if rank == 0:
+            _nccl_check(lib.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+        t = torch.tensor(list(bytes(uid.internal)), dtype=torch.uint8, device=buffers[0][0].device)
+        dist.broadcast(t, 0, group=group)
+        uid = _NcclUniqueId((C.c_uint8 * 128)(*t.cpu().tolist()))
+        self.comm = C.c_void_p()
+        _nccl_check(lib.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+        self.lib = lib
+
+    from_views = classmethod(SlabExchange.from_views.__func__)
+
+    def exchange(self):
+        import ctypes as C
+
+        import torch
+
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        lib = self.lib
+        _nccl_check(lib.ncclGroupStart(), "ncclGroupStart")
+        for full, mine, n in self.bufs:
+            _nccl_check(lib.ncclAllGather(C.c_void_p(mine), C.c_void_p(full), C.c_size_t(n), self.NCCL_UINT8, self.comm, s), "ncclAllGather")
+        _nccl_check(lib.ncclGroupEnd(), "ncclGroupEnd")
+
+    def async_error(self) -> int:
+        import ctypes as C
+
+        err = C.c_int(0)
+        rc = self.lib.ncclCommGetAsyncError(self.comm, C.byref(err))
+        return rc if rc != 0 else (err.value if err.value != 7 else 0)
+
+    def abort(self):
+        if self.comm:
+            self.lib.ncclCommAbort(self.comm)
+            self.comm = None
+
+    def close(self):
+        if self.comm:
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm = None
+
+
+def _nccl_unique_id_type():
+    import ctypes as C
+
+    class NcclUniqueId(C.Structure):  # ncclUniqueId: 128 opaque bytes, passed by value
+        _fields_ = [("internal", C.c_uint8 * 128)]
+
+    return NcclUniqueId
+
+
+_NcclUniqueId = _nccl_unique_id_type()
+
+
+def _rccl():
+    """The librccl.so torch already loaded (dlopen by soname returns that instance)."""
+    import ctypes as C
+
+    global _RCCL
+    if _RCCL is None:
+        _RCCL = C.CDLL("librccl.so")
+    lib = _RCCL
+    if not getattr(lib, "_ark_typed", False):
+        lib.ncclCommGetAsyncError.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        lib.ncclCommGetAsyncError.restype = C.c_int
+        lib.ncclGetUniqueId.argtypes = [C.POINTER(_NcclUniqueId)]
+        lib.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, _NcclUniqueId, C.c_int]
+        lib.ncclAllGather.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p]
+        lib.ncclCommAbort.argtypes = [C.c_void_p]
+        lib.ncclCommDestroy.argtypes = [C.c_void_p]
+        for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd", "ncclCommAbort", "ncclCommDestroy"):
+            getattr(lib, fn).restype = C.c_int
+        lib._ark_typed = True
+    return lib
+
+
+def _nccl_check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: ncclResult {rc}")
+
+
 EXCHANGE_FAILURE_EXIT_CODE = 14  # as the C++ ExchangeWatchdog (SlabExchange.h)
 
 
@@ -80,13 +184,9 @@ def _rccl_async_error(group) -> int:
         return 0
     if not comm:
         return 0
-    global _RCCL
-    if _RCCL is None:
-        _RCCL = C.CDLL("librccl.so")
-        _RCCL.ncclCommGetAsyncError.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
-        _RCCL.ncclCommGetAsyncError.restype = C.c_int
+    lib = _rccl()
     err = C.c_int(0)
-    rc = _RCCL.ncclCommGetAsyncError(C.c_void_p(comm), C.byref(err))
+    rc = lib.ncclCommGetAsyncError(C.c_void_p(comm), C.byref(err))
     # ncclInProgress (7) is a non-blocking communicator still initialising: not an error
     return rc if rc != 0 else (err.value if err.value != 7 else 0)
 
@@ -105,12 +205,13 @@ class ExchangeWatchdog:
     re-exec. A dead peer would otherwise hang every rank: the next frame's shading
     waits for the all-gather on the device and the host blocks at its next sync."""
 
-    def __init__(self, timeout_s: float | None = None, group=None, on_failure=None):
+    def __init__(self, timeout_s: float | None = None, group=None, on_failure=None, rccl=None):
         import os
 
         if timeout_s is None or timeout_s <= 0:
             timeout_s = float(os.environ.get("ARK_EXCHANGE_TIMEOUT_S", "0") or 0) or 120.0
         self.timeout_s, self.group = float(timeout_s), group
+        self.rccl = rccl  # a RcclBandExchange: its own communicator is polled and aborted too
         self.on_failure = on_failure or self.abort_and_exit
 
     def wait(self, event, what: str) -> bool:
@@ -119,7 +220,7 @@ class ExchangeWatchdog:
         t0 = time.monotonic()
         pause = 1e-5
         while not event.query():
-            err = _rccl_async_error(self.group)
+            err = _rccl_async_error(self.group) or (self.rccl.async_error() if self.rccl is not None else 0)
             if err:
                 self.on_failure(f"{what}: communicator error {err}")
                 return False
@@ -140,6 +241,8 @@ class ExchangeWatchdog:
         import torch.distributed as dist
 
         try:
+            if self.rccl is not None:
+                self.rccl.abort()
             if dist.is_initialized():
                 dist.distributed_c10d._abort_process_group(self.group)
         finally:
@@ -165,11 +268,22 @@ class OverlappedSlabExchange:
 
     RING = 3
 
-    def __init__(self, node, exchange, device, watchdog: ExchangeWatchdog | None = None):
+    def __init__(self, node, exchange, device, watchdog: ExchangeWatchdog | None = None, device_seq: bool | None = None):
+        """exchange: a callable that enqueues the all-gather on the current stream.
+        device_seq (default: on unless ARK_DDGI_SEQ_SYNC=0): the handovers between the
+        update stream and the exchange stream are the context's device-side sequence
+        words (ark_ddgi_update_exchanged / ark_ddgi_exchange_begin / _end) instead of
+        torch events; the events below then only bound the host."""
+        import os
+
         import torch
 
         self.node, self.exchange = node, exchange
-        self.watchdog = watchdog or ExchangeWatchdog()
+        if device_seq is None:
+            device_seq = os.environ.get("ARK_DDGI_SEQ_SYNC", "1") != "0"
+        self.device_seq = device_seq
+        owner = getattr(exchange, "__self__", None)  # a bound RcclBandExchange.exchange: watch its communicator
+        self.watchdog = watchdog or ExchangeWatchdog(rccl=owner if isinstance(owner, RcclBandExchange) else None)
         self.comm = torch.cuda.Stream(device)
         self.updated = torch.cuda.Event()
         # completion of frame n's all-gather in slot n % RING
@@ -189,11 +303,20 @@ class OverlappedSlabExchange:
         slot = self.gathered[self.frames % self.RING]
         if self.frames >= self.RING and not self.watchdog.wait(slot, f"slab exchange frame n-{self.RING}"):
             return None
-        p = self.node.execute_overlapped(app, stream_ptr, wait, self.updated.cuda_event)
-        with torch.cuda.stream(self.comm):
-            self.comm.wait_event(self.updated)
-            self.exchange()
-            slot.record(self.comm)
+        if self.device_seq:
+            ctx = self.node.ctx
+            p = self.node.execute_exchanged(app, stream_ptr)
+            with torch.cuda.stream(self.comm):
+                ctx.exchange_begin(self.comm.cuda_stream)
+                self.exchange()
+                ctx.exchange_end(self.comm.cuda_stream)
+                slot.record(self.comm)
+        else:
+            p = self.node.execute_overlapped(app, stream_ptr, wait, self.updated.cuda_event)
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(self.updated)
+                self.exchange()
+                slot.record(self.comm)
         self.frames += 1
         return p
 

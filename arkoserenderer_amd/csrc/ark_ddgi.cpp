@@ -207,6 +207,13 @@ struct ArkDdgiCtx {
     uint32_t setSeq[2] = { 0, 0 };
     bool setSeqValid[2] = { false, false };
     uint64_t seqTimeoutTicks = 0;
+    // Z-slab exchange sequencing (ark_ddgi_exchange_begin/_end, ark_ddgi_update_exchanged):
+    // seqWords [96] = the last exchange completed on the caller's exchange stream
+    uint32_t lastMainSeq = 0;        // the last update's caller-stream sequence number (0: not sequenced)
+    hipStream_t lastStream = nullptr; // the last update's stream
+    hipEvent_t evExchangeSrc = nullptr; // exchange_begin after an unsequenced update
+    uint32_t exchSeq = 0;            // exchanges ended so far
+    uint32_t pendingExchange = 0;    // the exchange the next update_exchanged waits for before shading
     uint32_t lastParity = 0;       // buffer set of the last update (debug hit records)
     uint32_t fibR[2] = { 0, 0 };
     uint64_t spillRegionWords = 0; // spill region 1 = the primary traversal's
@@ -505,6 +512,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     unsigned syncFlags = hipEventDisableTiming;
     if (const char* ef = std::getenv("ARK_SYNC_EVENT_FLAGS")) syncFlags |= static_cast<unsigned>(std::strtoul(ef, nullptr, 0));
     if ((e = hipEventCreateWithFlags(&ctx->evTraced, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evExchangeSrc, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->evFrameDone)
         if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
@@ -522,7 +530,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = ctx->surfels.alloc(K * R * 8)) != hipSuccess) return bad(e, "alloc surfels");
     if ((e = ctx->rayCounter.alloc(2 * kRayCounterWords * 4)) != hipSuccess) return bad(e, "alloc counter");
     if ((e = ctx->counters.alloc(8 * sizeof(unsigned long long))) != hipSuccess) return bad(e, "alloc counters");
-    if ((e = ctx->seqWords.alloc(96 * 4)) != hipSuccess) return bad(e, "alloc sequence words");
+    if ((e = ctx->seqWords.alloc(128 * 4)) != hipSuccess) return bad(e, "alloc sequence words");
     if ((e = hipMemset(ctx->seqWords.ptr, 0, ctx->seqWords.bytes)) != hipSuccess) return bad(e, "clear sequence words");
     {
         // k_seq_wait's bound: 10 s of the device wall clock (kHz attribute)
@@ -569,6 +577,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->evOrder) (void)hipEventDestroy(ctx->evOrder);
     if (ctx->evTraced) (void)hipEventDestroy(ctx->evTraced);
+    if (ctx->evExchangeSrc) (void)hipEventDestroy(ctx->evExchangeSrc);
     for (auto& ev : ctx->evFrameDone)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
@@ -894,7 +903,7 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
                       static_cast<uint32_t>(ctx->slabZ1), first, K);
 }
 
-static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent);
+static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent, uint32_t shadeWaitSeq = 0);
 
 
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
@@ -905,6 +914,41 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStrea
 int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent)
 {
     return updateImpl(ctx, p, hipStream, shadeWaitEvent, doneEvent);
+}
+
+int ark_ddgi_update_exchanged(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const uint32_t wait = ctx->pendingExchange;
+    const int r = updateImpl(ctx, p, hipStream, nullptr, nullptr, wait);
+    if (r == ARK_DDGI_OK) ctx->pendingExchange = 0;
+    return r;
+}
+
+int ark_ddgi_exchange_begin(ArkDdgiCtx* ctx, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const hipStream_t x = streamOf(hipStream);
+    ARK_HIP(hipSetDevice(ctx->device));
+    if (ctx->lastMainSeq) {
+        uint32_t* w = ctx->seqWords.as<uint32_t>();
+        ARK_HIP(launch_seq_wait(w + 32, ctx->lastMainSeq, w + 64, ctx->seqTimeoutTicks, x));
+    } else {
+        // the last update was not sequenced: everything enqueued on its stream so far
+        ARK_HIP(hipEventRecord(ctx->evExchangeSrc, ctx->lastStream));
+        ARK_HIP(hipStreamWaitEvent(x, ctx->evExchangeSrc, 0));
+    }
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* hipStream)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    ARK_HIP(hipSetDevice(ctx->device));
+    const uint32_t n = ++ctx->exchSeq;
+    ARK_HIP(launch_seq_signal(ctx->seqWords.as<uint32_t>() + 96, n, streamOf(hipStream)));
+    ctx->pendingExchange = n;
+    return ARK_DDGI_OK;
 }
 
 // The caller's stream s waits for the traversal stream's part of a pipelined frame
@@ -920,7 +964,7 @@ static hipError_t tracedSync(ArkDdgiCtx* ctx, bool seq, uint32_t seqN, hipStream
     return e != hipSuccess ? e : hipStreamWaitEvent(s, ctx->evTraced, 0);
 }
 
-static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent)
+static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent, uint32_t shadeWaitSeq)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!p || p->struct_size != sizeof(ArkDdgiFrameParams)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiFrameParams");
@@ -1057,6 +1101,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
         // rank it waits here for the previous exchange (the traversal above did not)
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->seqTimeoutTicks, s));
         ARK_HIP(launch_shade(ctx->scene, fs, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
@@ -1069,6 +1114,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     } else {
         if (pipe) ARK_HIP(tracedSync(ctx, seq, seqN, ts, s));
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
+        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->seqTimeoutTicks, s));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
             ARK_HIP(hipEventRecord(ctx->ev[5], s));
@@ -1086,6 +1132,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         ctx->setSeqValid[b] = false;
     }
     ctx->frameDoneValid[b] = true;
+    ctx->lastMainSeq = seq ? seqN : 0u;
+    ctx->lastStream = s;
     if (doneEvent) ARK_HIP(hipEventRecord(static_cast<hipEvent_t>(doneEvent), s));
     ARK_HIP(orderEnd(ctx, s));
     ctx->parity = b ^ 1u;

@@ -156,6 +156,19 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_update_overlapped(self.h, C.byref(params), v(stream), v(shade_wait_event), v(done_event)),
                    "ark_ddgi_update_overlapped")
 
+    def update_exchanged(self, params: abi.ArkDdgiFrameParams, stream: int | None):
+        """ark_ddgi_update_exchanged: shading waits (device-side) for the last exchange_end."""
+        self.check(self.lib.ark_ddgi_update_exchanged(self.h, C.byref(params), C.c_void_p(stream) if stream else None),
+                   "ark_ddgi_update_exchanged")
+
+    def exchange_begin(self, comm_stream: int | None):
+        """ark_ddgi_exchange_begin: comm_stream waits (device-side) for the last update."""
+        self.check(self.lib.ark_ddgi_exchange_begin(self.h, C.c_void_p(comm_stream) if comm_stream else None), "ark_ddgi_exchange_begin")
+
+    def exchange_end(self, comm_stream: int | None):
+        """ark_ddgi_exchange_end: the exchange enqueued on comm_stream so far completes the frame."""
+        self.check(self.lib.ark_ddgi_exchange_end(self.h, C.c_void_p(comm_stream) if comm_stream else None), "ark_ddgi_exchange_end")
+
     def synchronize(self):
         self.check(self.lib.ark_ddgi_synchronize(self.h), "ark_ddgi_synchronize")
 
@@ -331,6 +344,15 @@ class DDGINode:
             return None
         p = self.next_params(app)
         self.ctx.update_overlapped(p, stream, shade_wait_event, done_event)
+        self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
+        return p
+
+    def execute_exchanged(self, app: AppState, stream: int | None) -> abi.ArkDdgiFrameParams:
+        """execute() through ark_ddgi_update_exchanged (Z-slab ranks, see collective.py)."""
+        if self.ctx is None:
+            return None
+        p = self.next_params(app)
+        self.ctx.update_exchanged(p, stream)
         self.probe_update_idx = (self.probe_update_idx + p.probe_updates) % self.grid.probe_count()
         return p
 

@@ -119,9 +119,12 @@ def main():
     # frame N+1's primary traversal (collective.OverlappedSlabExchange)
     exch = None
     if world > 1:
-        from arkoserenderer_amd.collective import OverlappedSlabExchange
+        from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange
 
-        exch = OverlappedSlabExchange(node, SlabExchange.from_views(ctx.device_views(), rank, world, device).exchange, device)
+        # the two bands as one RCCL group on the exchange stream itself (RcclBandExchange);
+        # ARK_BENCH_TORCH_PG=1: through torch's process group instead
+        Ex = SlabExchange if os.environ.get("ARK_BENCH_TORCH_PG") == "1" else RcclBandExchange
+        exch = OverlappedSlabExchange(node, Ex.from_views(ctx.device_views(), rank, world, device).exchange, device)
     setup_s = time.time() - t_setup
 
     frame = 0

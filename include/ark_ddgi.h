@@ -335,6 +335,21 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
 int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream, void* shade_wait_event,
                                void* done_event);
 
+/* The same Z-slab frame loop with device-side handovers instead of events (each
+ * cross-queue event wait costs 12-16 us of queue latency on MI355X):
+ *   ark_ddgi_update_exchanged(ctx, params, stream)   the update; its shading first
+ *       waits for the exchange ended by the last ark_ddgi_exchange_end (if any
+ *       since the previous update_exchanged)
+ *   ark_ddgi_exchange_begin(ctx, comm_stream)        comm_stream waits until the last
+ *       update is complete (as its done_event would say)
+ *   ... the caller's all-gather of the atlas bands on comm_stream ...
+ *   ark_ddgi_exchange_end(ctx, comm_stream)          marks the exchange complete
+ * The waits are one-wave kernels bounded by 10 s (ark_ddgi_synchronize reports a
+ * timeout). Same work and results as ark_ddgi_update_overlapped. */
+int ark_ddgi_update_exchanged(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
+int ark_ddgi_exchange_begin(ArkDdgiCtx* ctx, void* comm_stream);
+int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* comm_stream);
+
 /* Resource geometry and transfers (blocking, for tests / state save-load). */
 int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* out_bytes);
 int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);

@@ -120,11 +120,14 @@ def test_golden_fixtures_on_gpu():
         ctx.close()
 
 
-def test_overlapped_update_two_slabs_one_gpu():
+@pytest.mark.parametrize("device_seq", [False, True], ids=["events", "device_seq"])
+def test_overlapped_update_two_slabs_one_gpu(device_seq):
     """ark_ddgi_update_overlapped on two Z-slab contexts sharing one GPU, each on its
     own stream, with the band exchange as device copies on a third stream ordered
     only by the events (the RCCL schedule of OverlappedSlabExchange): after several
-    frames enqueued without host synchronisation the atlases equal the oracle's."""
+    frames enqueued without host synchronisation the atlases equal the oracle's.
+    device_seq: the same through ark_ddgi_update_exchanged / ark_ddgi_exchange_begin /
+    ark_ddgi_exchange_end (device-side sequence words instead of events)."""
     import torch
 
     from arkoserenderer_amd.collective import device_bytes
@@ -156,15 +159,24 @@ def test_overlapped_update_two_slabs_one_gpu():
     for f in range(5):
         p = D.frame_params(cfg, grid, D.AppState(f), idx, **exposure)
         for c, s, e in zip(ctxs, streams, done):
-            c.update_overlapped(p, s.cuda_stream, gathered.cuda_event if f > 0 else None, e.cuda_event)
+            if device_seq:
+                c.update_exchanged(p, s.cuda_stream)
+            else:
+                c.update_overlapped(p, s.cuda_stream, gathered.cuda_event if f > 0 else None, e.cuda_event)
         with torch.cuda.stream(comm):
-            for e in done:
-                comm.wait_event(e)
+            for c, e in zip(ctxs, done):
+                if device_seq:
+                    c.exchange_begin(comm.cuda_stream)
+                else:
+                    comm.wait_event(e)
             for k in range(2):  # each owner's band into the other context
                 for r in range(2):
                     full, off, n = atlases[r][k]
                     other = atlases[1 - r][k][0]
                     other[off:off + n].copy_(full[off:off + n])
+            if device_seq:
+                for c in ctxs:
+                    c.exchange_end(comm.cuda_stream)
             gathered.record(comm)
         orc.update(p)
         idx = (idx + p.probe_updates) % N
@@ -176,17 +188,19 @@ def test_overlapped_update_two_slabs_one_gpu():
             assert r["mismatch"] == 0, (which, r)
 
 
-def test_bench_frame_loop_over_one_rank_rccl():
+@pytest.mark.parametrize("mode,port", [("torch_pg_events", 29541), ("torch_pg_seq", 29542), ("rccl_seq", 29543)])
+def test_bench_frame_loop_over_one_rank_rccl(mode, port):
     """bench.py's N > 1 frame loop as it runs on every rank: DDGINode.execute_overlapped
     driven by OverlappedSlabExchange (torch events, a side stream, the in-place RCCL
     all-gather of SlabExchange), here over a 1-rank communicator, several frames
     enqueued without host synchronisation: the atlases and offsets equal a plain
     node's (the exchange of one rank moves nothing, so only the event plumbing and
-    stream order are under test)."""
+    stream order are under test). torch_pg_seq: device-side sequence words instead
+    of events; rccl_seq: also the bench's direct RCCL group (RcclBandExchange)."""
     import torch
     import torch.distributed as dist
 
-    from arkoserenderer_amd.collective import OverlappedSlabExchange, SlabExchange
+    from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange, SlabExchange
 
     sc, ex = S.cornell_box()
     grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
@@ -199,10 +213,13 @@ def test_bench_frame_loop_over_one_rank_rccl():
     assert plain.construct(sc, grid, ex["z_far"], device=0, **exposure)
     assert ranked.construct(sc, grid, ex["z_far"], device=0, shard_rank=0, shard_count=1, **exposure)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = "29541"
+    os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    band = None
     try:
-        exch = OverlappedSlabExchange(ranked, SlabExchange.from_views(ranked.ctx.device_views(), 0, 1, dev).exchange, dev)
+        Ex = RcclBandExchange if mode == "rccl_seq" else SlabExchange
+        band = Ex.from_views(ranked.ctx.device_views(), 0, 1, dev)
+        exch = OverlappedSlabExchange(ranked, band.exchange, dev, device_seq=mode != "torch_pg_events")
         sptr = torch.cuda.current_stream(dev).cuda_stream
         for f in range(6):
             plain.execute(D.AppState(f), sptr)
@@ -212,6 +229,8 @@ def test_bench_frame_loop_over_one_rank_rccl():
             a, b = plain.ctx.read(which), ranked.ctx.read(which)
             assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), which
     finally:
+        if isinstance(band, RcclBandExchange):
+            band.close()
         dist.destroy_process_group()
         plain.ctx.close()
         ranked.ctx.close()
