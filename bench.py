@@ -123,8 +123,15 @@ def main():
 
         # the two bands as one RCCL group on the exchange stream itself (RcclBandExchange);
         # ARK_BENCH_TORCH_PG=1: through torch's process group instead
-        Ex = SlabExchange if os.environ.get("ARK_BENCH_TORCH_PG") == "1" else RcclBandExchange
-        exch = OverlappedSlabExchange(node, Ex.from_views(ctx.device_views(), rank, world, device).exchange, device)
+        band = None
+        if os.environ.get("ARK_BENCH_TORCH_PG") != "1":
+            try:
+                band = RcclBandExchange.from_views(ctx.device_views(), rank, world, device)
+            except (RuntimeError, OSError, AttributeError) as e:  # no direct RCCL: the process group's all-gather
+                print(f"warning: RcclBandExchange unavailable ({e}); using torch.distributed all-gather", file=sys.stderr)
+        if band is None:
+            band = SlabExchange.from_views(ctx.device_views(), rank, world, device)
+        exch = OverlappedSlabExchange(node, band.exchange, device)
     setup_s = time.time() - t_setup
 
     frame = 0
