@@ -212,6 +212,7 @@ struct ArkDdgiCtx {
     uint32_t lastMainSeq = 0;        // the last update's caller-stream sequence number (0: not sequenced)
     hipStream_t lastStream = nullptr; // the last update's stream
     hipEvent_t evExchangeSrc = nullptr; // exchange_begin after an unsequenced update
+    hipEvent_t evExchangeDone = nullptr; // exchange_end without sequence words (seqSync off)
     uint32_t exchSeq = 0;            // exchanges ended so far
     uint32_t pendingExchange = 0;    // the exchange the next update_exchanged waits for before shading
     uint32_t lastParity = 0;       // buffer set of the last update (debug hit records)
@@ -498,6 +499,11 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
         if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
+        // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
+        // across queues: a polling wait could then hold the GPU while the kernel it
+        // waits for queues behind it (it would give up after 10 s): events instead
+        if (const char* pc = std::getenv("ROCPROF_COUNTER_COLLECTION"))
+            if (*pc && std::strcmp(pc, "0") != 0 && std::strcmp(pc, "false") != 0) ctx->seqSync = false;
         // ARK_SHADOW_BIN_GRID: light-space cells per axis of the shadow-ray binning
         // (a power of 2 up to 256), 0 = the list in queue order
         if (const char* g = std::getenv("ARK_SHADOW_BIN_GRID")) {
@@ -513,6 +519,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if (const char* ef = std::getenv("ARK_SYNC_EVENT_FLAGS")) syncFlags |= static_cast<unsigned>(std::strtoul(ef, nullptr, 0));
     if ((e = hipEventCreateWithFlags(&ctx->evTraced, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeSrc, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evExchangeDone, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->evFrameDone)
         if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
@@ -578,6 +585,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (ctx->evOrder) (void)hipEventDestroy(ctx->evOrder);
     if (ctx->evTraced) (void)hipEventDestroy(ctx->evTraced);
     if (ctx->evExchangeSrc) (void)hipEventDestroy(ctx->evExchangeSrc);
+    if (ctx->evExchangeDone) (void)hipEventDestroy(ctx->evExchangeDone);
     for (auto& ev : ctx->evFrameDone)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
@@ -920,7 +928,9 @@ int ark_ddgi_update_exchanged(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     const uint32_t wait = ctx->pendingExchange;
-    const int r = updateImpl(ctx, p, hipStream, nullptr, nullptr, wait);
+    // without sequence words the exchange's end is an event (ark_ddgi_exchange_end)
+    const int r = ctx->seqSync ? updateImpl(ctx, p, hipStream, nullptr, nullptr, wait)
+                               : updateImpl(ctx, p, hipStream, wait ? ctx->evExchangeDone : nullptr, nullptr);
     if (r == ARK_DDGI_OK) ctx->pendingExchange = 0;
     return r;
 }
@@ -946,7 +956,8 @@ int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* hipStream)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ARK_HIP(hipSetDevice(ctx->device));
     const uint32_t n = ++ctx->exchSeq;
-    ARK_HIP(launch_seq_signal(ctx->seqWords.as<uint32_t>() + 96, n, streamOf(hipStream)));
+    if (ctx->seqSync) ARK_HIP(launch_seq_signal(ctx->seqWords.as<uint32_t>() + 96, n, streamOf(hipStream)));
+    else ARK_HIP(hipEventRecord(ctx->evExchangeDone, streamOf(hipStream)));
     ctx->pendingExchange = n;
     return ARK_DDGI_OK;
 }
