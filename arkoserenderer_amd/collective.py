@@ -83,16 +83,36 @@ class RcclBandExchange:
         for full, off, slab in buffers:
             assert slab * world == full.numel() and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
             self.bufs.append((full.data_ptr(), full.data_ptr() + off, slab))
-        lib = _rccl()
-        uid = _NcclUniqueId()
-        if rank == 0:
-            _nccl_check(lib.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
-        t = torch.tensor(list(bytes(uid.internal)), dtype=torch.uint8, device=buffers[0][0].device)
+        # Every rank reaches the same outcome: rank 0 broadcasts the id with a status
+        # byte (a failed ncclGetUniqueId does not leave the others in the broadcast),
+        # and after ncclCommInitRank the ranks agree (MIN all-reduce) before any rank
+        # uses the communicator, so a failure makes all of them raise (bench.py then
+        # falls back to SlabExchange on every rank).
+        dev = buffers[0][0].device
+        lib = uid = None
+        ok = 1
+        try:
+            lib = _rccl()
+            uid = _NcclUniqueId()
+            if rank == 0:
+                _nccl_check(lib.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+        except (OSError, AttributeError, RuntimeError):
+            ok = 0
+        t = torch.tensor([ok] + (list(bytes(uid.internal)) if uid is not None else [0] * 128), dtype=torch.uint8, device=dev)
         dist.broadcast(t, 0, group=group)
-        uid = _NcclUniqueId((C.c_uint8 * 128)(*t.cpu().tolist()))
-        self.comm = C.c_void_p()
-        _nccl_check(lib.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+        got = t.cpu().tolist()
+        if not got[0] or lib is None:
+            raise RuntimeError("RcclBandExchange: no ncclUniqueId from rank 0")
         self.lib = lib
+        self.comm = C.c_void_p()
+        rc = lib.ncclCommInitRank(C.byref(self.comm), world, _NcclUniqueId((C.c_uint8 * 128)(*got[1:])), rank)
+        flag = torch.tensor([1 if rc == 0 else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if int(flag.item()) != 1:
+            if rc == 0:
+                self.close()
+            self.comm = None
+            raise RuntimeError(f"RcclBandExchange: ncclCommInitRank failed on some rank (here: ncclResult {rc})")
 
     from_views = classmethod(SlabExchange.from_views.__func__)
 
