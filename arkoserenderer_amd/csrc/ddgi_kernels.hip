@@ -2184,14 +2184,18 @@ static uint32_t persistentBlocks(const void* fn, int block, uint32_t fallback)
 }
 
 // One-pass shading at <= 128 VGPRs, 4 waves/SIMD, no spill (round 1: 0.57 -> 0.50 ms
-// at C4 against the compiler's 133 VGPRs, 3 waves).
+// at C4 against the compiler's 133 VGPRs, 3 waves). Round 3: 5 waves (96 VGPRs)
+// spills 30 and shades in 0.525 instead of 0.469 ms (profiles/r03_ak).
+#ifndef ARK_SHADE_WPE
+#define ARK_SHADE_WPE 4
+#endif
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     if (count) {
         hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
     } else {
-        const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
-        hipLaunchKernelGGL((dev::k_shade<false, 4>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
+        const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, ARK_SHADE_WPE>);
+        hipLaunchKernelGGL((dev::k_shade<false, ARK_SHADE_WPE>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
     }
     return hipGetLastError();
 }
@@ -2240,7 +2244,7 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
 
 const void* kernel_shade_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, 4>);
+    return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, ARK_SHADE_WPE>);
 }
 
 const void* kernel_trace_shadow_ptr(bool count)
