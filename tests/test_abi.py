@@ -57,6 +57,11 @@ def test_invalid_arguments_fail_cleanly():
     d.struct_size = 3
     assert lib.ark_ddgi_create(C.byref(d), C.byref(h)) == -1
     assert lib.ark_ddgi_update(None, None, None) == -1
+    # the Z-slab exchange sequencing entry points (no device work without a context)
+    assert lib.ark_ddgi_update_exchanged(None, None, None) == -1
+    assert lib.ark_ddgi_exchange_begin(None, None) == -1
+    assert lib.ark_ddgi_exchange_end(None, None) == -1
+    assert lib.ark_ddgi_synchronize(None) == -1
     assert lib.ark_ddgi_last_error(None) == b"null context"
 
 
