@@ -319,6 +319,20 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // triangles as a bit mask over [tBase, tBase + 24) (2 VALU: triangle rows).
 // Node-visit instruction budget (tools/isa_budget.py): the defaults cut
 // k_trace's node block from 269 to 223 VALU (gfx950 ISA of this file)
+// GF dual steps (travStepDual<.., GF = true>) fetch every node from global memory, with
+// both sides' loads outside any branch (see travStepDual); per kernel:
+// k_trace: on (its LDS node cache is then not allocated: 22.3 -> 18.4 KB of LDS per
+// workgroup). C4 step 3.66 / 3.68 -> 3.57 / 3.54 ms, K = 4096 windows 0.606 -> 0.591 /
+// 0.585 ms, K = 2048 within 1 %, Z-slab proxy P = 8 0.578 -> 0.570 ms, although the
+// serial traversal itself is 1 % slower (1.975 -> 1.985 ms; profiles/r03_an, r03_ao).
+// k_trace_shadow: off (its any-hit rays gain from the cached top nodes: 0.704 -> 0.730
+// ms with global fetches).
+#ifndef ARK_TRACE_FETCH_GLOBAL
+#define ARK_TRACE_FETCH_GLOBAL 1
+#endif
+#ifndef ARK_SHADOW_FETCH_GLOBAL
+#define ARK_SHADOW_FETCH_GLOBAL 0
+#endif
 #ifndef ARK_NODE_LDEXP
 #define ARK_NODE_LDEXP 1 // per-axis step * idir as v_ldexp_f32 of the exponent byte instead of a float build + multiply
 #endif
@@ -547,7 +561,7 @@ __device__ __forceinline__ bool travDoneDual(const TravState& ts, uint32_t nBits
     return ts.tBits == 0 && nBits == 0 && (ts.gBits & 0xffu) == 0 && st.depth == 0;
 }
 
-template<int BLOCK, bool ANY>
+template<int BLOCK, bool ANY, bool GF = false>
 __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCache& nc, TravState& ts, uint32_t& nBase, uint32_t& nBits, Stack<BLOCK>& st,
                                              V3 o, V3 d, V3 idir, uint32_t oct, float tmin, RayHit& h, int pass, uint32_t& cNodes, uint32_t& cTris)
 {
@@ -558,6 +572,40 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
     // them cost ~34 VALU per iteration (the compiler materialised the zeros)
     uint4 a, b, c;
     uint32_t ti = 0;
+    uint4 w0, w1, w2, w3, w4;
+    if constexpr (GF) {
+    // Both sides' loads are issued by every lane outside any branch (a skipped side
+    // reads a resident dummy record: triangle 0, the root node), triangle loads first:
+    // the wait before the triangle test then covers only the triangle loads, and the
+    // test runs while the node loads are in flight (the branch-local loads of the
+    // other form make the compiler wait for both: vmcnt(0)). Nodes come from global
+    // memory only (the LDS node cache would make these generic flat loads).
+    (void)nc;
+    if (doTri) {
+        ti = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
+        ts.tBits &= ts.tBits - 1u;
+    }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.tris + ti);
+        a = src[0];
+        b = src[1];
+        c = src[2];
+    }
+    uint32_t child = static_cast<uint32_t>(sc.root_opaque >= 0 ? sc.root_opaque : 0);
+    if (doNode) {
+        if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
+        child = nextChild(ts.gBase, ts.gBits, oct);
+        if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
+    }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.nodes + child);
+        w0 = src[0];
+        w1 = src[1];
+        w2 = src[2];
+        w3 = src[3];
+        w4 = src[4];
+    }
+    } else {
     if (doTri) {
         ti = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
         ts.tBits &= ts.tBits - 1u;
@@ -566,7 +614,6 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
         b = src[1];
         c = src[2];
     }
-    uint4 w0, w1, w2, w3, w4;
     if (doNode) {
         if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
         const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
@@ -578,6 +625,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
         w2 = src[2];
         w3 = src[3];
         w4 = src[4];
+    }
     }
     if (doTri) {
         cTris++;
@@ -790,8 +838,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     unsigned long long tEx = 0, itAll = 0, itEx = 0;
 #endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
-    __shared__ uint4 ldsNodes[kLdsNodes * 5];
-    const NodeCache nc = loadNodeCache<kTraceBlock>(sc, ldsNodes);
+    constexpr bool kGF = ARK_TRACE_FETCH_GLOBAL != 0;
+    __shared__ uint4 ldsNodes[(kGF ? 1 : kLdsNodes) * 5];
+    const NodeCache nc = loadNodeCache<kTraceBlock, kGF ? 0 : kLdsNodes>(sc, ldsNodes);
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
@@ -870,7 +919,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- one step: a pending leaf triangle and the next node -------------------
         // (an active lane is never done here: the check after the step retires or
         // restarts it, and a step of a done lane would change nothing anyway)
-        if (active) travStepDual<kTraceBlock, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
+        if (active) travStepDual<kTraceBlock, false, kGF>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
@@ -1578,7 +1627,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         if (active) {
             // (a done lane - a root waiting for its helpers - steps as a no-op)
             RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-            const bool occluded = travStepDual<kTraceBlock, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
+            const bool occluded = travStepDual<kTraceBlock, true, ARK_SHADOW_FETCH_GLOBAL != 0>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
             const bool helper = pass >= 256;
             const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
             if (occluded) {
