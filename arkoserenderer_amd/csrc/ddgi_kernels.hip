@@ -327,6 +327,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // serial traversal itself is 1 % slower (1.975 -> 1.985 ms; profiles/r03_an, r03_ao).
 // k_trace_shadow: off (its any-hit rays gain from the cached top nodes: 0.704 -> 0.730
 // ms with global fetches).
+#ifndef ARK_SHADOW_LDS_NODES
+#define ARK_SHADOW_LDS_NODES (kLdsNodes - 8) // top nodes k_trace_shadow keeps in LDS
+#endif
 #ifndef ARK_TRACE_FETCH_GLOBAL
 #define ARK_TRACE_FETCH_GLOBAL 1
 #endif
@@ -1504,7 +1507,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 #endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
-    constexpr int kNodes = kLdsNodes - 8;
+    constexpr int kNodes = ARK_SHADOW_LDS_NODES;
     __shared__ uint4 ldsNodes[kNodes * 5];
     __shared__ uint8_t ldsTable[kTraceBlock];
     __shared__ uint32_t ldsBytes[kTraceBlock / 4];
