@@ -158,7 +158,7 @@ struct ArkDdgiCtx {
     hipStream_t orderStream = nullptr;
     bool orderValid = false;
     // traversal knobs, fixed at create: refill batch, grab chunk
-    uint32_t refillMin = 8, grabChunk = 64;
+    uint32_t refillMin = 16, grabChunk = 64;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -494,8 +494,11 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipEventCreateWithFlags(&ctx->evOrder, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     {
         // tuning knobs, read once: ARK_REFILL_MIN: refill idle trace lanes in batches
-        // of >= 8 (the refill then stalls a wave once per 8 finished rays, and the rays it
-        // starts descend from the root together: 2.98 vs 3.30 ms at 1 on C4; 16: 3.03);
+        // of >= 16 (the refill then stalls a wave once per 16 finished rays, and the rays
+        // it starts descend from the root together: 2.98 vs 3.30 ms at 1 on C4, 16 was
+        // 3.03 in round 1; with the traversal's fetches outside branches (round 3) 16 is
+        // the best: C4 step 3.53 -> 3.46 ms, K = 4096 +2 %, K = 2048 +1 %, 4: 3.67, 24:
+        // 3.47-3.49, 32: 3.64; profiles/r03_as, r03_at);
         // ARK_GRAB_CHUNK: rays per partition-head grab, 64 = a probe quarter of
         // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
