@@ -403,6 +403,8 @@ EXPORTS = {
     "ark_ddgi_get_next_probe_index": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ark_ddgi_update": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
     "ark_ddgi_synchronize": (C.c_int, [C.c_void_p]),
+    "ark_ddgi_set_sequencing": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
+    "ark_ddgi_get_sequencing": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "ark_ddgi_update_overlapped": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p, C.c_void_p, C.c_void_p]),
     "ark_ddgi_update_exchanged": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
     "ark_ddgi_exchange_begin": (C.c_int, [C.c_void_p, C.c_void_p]),

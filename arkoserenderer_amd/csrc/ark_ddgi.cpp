@@ -210,6 +210,14 @@ struct ArkDdgiCtx {
     uint32_t setSeq[2] = { 0, 0 };
     bool setSeqValid[2] = { false, false };
     uint64_t seqTimeoutTicks = 0;
+    uint32_t seqTimeoutMs = 10000;
+    uint64_t wallClockKhz = 100000;
+    // fail-closed sequencing: a k_seq_wait that gives up sets seqWords[64] (every path
+    // kernel then skips: frameAborted) and this host-mapped word, which the next
+    // update / exchange_begin / synchronize polls (checkSequencing)
+    uint32_t* hostAbort = nullptr;    // host pointer (hipHostMalloc, coherent)
+    uint32_t* hostAbortDev = nullptr; // its device address
+    uint32_t seqTimeouts = 0;         // timeouts reported so far
     // Z-slab exchange sequencing (ark_ddgi_exchange_begin/_end, ark_ddgi_update_exchanged):
     // seqWords [96] = the last exchange completed on the caller's exchange stream
     uint32_t lastMainSeq = 0;        // the last update's caller-stream sequence number (0: not sequenced)
@@ -507,7 +515,8 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
         // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
         // across queues: a polling wait could then hold the GPU while the kernel it
-        // waits for queues behind it (it would give up after 10 s): events instead
+        // waits for queues behind it: it would give up after its bound and fail closed
+        // (checkSequencing), dropping frames; such a context starts with events instead
         if (const char* pc = std::getenv("ROCPROF_COUNTER_COLLECTION"))
             if (*pc && std::strcmp(pc, "0") != 0 && std::strcmp(pc, "false") != 0) ctx->seqSync = false;
         // ARK_SHADOW_BIN_GRID: light-space cells per axis of the shadow-ray binning
@@ -549,8 +558,14 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // k_seq_wait's bound: 10 s of the device wall clock (kHz attribute)
         int rateKhz = 0;
         if (hipDeviceGetAttribute(&rateKhz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || rateKhz <= 0) rateKhz = 100000;
-        ctx->seqTimeoutTicks = static_cast<uint64_t>(rateKhz) * 1000ull * 10ull;
+        ctx->wallClockKhz = static_cast<uint64_t>(rateKhz);
+        ctx->seqTimeoutTicks = ctx->wallClockKhz * ctx->seqTimeoutMs;
     }
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hostAbort), 64, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+        return bad(e, "hipHostMalloc sequencing flag");
+    *reinterpret_cast<volatile uint32_t*>(ctx->hostAbort) = 0u;
+    if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->hostAbortDev), ctx->hostAbort, 0)) != hipSuccess)
+        return bad(e, "hipHostGetDevicePointer sequencing flag");
     // persistent grids: as many workgroups as are co-resident
     int occT = 0, occS = 0, occW = 0;
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occT, kernel_trace_ptr(false), kTraceBlock, 0)) != hipSuccess) return bad(e, "occupancy trace");
@@ -596,6 +611,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->hostAbort) (void)hipHostFree(ctx->hostAbort);
     delete ctx;
 }
 
@@ -919,6 +935,50 @@ static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t 
 
 static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream, void* shadeWaitEvent, void* doneEvent, uint32_t shadeWaitSeq = 0);
 
+// Fail-closed frame sequencing (VERDICT r03 "do this" #3): a k_seq_wait that gave up
+// has set the context's timed-out word, so every path kernel that starts after it
+// skips (frameAborted) and leaves atlases, surfels and offsets as they were (a launch
+// already running when the wait gave up completes). The first context
+// call that sees the host-mapped flag drains the device (the late producer ends by
+// itself), clears both words, switches the context to event sequencing (which no
+// queue order can stall) and reports ARK_DDGI_E_DEVICE; the calls after it run.
+static int checkSequencing(ArkDdgiCtx* ctx)
+{
+    if (!ctx->hostAbort || __atomic_load_n(ctx->hostAbort, __ATOMIC_ACQUIRE) == 0u) return ARK_DDGI_OK;
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    ARK_HIP(hipMemset(ctx->seqWords.as<uint32_t>() + 64, 0, 4));
+    __atomic_store_n(ctx->hostAbort, 0u, __ATOMIC_RELEASE);
+    ctx->seqSync = false;
+    ctx->pipeReady = false;
+    ++ctx->seqTimeouts;
+    return ctx->fail(ARK_DDGI_E_DEVICE,
+                     "a frame-sequencing wait between the context's streams gave up after %u ms: every update kernel that started after it skipped "
+                     "(its atlases, surfels and offsets left as they were); the context now orders its streams with events",
+                     ctx->seqTimeoutMs);
+}
+
+int ark_ddgi_set_sequencing(ArkDdgiCtx* ctx, int device_sequence_words, uint32_t timeout_ms)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (timeout_ms > 3600u * 1000u) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "sequencing timeout %u ms above one hour", timeout_ms);
+    ctx->seqSync = device_sequence_words != 0;
+    if (timeout_ms) {
+        ctx->seqTimeoutMs = timeout_ms;
+        ctx->seqTimeoutTicks = ctx->wallClockKhz * timeout_ms;
+    }
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_get_sequencing(const ArkDdgiCtx* ctx, int* out_device_sequence_words, uint32_t* out_timeout_ms, uint32_t* out_timeouts)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (out_device_sequence_words) *out_device_sequence_words = ctx->seqSync ? 1 : 0;
+    if (out_timeout_ms) *out_timeout_ms = ctx->seqTimeoutMs;
+    if (out_timeouts) *out_timeouts = ctx->seqTimeouts;
+    return ARK_DDGI_OK;
+}
+
 
 int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStream)
 {
@@ -945,10 +1005,11 @@ int ark_ddgi_exchange_begin(ArkDdgiCtx* ctx, void* hipStream)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     const hipStream_t x = streamOf(hipStream);
+    if (const int r = checkSequencing(ctx)) return r;
     ARK_HIP(hipSetDevice(ctx->device));
     if (ctx->lastMainSeq) {
         uint32_t* w = ctx->seqWords.as<uint32_t>();
-        ARK_HIP(launch_seq_wait(w + 32, ctx->lastMainSeq, w + 64, ctx->seqTimeoutTicks, x));
+        ARK_HIP(launch_seq_wait(w + 32, ctx->lastMainSeq, w + 64, ctx->hostAbortDev, ctx->seqTimeoutTicks, x));
     } else {
         // the last update was not sequenced: everything enqueued on its stream so far
         ARK_HIP(hipEventRecord(ctx->evExchangeSrc, ctx->lastStream));
@@ -975,7 +1036,7 @@ static hipError_t tracedSync(ArkDdgiCtx* ctx, bool seq, uint32_t seqN, hipStream
     if (seq) {
         uint32_t* w = ctx->seqWords.as<uint32_t>();
         hipError_t e = launch_seq_signal(w, seqN, ts);
-        return e != hipSuccess ? e : launch_seq_wait(w, seqN, w + 64, ctx->seqTimeoutTicks, s);
+        return e != hipSuccess ? e : launch_seq_wait(w, seqN, w + 64, ctx->hostAbortDev, ctx->seqTimeoutTicks, s);
     }
     hipError_t e = hipEventRecord(ctx->evTraced, ts);
     return e != hipSuccess ? e : hipStreamWaitEvent(s, ctx->evTraced, 0);
@@ -992,8 +1053,10 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     if (K == 0 || R == 0 || K > static_cast<uint32_t>(ctx->Kmax) || R > static_cast<uint32_t>(ctx->Rmax))
         return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "probe_updates %u / rays_per_probe %u outside [1,%d] / [1,%d]", K, R, ctx->Kmax, ctx->Rmax);
     const hipStream_t s = streamOf(hipStream);
+    if (const int r = checkSequencing(ctx)) return r;
     ARK_HIP(hipSetDevice(ctx->device));
     FrameArgs f {};
+    f.abort_word = ctx->seqWords.as<uint32_t>() + 64;
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
     f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
     for (int k = 0; k < 3; ++k) {
@@ -1085,7 +1148,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     uint32_t* seqTimedOut = seqTrace + 64;
     const bool seq = pipe && ctx->seqSync;
     const uint32_t seqN = seq ? ++ctx->frameSeq : 0u;
-    if (pipe && ctx->setSeqValid[b]) ARK_HIP(launch_seq_wait(seqMain, ctx->setSeq[b], seqTimedOut, ctx->seqTimeoutTicks, ts));
+    if (pipe && ctx->setSeqValid[b]) ARK_HIP(launch_seq_wait(seqMain, ctx->setSeq[b], seqTimedOut, ctx->hostAbortDev, ctx->seqTimeoutTicks, ts));
     else if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
     // a serial previous frame wrote its offsets on the caller's stream
     if (pipe && !ctx->prevPipelined && ctx->frameDoneValid[b ^ 1u]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b ^ 1u], 0));
@@ -1118,7 +1181,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         // shading reads the previous frame's atlases at arbitrary probes: on a Z-slab
         // rank it waits here for the previous exchange (the traversal above did not)
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->seqTimeoutTicks, s));
+        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->hostAbortDev, ctx->seqTimeoutTicks, s));
         ARK_HIP(launch_shade(ctx->scene, fs, ctx->shadeBlocks, count, s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[2], s));
         if (timing) ARK_HIP(hipEventRecord(ctx->ev[4], s));
@@ -1131,7 +1194,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     } else {
         if (pipe) ARK_HIP(tracedSync(ctx, seq, seqN, ts, s));
         if (shadeWaitEvent) ARK_HIP(hipStreamWaitEvent(s, static_cast<hipEvent_t>(shadeWaitEvent), 0));
-        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->seqTimeoutTicks, s));
+        if (shadeWaitSeq) ARK_HIP(launch_seq_wait(seqTrace + 96, shadeWaitSeq, seqTimedOut, ctx->hostAbortDev, ctx->seqTimeoutTicks, s));
         if (timing) {
             ARK_HIP(hipEventRecord(ctx->ev[1], s));
             ARK_HIP(hipEventRecord(ctx->ev[5], s));
@@ -1178,10 +1241,7 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx)
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     ARK_HIP(hipSetDevice(ctx->device));
     ARK_HIP(hipDeviceSynchronize());
-    uint32_t timedOut = 0;
-    ARK_HIP(hipMemcpy(&timedOut, ctx->seqWords.as<uint32_t>() + 64, 4, hipMemcpyDeviceToHost));
-    if (timedOut) return ctx->fail(ARK_DDGI_E_DEVICE, "a frame-sequencing wait between the context's streams timed out (10 s)");
-    return ARK_DDGI_OK;
+    return checkSequencing(ctx);
 }
 
 static int resourceInfo(const ArkDdgiCtx* ctx, int which, void** ptr, uint64_t* bytes)

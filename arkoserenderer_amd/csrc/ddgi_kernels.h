@@ -232,7 +232,24 @@ struct FrameArgs {
     // ray-list traversals (RT reflections): {origin, tmax}, {direction, pixel} per ray
     const float4* ray_list;
     const uint32_t* list_count;
+    // fail-closed frame sequencing: the context's timed-out word (set by a k_seq_wait
+    // that gave up); every kernel of the update leaves its outputs untouched once it is
+    // set (frameAborted). Null = never (consumers, serial instrumented paths).
+    const uint32_t* abort_word;
 };
+
+// Fail-closed frame sequencing (ark_ddgi.cpp updateImpl): true when a frame-sequencing
+// wait of this context has timed out, so this launch must not compute (its inputs may
+// not be ready). Read once per workgroup by thread 0 and broadcast through LDS, so the
+// workgroup takes one decision (its waves share barriers further on).
+__device__ __forceinline__ bool frameAborted(const uint32_t* abortWord)
+{
+    if (!abortWord) return false;
+    __shared__ uint32_t sAbort;
+    if (threadIdx.x == 0) sAbort = __hip_atomic_load(abortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return sAbort != 0u;
+}
 
 // AO / bent-normal bake of one mesh segment (ark_ddgi_bake_ao; ddgi_kernels.hip §5)
 struct BakeArgs {
@@ -269,7 +286,10 @@ hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s);
 hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t s);
 // frame sequencing between two streams of one context (k_seq_signal / k_seq_wait)
 hipError_t launch_seq_signal(uint32_t* word, uint32_t value, hipStream_t s);
-hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint64_t timeoutTicks, hipStream_t s);
+// k_seq_wait gives up after timeoutTicks of the device wall clock (or at once when
+// *timedOut is already set): it sets *timedOut (the kernels of the frame then skip,
+// frameAborted) and *hostFlag (host-mapped, polled by the next context call)
+hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint32_t* hostFlag, uint64_t timeoutTicks, hipStream_t s);
 const void* kernel_trace_ptr(bool count);
 const void* kernel_shade_ptr(bool count);
 const void* kernel_trace_shadow_ptr(bool count);

@@ -120,6 +120,7 @@ __device__ __forceinline__ bool inSlab(const FrameArgs& f, uint32_t probeIdx)
 // never a result.
 __global__ void __launch_bounds__(256) k_probe_slots(FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     const uint32_t X = static_cast<uint32_t>(f.X), Y = static_cast<uint32_t>(f.Y), Z = static_cast<uint32_t>(f.Z);
     const uint32_t N = X * Y * Z;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -836,6 +837,7 @@ struct ListRays {
 template<bool COUNT, int WPE, class Src = ProbeRays>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
 #ifdef ARK_TAIL_PROBE
     const unsigned long long tStart = wall_clock64();
     unsigned long long tEx = 0, itAll = 0, itEx = 0;
@@ -1259,6 +1261,7 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
     __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
     uint32_t cFront = 0;
@@ -1501,6 +1504,7 @@ __device__ __forceinline__ V3 shfl3(V3 v, uint32_t src)
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
 #ifdef ARK_TAIL_PROBE
     const unsigned long long tStart = wall_clock64();
     unsigned long long tEx = 0, itAll = 0, itEx = 0;
@@ -1749,6 +1753,7 @@ __device__ __forceinline__ uint32_t shadowBinKey(const SceneArgs& sc, const Fram
 template<bool REFL = false>
 __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     __shared__ uint32_t bitsL[kGenSpan];
     __shared__ uint32_t waveOff[kGenSteps][4];
     __shared__ uint32_t blockBase;
@@ -1850,6 +1855,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 constexpr uint32_t kBinScanBlock = 1024;
 __global__ void __launch_bounds__(kBinScanBlock) k_shadow_bin_scan(FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     __shared__ uint32_t waveSum[kBinScanBlock / 64];
     const uint32_t bins = f.light_count * f.shadow_bin_grid * f.shadow_bin_grid;
     const uint32_t per = (bins + kBinScanBlock - 1u) / kBinScanBlock;
@@ -1875,6 +1881,7 @@ __global__ void __launch_bounds__(kBinScanBlock) k_shadow_bin_scan(FrameArgs f)
 // start + its rank (grid-stride over the device-side count).
 __global__ void __launch_bounds__(256) k_shadow_scatter(FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     const uint32_t total = *f.shadow_count;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u)
         f.shadow_rays[f.shadow_bin_start[f.shadow_bin_key[i]] + f.shadow_bin_rank[i]] = f.shadow_rays_gen[i];
@@ -1887,20 +1894,27 @@ __global__ void __launch_bounds__(256) k_shadow_scatter(FrameArgs f)
 // cross-queue event wait costs 12-16 us of queue latency per frame, satisfied or not
 // (profiles/r03_v, r03_w); this pair costs two one-wave launches. Every wait ends:
 // the word is written by work enqueued earlier on the other stream, which nothing
-// blocks; after timeout_ticks of the wall clock the wave sets *timed_out and returns
-// (ark_ddgi_synchronize reports it).
+// blocks - unless something serialises the queues (a counter-collecting profiler
+// runs one kernel at a time: the wait can then be scheduled ahead of its signal).
+// The wait therefore fails closed: after timeout_ticks of the wall clock (or at once
+// when an earlier wait of the context already gave up) it sets *timed_out, which
+// every kernel of the path checks at entry (frameAborted: the frame's remaining
+// launches leave their outputs untouched), and the host-mapped *host_flag, which the
+// context's next call polls (ark_ddgi.cpp checkSequencing: ARK_DDGI_E_DEVICE, then
+// event sequencing). Signals are never skipped, so the sequence words stay in step.
 __global__ void __launch_bounds__(64) k_seq_signal(uint32_t* word, uint32_t value)
 {
     if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(64) k_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timed_out, uint64_t timeout_ticks)
+__global__ void __launch_bounds__(64) k_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timed_out, uint32_t* host_flag, uint64_t timeout_ticks)
 {
     if (threadIdx.x != 0) return;
     const uint64_t t0 = wall_clock64();
     while (static_cast<int32_t>(__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - value) < 0) {
-        if (wall_clock64() - t0 > timeout_ticks) {
-            atomicOr(timed_out, 1u);
+        if (wall_clock64() - t0 > timeout_ticks || __hip_atomic_load(timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            __hip_atomic_store(timed_out, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (host_flag) __hip_atomic_store(host_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -2279,9 +2293,9 @@ hipError_t launch_seq_signal(uint32_t* word, uint32_t value, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint64_t timeoutTicks, hipStream_t s)
+hipError_t launch_seq_wait(const uint32_t* word, uint32_t value, uint32_t* timedOut, uint32_t* hostFlag, uint64_t timeoutTicks, hipStream_t s)
 {
-    hipLaunchKernelGGL(dev::k_seq_wait, dim3(1), dim3(64), 0, s, word, value, timedOut, timeoutTicks);
+    hipLaunchKernelGGL(dev::k_seq_wait, dim3(1), dim3(64), 0, s, word, value, timedOut, hostFlag, timeoutTicks);
     return hipGetLastError();
 }
 

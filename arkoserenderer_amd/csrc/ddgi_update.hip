@@ -194,6 +194,7 @@ __device__ __forceinline__ void visibilityOrbitGeneric(const UpdateLds& L, int p
 
 __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     constexpr int IR = ARK_DDGI_IRRADIANCE_RES, VR = ARK_DDGI_VISIBILITY_RES;
     const uint32_t R = f.R;
     const UpdateLds L = updateLds(R);
@@ -381,6 +382,7 @@ __host__ __device__ __forceinline__ uint32_t offsetProbesPerBlock(uint32_t R)
 
 __global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
 {
+    if (frameAborted(f.abort_word)) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t R = f.R;
     const uint32_t P = offsetProbesPerBlock(R);

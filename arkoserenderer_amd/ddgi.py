@@ -172,6 +172,17 @@ class DDGIContext:
     def synchronize(self):
         self.check(self.lib.ark_ddgi_synchronize(self.h), "ark_ddgi_synchronize")
 
+    def set_sequencing(self, device_sequence_words: bool, timeout_ms: int = 0):
+        """ark_ddgi_set_sequencing: device sequence words (True) or events between the
+        context's streams, and the bound of each wait (0 = keep)."""
+        self.check(self.lib.ark_ddgi_set_sequencing(self.h, int(device_sequence_words), int(timeout_ms)), "ark_ddgi_set_sequencing")
+
+    def sequencing(self) -> dict:
+        """ark_ddgi_get_sequencing: {device_sequence_words, timeout_ms, timeouts}."""
+        w, t, n = C.c_int(), C.c_uint32(), C.c_uint32()
+        self.check(self.lib.ark_ddgi_get_sequencing(self.h, C.byref(w), C.byref(t), C.byref(n)), "ark_ddgi_get_sequencing")
+        return {"device_sequence_words": bool(w.value), "timeout_ms": int(t.value), "timeouts": int(n.value)}
+
     def size(self, which: int) -> int:
         n = C.c_uint64()
         self.check(self.lib.ark_ddgi_resource_size(self.h, which, C.byref(n)), "ark_ddgi_resource_size")

@@ -177,6 +177,9 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # a frame-sequencing wait that gave up inside the timed region dropped frames
+    # (fail-closed, ark_ddgi_set_sequencing): that raises here, and no line is printed
+    ctx.synchronize()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

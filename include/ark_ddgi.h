@@ -321,9 +321,24 @@ int ark_ddgi_update(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip
  * starting its traversal on the internal stream (see Frames in flight above). */
 int ark_ddgi_mark_external_write(ArkDdgiCtx* ctx);
 /* Waits for all work of the device; ARK_DDGI_E_DEVICE if a frame-sequencing wait
- * between the context's streams gave up after 10 s (its frame's results are then
- * unspecified). */
+ * between the context's streams gave up (see ark_ddgi_set_sequencing). */
 int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
+
+/* Frame sequencing between the context's streams (no reference counterpart: the
+ * reference records one command buffer per frame, VulkanBackend.cpp:1912-1935).
+ * device_sequence_words = 1 (default): one-wave signal / bounded-wait kernels;
+ * 0: cross-queue events. timeout_ms bounds each wait (0 keeps the current bound;
+ * default 10,000 ms). A wait that gives up FAILS CLOSED: every update kernel that
+ * starts after it skips (atlases, surfels and offsets are left as they were; a
+ * launch already running completes), and the next ark_ddgi_update,
+ * ark_ddgi_exchange_begin or ark_ddgi_synchronize drains the device, returns
+ * ARK_DDGI_E_DEVICE and switches the context to events; the calls after it run
+ * normally. ark_ddgi_get_sequencing reports the mode, the bound and the number of
+ * timeouts reported so far. A context created under a counter-collecting profiler
+ * (ROCPROF_COUNTER_COLLECTION set: kernels run one at a time across queues) starts
+ * with events. */
+int ark_ddgi_set_sequencing(ArkDdgiCtx* ctx, int device_sequence_words, uint32_t timeout_ms);
+int ark_ddgi_get_sequencing(const ArkDdgiCtx* ctx, int* out_device_sequence_words, uint32_t* out_timeout_ms, uint32_t* out_timeouts);
 
 /* ark_ddgi_update for a Z-slab rank that overlaps the atlas exchange with the next
  * frame's primary traversal: the traversal is enqueued at once, the shading work
@@ -344,8 +359,8 @@ int ark_ddgi_update_overlapped(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params
  *       update is complete (as its done_event would say)
  *   ... the caller's all-gather of the atlas bands on comm_stream ...
  *   ark_ddgi_exchange_end(ctx, comm_stream)          marks the exchange complete
- * The waits are one-wave kernels bounded by 10 s (ark_ddgi_synchronize reports a
- * timeout). Same work and results as ark_ddgi_update_overlapped. */
+ * The waits are one-wave kernels, bounded and failing closed as described at
+ * ark_ddgi_set_sequencing. Same work and results as ark_ddgi_update_overlapped. */
 int ark_ddgi_update_exchanged(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params, void* hip_stream);
 int ark_ddgi_exchange_begin(ArkDdgiCtx* ctx, void* comm_stream);
 int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* comm_stream);
