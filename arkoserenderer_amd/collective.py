@@ -83,11 +83,12 @@ class RcclBandExchange:
         for full, off, slab in buffers:
             assert slab * world == full.numel() and off == rank * slab, "Z-slab bands must tile the atlas in rank order"
             self.bufs.append((full.data_ptr(), full.data_ptr() + off, slab))
-        # Every rank reaches the same outcome: rank 0 broadcasts the id with a status
-        # byte (a failed ncclGetUniqueId does not leave the others in the broadcast),
-        # and after ncclCommInitRank the ranks agree (MIN all-reduce) before any rank
-        # uses the communicator, so a failure makes all of them raise (bench.py then
-        # falls back to SlabExchange on every rank).
+        # Every rank reaches the same outcome: before any rank calls ncclCommInitRank
+        # (which would block until all ranks join it), the ranks agree on their local
+        # status - librccl loaded everywhere, the unique id obtained on rank 0 - by a
+        # MIN all-reduce, and raise together if any failed; after ncclCommInitRank they
+        # agree again before any rank uses the communicator. bench.py then falls back
+        # to SlabExchange on every rank.
         dev = buffers[0][0].device
         lib = uid = None
         ok = 1
@@ -98,11 +99,13 @@ class RcclBandExchange:
                 _nccl_check(lib.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         except (OSError, AttributeError, RuntimeError):
             ok = 0
-        t = torch.tensor([ok] + (list(bytes(uid.internal)) if uid is not None else [0] * 128), dtype=torch.uint8, device=dev)
+        status = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(status, op=dist.ReduceOp.MIN, group=group)
+        if int(status.item()) != 1:
+            raise RuntimeError(f"RcclBandExchange: librccl or the ncclUniqueId unavailable on some rank (here: {'ok' if ok else 'failed'})")
+        t = torch.tensor(list(bytes(uid.internal)), dtype=torch.uint8, device=dev)
         dist.broadcast(t, 0, group=group)
-        got = t.cpu().tolist()
-        if not got[0] or lib is None:
-            raise RuntimeError("RcclBandExchange: no ncclUniqueId from rank 0")
+        got = [1] + t.cpu().tolist()
         self.lib = lib
         self.comm = C.c_void_p()
         rc = lib.ncclCommInitRank(C.byref(self.comm), world, _NcclUniqueId((C.c_uint8 * 128)(*got[1:])), rank)

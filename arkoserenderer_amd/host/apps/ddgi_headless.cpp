@@ -15,8 +15,9 @@
 //                 [--world P --rank r --nccl-id FILE]   rank r of P processes (one per GPU), bands
 //                 [--nccl-nonce S]                      exchanged by RCCL all-gather; rank 0 writes
 //                                                       the ncclUniqueId (+ nonce S) to FILE, the
-//                                                       others read it (a file without S, or older
-//                                                       than their own start, is stale: they wait)
+//                                                       others read it (a file without S is stale:
+//                                                       they wait). S is required for P > 1 (one
+//                                                       value per launch, the same on every rank)
 //                 [--save-state FILE] [--load-state FILE] [--first-frame F]
 //                                                       checkpoint of the (unsharded) node after the
 //                                                       last frame / before the first; frame indices
@@ -198,8 +199,9 @@ bool writeFile(const std::string& path, const std::vector<uint8_t>& buf)
 // rendezvous of the RCCL ranks through a shared file: rank 0 removes any old file,
 // then publishes the 128-byte id followed by the launch nonce (written then renamed,
 // so readers never see a partial file). A reader takes only a file with this
-// launch's nonce; without a nonce, only a file written after its own start (a file
-// left by an earlier run holds a dead id, and ncclCommInitRank on it would hang).
+// launch's nonce (a file left by an earlier run holds a dead id, and ncclCommInitRank
+// on it would hang). The nonce is required for P > 1 (main); a 1-rank run reads
+// nothing, so without a nonce the file only has to be newer than the process start.
 bool shareUniqueId(const std::string& path, int rank, const std::string& nonce, std::time_t startedAt, std::vector<uint8_t>& id)
 {
     if (rank == 0) {
@@ -323,6 +325,9 @@ int main(int argc, char** argv)
     scene.camera().setFarClipPlane(zFar);
     scene.camera().setExposure(exposure);
 
+    if (world > 1 && ncclNonce.empty())
+        ARKOSE_LOG(Fatal, "--world %d needs --nccl-nonce S (one value per launch, the same on every rank): a rendezvous file's age "
+                          "cannot tell this launch's id from a stale one", world);
     if (shards < 1 || world < 1 || rank < 0 || rank >= world || (shards > 1 && world > 1) || (world > 1 && ncclIdPath.empty()))
         ARKOSE_LOG(Fatal, "bad sharding arguments (--shards %d, --world %d --rank %d)", shards, world, rank);
     const bool rccl = !ncclIdPath.empty();

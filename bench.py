@@ -14,7 +14,8 @@ times; config C2 (Cornell 8^3 x 64) on the GPU; the CPU baseline (the oracle on 
 box's host cores, one warm-up then the median of >= 5 frames, C4 and C2); the C1 AO
 bake; the DDGI consumers. The roofline object's `achieved` / `frac` are the
 measured HBM traffic of the dominant kernel (a rocprofv3 PMC pass of this same
-library build, matched by its sha256) over its HIP-event launch time; the SURVEY
+library build, matched by its sha256) over that pass's own launch duration (beside
+it, `frac_hip_event`: over this run's HIP-event launch time); the SURVEY
 §8d algorithmic model is kept beside it as `cache_inclusive_frac` (most of its
 node fetches hit L2 / Infinity Cache), with the VALU issue fractions and the
 whole-update figures (roofline()).
@@ -321,8 +322,9 @@ def roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G):
 
     `achieved` / `frac` are MEASURED HBM bytes: (2 FETCH_SIZE + WRITE_SIZE) x 1024 per
     launch (tools/pmc_summary.py; the gfx950 FETCH_SIZE halving of MI355X_MICROARCH.md
-    §HBM) from a rocprofv3 PMC pass of this same library build, divided by this run's
-    HIP-event launch time. The SURVEY §8(d) algorithmic model (80-B nodes and 48-B
+    §HBM) from a rocprofv3 PMC pass of this same library build, divided by that
+    pass's own average launch duration; `achieved_hip_event` / `frac_hip_event` divide
+    the same bytes by this run's HIP-event launch time. The SURVEY §8(d) algorithmic model (80-B nodes and 48-B
     triangles per visit, counter-instrumented visit counts) is kept beside it as
     `cache_inclusive_*`: it counts every node fetch, and most of them are L2 / Infinity
     Cache hits (LDS-cached top nodes included), so it is a cache-inclusive request
@@ -357,12 +359,18 @@ def roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G):
         if any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
             pm, why = None, f"PMC summary {pm.get('tag')} lacks {dom}"
     if pm is not None:
+        # achieved / frac: the PMC pass's bytes over the PMC pass's own average launch
+        # duration (one run, self-consistent); *_hip_event: the same bytes over this
+        # run's HIP-event launch time (the two runs' times differ by a few %)
         traffic = sum(k["hbm_bytes_per_launch"] for k in ks)
+        t_prof = sum(k["avg_ms"] for k in ks) * 1e-3
         roof["traffic"] = int(traffic)
-        roof["achieved"] = round(traffic / t / 1e9, 2)
-        roof["frac"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 4)
+        roof["achieved"] = round(traffic / t_prof / 1e9, 2)
+        roof["frac"] = round(traffic / t_prof / 1e9 / HBM_PEAK_GBS, 4)
         roof["traffic_source"] = pm.get("source")
-        roof["traffic_profile_avg_launch_ms"] = round(sum(k["avg_ms"] for k in ks), 4)
+        roof["traffic_profile_avg_launch_ms"] = round(t_prof * 1e3, 4)
+        roof["achieved_hip_event"] = round(traffic / t / 1e9, 2)
+        roof["frac_hip_event"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 4)
     else:
         roof["traffic_source"] = why
     sq, why_sq = _load_summary(args.sq, lib_sha, "SQ")

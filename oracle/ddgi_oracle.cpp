@@ -20,7 +20,8 @@
 //  * compiled with -ffp-contract=off; vector expressions are evaluated per component
 //    left to right exactly as written in GLSL;
 //  * GLSL transcendentals use ark_fmath.h (same algorithm on CPU and GPU; accuracy
-//    vs libm pinned by tests/test_fmath.py);
+//    vs libm pinned by tests/test_fmath.py) - or glibc's in the -DARK_ORACLE_LIBM
+//    build (libddgi_oracle_libm.so), the independent witness (namespace om below);
 //  * max/min/clamp use fmaxf/fminf (IEEE maxNum) semantics;
 //  * every image store rounds fp32 -> fp16 with round-to-nearest-even; NaN is
 //    canonicalised to 0x7e00.
@@ -42,6 +43,37 @@
 #include <vector>
 
 using namespace ark;
+
+// GLSL transcendentals of the restatement (sin, cos, acos, atan, log2, exp2, pow).
+// Default build (libddgi_oracle.so): ark_fmath.h, the same Cody-Waite + polynomial
+// code the HIP kernels run, so the oracle and the product agree bit for bit.
+// -DARK_ORACLE_LIBM build (libddgi_oracle_libm.so): glibc's
+// sinf/cosf/acosf/atan2f/log2f/exp2f/powf instead, so that this build shares none of
+// the product's transcendental code; tests/test_libm_parity.py and
+// tests/test_gpu_libm_parity.py compare against it at SURVEY §8(d)'s tolerances.
+namespace om {
+#ifdef ARK_ORACLE_LIBM
+inline void sincosf_(float x, float* s, float* c) { *s = ::sinf(x); *c = ::cosf(x); }
+inline float sinf_(float x) { return ::sinf(x); }
+inline float cosf_(float x) { return ::cosf(x); }
+inline float acosf_(float x) { return ::acosf(x); }
+inline float atan2f_(float y, float x) { return ::atan2f(y, x); }
+inline float log2f_(float x) { return ::log2f(x); }
+inline float exp2f_(float x) { return ::exp2f(x); }
+inline float powf_(float x, float y) { return ::powf(x, y); }
+constexpr bool kLibm = true;
+#else
+using ark::sincosf_;
+using ark::sinf_;
+using ark::cosf_;
+using ark::acosf_;
+using ark::atan2f_;
+using ark::log2f_;
+using ark::exp2f_;
+using ark::powf_;
+constexpr bool kLibm = false;
+#endif
+} // namespace om
 
 namespace {
 
@@ -116,7 +148,7 @@ inline float square(float x) { return x * x; }
 // GLSL mix(x, y, a) = x * (1 - a) + y * a
 inline float mixf(float x, float y, float a) { return x * (1.0f - a) + y * a; }
 inline V3 mix3(V3 x, V3 y, float a) { return { mixf(x.x, y.x, a), mixf(x.y, y.y, a), mixf(x.z, y.z, a) }; }
-inline V3 pow3(V3 v, float e) { return { powf_(v.x, e), powf_(v.y, e), powf_(v.z, e) }; }
+inline V3 pow3(V3 v, float e) { return { om::powf_(v.x, e), om::powf_(v.y, e), om::powf_(v.z, e) }; }
 inline V3 splat(float s) { return { s, s, s }; }
 
 // ---------------------------------------------------------------------------
@@ -154,7 +186,7 @@ struct Rng {
         float u = 2.0f * randomFloat() - 1.0f;
         float sr = sqrtf_(1.0f - u * u);
         float s, c;
-        sincosf_(theta, &s, &c);
+        om::sincosf_(theta, &s, &c);
         return { sr * c, sr * s, u };
     }
 };
@@ -163,18 +195,18 @@ struct Rng {
 V3 sphericalFibonacciSample(uint32_t i, uint32_t n)
 {
     float theta = kTwoPi * static_cast<float>(i) / kGoldenRatio;
-    float phi = acosf_(2.0f * (static_cast<float>(i) / static_cast<float>(n)) - 1.0f);
-    float sinPhi = sinf_(phi);
+    float phi = om::acosf_(2.0f * (static_cast<float>(i) / static_cast<float>(n)) - 1.0f);
+    float sinPhi = om::sinf_(phi);
     float st, ct;
-    sincosf_(theta, &st, &ct);
-    return { ct * sinPhi, st * sinPhi, cosf_(phi) };
+    om::sincosf_(theta, &st, &ct);
+    return { ct * sinPhi, st * sinPhi, om::cosf_(phi) };
 }
 
 // common.glsl:133-142 (Rodrigues)
 V3 axisAngleRotate(V3 v, V3 k, float angle)
 {
     float s, c;
-    sincosf_(angle, &s, &c);
+    om::sincosf_(angle, &s, &c);
     return v * c + cross(k, v) * s + k * dot(k, v) * (1.0f - c);
 }
 
@@ -224,8 +256,8 @@ V3 octahedralDecode(float ox, float oy)
 // common/spherical.glsl:6-13
 void sphericalUvFromDirection(V3 d, float* u, float* v)
 {
-    float phi = atan2f_(d.z, d.x);
-    float theta = acosf_(clampf(d.y, -1.0f, 1.0f));
+    float phi = om::atan2f_(d.z, d.x);
+    float theta = om::acosf_(clampf(d.y, -1.0f, 1.0f));
     if (phi < 0.0f) phi += kTwoPi;
     *u = phi / kTwoPi;
     *v = theta / kPi;
@@ -276,7 +308,7 @@ struct Tex {
 
 float srgbToLinear(float c)
 {
-    return c <= 0.04045f ? c / 12.92f : powf_((c + 0.055f) / 1.055f, 2.4f);
+    return c <= 0.04045f ? c / 12.92f : om::powf_((c + 0.055f) / 1.055f, 2.4f);
 }
 
 Tex makeTex(const ArkTexture& t)
@@ -756,10 +788,10 @@ float D_GGX(float NdotH, float a) // brdf.glsl:17-22
     float x = a2 / (kPi * f * f + 1e-20f);
     return x;
 }
-float F_Schlick1(float VdotH, float f0) { return f0 + (1.0f - f0) * powf_(1.0f - VdotH, 5.0f); } // :24-26
+float F_Schlick1(float VdotH, float f0) { return f0 + (1.0f - f0) * om::powf_(1.0f - VdotH, 5.0f); } // :24-26
 V3 F_Schlick3(float VdotH, V3 f0) // :28-30
 {
-    float p = powf_(1.0f - VdotH, 5.0f);
+    float p = om::powf_(1.0f - VdotH, 5.0f);
     return f0 + (splat(1.0f) - f0) * p;
 }
 float V_SmithGGXCorrelated(float NdotV, float NdotL, float a) // :43-48
@@ -814,8 +846,8 @@ float evaluateIESLookupTable(const Tex& lut, float outerConeHalfAngle, V3 m0, V3
     if (angleV <= 0.0f) return 0.0f;
     float hx = dot(lightRayDir, m0);
     float hy = dot(lightRayDir, m1);
-    float angleH = atan2f_(hy, hx) + kPi;
-    float lx = acosf_(angleV) / (2.0f * outerConeHalfAngle);
+    float angleH = om::atan2f_(hy, hx) + kPi;
+    float lx = om::acosf_(angleV) / (2.0f * outerConeHalfAngle);
     float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
     float c[4];
     sampleBilinear(lut, lx, ly, c);
@@ -946,7 +978,7 @@ V3 sampleDynamicDiffuseGlobalIllumination(const Oracle& o, V3 P, V3 N, V3 Vw)
         V3 directionToProbe = normalize(pointToProbe);
         V3 unbiasedDirectionToProbe = normalize(probePos - P);
         const float smoothFloor = 0.02f, additionalSmoothening = 0.25f;
-        weight *= smoothFloor + (1.0f - smoothFloor) * powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
+        weight *= smoothFloor + (1.0f - smoothFloor) * om::powf_(saturate(dot(unbiasedDirectionToProbe, N)), additionalSmoothening);
         {
             float u, v;
             atlasSampleUV(g, px, py, pz, -directionToProbe, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, invWv, invHv, &u, &v);
@@ -1413,7 +1445,7 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                 atlasTexelCoord(g, probeIdx, tx, ty, ARK_DDGI_VISIBILITY_RES, ARK_DDGI_ATLAS_PADDING, &ax, &ay);
                 float nv0 = 0.0f, nv1 = 0.0f, totalWeight = 0.0f;
                 for (uint32_t s = 0; s < R; ++s) {
-                    float weight = powf_(fmaxf_(0.0f, dotFma(texelDirection, dirs[s])), p->visibility_sharpness);
+                    float weight = om::powf_(fmaxf_(0.0f, dotFma(texelDirection, dirs[s])), p->visibility_sharpness);
                     float d = f16_to_f32(sf[s * 4 + 3]);
                     d = fminf_(fabsf_(d), maxDistance);
                     nv0 = fmaf(weight, d, nv0);
@@ -1499,7 +1531,7 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                 offset = offset - currentOffset * stepSize;
             V3 newOffset = currentOffset + offset;
             if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-            newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * p->delta_time));
+            newOffset = mix3(newOffset, currentOffset, om::exp2f_(-lerpSpeed * p->delta_time));
             cur[0] = newOffset.x;
             cur[1] = newOffset.y;
             cur[2] = newOffset.z;
@@ -1784,8 +1816,8 @@ int oracle_rt_reflections(void* ctx, const ArkReflectionsDesc* r, int threads)
         const V3 T2 = cross(Vh, T1);
         const float rr = sqrtf_(rx);
         const float phi = 2.0f * kPi * ry;
-        const float t1 = rr * cosf_(phi);
-        float t2 = rr * sinf_(phi);
+        const float t1 = rr * om::cosf_(phi);
+        float t2 = rr * om::sinf_(phi);
         const float sh = 0.5f * (1.0f + Vh.z);
         t2 = (1.0f - sh) * sqrtf_(1.0f - t1 * t1) + sh * t2;
         const V3 Nh = t1 * T1 + t2 * T2 + sqrtf_(fmaxf_(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
@@ -1893,18 +1925,21 @@ void oracle_f16_to_f32(const uint16_t* in, float* out, uint64_t n)
 {
     for (uint64_t i = 0; i < n; ++i) out[i] = f16_to_f32(in[i]);
 }
-// op: 0 sin 1 cos 2 acos 3 atan2 4 log2 5 exp2 6 pow
+// 1 for the -DARK_ORACLE_LIBM build (glibc transcendentals), 0 for the default build
+int oracle_math_is_libm() { return om::kLibm ? 1 : 0; }
+
+// ark_fmath.h on the host (both builds): op: 0 sin 1 cos 2 acos 3 atan2 4 log2 5 exp2 6 pow
 void oracle_fmath(int op, const float* x, const float* y, float* out, uint64_t n)
 {
     for (uint64_t i = 0; i < n; ++i) {
         switch (op) {
-        case 0: out[i] = sinf_(x[i]); break;
-        case 1: out[i] = cosf_(x[i]); break;
-        case 2: out[i] = acosf_(x[i]); break;
-        case 3: out[i] = atan2f_(x[i], y[i]); break;
-        case 4: out[i] = log2f_(x[i]); break;
-        case 5: out[i] = exp2f_(x[i]); break;
-        case 6: out[i] = powf_(x[i], y[i]); break;
+        case 0: out[i] = ark::sinf_(x[i]); break;
+        case 1: out[i] = ark::cosf_(x[i]); break;
+        case 2: out[i] = ark::acosf_(x[i]); break;
+        case 3: out[i] = ark::atan2f_(x[i], y[i]); break;
+        case 4: out[i] = ark::log2f_(x[i]); break;
+        case 5: out[i] = ark::exp2f_(x[i]); break;
+        case 6: out[i] = ark::powf_(x[i], y[i]); break;
         default: out[i] = 0; break;
         }
     }

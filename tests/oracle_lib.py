@@ -14,16 +14,21 @@ from arkoserenderer_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_PATH = os.path.join(ROOT, "oracle", "build", "libddgi_oracle.so")
+# the -DARK_ORACLE_LIBM build: glibc transcendentals instead of ark_fmath.h (the
+# independent witness, oracle/Makefile)
+ORACLE_LIBM_PATH = os.path.join(ROOT, "oracle", "build", "libddgi_oracle_libm.so")
 
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(ORACLE_PATH):
-            raise RuntimeError(f"oracle not built: {ORACLE_PATH} (run __graft_entry__.build())")
-        lib = C.CDLL(ORACLE_PATH)
+def load(libm: bool = False):
+    """The oracle library: the bit-exact build (ark_fmath.h), or with libm=True the
+    glibc-math build."""
+    if libm not in _libs:
+        path = ORACLE_LIBM_PATH if libm else ORACLE_PATH
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: {path} (run __graft_entry__.build())")
+        lib = C.CDLL(path)
         lib.oracle_create.restype = C.c_void_p
         lib.oracle_create.argtypes = [C.POINTER(abi.ArkDdgiDesc)]
         lib.oracle_destroy.argtypes = [C.c_void_p]
@@ -50,15 +55,18 @@ def load():
         lib.oracle_lighting_compose.argtypes = [C.c_void_p, C.POINTER(abi.ArkComposeDesc), C.c_int]
         lib.oracle_rt_reflections.argtypes = [C.c_void_p, C.POINTER(abi.ArkReflectionsDesc), C.c_int]
         lib.oracle_probe_debug.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
-        _lib = lib
-    return _lib
+        lib.oracle_math_is_libm.restype = C.c_int
+        if lib.oracle_math_is_libm() != int(libm):
+            raise RuntimeError(f"{path}: oracle_math_is_libm() = {lib.oracle_math_is_libm()}, expected {int(libm)}")
+        _libs[libm] = lib
+    return _libs[libm]
 
 
 class Oracle:
     """CPU restatement of the DDGI node; same inputs as the C-ABI."""
 
-    def __init__(self, desc: abi.ArkDdgiDesc):
-        self.lib = load()
+    def __init__(self, desc: abi.ArkDdgiDesc, libm: bool = False):
+        self.lib = load(libm)
         self.desc = desc
         self.h = self.lib.oracle_create(C.byref(desc))
         if not self.h:

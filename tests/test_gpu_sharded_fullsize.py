@@ -15,7 +15,12 @@ exchange), for 2 frames. Checked:
     border) and owner offsets, bit for bit, as test_gpu_fullsize.py does unsharded.
 
 P = 8 slabs are 4 probe layers deep (a 4,096-probe, 1 M-ray window per rank): the
-half-occupancy pipelined traversal (below 5 M rays) and 4-layer slot compaction run."""
+half-occupancy pipelined traversal (below 5 M rays) and 4-layer slot compaction run.
+
+The same for BASELINE config 5 (the C5 substitute: instanced city block, 48x16x48
+probes x 512 rays, sun + 4 IES spot lights, i.e. 5 shadow rays per lit hit,
+opaque.rchit:152-158) as 8 slabs of 6 layers (a 4,608-probe, 2.4 M-ray window per
+rank; VERDICT r03 "do this" #2)."""
 import numpy as np
 import pytest
 
@@ -40,24 +45,20 @@ def _tile_mask(dims, probes, res):
     return m
 
 
-@pytest.mark.parametrize("P", [8])
-def test_c4_eight_zslabs_one_gpu_full_size(P):
+def _sharded_full_size(scene, dims, spacing, origin, R, z_far, exposure, P):
     import torch
 
     from arkoserenderer_amd.collective import device_bytes
 
-    scene = S.soup(10_000_000)
-    dims = (32, 32, 32)
     X, Y, Z = dims
-    grid = D.ProbeGrid(dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
-    N, R, Zs = grid.probe_count(), 256, Z // P
-    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    grid = D.ProbeGrid(dims, spacing, origin)
+    N, Zs = grid.probe_count(), Z // P
     cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    full = D.DDGIContext(grid, 10000.0, cfg)
+    full = D.DDGIContext(grid, z_far, cfg)
     full.set_scene(scene)
-    slabs = [D.DDGIContext(grid, 10000.0, cfg, 0, r, P) for r in range(P)]
+    slabs = [D.DDGIContext(grid, z_far, cfg, 0, r, P) for r in range(P)]
     for c in slabs:
         c.share_scene(full)
     views = [c.device_views() for c in slabs]
@@ -74,7 +75,7 @@ def test_c4_eight_zslabs_one_gpu_full_size(P):
     zof = (np.arange(N) % (X * Z)) // X
     owner = zof // Zs
     ocfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=X, max_rays_per_probe=R, max_probe_updates=X, compute_probe_offsets=True)
-    orc = O.Oracle(D.desc_for(grid, 10000.0, ocfg))
+    orc = O.Oracle(D.desc_for(grid, z_far, ocfg))
     orc.set_scene(scene, threads=16)
     # one x-row of X probes per slab: z = the slab's 2nd layer (or its 1st), y spread
     windows = [(r, X * (r * Zs + (r % 2) * (Zs // 2)) + X * Z * ((5 * r + 3) % Y)) for r in range(P)]
@@ -141,3 +142,18 @@ def test_c4_eight_zslabs_one_gpu_full_size(P):
     for c in slabs + [full]:
         c.close()
     orc.close()
+
+
+@pytest.mark.parametrize("P", [8])
+def test_c4_eight_zslabs_one_gpu_full_size(P):
+    _sharded_full_size(S.soup(10_000_000), (32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), 256, 10000.0,
+                       dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), P)
+
+
+@pytest.mark.parametrize("P", [8])
+def test_c5_eight_zslabs_one_gpu_full_size(P):
+    """C5 substitute as 8 Z-slabs of 6 layers: R = 512 slab windows, per-slab spot
+    shadow lists (sun + 4 IES spots), 2 frames (probeSampling.glsl:64-163 reads the
+    gathered frame-0 atlases in frame 1)."""
+    _sharded_full_size(S.city_block(), (48, 16, 48), (5.0, 2.5, 5.0), (2.5, 0.5, 2.5), 512, 1000.0,
+                       dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), P)
