@@ -443,6 +443,7 @@ EXPORTS = {
     "ark_ddgi_debug_struct_sizes": (C.c_int, [C.POINTER(C.c_uint32), C.c_int]),
     "ark_ddgi_debug_bvh8_check": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_bvh8_trace_stats": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
+    "ark_ddgi_debug_sun_bvh_check": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_float, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

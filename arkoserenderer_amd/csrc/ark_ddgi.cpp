@@ -130,6 +130,8 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 struct SceneStore {
     int device = 0;
     DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
+    DeviceBuffer sunNodes; // light-space BVH8 of the sun's shadow rays + its world-space triangle records
+    uint64_t sunBvhNodes = 0;
     std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
     std::vector<ArkRTTriangleMesh> meshHost;
     SceneArgs args {};
@@ -143,7 +145,7 @@ struct SceneStore {
     ~SceneStore()
     {
         (void)hipSetDevice(device);
-        for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &spots })
+        for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &spots, &sunNodes })
             b->release();
     }
 };
@@ -187,6 +189,7 @@ struct ArkDdgiCtx {
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
+    bool sunBvh = true;            // ARK_SUN_BVH=0: the sun's shadow rays traverse the world BVHs
     uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined window below kPipeHalfRays rays
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
@@ -512,6 +515,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
+        if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0;
         if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
         // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
         // across queues: a polling wait could then hold the GPU while the kernel it
@@ -617,6 +621,46 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
 
 const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx) { return ctx ? ctx->lastError.c_str() : "null context"; }
 
+// Structural check of a BVH8 before anything reaches the GPU: every node is
+// referenced once from a root-reachable parent (no cycles, no sharing), every leaf's
+// triangles lie inside the triangle array and every triangle (every record but the
+// holes of the rows) is covered once.
+static int checkBvh8(ArkDdgiCtx* ctx, const std::vector<GpuBvh8Node>& allNodes, const std::vector<GpuTriangle>& allTris, const int32_t* roots, int nRoots)
+{
+    std::vector<uint8_t> seenNode(allNodes.size(), 0);
+    std::vector<uint8_t> seenTri(allTris.size(), 0);
+    std::vector<uint32_t> work;
+    for (int c = 0; c < nRoots; ++c)
+        if (roots[c] >= 0) work.push_back(static_cast<uint32_t>(roots[c]));
+    while (!work.empty()) {
+        const uint32_t n = work.back();
+        work.pop_back();
+        if (n >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u", n);
+        seenNode[n] = 1;
+        const GpuBvh8Node& nd = allNodes[n];
+        uint32_t internal = 0;
+        if ((nd.leaf_tris >> 24) || (nd.leaf_mask & nd.imask)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
+        for (int sl = 0; sl < 8; ++sl) {
+            const bool isInternal = (nd.imask >> sl) & 1u;
+            uint32_t slotTris[kBvh8MaxLeafSize];
+            const int cnt = bvh8SlotTriangles(nd, sl, slotTris);
+            if (cnt < 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
+            if (isInternal) work.push_back(nd.child_base + internal++);
+            for (int i = 0; i < cnt; ++i) {
+                const uint32_t t = slotTris[i];
+                if (t >= allTris.size() || isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
+                if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
+                seenTri[t] = 1;
+            }
+            for (int a = 0; a < 3; ++a)
+                if ((isInternal || cnt > 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
+        }
+    }
+    for (size_t t = 0; t < seenTri.size(); ++t)
+        if (!seenTri[t] && !isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
+    return ARK_DDGI_OK;
+}
+
 int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
@@ -706,6 +750,17 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
     if (const char* e = std::getenv("ARK_BVH8_NODE_COST")) copt.node_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
+    // the sun's light-space BVH input, before the class builds free their triangles
+    const bool sunBvh = s->has_directional_light && ctx->sunBvh;
+    SunBvhInput sunIn;
+    if (sunBvh) {
+        sun_frame(s->directional_light.world_space_direction, sunIn.frame);
+        size_t total = 0;
+        for (int c = 0; c < 3; ++c) total += cls[c].size();
+        sunIn.tris.reserve(total);
+        sunIn.world.reserve(total);
+        for (int c = 0; c < 3; ++c) sun_add_triangles(sunIn, cls[c]);
+    }
     std::vector<GpuBvh8Node> allNodes;
     std::vector<GpuTriangle> allTris;
     int32_t roots[3] = { -1, -1, -1 };
@@ -729,43 +784,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
     }
     if (allNodes.size() >= (1ull << 31) || allTris.size() >= (1ull << 31)) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "scene too large for 31-bit BVH indices");
-    // Structural check before anything reaches the GPU: every node is referenced
-    // once from a root-reachable parent (no cycles, no sharing), every leaf's
-    // triangles lie inside the triangle array and every triangle (every record but
-    // the holes of the rows) is covered once.
-    {
-        std::vector<uint8_t> seenNode(allNodes.size(), 0);
-        std::vector<uint8_t> seenTri(allTris.size(), 0);
-        std::vector<uint32_t> work;
-        for (int c = 0; c < 3; ++c)
-            if (roots[c] >= 0) work.push_back(static_cast<uint32_t>(roots[c]));
-        while (!work.empty()) {
-            const uint32_t n = work.back();
-            work.pop_back();
-            if (n >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u", n);
-            seenNode[n] = 1;
-            const GpuBvh8Node& nd = allNodes[n];
-            uint32_t internal = 0;
-            if ((nd.leaf_tris >> 24) || (nd.leaf_mask & nd.imask)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
-            for (int sl = 0; sl < 8; ++sl) {
-                const bool isInternal = (nd.imask >> sl) & 1u;
-                uint32_t slotTris[kBvh8MaxLeafSize];
-                const int cnt = bvh8SlotTriangles(nd, sl, slotTris);
-                if (cnt < 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
-                if (isInternal) work.push_back(nd.child_base + internal++);
-                for (int i = 0; i < cnt; ++i) {
-                    const uint32_t t = slotTris[i];
-                    if (t >= allTris.size() || isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
-                    if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
-                    seenTri[t] = 1;
-                }
-                for (int a = 0; a < 3; ++a)
-                    if ((isInternal || cnt > 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
-            }
-        }
-        for (size_t t = 0; t < seenTri.size(); ++t)
-            if (!seenTri[t] && !isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
-    }
+    if (const int rc = checkBvh8(ctx, allNodes, allTris, roots, 3)) return rc;
     // textures: decoded to float4 texels (sRGB EOTF per texel), + trailing 1x1 white
     std::vector<GpuTextureInfo> infos;
     std::vector<float> texels;
@@ -834,6 +853,22 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     allTris.push_back(GpuTriangle {}); // padding: a five-load fetch of the last triangle stays in bounds (ARK_FETCH5)
     ARK_HIP(hipMemcpy(static_cast<char*>(st->nodes.ptr) + triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
     allTris.pop_back();
+    uint64_t sunNodeCount = 0;
+    size_t sunTriOffset = 0;
+    if (sunBvh && !sunIn.tris.empty()) {
+        Bvh8BuildResult r;
+        if (!build_sun_bvh(sunIn, opt, copt, r)) return ctx->fail(ARK_DDGI_E_DEVICE, "sun BVH2 leaf over %d triangles", kBvh8MaxLeafSize);
+        const int32_t sroot = 0;
+        if (const int rc2 = checkBvh8(ctx, r.nodes, r.tris, &sroot, 1)) return rc2;
+        const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
+        sunTriOffset = (nb + 255) & ~static_cast<size_t>(255);
+        r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
+        ARK_HIP(st->sunNodes.alloc(sunTriOffset + r.tris.size() * sizeof(GpuTriangle)));
+        ARK_HIP(hipMemcpy(st->sunNodes.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice));
+        ARK_HIP(hipMemcpy(static_cast<char*>(st->sunNodes.ptr) + sunTriOffset, r.tris.data(), r.tris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
+        sunNodeCount = r.nodes.size();
+    }
+    std::vector<GpuTriangle>().swap(sunIn.world);
     if ((rc = upload(ctx, st->indices, s->indices, s->index_count)) != 0) return rc;
     if ((rc = upload(ctx, st->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
     if ((rc = upload(ctx, st->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
@@ -896,6 +931,15 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     }
     sc.spot_count = static_cast<int32_t>(s->spot_light_count);
     sc.spots = st->spots.as<GpuSpotLight>();
+    sc.sun_root = -1;
+    if (sunNodeCount) {
+        sc.sun_nodes = st->sunNodes.as<GpuBvh8Node>();
+        sc.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st->sunNodes.ptr) + sunTriOffset);
+        sc.sun_root = 0;
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) sc.sun_frame[r * 3 + k] = static_cast<float>(sunIn.frame[r][k]);
+    }
+    st->sunBvhNodes = sunNodeCount;
     st->bvhMaxDepth = maxDepth;
     if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
     st->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
@@ -1140,6 +1184,15 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     }
     f.shadow_count = f.ray_counter + kShadowCountWord;
     f.shadow_heads = f.ray_counter + kShadowHeadWord;
+    // the sun's shadow rays in their own list (the first Kmax x Rmax entries of the
+    // list area, the other lights' after them) for the light-space BVH
+    if (ctx->scene.sun_root >= 0 && f.shadow_bin_grid == 0) {
+        f.sun_rays = f.shadow_rays;
+        f.shadow_rays += Kmax * Rmax;
+        f.shadow_rays_gen = f.shadow_rays;
+        f.sun_count = f.ray_counter + kSunCountWord;
+        f.sun_heads = f.ray_counter + kSunHeadWord;
+    }
     // the slot table and the primary traversal: on traceStream after frame n - 2 (the
     // last user of buffer set b) when pipelined, else in line on the caller's stream
     const hipStream_t ts = pipe ? ctx->traceStream : s;

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 
@@ -36,6 +37,15 @@ struct Aabb {
         float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
         if (!(d0 >= 0.0f)) return 0.0f;
         return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+    // SAH surface with per-face weights w = {xy, yz, zx} (BvhBuildOptions::area_w):
+    // {1, 1, 1} is the surface area; rays parallel to z (the light-space BVH of the
+    // sun's shadow rays) cross a box with a probability proportional to its xy face
+    float area(const float* w) const
+    {
+        float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+        if (!(d0 >= 0.0f)) return 0.0f;
+        return 2.0f * (w[0] * d0 * d1 + w[1] * d1 * d2 + w[2] * d2 * d0);
     }
 };
 
@@ -86,21 +96,7 @@ public:
         m_nodes.resize(m_nodeCount);
         res.nodes = std::move(m_nodes);
         res.tris.resize(n);
-        for (uint32_t i = 0; i < n; ++i) {
-            const BuildTriangle& t = tris[m_idx[i]];
-            GpuTriangle& g = res.tris[i];
-            float e1[3], e2[3];
-            for (int a = 0; a < 3; ++a) {
-                e1[a] = t.v1[a] - t.v0[a];
-                e2[a] = t.v2[a] - t.v0[a];
-            }
-            g.t0[0] = t.v0[0]; g.t0[1] = t.v0[1]; g.t0[2] = t.v0[2]; g.t0[3] = e1[0];
-            g.t1[0] = e1[1]; g.t1[1] = e1[2]; g.t1[2] = e2[0]; g.t1[3] = e2[1];
-            g.t2[0] = e2[2];
-            std::memcpy(&g.t2[1], &t.instance, 4);
-            std::memcpy(&g.t2[2], &t.primitive, 4);
-            std::memcpy(&g.t2[3], &t.flip_facing, 4);
-        }
+        for (uint32_t i = 0; i < n; ++i) res.tris[i] = make_gpu_triangle(tris[m_idx[i]]);
         res.max_depth = m_maxDepth.load();
         res.max_leaf = m_maxLeaf.load();
         res.sah_cost = sahCost(res.nodes, root.box);
@@ -204,7 +200,7 @@ private:
                 for (int k = 0; k < B - 1; ++k) {
                     acc.grow(bb[k]);
                     n += bc[k];
-                    leftArea[k] = acc.area();
+                    leftArea[k] = acc.area(m_opt.area_w);
                     leftCount[k] = n;
                 }
                 Aabb accR;
@@ -214,7 +210,7 @@ private:
                     nr += bc[k];
                     const uint32_t nl = leftCount[k - 1];
                     if (nl == 0 || nr == 0) continue;
-                    const float cost = leftArea[k - 1] * nl + accR.area() * nr;
+                    const float cost = leftArea[k - 1] * nl + accR.area(m_opt.area_w) * nr;
                     if (cost < bestCost) {
                         bestCost = cost;
                         bestAxis = a;
@@ -222,7 +218,7 @@ private:
                     }
                 }
             }
-            const float area = box.area();
+            const float area = box.area(m_opt.area_w);
             const float splitCost = m_opt.traversal_cost + (area > 0.0f ? bestCost / area : 0.0f) * m_opt.intersection_cost;
             const float leafCost = m_opt.intersection_cost * count;
             if (static_cast<int>(count) <= maxLeaf && (bestAxis < 0 || leafCost <= splitCost)) split = false;
@@ -406,6 +402,23 @@ uint32_t leafRowStride(const uint32_t cnt[8])
 
 } // namespace
 
+GpuTriangle make_gpu_triangle(const BuildTriangle& t)
+{
+    GpuTriangle g;
+    float e1[3], e2[3];
+    for (int a = 0; a < 3; ++a) {
+        e1[a] = t.v1[a] - t.v0[a];
+        e2[a] = t.v2[a] - t.v0[a];
+    }
+    g.t0[0] = t.v0[0]; g.t0[1] = t.v0[1]; g.t0[2] = t.v0[2]; g.t0[3] = e1[0];
+    g.t1[0] = e1[1]; g.t1[1] = e1[2]; g.t1[2] = e2[0]; g.t1[3] = e2[1];
+    g.t2[0] = e2[2];
+    std::memcpy(&g.t2[1], &t.instance, 4);
+    std::memcpy(&g.t2[2], &t.primitive, 4);
+    std::memcpy(&g.t2[3], &t.flip_facing, 4);
+    return g;
+}
+
 GpuTriangle holeTriangle()
 {
     GpuTriangle t;
@@ -469,19 +482,21 @@ struct CollapsePlan {
     std::vector<uint8_t> pick;  // [node][8]: i = 1: 0 node, 1 leaf; i >= 2: 0 = as i - 1, else k slots to the left child
     std::vector<uint32_t> first, count; // triangle range of the subtree (leaf order)
     float cNode = 1.0f, cTri = 1.0f;
+    float areaW[3] = { 1.0f, 1.0f, 1.0f };
 };
 
 float childCost(const CollapsePlan& P, const Child8& c, int i)
 {
     if (c.code >= 0) return P.cost[8u * static_cast<uint32_t>(c.code) + (i - 1)];
-    return P.cTri * c.box.area() * static_cast<float>((static_cast<uint32_t>(~c.code) & (kMaxLeafSize - 1)) + 1);
+    return P.cTri * c.box.area(P.areaW) * static_cast<float>((static_cast<uint32_t>(~c.code) & (kMaxLeafSize - 1)) + 1);
 }
 
-CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri)
+CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri, const float* areaW)
 {
     CollapsePlan P;
     P.cNode = cNode;
     P.cTri = cTri;
+    for (int k = 0; k < 3; ++k) P.areaW[k] = areaW[k];
     const size_t N = bvh2.nodes.size();
     P.cost.assign(8 * N, 0.0f);
     P.pick.assign(8 * N, 0);
@@ -507,7 +522,7 @@ CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri)
         P.count[k] = tot;
         Aabb box;
         for (int c = 0; c < m; ++c) box.grow(ch[c].box);
-        const float area = box.area();
+        const float area = box.area(P.areaW);
         float* C = &P.cost[8 * k];
         uint8_t* pk = &P.pick[8 * k];
         // distributions of j slots over the two subtrees
@@ -580,7 +595,7 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
     Bvh8BuildResult res;
     if (bvh2.nodes.empty()) return res;
     CollapsePlan plan;
-    if (copt.sah_optimal) plan = planCollapse(bvh2, copt.node_cost, copt.tri_cost);
+    if (copt.sah_optimal) plan = planCollapse(bvh2, copt.node_cost, copt.tri_cost, copt.area_w);
     struct Item {
         uint32_t src;
         uint32_t dst;
@@ -671,24 +686,38 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
         static const bool leafOctant = std::getenv("ARK_BVH8_LEAF_SLOTS") && std::strcmp(std::getenv("ARK_BVH8_LEAF_SLOTS"), "octant") == 0;
         Cand cand[64];
         int nc = 0;
-        for (int c = 0; c < n; ++c)
-            for (int s = 0; s < 8; ++s) {
-                if (!leafOctant && ch[c].code < 0) break;
-                float sc = 0.0f;
-                for (int a = 0; a < 3; ++a) {
-                    const float off = 0.5f * (ch[c].box.lo[a] + ch[c].box.hi[a]) - pc[a];
-                    sc += ((s >> a) & 1) ? off : -off;
-                }
-                cand[nc++] = { sc, c, s };
-            }
-        std::stable_sort(cand, cand + nc, [](const Cand& x, const Cand& y) { return x.score > y.score; });
         int slotOf[8], childIn[8];
         for (int k = 0; k < 8; ++k) slotOf[k] = childIn[k] = -1;
-        for (int k = 0; k < nc; ++k)
-            if (slotOf[cand[k].c] < 0 && childIn[cand[k].s] < 0) {
-                slotOf[cand[k].c] = cand[k].s;
-                childIn[cand[k].s] = cand[k].c;
+        if (copt.slot_sort_axis >= 0 && copt.slot_sort_axis < 3) {
+            // one ray direction (+axis): internal children in slots 0, 1, ... by the
+            // lower bound of their box along it, the order a ray from below meets them
+            const int ax = copt.slot_sort_axis;
+            int internal[8], ni = 0;
+            for (int c = 0; c < n; ++c)
+                if (ch[c].code >= 0 || leafOctant) internal[ni++] = c;
+            std::stable_sort(internal, internal + ni, [&](int a, int b) { return ch[a].box.lo[ax] < ch[b].box.lo[ax]; });
+            for (int k = 0; k < ni; ++k) {
+                slotOf[internal[k]] = k;
+                childIn[k] = internal[k];
             }
+        } else {
+            for (int c = 0; c < n; ++c)
+                for (int s = 0; s < 8; ++s) {
+                    if (!leafOctant && ch[c].code < 0) break;
+                    float sc = 0.0f;
+                    for (int a = 0; a < 3; ++a) {
+                        const float off = 0.5f * (ch[c].box.lo[a] + ch[c].box.hi[a]) - pc[a];
+                        sc += ((s >> a) & 1) ? off : -off;
+                    }
+                    cand[nc++] = { sc, c, s };
+                }
+            std::stable_sort(cand, cand + nc, [](const Cand& x, const Cand& y) { return x.score > y.score; });
+            for (int k = 0; k < nc; ++k)
+                if (slotOf[cand[k].c] < 0 && childIn[cand[k].s] < 0) {
+                    slotOf[cand[k].c] = cand[k].s;
+                    childIn[cand[k].s] = cand[k].c;
+                }
+        }
         if (!leafOctant) {
             int leaves[8], nl = 0;
             for (int c = 0; c < n; ++c)
@@ -884,6 +913,113 @@ extern "C" int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uin
     return violations == 0 ? 0 : 1;
 }
 
+namespace ark {
+
+// The sun's shadow rays (opaque.rchit:35-54, the sun branch :56-73) all travel along
+// L = -normalize(sun direction) - the fp32 value k_shadow_gen gives them. In the
+// orthonormal frame (u, v, w = L / |L|) they are rays along +w: a child box is crossed
+// iff the ray's (u, v) lies in the box's u-v rectangle and the box reaches above its
+// origin, a containment test in the node's quantized grid with no division and no
+// per-child multiply (k_trace_shadow<SUN>, visitNodeSun). The light-space BVH holds
+// every triangle of every hit-mask class (shadow rays test all three with the Opaque
+// flag, no alpha test) with the world-space triangle records, so the any-hit tests and
+// their results are those of the world BVHs.
+void sun_frame(const float sunDir[3], double frame[3][3])
+{
+    // L = -normalize(dir) in fp32, the operation order of normalize() in the kernels
+    // (v * (1 / sqrt(dot(v, v))), dot left to right)
+    const float dd = sunDir[0] * sunDir[0] + sunDir[1] * sunDir[1] + sunDir[2] * sunDir[2];
+    const float sc = 1.0f / std::sqrt(dd);
+    const float L[3] = { -(sunDir[0] * sc), -(sunDir[1] * sc), -(sunDir[2] * sc) };
+    double w[3] = { L[0], L[1], L[2] };
+    const double wl = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    for (double& x : w) x /= wl;
+    const double h[3] = { std::fabs(w[0]) < 0.9 ? 1.0 : 0.0, std::fabs(w[0]) < 0.9 ? 0.0 : 1.0, 0.0 };
+    double u[3] = { h[1] * w[2] - h[2] * w[1], h[2] * w[0] - h[0] * w[2], h[0] * w[1] - h[1] * w[0] };
+    const double ul = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    for (double& x : u) x /= ul;
+    const double v[3] = { w[1] * u[2] - w[2] * u[1], w[2] * u[0] - w[0] * u[2], w[0] * u[1] - w[1] * u[0] };
+    for (int k = 0; k < 3; ++k) {
+        frame[0][k] = u[k];
+        frame[1][k] = v[k];
+        frame[2][k] = w[k];
+    }
+}
+
+void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris)
+{
+    for (const BuildTriangle& t : tris) {
+        const GpuTriangle rec = make_gpu_triangle(t);
+        // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2 (exact, from the record)
+        double V[3][3];
+        for (int a = 0; a < 3; ++a) V[0][a] = rec.t0[a];
+        const double e1[3] = { rec.t0[3], rec.t1[0], rec.t1[1] }, e2[3] = { rec.t1[2], rec.t1[3], rec.t2[0] };
+        for (int a = 0; a < 3; ++a) {
+            V[1][a] = V[0][a] + e1[a];
+            V[2][a] = V[0][a] + e2[a];
+            in.maxAbs = std::max(in.maxAbs, static_cast<float>(std::max({ std::fabs(V[0][a]), std::fabs(V[1][a]), std::fabs(V[2][a]) })));
+        }
+        BuildTriangle l;
+        float* dst[3] = { l.v0, l.v1, l.v2 };
+        for (int k = 0; k < 3; ++k)
+            for (int r = 0; r < 3; ++r)
+                dst[k][r] = static_cast<float>(in.frame[r][0] * V[k][0] + in.frame[r][1] * V[k][1] + in.frame[r][2] * V[k][2]);
+        l.instance = 0;
+        l.primitive = static_cast<uint32_t>(in.world.size());
+        l.flip_facing = 0;
+        in.tris.push_back(l);
+        in.world.push_back(rec);
+    }
+}
+
+bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8CollapseOptions& copt, Bvh8BuildResult& out)
+{
+    // light-space box inflation: the rounding of the light coordinates to fp32 here and
+    // of the origin's (u, v, w) in the kernel (a 3-term fp32 dot product, about 3 ulp of
+    // |P|), Möller–Trumbore's acceptance margin (as the world BVHs: bvh8_inflation_box,
+    // 1e-6 of the diagonal) - each covered twice over
+    float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    for (const BuildTriangle& t : in.tris)
+        for (const float* v : { t.v0, t.v1, t.v2 })
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], v[a]);
+                hi[a] = std::max(hi[a], v[a]);
+            }
+    BvhBuildOptions lopt = opt;
+    lopt.max_leaf_size = kBvh8MaxLeafSize;
+    lopt.inflate_abs = 2.0f * bvh8_inflation_box(lo, hi) + 2e-6f * in.maxAbs;
+    BvhBuildResult r2 = build_bvh(in.tris, lopt, 0u, 0u);
+    std::vector<BuildTriangle>().swap(in.tris);
+    if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return false;
+    Bvh8CollapseOptions lc = copt;
+    lc.slot_sort_axis = 2; // every ray goes along +w
+    out = collapse_bvh8(r2, 0u, 0u, lc);
+    // the leaves' records become the world-space ones (primitive = world index)
+    for (GpuTriangle& g : out.tris) {
+        if (isHoleTriangle(g)) continue;
+        uint32_t idx;
+        std::memcpy(&idx, &g.t2[2], 4);
+        g = in.world[idx];
+    }
+    std::vector<GpuTriangle>().swap(in.world);
+    return true;
+}
+
+} // namespace ark
+
+// Round to the nearest fp16 value (RNE; +-inf above the largest finite value),
+// returned as a double: the host emulation of the packed-f16 box test below.
+static double rn16(double x)
+{
+    const double ax = std::fabs(x);
+    if (ax >= 65520.0) return x < 0 ? -INFINITY : INFINITY;
+    if (ax == 0.0) return x;
+    int e = std::ilogb(ax);
+    if (e < -14) e = -14;
+    const double ulp = std::ldexp(1.0, e - 10);
+    return std::nearbyint(x / ulp) * ulp;
+}
+
 // ark_ddgi_debug.h: traversal statistics of the BVH8 that set_scene would upload
 // (host simulation of k_trace's closest-hit order: per node the hit children,
 // those whose box holds the origin first, then octant order; a node's leaf
@@ -908,14 +1044,45 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     opt.inflate_abs = bvh8_inflation(triangles, n);
     opt.threads = threads > 0 ? threads : 8;
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
+    // ARK_BVH_AREA_W="xy,yz,zx": SAH face weights of both the BVH2 build and the collapse
+    if (const char* e = std::getenv("ARK_BVH_AREA_W"))
+        std::sscanf(e, "%f,%f,%f", &opt.area_w[0], &opt.area_w[1], &opt.area_w[2]);
     const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
     Bvh8CollapseOptions copt;
     if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
     if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
+    for (int k = 0; k < 3; ++k) copt.area_w[k] = opt.area_w[k];
     const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u, copt);
-    std::atomic<uint64_t> nodes { 0 }, triTests { 0 }, hits { 0 }, maxSteps { 0 };
+    std::atomic<uint64_t> nodes { 0 }, triTests { 0 }, hits { 0 }, maxSteps { 0 }, boxViolations { 0 };
     // ARK_SIM_ORDER=distance: exact front-to-back child order (what octant order approximates)
     const bool sortByDistance = std::getenv("ARK_SIM_ORDER") && std::strcmp(std::getenv("ARK_SIM_ORDER"), "distance") == 0;
+    // ARK_SIM_BOX: the child box test. "exact" (default): decoded planes, (p - o) * idir;
+    // "kernel32": k_trace's fp32 form t = fma(q, step * idir, (anchor - o) * idir);
+    // "f16": the packed-f16 form (visitNode8 with ARK_NODE_F16): per-ray scale 2^-s,
+    // t = RN16((1024 + q) * RN16(a) + RN16(b - 1024 a)), near/far reduced in f16, the
+    // test tn <= RN16(tf * (1 + 2^-8) + 2E) with the per-node error bound E. In the
+    // non-exact modes, a child that the exact test accepts and the chosen form rejects
+    // is counted in out[8] (must stay 0: the form must be conservative).
+    const char* boxEnv = std::getenv("ARK_SIM_BOX");
+    const int boxMode = !boxEnv ? 0 : std::strcmp(boxEnv, "kernel32") == 0 ? 1 : std::strcmp(boxEnv, "f16") == 0 ? 2 : std::strcmp(boxEnv, "f16s") == 0 ? 3 : 0;
+    // f16s: q as the fp16 subnormal q * 2^-24 (no 1024 bias), A = a * 2^24 (per-ray
+    // scale so that the largest step of any node fits)
+    double maxStep = 0.0;
+    for (const GpuBvh8Node& nd : r8.nodes)
+        for (int a = 0; a < 3; ++a) maxStep = std::max(maxStep, std::ldexp(1.0, static_cast<int>(nd.e[a]) - 127));
+    // the f16 form's error bound e = EA |a| + EB |B'| + 2^-22 (sensitivity runs only:
+    // the defaults are the proven bound)
+    const float simEA = std::getenv("ARK_SIM_E_A") ? static_cast<float>(std::atof(std::getenv("ARK_SIM_E_A"))) : 1.3f;
+    const float simEB = std::getenv("ARK_SIM_E_B") ? static_cast<float>(std::atof(std::getenv("ARK_SIM_E_B"))) : 0x1p-9f;
+    // scene bounds of the anchors (every node box lies inside the root's planes)
+    double sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };
+    if (!r8.nodes.empty()) {
+        const GpuBvh8Node& root = r8.nodes[0];
+        for (int a = 0; a < 3; ++a) {
+            sceneLo[a] = root.p[a];
+            sceneHi[a] = root.p[a] + 255.0 * std::ldexp(1.0, static_cast<int>(root.e[a]) - 127);
+        }
+    }
     auto worker = [&](uint64_t r0, uint64_t r1) {
         uint64_t cn = 0, ct = 0, ch = 0, ms = 0;
         for (uint64_t r = r0; r < r1; ++r) {
@@ -929,6 +1096,19 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
             std::vector<uint32_t> stack { 0u };
             bool hit = false;
             uint64_t steps = 0;
+            // f16 form: per-ray scale 2^-s so that |b - 1024 a| and every t fit fp16
+            int sExp = 0;
+            if (boxMode == 3) {
+                double mi = 0.0;
+                for (int a = 0; a < 3; ++a) mi = std::max(mi, std::fabs(static_cast<double>(idir[a])));
+                sExp = std::max(0, std::ilogb(std::max(maxStep * mi, 1e-30)) + 1 + 24 - 15);
+            }
+            if (boxMode == 2) {
+                double m = 0.0;
+                for (int a = 0; a < 3; ++a)
+                    m = std::max(m, std::max(std::fabs(sceneHi[a] - o[a]), std::fabs(sceneLo[a] - o[a])) * std::fabs(static_cast<double>(idir[a])));
+                sExp = std::max(0, std::ilogb(std::max(m * 10.0, 1e-30)) + 1 - 15);
+            }
             while (!stack.empty()) {
                 const uint32_t ni = stack.back();
                 stack.pop_back();
@@ -938,6 +1118,44 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                 struct C { float tn; uint32_t k; bool inside; int s; };
                 C hitc[8];
                 int nh = 0;
+                // per-node terms of the kernel forms
+                float a32[3], b32[3];
+                double A16[3], Bn16[3], Bf16[3];
+                double tmin16 = 0.0, tmax16 = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    a32[a] = std::ldexp(idir[a], static_cast<int>(nd.e[a]) - 127);
+                    b32[a] = (nd.p[a] - o[a]) * idir[a];
+                }
+                if (boxMode == 2) {
+                    for (int a = 0; a < 3; ++a) {
+                        // per axis: B' = b - 1024 a (fp32), its error bound e (the rounding
+                        // of A over 1279 steps, of B', of the result and of B' +- e),
+                        // and the near / far biases B' -+ e (the planes move outward)
+                        const float as = std::ldexp(a32[a], -sExp), bs = std::ldexp(b32[a], -sExp);
+                        const float Bp = std::fma(-1024.0f, as, bs);
+                        const float e = std::fma(std::fabs(as), simEA, std::fma(std::fabs(Bp), simEB, 0x1p-22f));
+                        A16[a] = rn16(as);
+                        const bool flip = idir[a] < 0.0f;
+                        // near planes (the smaller t) move down, far planes up; with a
+                        // negative a the near plane is qhi's, still the smaller t
+                        Bn16[a] = rn16(static_cast<double>(Bp - e));
+                        Bf16[a] = rn16(static_cast<double>(Bp + e));
+                        (void)flip;
+                    }
+                    tmin16 = rn16(std::ldexp(static_cast<double>(tmin), -sExp) * (1.0 - 0x1p-9));
+                    tmax16 = rn16(std::ldexp(static_cast<double>(tmax), -sExp) * (1.0 + 0x1p-9));
+                }
+                if (boxMode == 3) {
+                    for (int a = 0; a < 3; ++a) {
+                        const float as = std::ldexp(a32[a], -sExp), bs = std::ldexp(b32[a], -sExp);
+                        const float e = std::fma(std::fabs(as), simEA, std::fma(std::fabs(bs), simEB, 0x1p-22f));
+                        A16[a] = rn16(std::ldexp(static_cast<double>(as), 24));
+                        Bn16[a] = rn16(static_cast<double>(bs - e));
+                        Bf16[a] = rn16(static_cast<double>(bs + e));
+                    }
+                    tmin16 = rn16(std::ldexp(static_cast<double>(tmin), -sExp) * (1.0 - 0x1p-9));
+                    tmax16 = rn16(std::ldexp(static_cast<double>(tmax), -sExp) * (1.0 + 0x1p-9));
+                }
                 for (int s = 0; s < 8; ++s) {
                     const bool internal = (nd.imask >> s) & 1u;
                     if (!internal && !((nd.leaf_mask >> s) & 1u)) continue;
@@ -951,7 +1169,34 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                         tn = std::max(tn, t0);
                         tf = std::min(tf, t1);
                     }
-                    if (tn <= tf * 1.00001f + 1e-7f) hitc[nh++] = { tn, static_cast<uint32_t>(s) ^ oct, tn <= tmin, s };
+                    const bool exactHit = tn <= tf * 1.00001f + 1e-7f;
+                    bool accept = exactHit;
+                    if (boxMode == 1) {
+                        float kn = tmin, kf = tmax;
+                        for (int a = 0; a < 3; ++a) {
+                            const bool flip = idir[a] < 0.0f;
+                            const float qn = static_cast<float>(flip ? nd.qhi[a][s] : nd.qlo[a][s]);
+                            const float qf = static_cast<float>(flip ? nd.qlo[a][s] : nd.qhi[a][s]);
+                            kn = std::max(kn, std::fma(qn, a32[a], b32[a]));
+                            kf = std::min(kf, std::fma(qf, a32[a], b32[a]));
+                        }
+                        accept = kn <= std::fma(kf, 1.00001f, 1e-7f);
+                    } else if (boxMode >= 2) {
+                        double kn = -INFINITY, kf = INFINITY;
+                        const double bias = boxMode == 2 ? 1024.0 : 0.0, qs = boxMode == 2 ? 1.0 : 0x1p-24;
+                        for (int a = 0; a < 3; ++a) {
+                            const bool flip = idir[a] < 0.0f;
+                            const double qn = (bias + (flip ? nd.qhi[a][s] : nd.qlo[a][s])) * qs;
+                            const double qf = (bias + (flip ? nd.qlo[a][s] : nd.qhi[a][s])) * qs;
+                            kn = std::max(kn, rn16(qn * A16[a] + Bn16[a]));
+                            kf = std::min(kf, rn16(qf * A16[a] + Bf16[a]));
+                        }
+                        kn = std::max(kn, tmin16);
+                        kf = std::min(kf, tmax16);
+                        accept = kn <= kf;
+                    }
+                    if (exactHit && !accept) boxViolations++;
+                    if (accept) hitc[nh++] = { tn, static_cast<uint32_t>(s) ^ oct, tn <= tmin, s };
                 }
                 // leaf triangles of this node now, internal children by (inside first, k order)
                 uint32_t internalBefore[8];
@@ -1019,6 +1264,146 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
         out[5] = maxSteps.load();
         out[6] = r8.max_depth;
         out[7] = r8.tris.size();
+        out[8] = boxViolations.load();
     }
     return 0;
 }
+
+// ark_ddgi_debug.h: the sun's light-space BVH on the host (no GPU), checked against
+// brute force. Builds it as set_scene does (sun_frame, sun_add_triangles,
+// build_sun_bvh), then for every origin traces a sun shadow ray (L = -normalize(sun
+// dir) in fp32, [0.025, tmax]) twice: through the BVH with a host restatement of
+// k_trace_shadow<SUN>'s node test (visitNodeSun: the same fp32 quantized coordinate,
+// floor / ceil, integer plane compares) and against every triangle; both use the same
+// Möller–Trumbore (the kernels' operation order). out[8] = {rays, occluded (brute
+// force), occluded (BVH), mismatches, node visits, triangle tests, BVH8 nodes, max
+// stack depth}. A mismatch would be a culled occluder: the node test must be
+// conservative.
+extern "C" int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, const float* sun_dir, const float* origins, uint64_t n_rays, float tmax,
+                                             uint64_t* out)
+{
+    using namespace ark;
+    std::vector<BuildTriangle> tris(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            tris[i].v0[a] = triangles[9 * i + a];
+            tris[i].v1[a] = triangles[9 * i + 3 + a];
+            tris[i].v2[a] = triangles[9 * i + 6 + a];
+        }
+        tris[i].instance = 0;
+        tris[i].primitive = static_cast<uint32_t>(i);
+        tris[i].flip_facing = 0;
+    }
+    SunBvhInput in;
+    sun_frame(sun_dir, in.frame);
+    sun_add_triangles(in, tris);
+    std::vector<GpuTriangle> world = in.world;
+    BvhBuildOptions opt;
+    opt.threads = 8;
+    Bvh8CollapseOptions copt;
+    Bvh8BuildResult r;
+    if (n == 0 || !build_sun_bvh(in, opt, copt, r)) return 1;
+    float F[9];
+    for (int a = 0; a < 3; ++a)
+        for (int k = 0; k < 3; ++k) F[a * 3 + k] = static_cast<float>(in.frame[a][k]);
+    const float dd = sun_dir[0] * sun_dir[0] + sun_dir[1] * sun_dir[1] + sun_dir[2] * sun_dir[2];
+    const float sc = 1.0f / std::sqrt(dd);
+    const float L[3] = { -(sun_dir[0] * sc), -(sun_dir[1] * sc), -(sun_dir[2] * sc) };
+    const float tmin = 0.025f;
+    // the kernels' Möller–Trumbore (intersectTri: crossFma / dotFma3, 1 / det)
+    auto mt = [&](const float o[3], const GpuTriangle& g) {
+        const float v0[3] = { g.t0[0], g.t0[1], g.t0[2] }, e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+        auto cr = [](const float* a, const float* b, float* c) {
+            c[0] = std::fma(a[1], b[2], -(a[2] * b[1]));
+            c[1] = std::fma(a[2], b[0], -(a[0] * b[2]));
+            c[2] = std::fma(a[0], b[1], -(a[1] * b[0]));
+        };
+        auto dt = [](const float* a, const float* b) { return std::fma(a[0], b[0], std::fma(a[1], b[1], a[2] * b[2])); };
+        float p[3], q[3];
+        cr(L, e2, p);
+        const float det = dt(e1, p);
+        const float inv = 1.0f / det;
+        const float s[3] = { o[0] - v0[0], o[1] - v0[1], o[2] - v0[2] };
+        const float u = dt(s, p) * inv;
+        cr(s, e1, q);
+        const float v = dt(L, q) * inv;
+        const float t = dt(e2, q) * inv;
+        return (u >= 0.0f) & (v >= 0.0f) & (u + v <= 1.0f) & (t >= tmin) & (t <= tmax);
+    };
+    std::atomic<uint64_t> occB { 0 }, occV { 0 }, mism { 0 }, visits { 0 }, tests { 0 }, maxDepth { 0 };
+    auto worker = [&](uint64_t r0, uint64_t r1) {
+        for (uint64_t ri = r0; ri < r1; ++ri) {
+            const float* o = origins + 3 * ri;
+            bool brute = false;
+            for (const GpuTriangle& g : world)
+                if (mt(o, g)) {
+                    brute = true;
+                    break;
+                }
+            // light-space traversal (visitNodeSun)
+            const float pl[3] = { std::fma(o[0], F[0], std::fma(o[1], F[1], o[2] * F[2])), std::fma(o[0], F[3], std::fma(o[1], F[4], o[2] * F[5])),
+                                  std::fma(o[0], F[6], std::fma(o[1], F[7], o[2] * F[8])) };
+            std::vector<uint32_t> stack { 0u };
+            bool bvh = false;
+            uint64_t nv = 0, nt = 0, md = 0;
+            while (!stack.empty() && !bvh) {
+                const GpuBvh8Node& nd = r.nodes[stack.back()];
+                stack.pop_back();
+                nv++;
+                int F_[2], C_[3];
+                float Q[3];
+                for (int a = 0; a < 3; ++a) {
+                    const float q = std::ldexp(pl[a] - nd.p[a], 127 - static_cast<int>(nd.e[a]));
+                    Q[a] = std::min(258.0f, std::max(-2.0f, q));
+                }
+                F_[0] = static_cast<int>(std::floor(Q[0]));
+                F_[1] = static_cast<int>(std::floor(Q[1]));
+                for (int a = 0; a < 3; ++a) C_[a] = static_cast<int>(std::ceil(Q[a]));
+                uint32_t internalBefore = 0;
+                std::vector<uint32_t> push;
+                for (int sl = 0; sl < 8; ++sl) {
+                    const bool internal = (nd.imask >> sl) & 1u;
+                    const bool hitc = nd.qlo[0][sl] <= F_[0] && nd.qhi[0][sl] >= C_[0] && nd.qlo[1][sl] <= F_[1] && nd.qhi[1][sl] >= C_[1] &&
+                                      nd.qhi[2][sl] >= C_[2];
+                    if (internal) {
+                        if (hitc) push.push_back(nd.child_base + internalBefore);
+                        internalBefore++;
+                        continue;
+                    }
+                    if (!hitc || !((nd.leaf_mask >> sl) & 1u)) continue;
+                    uint32_t st[kBvh8MaxLeafSize];
+                    const int cnt = bvh8SlotTriangles(nd, sl, st);
+                    for (int i = 0; i < cnt && !bvh; ++i) {
+                        nt++;
+                        bvh = mt(o, r.tris[st[i]]);
+                    }
+                }
+                for (size_t i = push.size(); i-- > 0;) stack.push_back(push[i]);
+                md = std::max<uint64_t>(md, stack.size());
+            }
+            occB += brute ? 1 : 0;
+            occV += bvh ? 1 : 0;
+            mism += brute != bvh ? 1 : 0;
+            visits += nv;
+            tests += nt;
+            uint64_t m = maxDepth.load();
+            while (md > m && !maxDepth.compare_exchange_weak(m, md)) {}
+        }
+    };
+    const int T = 8;
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(worker, n_rays * t / T, n_rays * (t + 1) / T);
+    for (auto& th : pool) th.join();
+    if (out) {
+        out[0] = n_rays;
+        out[1] = occB.load();
+        out[2] = occV.load();
+        out[3] = mism.load();
+        out[4] = visits.load();
+        out[5] = tests.load();
+        out[6] = r.nodes.size();
+        out[7] = maxDepth.load();
+    }
+    return mism.load() == 0 ? 0 : 2;
+}
+

@@ -26,6 +26,7 @@ struct BvhBuildOptions {
     float inflate_abs = 0.0f; // absolute box inflation on top of the relative one (see collapse_bvh8 / visitNode8)
     float traversal_cost = 1.0f;
     float intersection_cost = 1.0f;
+    float area_w[3] = { 1.0f, 1.0f, 1.0f }; // SAH face weights {xy, yz, zx} (surface area: all 1)
 };
 
 struct BvhBuildResult {
@@ -64,8 +65,17 @@ struct Bvh8CollapseOptions {
     bool sah_optimal = true;
     float node_cost = 1.0f; // SAH cost of visiting a BVH8 node (8 box tests)
     float tri_cost = 1.0f;  // SAH cost of one triangle test
+    float area_w[3] = { 1.0f, 1.0f, 1.0f }; // SAH face weights {xy, yz, zx}, as BvhBuildOptions::area_w
+    // -1: internal children in octant slots (visited in slot ^ ray octant order);
+    // 0-2: in slots 0, 1, ... by their box's lower bound along that axis (a BVH that
+    // only rays along +axis traverse: the sun's light-space BVH, slot order = octant 0)
+    int slot_sort_axis = -1;
 };
 Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& opt);
+
+// The 48-B triangle record of a build triangle (v0, e1 = v1 - v0, e2 = v2 - v0 in
+// fp32, instance, primitive, facing flip): what the traversal's Möller–Trumbore reads.
+GpuTriangle make_gpu_triangle(const BuildTriangle& t);
 
 // Hole records of the triangle rows (kHoleInstance)
 GpuTriangle holeTriangle();
@@ -82,5 +92,21 @@ int bvh8SlotTriangles(const GpuBvh8Node& nd, int s, uint32_t out[kBvh8MaxLeafSiz
 // (about 2 ulp of the diagonal, i.e. 2.4e-7 of it) with a 4x margin.
 float bvh8_inflation(const float* xyz, uint64_t nTriangles);
 float bvh8_inflation_box(const float lo[3], const float hi[3]);
+
+// The sun's light-space BVH (k_trace_shadow<SUN>): every triangle of every hit-mask
+// class in the frame (u, v, w = the shadow rays' direction L = -normalize(sun dir) as
+// the kernels compute it in fp32), leaves holding the world-space records.
+struct SunBvhInput {
+    std::vector<BuildTriangle> tris;  // light-space vertices; primitive = index into world
+    std::vector<GpuTriangle> world;   // world-space records (make_gpu_triangle)
+    double frame[3][3] = {};          // rows u, v, w
+    float maxAbs = 0.0f;              // largest |world coordinate|
+};
+void sun_frame(const float sun_dir[3], double frame[3][3]);
+void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_tris);
+// Builds the BVH2 (opt; its inflation replaced by the light-space bound), the BVH8
+// (copt, slots sorted by w) and swaps in the world records; consumes in.tris and
+// in.world. False when a BVH2 leaf exceeds kBvh8MaxLeafSize.
+bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8CollapseOptions& copt, Bvh8BuildResult& out);
 
 } // namespace ark

@@ -130,7 +130,10 @@ struct alignas(16) ShadowRay {
 constexpr int kShadeHeadWord = kRayParts * kRayCounterStride;
 constexpr int kShadowCountWord = 2 * kRayParts * kRayCounterStride;
 constexpr int kShadowHeadWord = kShadowCountWord + kRayCounterStride; // kRayParts partition heads
-constexpr int kRayCounterWords = kShadowHeadWord + kRayParts * kRayCounterStride;
+// the sun's shadow-ray list (FrameArgs::sun_rays): count + partition heads
+constexpr int kSunCountWord = kShadowHeadWord + kRayParts * kRayCounterStride;
+constexpr int kSunHeadWord = kSunCountWord + kRayCounterStride;
+constexpr int kRayCounterWords = kSunHeadWord + kRayParts * kRayCounterStride;
 
 // Read-only scene views in HBM (SceneRTMeshDataSet + material set + SceneLightSet + TLAS).
 struct SceneArgs {
@@ -160,6 +163,14 @@ struct SceneArgs {
     // instance index; BVH triangle order. Lets k_trace find the shading normal of a
     // front hit with two dependent loads instead of five (set when lights exist).
     const float4* tri_normals; // per-triangle shading records [4]: n0 n1 n2 (9), instance, uv0 uv1 uv2
+    // the sun's light-space BVH8 (ark_ddgi.cpp sunFrame): every triangle of every
+    // hit-mask class, boxes in the frame (u, v, w = the shadow rays' direction), leaves
+    // holding the world-space triangle records; sun_root = -1: none (the sun's shadow
+    // rays then traverse the world BVHs)
+    const GpuBvh8Node* sun_nodes;
+    const GpuTriangle* sun_tris;
+    int32_t sun_root;
+    float sun_frame[9]; // rows u, v, w
 
     __device__ __forceinline__ int resolveTexture(int idx) const
     {
@@ -211,6 +222,12 @@ struct FrameArgs {
     ShadowRay* shadow_rays;  // k_shadow_gen's list: [window_rays * light_count] worst case
     uint32_t* shadow_count;  // = ray_counter + kShadowCountWord
     uint32_t* shadow_heads;  // = ray_counter + kShadowHeadWord (kRayParts heads, kRayCounterStride apart)
+    // with a sun light-space BVH (SceneArgs::sun_root >= 0): k_shadow_gen puts the
+    // sun's shadow rays in this list instead (null: every shadow ray in shadow_rays),
+    // traced by k_trace_shadow<.., SUN = true>
+    ShadowRay* sun_rays;
+    uint32_t* sun_count;     // = ray_counter + kSunCountWord
+    uint32_t* sun_heads;     // = ray_counter + kSunHeadWord
     // Light-space binning of the shadow-ray list (shadow_bin_grid = G > 0): k_shadow_gen
     // writes shadow_rays_gen with a bin key (light, Morton cell of the G x G light-space
     // grid) and its rank in the bin, k_shadow_bin_scan turns the bin counts into bin

@@ -673,6 +673,142 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
     return anyHit;
 }
 
+// ---------------------------------------------------------------------------
+// 1b. The sun's shadow rays in light space (SceneArgs::sun_root, ark_ddgi.cpp sunFrame)
+// ---------------------------------------------------------------------------
+// Light-space coordinates (u, v, w) of a world point: three fp32 dot products (the
+// BVH's box inflation covers their rounding, ark_ddgi.cpp).
+__device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
+{
+    const float* F = sc.sun_frame;
+    return { fmaf(p.x, F[0], fmaf(p.y, F[1], p.z * F[2])), fmaf(p.x, F[3], fmaf(p.y, F[4], p.z * F[5])), fmaf(p.x, F[6], fmaf(p.y, F[7], p.z * F[8])) };
+}
+
+// Child s of slot byte B (word LO / HI of the plane pairs): crossed iff
+// qlo_u <= Fu, qhi_u >= Cu, qlo_v <= Fv, qhi_v >= Cv and qhi_w >= Cw - five SDWA byte
+// compares (unsigned byte vs a signed lane value), ANDed in an SGPR pair, the result
+// shifted into the lane's slot mask as v_addc's carry (m = 2m + hit).
+#define ARK_SUN_CHILD(LU, HU, LV, HV, HW, B)                                               \
+    "v_cmp_le_i32_sdwa %[m], %[" LU "], %[fu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"     \
+    "v_cmp_ge_i32_sdwa vcc, %[" HU "], %[cu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
+    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
+    "v_cmp_le_i32_sdwa vcc, %[" LV "], %[fv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
+    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
+    "v_cmp_ge_i32_sdwa vcc, %[" HV "], %[cv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
+    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
+    "v_cmp_ge_i32_sdwa vcc, %[" HW "], %[cw] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
+    "s_and_b64 vcc, %[m], vcc\n\t"                                                         \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
+
+// Node visit of a ray along +w from light-space point pl (k_trace_shadow<SUN>). With
+// the direction exactly +w the slab test of u and v degenerates to "pl's coordinate
+// lies in the child's interval" and that of w to "the box reaches above pl": in the
+// node's quantized grid, qlo <= floor(Q) and qhi >= ceil(Q) for Q = (pl - anchor) /
+// step - no reciprocal, no per-child multiply (the world test: 8 x 19 VALU). The ray's
+// tmin is not used (a box between pl and pl + tmin is visited, conservatively). The
+// children are visited in slot order: the builder sorted them by their lower w bound
+// (Bvh8CollapseOptions::slot_sort_axis), the order the ray meets them.
+__device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 pl, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase,
+                                             uint32_t& tBits)
+{
+    // quantized coordinate, clamped to [-2, 258] (outside [0, 255] no child holds it)
+    // so the conversions stay in range
+    auto quant = [](float c, uint32_t p, uint32_t ebyte) {
+        return __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(c - __uint_as_float(p), 127 - static_cast<int>(ebyte)), -2.0f, 258.0f);
+    };
+    const float qu = quant(pl.x, w0.x, w0.w & 0xffu), qv = quant(pl.y, w0.y, (w0.w >> 8) & 0xffu), qw = quant(pl.z, w0.z, (w0.w >> 16) & 0xffu);
+    const int fu = static_cast<int>(floorf(qu)), cu = static_cast<int>(ceilf(qu));
+    const int fv = static_cast<int>(floorf(qv)), cv = static_cast<int>(ceilf(qv));
+    const int cw = static_cast<int>(ceilf(qw));
+    uint32_t hit = 0;
+    uint64_t m;
+    // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
+    // qhi w = w4.z|w (children 0-3 | 4-7); slots 7 .. 0 shifted in
+    asm(ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "3") ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "2")
+        ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "1") ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "0")
+        ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "3") ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "2")
+        ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "1") ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "0")
+        : [acc] "+v"(hit), [m] "=&s"(m)
+        : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
+          [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
+        : "vcc");
+    const uint32_t imask = w0.w >> 24;
+    gBase = w1.x;
+    gBits = (hit & imask) | (imask << 8);
+    tBase = w1.y;
+    const uint32_t stride = w1.w & 31u, leafHits = hit & (w1.w >> 8) & 0xffu;
+    const uint32_t x = (leafHits << stride) | leafHits;
+    tBits = ((x << stride) | x) & w1.z;
+}
+#undef ARK_SUN_CHILD
+
+// travStepDual for a sun shadow ray in the light-space BVH: both sides' loads issued
+// by every lane (a skipped side reads the resident record 0 / the root), the
+// world-space Möller–Trumbore of the leaf records (the any-hit test of the world
+// BVHs, bit for bit), the light-space node test.
+template<int BLOCK>
+__device__ __forceinline__ bool travStepSun(const SceneArgs& sc, TravState& ts, uint32_t& nBase, uint32_t& nBits, Stack<BLOCK>& st, V3 o, V3 d, V3 pl,
+                                            float tmin, float tmax, uint32_t& cNodes, uint32_t& cTris)
+{
+    bool anyHit = false;
+    const bool doTri = ts.tBits != 0;
+    const bool doNode = nBits == 0 && ((ts.gBits & 0xffu) != 0 || st.depth != 0);
+    uint32_t ti = 0;
+    if (doTri) {
+        ti = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
+        ts.tBits &= ts.tBits - 1u;
+    }
+    uint4 a, b, c;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.sun_tris + ti);
+        a = src[0];
+        b = src[1];
+        c = src[2];
+    }
+    uint32_t child = static_cast<uint32_t>(sc.sun_root);
+    if (doNode) {
+        if ((ts.gBits & 0xffu) == 0) st.pop(ts.gBase, ts.gBits);
+        child = nextChild(ts.gBase, ts.gBits, 0u);
+        if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
+    }
+    uint4 w0, w1, w2, w3, w4;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.sun_nodes + child);
+        w0 = src[0];
+        w1 = src[1];
+        w2 = src[2];
+        w3 = src[3];
+        w4 = src[4];
+    }
+    if (doTri) {
+        cTris++;
+        const GpuTriangle tr = triFromWords(a, b, c);
+        bool bf;
+        float tt, uu, vv;
+        anyHit = intersectTri(o, d, tmin, tmax, tr, &tt, &uu, &vv, &bf);
+    }
+    if (doNode) {
+        cNodes++;
+        uint32_t lb, lbits;
+        visitNodeSun(w0, w1, w2, w3, w4, pl, ts.gBase, ts.gBits, lb, lbits);
+        if (lbits) {
+            if (ts.tBits == 0) {
+                ts.tBase = lb;
+                ts.tBits = lbits;
+            } else {
+                nBase = lb;
+                nBits = lbits;
+            }
+        }
+    }
+    if (ts.tBits == 0 && nBits != 0) {
+        ts.tBase = nBase;
+        ts.tBits = nBits;
+        nBits = 0;
+    }
+    return anyHit;
+}
+
 // opaque.rchit:118-131: world-space shading normal of a front hit. The trace
 // kernel's shadow phase and the shading kernel both evaluate exactly this
 // expression, so they agree on N (and on which lights need a shadow ray).
@@ -1501,7 +1637,10 @@ __device__ __forceinline__ V3 shfl3(V3 v, uint32_t src)
 // three hit-mask classes in turn, no alpha test, dual steps. Lanes are refilled
 // from a wave-private pool like k_trace; an occluded ray sets bit 16 + light of its
 // probe ray's word. `pass` of a helper lane holds (root lane + 1) << 8.
-template<bool COUNT, int WPE>
+// SUN: the sun's list (FrameArgs::sun_rays) through the light-space BVH (one pass,
+// travStepSun); else the rest of the shadow rays (or all of them, without a sun BVH)
+// through the three world BVHs.
+template<bool COUNT, int WPE, bool SUN = false>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
     if (frameAborted(f.abort_word)) return;
@@ -1511,19 +1650,24 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 #endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
-    constexpr int kNodes = ARK_SHADOW_LDS_NODES;
+    // (the light-space traversal caches none)
+    constexpr int kNodes = SUN ? 1 : ARK_SHADOW_LDS_NODES;
     __shared__ uint4 ldsNodes[kNodes * 5];
     __shared__ uint8_t ldsTable[kTraceBlock];
     __shared__ uint32_t ldsBytes[kTraceBlock / 4];
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     if (lane < 16u) ldsBytes[(wbase >> 2) + lane] = 0u; // wave-private
-    const NodeCache nc = loadNodeCache<kTraceBlock, kNodes>(sc, ldsNodes);
+    NodeCache nc { nullptr, 0u, 0u };
+    if constexpr (!SUN) nc = loadNodeCache<kTraceBlock, kNodes>(sc, ldsNodes);
+    (void)ldsNodes;
     const TailLds tl { ldsTable, ldsBytes };
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
     const float tmin = 0.025f;
-    const uint32_t total = *f.shadow_count;
-    const int32_t roots[3] = { sc.root_opaque, sc.root_masked, sc.root_blend };
+    const uint32_t total = SUN ? *f.sun_count : *f.shadow_count;
+    uint32_t* const heads = SUN ? f.sun_heads : f.shadow_heads;
+    const ShadowRay* const list = SUN ? f.sun_rays : f.shadow_rays;
+    const int32_t roots[3] = { SUN ? sc.sun_root : sc.root_opaque, SUN ? -1 : sc.root_masked, SUN ? -1 : sc.root_blend };
     uint32_t cNodes = 0, cTris = 0, cShadow = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
@@ -1548,7 +1692,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             uint32_t fb = 0, fe = 0;
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) grabItems(f.shadow_heads, total, home, t, b, e, f.grab_chunk);
+                if (lane == 0) grabItems(heads, total, home, t, b, e, f.grab_chunk);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);
@@ -1558,13 +1702,14 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 if (rank < avail) r = poolNext + rank;
                 else if (fb + (rank - avail) < fe) r = fb + (rank - avail);
                 if (r != kNoHit) {
-                    const ShadowRay sr = f.shadow_rays[r];
+                    const ShadowRay sr = list[r];
                     o = v3(sr.origin_tmax.x, sr.origin_tmax.y, sr.origin_tmax.z);
                     d = v3(sr.dir_owner.x, sr.dir_owner.y, sr.dir_owner.z);
                     tmax = sr.origin_tmax.w;
                     owner = __float_as_uint(sr.dir_owner.w);
-                    idir = safeInv(d);
-                    oct = rayOctant(idir);
+                    // SUN: idir holds the origin's light-space coordinates
+                    idir = SUN ? sunCoords(sc, o) : safeInv(d);
+                    oct = SUN ? 0u : rayOctant(idir);
                     stop();
                     pass = 0;
                     active = true;
@@ -1622,8 +1767,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                 gB = __shfl(gB, static_cast<int>(src));
                 gBits = __shfl(gBits, static_cast<int>(src));
                 if (take) {
-                    idir = safeInv(d);
-                    oct = rayOctant(idir);
+                    idir = SUN ? sunCoords(sc, o) : safeInv(d);
+                    oct = SUN ? 0u : rayOctant(idir);
                     pass = static_cast<int>((sroot + 1u) << 8);
                     stop();
                     ts = TravState { gB, gBits, 0u, 0u };
@@ -1633,8 +1778,13 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (active) {
             // (a done lane - a root waiting for its helpers - steps as a no-op)
-            RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-            const bool occluded = travStepDual<kTraceBlock, true, ARK_SHADOW_FETCH_GLOBAL != 0>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
+            bool occluded;
+            if constexpr (SUN) {
+                occluded = travStepSun<kTraceBlock>(sc, ts, nBase, nBits, st, o, d, idir, tmin, tmax, cNodes, cTris);
+            } else {
+                RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
+                occluded = travStepDual<kTraceBlock, true, ARK_SHADOW_FETCH_GLOBAL != 0>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
+            }
             const bool helper = pass >= 256;
             const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
             if (occluded) {
@@ -1756,7 +1906,9 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     if (frameAborted(f.abort_word)) return;
     __shared__ uint32_t bitsL[kGenSpan];
     __shared__ uint32_t waveOff[kGenSteps][4];
-    __shared__ uint32_t blockBase;
+    __shared__ uint32_t blockBase, sunBlockBase;
+    // the sun's rays (light 0) to their own list when the scene has a light-space BVH
+    const bool splitSun = !REFL && f.sun_rays != nullptr;
     const uint32_t total = REFL ? *f.list_count : f.window_rays;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t first = blockIdx.x * kGenSpan;
@@ -1792,9 +1944,15 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         }
         bitsL[k * 256u + threadIdx.x] = bits;
     }
+    // counts packed: world-list rays in bits 0-15, sun-list rays in bits 16-31 (a
+    // block has at most kGenSpan x kMaxLights = 11,264 of either, no carry)
+    auto packedCount = [&](uint32_t bits) {
+        const uint32_t sun = splitSun ? (bits & 1u) : 0u;
+        return static_cast<uint32_t>(__builtin_popcount(bits & ~sun)) | (sun << 16);
+    };
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
-        const uint32_t x = waveInclusiveScan(static_cast<uint32_t>(__builtin_popcount(bitsL[k * 256u + threadIdx.x])));
+        const uint32_t x = waveInclusiveScan(packedCount(bitsL[k * 256u + threadIdx.x]));
         if (__lane_id() == 63u) waveOff[k][wave] = x;
     }
     __syncthreads();
@@ -1806,13 +1964,16 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
                 waveOff[k][w] = run;
                 run += c;
             }
-        blockBase = run ? atomicAdd(f.shadow_count, run) : 0u;
+        blockBase = (run & 0xffffu) ? atomicAdd(f.shadow_count, run & 0xffffu) : 0u;
+        sunBlockBase = (run >> 16) ? atomicAdd(f.sun_count, run >> 16) : 0u;
     }
     __syncthreads();
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         const uint32_t bits = bitsL[k * 256u + threadIdx.x];
-        const uint32_t c = static_cast<uint32_t>(__builtin_popcount(bits));
-        uint32_t sj = blockBase + waveOff[k][wave] + waveInclusiveScan(c) - c;
+        const uint32_t c = packedCount(bits);
+        const uint32_t before = waveOff[k][wave] + waveInclusiveScan(c) - c;
+        uint32_t sj = blockBase + (before & 0xffffu);
+        uint32_t sunj = sunBlockBase + (before >> 16);
         if (bits == 0) continue;
         const uint32_t pos = first + k * 256u + threadIdx.x;
         uint32_t ray;
@@ -1838,7 +1999,9 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             float tmax;
             shadowRayOf(sc, f.z_far, l, hitPoint, &ld, &tmax);
             const ShadowRay sr { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax), make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
-            if (binned) {
+            if (splitSun && l == 0u) {
+                f.sun_rays[sunj++] = sr;
+            } else if (binned) {
                 const uint32_t key = shadowBinKey(sc, f, l, hitPoint);
                 f.shadow_bin_key[sj] = key;
                 f.shadow_bin_rank[sj] = atomicAdd(f.shadow_bin_count + key * kBinStride, 1u);
@@ -2266,9 +2429,18 @@ hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks
     return hipGetLastError();
 }
 
+// The sun's list through the light-space BVH (when k_shadow_gen split it off), then
+// the other shadow rays through the world BVHs (when there are lights besides the sun,
+// or no sun list).
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     void* args[] = { const_cast<SceneArgs*>(&sc), const_cast<FrameArgs*>(&f) };
+    if (f.sun_rays) {
+        const void* fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, true>)
+                               : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, true>);
+        const hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(kTraceBlock), args, 0, s);
+        if (e != hipSuccess || f.light_count <= 1u) return e;
+    }
     return hipLaunchKernel(kernel_trace_shadow_ptr(count), dim3(blocks), dim3(kTraceBlock), args, 0, s);
 }
 

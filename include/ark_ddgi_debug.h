@@ -53,14 +53,25 @@ int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out)
 /* Traversal statistics of that BVH8 on the host (a scalar simulation of k_trace's
  * closest-hit order: hit children, origin-containing first, then octant order; the
  * leaf triangles of a node right after it): nRays rays of 7 floats (origin,
- * direction, tmax) over `threads` host threads. out[8] = {node visits, triangle
+ * direction, tmax) over `threads` host threads. out[9] = {node visits, triangle
  * tests, hits, BVH8 nodes, SAH cost x 1e6, max steps of one ray, max depth,
- * triangle records (leaf triangle rows, holes included)};
+ * triangle records (leaf triangle rows, holes included), children the exact box
+ * test accepts and the ARK_SIM_BOX form (kernel32 | f16) rejects (must be 0)};
  * per_ray_steps (if not NULL) gets each ray's node visits + triangle tests.
  * For comparing BVH builds (ARK_BVH8_COLLAPSE, ARK_BVH8_TRI_COST,
  * ARK_BVH_INTERSECTION_COST) without a GPU: tools/bvh_stats.py. */
 int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const float* rays, uint64_t n_rays, int threads, uint64_t* out,
                                     uint32_t* per_ray_steps /* nullable: node visits + triangle tests of each ray */);
+
+/* The sun's light-space BVH (the one set_scene builds for k_trace_shadow<SUN>) built
+ * on the host from n world triangles (9 floats each) and checked without a GPU: a sun
+ * shadow ray from each of n_rays origins (3 floats) along L = -normalize(sun_dir),
+ * [0.025, tmax], any hit through the BVH with a host restatement of the kernel's
+ * light-space node test, and against every triangle. out[8] = {rays, occluded (brute
+ * force), occluded (BVH), mismatches, node visits, triangle tests, BVH8 nodes, max
+ * stack depth}. Returns 0 when no ray differs, 2 on a mismatch, 1 on a build error. */
+int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, const float* sun_dir, const float* origins, uint64_t n_rays, float tmax,
+                                 uint64_t* out);
 
 #ifdef __cplusplus
 }

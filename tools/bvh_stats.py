@@ -75,7 +75,7 @@ def main():
             os.environ["ARK_BVH8_TRI_COST"] = parts[1]
         else:
             os.environ.pop("ARK_BVH8_TRI_COST", None)
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 9)()
         t = time.time()
         steps = np.zeros(rays.shape[0], np.uint32)
         lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out, steps.ctypes.data)
@@ -84,7 +84,7 @@ def main():
         n = rays.shape[0]
         res[v] = {"nodes_per_ray": round(out[0] / n, 3), "tris_per_ray": round(out[1] / n, 3), "hit_frac": round(out[2] / n, 4),
                   "bvh8_nodes": out[3], "sah": out[4] / 1e6, "max_steps": out[5], "depth": out[6],
-                  "triangle_records_per_triangle": round(out[7] / tris.shape[0], 4), "s": round(time.time() - t, 1)}
+                  "triangle_records_per_triangle": round(out[7] / tris.shape[0], 4), "box_violations": out[8], "box": os.environ.get("ARK_SIM_BOX", "exact"), "s": round(time.time() - t, 1)}
         print(v, json.dumps(res[v]), flush=True)
 
 
