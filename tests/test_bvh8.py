@@ -12,7 +12,7 @@ from arkoserenderer_amd import abi
 def check(tris):
     lib = abi.load_library()
     tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
-    out = (C.c_uint64 * 9)()
+    out = (C.c_uint64 * 8)()
     rc = lib.ark_ddgi_debug_bvh8_check(tris.ctypes.data, tris.shape[0], out)
     return rc, list(out)
 
