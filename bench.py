@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--ao-samples", type=int, default=64)
     ap.add_argument("--ao-cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-compose", action="store_true", help="skip the DDGI consumer (lighting compose) line")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C5 / C3 substitute lines")
     ap.add_argument("--compose-size", default="1920x1080")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "latest_pmc.json"),
                     help="PMC traffic summary (tools/pmc_summary.py --latest); used only if its library hash matches")
@@ -235,6 +236,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_windows:
         result["reference_windows"] = reference_windows(node, ctx, torch, device, sptr, frame)
         result["c2"] = c2_line(args, torch, device)
+
+    if rank == 0 and world == 1 and not args.no_configs:
+        for name in ("c5", "c3"):
+            result[name] = config_line(name, torch, device)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, grid, R, args, exposure)
@@ -471,6 +476,68 @@ def c2_line(args, torch, device):
     return {"workload": "C2: Cornell box (100 triangles), 8x8x8 probes x 64 rays, all probes per frame",
             "gpu_ms_per_frame": round(ms, 4), "gpu_mrays_per_s": round(512 * 64 / ms / 1e3, 1),
             "note": "32,768 rays per frame: launch-bound on the GPU (five launches)"}
+
+
+def config_line(name, torch, device, steps=10, warmup=3):
+    """The other GPU configs of BASELINE.json at N = 1, whole grid per step (K = N),
+    with their substitutes for the scenes the reference tree lacks: C5 =
+    the instanced city block for Bistro (~3 M triangles, 48x16x48 probes x 512 rays, sun
+    + 4 IES spot lights: 5 shadow rays per lit hit), C3 = a 262,272-triangle strip soup
+    for Sponza (Sponza.bin is missing; 24x12x24 x 256, sun + 3 IES spots). Wall clock
+    over `steps` steps after `warmup` on torch's current stream (frames in flight), plus
+    the per-kernel HIP-event times of 3 instrumented (serial) steps."""
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+
+    if name == "c5":
+        sc = S.city_block()
+        grid = D.ProbeGrid((48, 16, 48), (5.0, 2.5, 5.0), (2.5, 0.5, 2.5))
+        R, zf = 512, 1000.0
+        workload = "C5 substitute: instanced city block, 48x16x48 probes x 512 rays, sun + 4 IES spots, whole grid per step"
+    else:
+        sc = S.sponza_substitute()
+        grid = D.ProbeGrid(*S.sponza_substitute_grid())
+        R, zf = 256, 10000.0
+        workload = "C3 substitute: 262,272-triangle strip soup, 24x12x24 probes x 256 rays, sun + 3 IES spots, whole grid per step"
+    N = grid.probe_count()
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+    node = D.DDGINode(cfg)
+    t = time.time()
+    node.construct(sc, grid, zf, device=device.index or 0, light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
+    setup = time.time() - t
+    sptr = torch.cuda.current_stream(device).cuda_stream
+    frame = 0
+    for _ in range(warmup):
+        node.execute(D.AppState(frame), sptr)
+        frame += 1
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        node.execute(D.AppState(frame), sptr)
+        frame += 1
+    torch.cuda.synchronize(device)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    node.ctx.synchronize()
+    node.ctx.set_timing(True)
+    kt = []
+    for _ in range(3):
+        node.execute(D.AppState(frame), sptr)
+        frame += 1
+        kt.append(node.ctx.last_timings())
+    node.ctx.set_timing(False)
+    node.ctx.set_counting(True)
+    node.execute(D.AppState(frame), sptr)
+    torch.cuda.synchronize(device)
+    c = node.ctx.counters()
+    node.ctx.set_counting(False)
+    a = [sum(k[i] for k in kt) / len(kt) for i in range(5)]
+    node.ctx.close()
+    rays = N * R
+    return {"workload": workload, "triangles": sc.triangle_count, "mrays_per_s": round(rays / ms / 1e3, 1),
+            "probes_updated_per_s": round(N / ms * 1e3, 1), "ms_per_step": round(ms, 4), "steps": steps,
+            "kernels_ms": {"k_trace": round(a[1], 4), "k_shadow": round(a[4], 4), "k_shade": round(a[2], 4), "k_probe_update": round(a[3], 4)},
+            "shadow_rays_per_ray": round(c.shadow_rays / rays, 4), "primary_nodes_per_ray": round(c.primary_node_visits / rays, 2),
+            "setup_s": round(setup, 1)}
 
 
 def cpu_cores():
