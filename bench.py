@@ -296,11 +296,15 @@ def per_ray(cnt):
 
 
 # rocprofv3 kernel names -> the bench's kernel keys
-PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow"], "k_probe_update": ["k_probe_update"]}
+PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun"],
+               "k_probe_update": ["k_probe_update"]}
+# launched only for some scenes: the sun's light-space shadow traversal (a scene with a
+# sun), the world-BVH shadow traversal (other lights, or no sun BVH)
+PMC_OPTIONAL = {"k_trace_shadow", "k_trace_shadow_sun"}
 
 
 # every kernel of one probe-path update (the whole-update counter figure)
-PMC_PATH_KERNELS = ("k_probe_slots", "k_trace", "k_probe_offsets", "k_shadow_gen", "k_trace_shadow", "k_shade", "k_probe_update")
+PMC_PATH_KERNELS = ("k_probe_slots", "k_trace", "k_probe_offsets", "k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun", "k_shade", "k_probe_update")
 CLOCK_GHZ = 2.4      # MI355X max engine clock (MI355X_MICROARCH.md); the VALU fractions below use it
 SIMDS = 256 * 4      # 256 CUs x 4 SIMDs
 WAVE64_VALU_CYCLES = 2  # a wave64 VALU instruction issues over 2 cycles on the 32-wide CDNA4 SIMD
@@ -360,8 +364,8 @@ def roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G):
         if cfg.get("triangles") != args.triangles or cfg.get("grid") != G:
             pm, why = None, f"PMC summary {pm.get('tag')} is of another workload: not used"
     if pm is not None:
-        ks = [pm["kernels"].get(k) for k in PMC_KERNELS[dom]]
-        if any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
+        ks = [pm["kernels"].get(k) for k in PMC_KERNELS[dom] if k not in PMC_OPTIONAL or k in pm["kernels"]]
+        if not ks or any(k is None or "hbm_bytes_per_launch" not in k for k in ks):
             pm, why = None, f"PMC summary {pm.get('tag')} lacks {dom}"
     if pm is not None:
         # achieved / frac: the PMC pass's bytes over the PMC pass's own average launch
@@ -396,8 +400,9 @@ def roofline(args, dom, kernel_bytes, kernel_ms, ms_per_step, lib_sha, G):
              "cache_inclusive_achieved": round(step_alg / (ms_per_step * 1e-3) / 1e9, 2),
              "cache_inclusive_frac": round(step_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
              "hbm_bytes_per_step": None, "achieved": None, "frac": None}
-    if pm is not None and all(k in pm["kernels"] and "hbm_bytes_per_launch" in pm["kernels"][k] for k in PMC_PATH_KERNELS):
-        hbm = sum(pm["kernels"][k]["hbm_bytes_per_launch"] for k in PMC_PATH_KERNELS)
+    path = [k for k in PMC_PATH_KERNELS if k not in PMC_OPTIONAL or (pm is not None and k in pm["kernels"])]
+    if pm is not None and all(k in pm["kernels"] and "hbm_bytes_per_launch" in pm["kernels"][k] for k in path):
+        hbm = sum(pm["kernels"][k]["hbm_bytes_per_launch"] for k in path)
         whole.update(hbm_bytes_per_step=int(hbm), achieved=round(hbm / (ms_per_step * 1e-3) / 1e9, 2),
                      frac=round(hbm / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     roof["whole_update"] = whole

@@ -22,11 +22,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name: str) -> str:
     """ark::dev::k_trace<false, 6, ProbeRays>(...) -> k_trace; <true, ...> -> k_trace_counting;
-    the reflections' instantiations -> k_refl_trace / k_refl_shadow_gen."""
+    the reflections' instantiations -> k_refl_trace / k_refl_shadow_gen; the sun's
+    shadow traversal k_trace_shadow<.., .., true> -> k_trace_shadow_sun."""
     m = re.search(r"\b(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
     if not m:
         return name
     base = m.group(1)
+    if base == "k_trace_shadow" and m.group(2) and m.group(2).rstrip(">").split(",")[-1].strip() == "true":
+        base = "k_trace_shadow_sun"  # <COUNT, WPE, SUN = true>: the sun's light-space traversal
     if base == "k_trace" and "ListRays" in name:
         return "k_refl_trace"
     if base == "k_shadow_gen":
