@@ -26,9 +26,11 @@ def short(name):
 
 def base_name(name):
     """k_trace<false, 6> -> k_trace (timed variants only; counting ones are skipped)."""
-    m = re.match(r"(k_[a-z0-9_]+)(<([a-z]+))?", name)
+    m = re.match(r"(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
     if not m or m.group(3) == "true":
         return None
+    if m.group(1) == "k_trace_shadow" and m.group(2) and m.group(2).rstrip(">").split(",")[-1].strip() == "true":
+        return "k_trace_shadow_sun"  # <.., .., SUN = true>: the sun's light-space traversal
     return m.group(1)
 
 
