@@ -1065,14 +1065,11 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     // is counted in out[8] (must stay 0: the form must be conservative).
     const char* boxEnv = std::getenv("ARK_SIM_BOX");
     const int boxMode = !boxEnv ? 0 : std::strcmp(boxEnv, "kernel32") == 0 ? 1 : std::strcmp(boxEnv, "f16") == 0 ? 2 : std::strcmp(boxEnv, "f16s") == 0 ? 3 : 0;
-    // f16s: q as the fp16 subnormal q * 2^-24 (no 1024 bias), A = a * 2^24 (per-ray
-    // scale so that the largest step of any node fits)
-    double maxStep = 0.0;
-    for (const GpuBvh8Node& nd : r8.nodes)
-        for (int a = 0; a < 3; ++a) maxStep = std::max(maxStep, std::ldexp(1.0, static_cast<int>(nd.e[a]) - 127));
+    // f16s: q as the fp16 subnormal q * 2^-24 (no 1024 bias), A = a * 2^(24 - s) with a
+    // per-node scale s (ARK_NODE_F16's visitNode8)
     // the f16 form's error bound e = EA |a| + EB |B'| + 2^-22 (sensitivity runs only:
     // the defaults are the proven bound)
-    const float simEA = std::getenv("ARK_SIM_E_A") ? static_cast<float>(std::atof(std::getenv("ARK_SIM_E_A"))) : 1.3f;
+    const float simEA = std::getenv("ARK_SIM_E_A") ? static_cast<float>(std::atof(std::getenv("ARK_SIM_E_A"))) : (boxMode == 3 ? 0.3f : 1.3f);
     const float simEB = std::getenv("ARK_SIM_E_B") ? static_cast<float>(std::atof(std::getenv("ARK_SIM_E_B"))) : 0x1p-9f;
     // scene bounds of the anchors (every node box lies inside the root's planes)
     double sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };
@@ -1098,11 +1095,6 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
             uint64_t steps = 0;
             // f16 form: per-ray scale 2^-s so that |b - 1024 a| and every t fit fp16
             int sExp = 0;
-            if (boxMode == 3) {
-                double mi = 0.0;
-                for (int a = 0; a < 3; ++a) mi = std::max(mi, std::fabs(static_cast<double>(idir[a])));
-                sExp = std::max(0, std::ilogb(std::max(maxStep * mi, 1e-30)) + 1 + 24 - 15);
-            }
             if (boxMode == 2) {
                 double m = 0.0;
                 for (int a = 0; a < 3; ++a)
@@ -1146,15 +1138,24 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                     tmax16 = rn16(std::ldexp(static_cast<double>(tmax), -sExp) * (1.0 + 0x1p-9));
                 }
                 if (boxMode == 3) {
+                    // per-node scale 2^-s (visitNode8 with ARK_NODE_F16): the largest
+                    // A = a * 2^(24 - s) of the node stays below 2^15
+                    int L = 0;
+                    (void)std::frexp(std::max({ std::fabs(idir[0]), std::fabs(idir[1]), std::fabs(idir[2]) }), &L);
+                    const int emax = std::max({ static_cast<int>(nd.e[0]), static_cast<int>(nd.e[1]), static_cast<int>(nd.e[2]) });
+                    const int sN = std::max(0, emax - 127 + L + 9);
                     for (int a = 0; a < 3; ++a) {
-                        const float as = std::ldexp(a32[a], -sExp), bs = std::ldexp(b32[a], -sExp);
-                        const float e = std::fma(std::fabs(as), simEA, std::fma(std::fabs(bs), simEB, 0x1p-22f));
-                        A16[a] = rn16(std::ldexp(static_cast<double>(as), 24));
-                        Bn16[a] = rn16(static_cast<double>(bs - e));
-                        Bf16[a] = rn16(static_cast<double>(bs + e));
+                        const float Aa = std::ldexp(idir[a], static_cast<int>(nd.e[a]) - 103 - sN);
+                        const float bs = std::ldexp(b32[a], -sN);
+                        const float e = std::fma(std::fabs(Aa), simEA * 0x1p-24f, std::fma(std::fabs(bs), simEB, 0x1p-22f));
+                        A16[a] = rn16(Aa);
+                        // (B, e) rounded to fp16 first, then one packed add each way
+                        const double b16 = rn16(bs), e16 = rn16(e);
+                        Bn16[a] = rn16(b16 - e16);
+                        Bf16[a] = rn16(b16 + e16);
                     }
-                    tmin16 = rn16(std::ldexp(static_cast<double>(tmin), -sExp) * (1.0 - 0x1p-9));
-                    tmax16 = rn16(std::ldexp(static_cast<double>(tmax), -sExp) * (1.0 + 0x1p-9));
+                    tmin16 = 0.0;  // the kernel does not apply tmin (conservative)
+                    tmax16 = rn16(static_cast<double>(std::ldexp(tmax, -sN) * (1.0f + 0x1p-9f)));
                 }
                 for (int s = 0; s < 8; ++s) {
                     const bool internal = (nd.imask >> s) & 1u;

@@ -346,6 +346,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_NODE_INSIDE
 #define ARK_NODE_INSIDE 0 // 1: origin-containing children first, else plain octant order (40 VALU per node for +0.8 % node visits)
 #endif
+#ifndef ARK_NODE_F16
+#define ARK_NODE_F16 0 // 1: the child box tests in packed fp16 (visitNode8: two children per instruction, outward margins)
+#endif
 // LDS octant permutation table of the node visit (loadNodeCache fills it; every
 // kernel that visits nodes calls loadNodeCache first)
 __shared__ uint8_t g_octPerm[8 * 256];
@@ -361,9 +364,95 @@ __device__ __forceinline__ uint32_t shiftInLe(uint32_t m, float a, float b)
 }
 #endif
 
+#if ARK_NODE_F16
+// One pair of children (slots 2j + 1, 2j of a plane word) in packed fp16: the eight
+// plane bytes as fp16 subnormals q * 2^-24 (v_perm_b32 with a zero high byte, SEL),
+// t = fma(q * 2^-24, A, B) per plane, A and B broadcast from their register's half by
+// op_sel, near planes with B - e (the low half of the axis's B register), far planes
+// with B + e (its high half), max3 with 0 / min3 with tmax (the low half of TMX), the
+// odd slot's then the even slot's compare shifted in.
+#define ARK_F16_PAIR(NX, NY, NZ, FX, FY, FZ, SEL)                                                              \
+    "v_perm_b32 %[t0], %[" NX "], %[" NX "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t1], %[" NY "], %[" NY "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t2], %[" NZ "], %[" NZ "], %[" SEL "]\n\t"                                                  \
+    "v_pk_fma_f16 %[t0], %[t0], %[axy], %[bx] op_sel:[0,0,0] op_sel_hi:[1,0,0]\n\t"                          \
+    "v_pk_fma_f16 %[t1], %[t1], %[axy], %[by] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"                          \
+    "v_pk_fma_f16 %[t2], %[t2], %[az], %[bz] op_sel:[0,0,0] op_sel_hi:[1,0,0]\n\t"                           \
+    "v_pk_maximum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
+    "v_pk_max_f16 %[t0], %[t0], 0\n\t"                                                                        \
+    "v_perm_b32 %[t1], %[" FX "], %[" FX "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t2], %[" FY "], %[" FY "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t3], %[" FZ "], %[" FZ "], %[" SEL "]\n\t"                                                  \
+    "v_pk_fma_f16 %[t1], %[t1], %[axy], %[bx] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                          \
+    "v_pk_fma_f16 %[t2], %[t2], %[axy], %[by] op_sel:[0,1,1] op_sel_hi:[1,1,1]\n\t"                          \
+    "v_pk_fma_f16 %[t3], %[t3], %[az], %[bz] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_minimum3_f16 %[t1], %[t1], %[t2], %[t3]\n\t"                                                        \
+    "v_pk_min_f16 %[t1], %[t1], %[tmx] op_sel:[0,0] op_sel_hi:[1,0]\n\t"                                      \
+    "v_cmp_le_f16_sdwa vcc, %[t0], %[t1] src0_sel:WORD_1 src1_sel:WORD_1\n\t"                                \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"                                                  \
+    "v_cmp_le_f16_e32 vcc, %[t0], %[t1]\n\t"                                                                  \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
+
+__device__ __forceinline__ uint32_t cvtPkF16(float lo, float hi)
+{
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+#endif
+
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
+#if ARK_NODE_F16
+    // Packed-fp16 child tests. Per node: a scale 2^-s that keeps the node's largest
+    // A = step * idir * 2^(24 - s) below 2^15 (fp16 range), A per axis (the q factor:
+    // q enters as the fp16 subnormal q * 2^-24), B = (anchor - o) * idir * 2^-s, and
+    // an error bound per axis e = 0.3 |A| 2^-24 + 2^-9 |B| + 2^-22 that covers the
+    // rounding of A to fp16 over q <= 255 steps (0.125 |a|), of the product-sum
+    // (0.125 |a| + 2^-11 |t|), of B and B -+ e (2^-11 each): near planes use B - e, far
+    // planes B + e, tmin rounds down and tmax up, so no box holding an exact hit is
+    // culled (the host simulation, ark_ddgi_debug_bvh8_trace_stats ARK_SIM_BOX=f16s,
+    // counts none; the hits themselves stay fp32 and bit-exact).
+    const int ex = static_cast<int>(w0.w & 0xffu), ey = static_cast<int>((w0.w >> 8) & 0xffu), ez = static_cast<int>((w0.w >> 16) & 0xffu);
+    const int emax = max(max(ex, ey), ez);
+    const int L = __builtin_amdgcn_frexp_expf(fmaxf(fmaxf(fabsf(idir.x), fabsf(idir.y)), fabsf(idir.z)));
+    const int sN = max(0, emax - 127 + L + 9);
+    const float Ax = __builtin_amdgcn_ldexpf(idir.x, ex - 103 - sN), Ay = __builtin_amdgcn_ldexpf(idir.y, ey - 103 - sN),
+                Az = __builtin_amdgcn_ldexpf(idir.z, ez - 103 - sN);
+    const float bx = __builtin_amdgcn_ldexpf((__uint_as_float(w0.x) - o.x) * idir.x, -sN);
+    const float by = __builtin_amdgcn_ldexpf((__uint_as_float(w0.y) - o.y) * idir.y, -sN);
+    const float bz = __builtin_amdgcn_ldexpf((__uint_as_float(w0.z) - o.z) * idir.z, -sN);
+    auto err = [](float A, float b) { return fmaf(fabsf(A), 0.3f * 0x1p-24f, fmaf(fabsf(b), 0x1p-9f, 0x1p-22f)); };
+    const uint32_t axy = cvtPkF16(Ax, Ay), az = cvtPkF16(Az, Az);
+    // per axis (B - e, B + e): (B, e) in fp16, then one packed add with the low lane's e
+    // negated; its rounding is in e's budget
+    auto biases = [](float b, float e) {
+        uint32_t r;
+        asm("v_cvt_pk_f16_f32 %0, %1, %2\n\tv_pk_add_f16 %0, %0, %0 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[0,1]" : "=&v"(r) : "v"(b), "v"(e));
+        return r;
+    };
+    const uint32_t bxp = biases(bx, err(Ax, bx)), byp = biases(by, err(Ay, by)), bzp = biases(bz, err(Az, bz));
+    // tmin is not applied (0 instead: a box within tmin of the origin is visited, which
+    // is conservative); tmax rounds up
+    (void)tmin;
+    const uint32_t tmx = cvtPkF16(__builtin_amdgcn_ldexpf(tmax, -sN) * (1.0f + 0x1p-9f), 0.0f);
+    const uint32_t imask = w0.w >> 24;
+    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
+    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
+    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
+    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
+    uint32_t hitSlots = 0, t0, t1, t2, t3;
+    const uint32_t selLo = 0x0c010c00u, selHi = 0x0c030c02u; // bytes (0, 1) / (2, 3) as fp16 subnormals
+    asm(ARK_F16_PAIR("nx1", "ny1", "nz1", "fx1", "fy1", "fz1", "shi") ARK_F16_PAIR("nx1", "ny1", "nz1", "fx1", "fy1", "fz1", "slo")
+        ARK_F16_PAIR("nx0", "ny0", "nz0", "fx0", "fy0", "fz0", "shi") ARK_F16_PAIR("nx0", "ny0", "nz0", "fx0", "fy0", "fz0", "slo")
+        : [acc] "+v"(hitSlots), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+        : [nx0] "v"(nX0), [nx1] "v"(nX1), [ny0] "v"(nY0), [ny1] "v"(nY1), [nz0] "v"(nZ0), [nz1] "v"(nZ1), [fx0] "v"(fX0), [fx1] "v"(fX1),
+          [fy0] "v"(fY0), [fy1] "v"(fY1), [fz0] "v"(fZ0), [fz1] "v"(fZ1), [axy] "v"(axy), [az] "v"(az), [bx] "v"(bxp), [by] "v"(byp),
+          [bz] "v"(bzp), [tmx] "v"(tmx), [slo] "s"(selLo), [shi] "s"(selHi)
+        : "vcc");
+    const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
+#else
 #if ARK_NODE_LDEXP
     // exponent byte e: the step is 2^(e - 127) (e = 0 never occurs for a used axis:
     // the builder's steps are normal numbers)
@@ -420,6 +509,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     (void)insideLo;
     const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
 #endif
+#endif // ARK_NODE_F16
     // leaf children: their triangle rows (GpuBvh8Node: bit s + stride i = triangle
     // i of leaf slot s), the hit leaf slots spread over the three rows and masked
     gBase = w1.x;
