@@ -236,6 +236,9 @@ class ArkDdgiBvhStats(C.Structure):
         ("build_ms", C.c_float),
         ("node_bytes", C.c_uint64),
         ("triangle_bytes", C.c_uint64),
+        ("sun_node_count", C.c_uint64),
+        ("sun_cost_world", C.c_float),
+        ("sun_cost_light", C.c_float),
     ]
 
 
@@ -444,6 +447,7 @@ EXPORTS = {
     "ark_ddgi_debug_bvh8_check": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_bvh8_trace_stats": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
     "ark_ddgi_debug_sun_bvh_check": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_float, C.POINTER(C.c_uint64)]),
+    "ark_ddgi_debug_sun_choice": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
 }
 
 _lib = None

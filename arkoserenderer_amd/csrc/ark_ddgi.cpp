@@ -132,6 +132,7 @@ struct SceneStore {
     DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
     DeviceBuffer sunNodes; // light-space BVH8 of the sun's shadow rays + its world-space triangle records
     uint64_t sunBvhNodes = 0;
+    float sunCostWorld = 0.0f, sunCostLight = 0.0f; // sampled sun shadow-ray steps per ray (sun_shadow_cost)
     std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
     std::vector<ArkRTTriangleMesh> meshHost;
     SceneArgs args {};
@@ -189,7 +190,7 @@ struct ArkDdgiCtx {
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
-    bool sunBvh = true;            // ARK_SUN_BVH=0: the sun's shadow rays traverse the world BVHs
+    int sunBvh = -1;               // ARK_SUN_BVH: 0 the sun's shadow rays traverse the world BVHs, 1 the light-space BVH, unset: by cost (sun_bvh_pays)
     uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined window below kPipeHalfRays rays
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
@@ -515,7 +516,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
-        if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0;
+        if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0 ? 1 : 0;
         if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
         // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
         // across queues: a polling wait could then hold the GPU while the kernel it
@@ -751,7 +752,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BVH8_NODE_COST")) copt.node_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     // the sun's light-space BVH input, before the class builds free their triangles
-    const bool sunBvh = s->has_directional_light && ctx->sunBvh;
+    const bool sunBvh = s->has_directional_light && ctx->sunBvh != 0;
     SunBvhInput sunIn;
     if (sunBvh) {
         sun_frame(s->directional_light.world_space_direction, sunIn.frame);
@@ -855,11 +856,24 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     allTris.pop_back();
     uint64_t sunNodeCount = 0;
     size_t sunTriOffset = 0;
+    Bvh8BuildResult r;
+    bool sunBuilt = false;
     if (sunBvh && !sunIn.tris.empty()) {
-        Bvh8BuildResult r;
+        sunBuilt = true;
         if (!build_sun_bvh(sunIn, opt, copt, r)) return ctx->fail(ARK_DDGI_E_DEVICE, "sun BVH2 leaf over %d triangles", kBvh8MaxLeafSize);
         const int32_t sroot = 0;
         if (const int rc2 = checkBvh8(ctx, r.nodes, r.tris, &sroot, 1)) return rc2;
+        // by cost unless forced: sample sun shadow rays through both structures on the host
+        const float* sd = s->directional_light.world_space_direction;
+        const float dd = sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2];
+        const float isc = 1.0f / std::sqrt(dd);
+        const float L[3] = { -(sd[0] * isc), -(sd[1] * isc), -(sd[2] * isc) };
+        std::vector<float> origins;
+        sun_sample_origins(allTris, L, 4096u, origins);
+        st->sunCostWorld = static_cast<float>(sun_shadow_cost(allNodes, allTris, roots, 3, nullptr, L, origins));
+        st->sunCostLight = static_cast<float>(sun_shadow_cost(r.nodes, r.tris, &sroot, 1, sunIn.frame, L, origins));
+    }
+    if (sunBuilt && (ctx->sunBvh == 1 || sun_bvh_pays(st->sunCostWorld, st->sunCostLight))) {
         const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
         sunTriOffset = (nb + 255) & ~static_cast<size_t>(255);
         r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
@@ -952,6 +966,9 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     st->bvhStats.build_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
     st->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvh8Node);
     st->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
+    st->bvhStats.sun_node_count = sunNodeCount;
+    st->bvhStats.sun_cost_world = st->sunCostWorld;
+    st->bvhStats.sun_cost_light = st->sunCostLight;
     return adoptScene(ctx, std::move(st));
 }
 

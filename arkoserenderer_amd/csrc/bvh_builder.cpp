@@ -1005,6 +1005,107 @@ bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8Collap
     return true;
 }
 
+void sun_sample_origins(const std::vector<GpuTriangle>& tris, const float L[3], uint32_t n, std::vector<float>& out)
+{
+    out.clear();
+    if (tris.empty() || n == 0) return;
+    uint64_t x = 0x9E3779B97F4A7C15ull; // xorshift64: the same samples every build
+    auto next = [&]() {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return x;
+    };
+    for (uint64_t tries = 0; out.size() < 3ull * n && tries < 32ull * n; ++tries) {
+        const GpuTriangle& g = tris[next() % tris.size()];
+        if (isHoleTriangle(g)) continue;
+        const double e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+        const double nrm[3] = { e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0] };
+        uint32_t flip;
+        std::memcpy(&flip, &g.t2[3], 4);
+        const double dn = (nrm[0] * L[0] + nrm[1] * L[1] + nrm[2] * L[2]) * (flip ? -1.0 : 1.0);
+        if (!(dn > 0.0)) continue; // the front face (CCW, mirrored instances flipped) must face the sun
+        const double r1 = static_cast<double>(next() >> 11) * 0x1p-53, r2 = static_cast<double>(next() >> 11) * 0x1p-53;
+        const double sq = std::sqrt(r1), b1 = sq * (1.0 - r2), b2 = sq * r2;
+        for (int a = 0; a < 3; ++a) out.push_back(static_cast<float>(g.t0[a] + b1 * e1[a] + b2 * e2[a]));
+    }
+}
+
+double sun_shadow_cost(const std::vector<GpuBvh8Node>& nodes, const std::vector<GpuTriangle>& tris, const int32_t* roots, int nRoots,
+                       const double (*frame)[3], const float L[3], const std::vector<float>& origins)
+{
+    const size_t n = origins.size() / 3;
+    if (n == 0) return 0.0;
+    const float tmin = 0.025f, tmax = 1e30f;
+    uint64_t steps = 0;
+    std::vector<uint32_t> stack;
+    for (size_t r = 0; r < n; ++r) {
+        const float* P = &origins[3 * r];
+        float ob[3], db[3];
+        for (int a = 0; a < 3; ++a) {
+            ob[a] = frame ? static_cast<float>(frame[a][0] * P[0] + frame[a][1] * P[1] + frame[a][2] * P[2]) : P[a];
+            db[a] = frame ? (a == 2 ? 1.0f : 0.0f) : L[a];
+        }
+        float idir[3];
+        for (int a = 0; a < 3; ++a) idir[a] = 1.0f / (std::fabs(db[a]) < 1e-20f ? std::copysign(1e-20f, db[a]) : db[a]);
+        bool hit = false;
+        for (int k = 0; k < nRoots && !hit; ++k) {
+            if (roots[k] < 0) continue;
+            stack.assign(1, static_cast<uint32_t>(roots[k]));
+            while (!stack.empty() && !hit) {
+                const GpuBvh8Node& nd = nodes[stack.back()];
+                stack.pop_back();
+                steps++;
+                struct Cand { float tn; int s; } hc[8];
+                int nh = 0;
+                uint32_t before[8], cnt = 0;
+                for (int s = 0; s < 8; ++s) {
+                    before[s] = cnt;
+                    if ((nd.imask >> s) & 1u) cnt++;
+                    if (!((nd.imask >> s) & 1u) && !((nd.leaf_mask >> s) & 1u)) continue;
+                    float tn = tmin, tf = tmax;
+                    for (int a = 0; a < 3; ++a) {
+                        const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
+                        float t0 = (std::fma(static_cast<float>(nd.qlo[a][s]), step, nd.p[a]) - ob[a]) * idir[a];
+                        float t1 = (std::fma(static_cast<float>(nd.qhi[a][s]), step, nd.p[a]) - ob[a]) * idir[a];
+                        if (t0 > t1) std::swap(t0, t1);
+                        tn = std::max(tn, t0);
+                        tf = std::min(tf, t1);
+                    }
+                    if (tn <= tf * 1.00001f + 1e-7f) hc[nh++] = { tn, s };
+                }
+                std::sort(hc, hc + nh, [](const Cand& p, const Cand& q) { return p.tn < q.tn; });
+                // the node's leaf triangles first (the dual step), nearest leaf first
+                for (int i = 0; i < nh && !hit; ++i) {
+                    if ((nd.imask >> hc[i].s) & 1u) continue;
+                    uint32_t t[kBvh8MaxLeafSize];
+                    const int c = bvh8SlotTriangles(nd, hc[i].s, t);
+                    for (int j = 0; j < c && !hit; ++j) {
+                        steps++;
+                        const GpuTriangle& g = tris[t[j]];
+                        const float v0[3] = { g.t0[0], g.t0[1], g.t0[2] }, e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+                        const float pv[3] = { L[1] * e2[2] - L[2] * e2[1], L[2] * e2[0] - L[0] * e2[2], L[0] * e2[1] - L[1] * e2[0] };
+                        const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+                        if (det == 0.0f) continue;
+                        const float inv = 1.0f / det;
+                        const float sv[3] = { P[0] - v0[0], P[1] - v0[1], P[2] - v0[2] };
+                        const float u = (sv[0] * pv[0] + sv[1] * pv[1] + sv[2] * pv[2]) * inv;
+                        if (!(u >= 0.0f && u <= 1.0f)) continue;
+                        const float q[3] = { sv[1] * e1[2] - sv[2] * e1[1], sv[2] * e1[0] - sv[0] * e1[2], sv[0] * e1[1] - sv[1] * e1[0] };
+                        const float v = (L[0] * q[0] + L[1] * q[1] + L[2] * q[2]) * inv;
+                        if (!(v >= 0.0f && u + v <= 1.0f)) continue;
+                        const float tt = (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]) * inv;
+                        hit = tt >= tmin && tt <= tmax;
+                    }
+                }
+                for (int i = nh - 1; i >= 0 && !hit; --i)
+                    if ((nd.imask >> hc[i].s) & 1u) stack.push_back(nd.child_base + before[hc[i].s]);
+            }
+        }
+    }
+    return static_cast<double>(steps) / static_cast<double>(n);
+}
+
 } // namespace ark
 
 // Round to the nearest fp16 value (RNE; +-inf above the largest finite value),
@@ -1056,6 +1157,9 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     std::atomic<uint64_t> nodes { 0 }, triTests { 0 }, hits { 0 }, maxSteps { 0 }, boxViolations { 0 };
     // ARK_SIM_ORDER=distance: exact front-to-back child order (what octant order approximates)
     const bool sortByDistance = std::getenv("ARK_SIM_ORDER") && std::strcmp(std::getenv("ARK_SIM_ORDER"), "distance") == 0;
+    // ARK_SIM_ANYHIT=1: shadow-ray statistics - tmin 0.025 (k_shadow_gen's), the ray
+    // ends at its first hit (any-hit, k_trace_shadow)
+    const bool anyHit = std::getenv("ARK_SIM_ANYHIT") && std::atoi(std::getenv("ARK_SIM_ANYHIT")) != 0;
     // ARK_SIM_BOX: the child box test. "exact" (default): decoded planes, (p - o) * idir;
     // "kernel32": k_trace's fp32 form t = fma(q, step * idir, (anchor - o) * idir);
     // "f16": the packed-f16 form (visitNode8 with ARK_NODE_F16): per-ray scale 2^-s,
@@ -1086,7 +1190,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
             const float* ry = rays + 7 * r;
             const float o[3] = { ry[0], ry[1], ry[2] }, d[3] = { ry[3], ry[4], ry[5] };
             float tmax = ry[6];
-            const float tmin = 1e-4f;
+            const float tmin = anyHit ? 0.025f : 1e-4f;
             float idir[3];
             for (int a = 0; a < 3; ++a) idir[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? (d[a] < 0.0f ? -1e-20f : 1e-20f) : d[a]);
             const uint32_t oct = (idir[0] < 0 ? 1u : 0u) | (idir[1] < 0 ? 2u : 0u) | (idir[2] < 0 ? 4u : 0u);
@@ -1101,7 +1205,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                     m = std::max(m, std::max(std::fabs(sceneHi[a] - o[a]), std::fabs(sceneLo[a] - o[a])) * std::fabs(static_cast<double>(idir[a])));
                 sExp = std::max(0, std::ilogb(std::max(m * 10.0, 1e-30)) + 1 - 15);
             }
-            while (!stack.empty()) {
+            while (!stack.empty() && !(anyHit && hit)) {
                 const uint32_t ni = stack.back();
                 stack.pop_back();
                 const GpuBvh8Node& nd = r8.nodes[ni];
@@ -1206,7 +1310,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                     internalBefore[s] = cntInt;
                     if ((nd.imask >> s) & 1u) cntInt++;
                 }
-                for (int i = 0; i < nh; ++i) {
+                for (int i = 0; i < nh && !(anyHit && hit); ++i) {
                     const int s = hitc[i].s;
                     if ((nd.imask >> s) & 1u) continue;
                     uint32_t slotTris[kBvh8MaxLeafSize];
@@ -1231,6 +1335,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                         if (tt >= tmin && tt <= tmax) {
                             tmax = tt;
                             hit = true;
+                            if (anyHit) break;
                         }
                     }
                 }
@@ -1408,3 +1513,48 @@ extern "C" int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, 
     return mism.load() == 0 ? 0 : 2;
 }
 
+
+// ark_ddgi_debug.h: set_scene's choice between the light-space BVH and the world BVH
+// for the sun's shadow rays, on a triangle soup (one hit-mask class).
+extern "C" int ark_ddgi_debug_sun_choice(const float* triangles, uint64_t n, const float* sun_dir, uint32_t n_samples, double* out)
+{
+    using namespace ark;
+    if (n == 0 || !out) return 1;
+    std::vector<BuildTriangle> tris(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            tris[i].v0[a] = triangles[9 * i + a];
+            tris[i].v1[a] = triangles[9 * i + 3 + a];
+            tris[i].v2[a] = triangles[9 * i + 6 + a];
+        }
+        tris[i].instance = 0;
+        tris[i].primitive = static_cast<uint32_t>(i);
+        tris[i].flip_facing = 0;
+    }
+    SunBvhInput in;
+    sun_frame(sun_dir, in.frame);
+    sun_add_triangles(in, tris);
+    double frame[3][3];
+    std::memcpy(frame, in.frame, sizeof(frame));
+    BvhBuildOptions opt;
+    opt.max_leaf_size = kBvh8MaxLeafSize;
+    opt.inflate_abs = bvh8_inflation(triangles, n);
+    opt.threads = 8;
+    Bvh8CollapseOptions copt;
+    const BvhBuildResult r2 = build_bvh(tris, opt, 0u, 0u);
+    if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return 1;
+    const Bvh8BuildResult w8 = collapse_bvh8(r2, 0u, 0u, copt);
+    Bvh8BuildResult s8;
+    if (!build_sun_bvh(in, opt, copt, s8)) return 1;
+    const float dd = sun_dir[0] * sun_dir[0] + sun_dir[1] * sun_dir[1] + sun_dir[2] * sun_dir[2];
+    const float sc = 1.0f / std::sqrt(dd);
+    const float L[3] = { -(sun_dir[0] * sc), -(sun_dir[1] * sc), -(sun_dir[2] * sc) };
+    std::vector<float> origins;
+    sun_sample_origins(w8.tris, L, n_samples, origins);
+    const int32_t root = 0;
+    out[0] = sun_shadow_cost(w8.nodes, w8.tris, &root, 1, nullptr, L, origins);
+    out[1] = sun_shadow_cost(s8.nodes, s8.tris, &root, 1, frame, L, origins);
+    out[2] = sun_bvh_pays(out[0], out[1]) ? 1.0 : 0.0;
+    out[3] = static_cast<double>(origins.size() / 3);
+    return 0;
+}

@@ -108,5 +108,17 @@ void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_
 // (copt, slots sorted by w) and swaps in the world records; consumes in.tris and
 // in.world. False when a BVH2 leaf exceeds kBvh8MaxLeafSize.
 bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8CollapseOptions& copt, Bvh8BuildResult& out);
+// Whether the light-space BVH pays for a scene: n sample sun shadow rays (points on
+// triangles whose front face faces the sun, deterministic) traced any-hit on the host
+// through both structures (exact decoded planes, tmin 0.025; frame == nullptr: the
+// world BVHs and their roots, else the light frame with rays along +w), cost = node
+// visits + triangle tests per ray - the persistent traversals' steps. Large
+// axis-aligned surfaces (walls, a ground plane: C5's city block) become long slanted
+// boxes in light space, where the world BVH culls them.
+void sun_sample_origins(const std::vector<GpuTriangle>& tris, const float L[3], uint32_t n, std::vector<float>& out_xyz);
+double sun_shadow_cost(const std::vector<GpuBvh8Node>& nodes, const std::vector<GpuTriangle>& tris, const int32_t* roots, int nRoots,
+                       const double (*frame)[3], const float L[3], const std::vector<float>& origins_xyz);
+// The light-space traversal has no LDS node cache: it must save a tenth of the steps.
+inline bool sun_bvh_pays(double costWorld, double costLight) { return costLight < 0.9 * costWorld; }
 
 } // namespace ark

@@ -1727,38 +1727,28 @@ __device__ __forceinline__ V3 shfl3(V3 v, uint32_t src)
 // three hit-mask classes in turn, no alpha test, dual steps. Lanes are refilled
 // from a wave-private pool like k_trace; an occluded ray sets bit 16 + light of its
 // probe ray's word. `pass` of a helper lane holds (root lane + 1) << 8.
-// SUN: the sun's list (FrameArgs::sun_rays) through the light-space BVH (one pass,
-// travStepSun); else the rest of the shadow rays (or all of them, without a sun BVH)
-// through the three world BVHs.
-template<bool COUNT, int WPE, bool SUN = false>
-__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
-{
-    if (frameAborted(f.abort_word)) return;
+// MODE: kShadowWorld - the shadow rays through the three world BVHs; kShadowSun - the
+// sun's list (FrameArgs::sun_rays) through the light-space BVH (one pass, travStepSun);
+// kShadowSunWorld - both in one launch: each wave drains the sun's list, then takes
+// rays from the other list, so the first list's tail overlaps the second list's work
+// instead of ending a launch (C5: 1.98 ms one list, 3.27 ms two launches).
+constexpr int kShadowWorld = 0, kShadowSun = 1, kShadowSunWorld = 2;
+
+template<bool COUNT, bool SUN>
+__device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs& f, const NodeCache& nc, Stack<kTraceBlock>& st, const TailLds& tl,
+                                            uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow
 #ifdef ARK_TAIL_PROBE
-    const unsigned long long tStart = wall_clock64();
-    unsigned long long tEx = 0, itAll = 0, itEx = 0;
+                                            , unsigned long long* tp
 #endif
-    __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
-    // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
-    // (the light-space traversal caches none)
-    constexpr int kNodes = SUN ? 1 : ARK_SHADOW_LDS_NODES;
-    __shared__ uint4 ldsNodes[kNodes * 5];
-    __shared__ uint8_t ldsTable[kTraceBlock];
-    __shared__ uint32_t ldsBytes[kTraceBlock / 4];
+)
+{
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
-    if (lane < 16u) ldsBytes[(wbase >> 2) + lane] = 0u; // wave-private
-    NodeCache nc { nullptr, 0u, 0u };
-    if constexpr (!SUN) nc = loadNodeCache<kTraceBlock, kNodes>(sc, ldsNodes);
-    (void)ldsNodes;
-    const TailLds tl { ldsTable, ldsBytes };
-    const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
-    Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
+    if (lane < 16u) tl.bytes[(wbase >> 2) + lane] = 0u; // wave-private tail bytes
     const float tmin = 0.025f;
     const uint32_t total = SUN ? *f.sun_count : *f.shadow_count;
     uint32_t* const heads = SUN ? f.sun_heads : f.shadow_heads;
     const ShadowRay* const list = SUN ? f.sun_rays : f.shadow_rays;
     const int32_t roots[3] = { SUN ? sc.sun_root : sc.root_opaque, SUN ? -1 : sc.root_masked, SUN ? -1 : sc.root_blend };
-    uint32_t cNodes = 0, cTris = 0, cShadow = 0;
 
     uint32_t poolNext = 0, poolEnd = 0;
     const uint32_t home = xccId();
@@ -1826,8 +1816,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         }
         if (__ballot(active) == 0) break;
 #ifdef ARK_TAIL_PROBE
-        itAll++;
-        if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
+        tp[1]++;
+        if (exhausted) { if (!tp[0]) tp[0] = wall_clock64(); tp[2]++; }
 #endif
         if (exhausted) {
             // ---- tail: resolved rays stop, idle lanes take stack bottoms --------------
@@ -1902,12 +1892,45 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
     }
+}
+
+template<bool COUNT, int WPE, int MODE = kShadowWorld>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
+{
+    if (frameAborted(f.abort_word)) return;
+#ifdef ARK_TAIL_PROBE
+    const unsigned long long tStart = wall_clock64();
+    unsigned long long tp[3] = { 0, 0, 0 }; // first exhausted clock, iterations, exhausted iterations
+#endif
+    __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
+    // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
+    // (the light-space traversal caches none)
+    constexpr int kNodes = MODE == kShadowSun ? 1 : ARK_SHADOW_LDS_NODES;
+    __shared__ uint4 ldsNodes[kNodes * 5];
+    __shared__ uint8_t ldsTable[kTraceBlock];
+    __shared__ uint32_t ldsBytes[kTraceBlock / 4];
+    NodeCache nc { nullptr, 0u, 0u };
+    if constexpr (MODE != kShadowSun) nc = loadNodeCache<kTraceBlock, kNodes>(sc, ldsNodes);
+    (void)ldsNodes;
+    const TailLds tl { ldsTable, ldsBytes };
+    const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
+    Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
+    uint32_t cNodes = 0, cTris = 0, cShadow = 0;
+#ifdef ARK_TAIL_PROBE
+#define ARK_TP , tp
+#else
+#define ARK_TP
+#endif
+    if constexpr (MODE != kShadowWorld) shadowPhase<COUNT, true>(sc, f, nc, st, tl, cNodes, cTris, cShadow ARK_TP);
+    if constexpr (MODE != kShadowSun) shadowPhase<COUNT, false>(sc, f, nc, st, tl, cNodes, cTris, cShadow ARK_TP);
+#undef ARK_TP
 #ifdef ARK_TAIL_PROBE
     {
+        const uint32_t lane = threadIdx.x & 63u;
         const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
         if (lane == 0 && w < 32768) {
             unsigned long long* r = g_tail[1][w];
-            r[0] = tStart; r[1] = tEx; r[2] = wall_clock64(); r[3] = itAll; r[4] = itEx; r[5] = 0;
+            r[0] = tStart; r[1] = tp[0]; r[2] = wall_clock64(); r[3] = tp[1]; r[4] = tp[2]; r[5] = 0;
         }
     }
 #endif
@@ -2519,19 +2542,20 @@ hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks
     return hipGetLastError();
 }
 
-// The sun's list through the light-space BVH (when k_shadow_gen split it off), then
-// the other shadow rays through the world BVHs (when there are lights besides the sun,
-// or no sun list).
+// One launch: the sun's list through the light-space BVH (when k_shadow_gen split it
+// off; then the other lights' list in the same launch, kShadowSunWorld), or every
+// shadow ray through the world BVHs.
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     void* args[] = { const_cast<SceneArgs*>(&sc), const_cast<FrameArgs*>(&f) };
-    if (f.sun_rays) {
-        const void* fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, true>)
-                               : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, true>);
-        const hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(kTraceBlock), args, 0, s);
-        if (e != hipSuccess || f.light_count <= 1u) return e;
-    }
-    return hipLaunchKernel(kernel_trace_shadow_ptr(count), dim3(blocks), dim3(kTraceBlock), args, 0, s);
+    const void* fn = kernel_trace_shadow_ptr(count);
+    if (f.sun_rays && f.light_count <= 1u)
+        fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, dev::kShadowSun>)
+                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, dev::kShadowSun>);
+    else if (f.sun_rays)
+        fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, dev::kShadowSunWorld>)
+                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, dev::kShadowSunWorld>);
+    return hipLaunchKernel(fn, dim3(blocks), dim3(kTraceBlock), args, 0, s);
 }
 
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s)

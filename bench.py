@@ -224,6 +224,7 @@ def main():
             "bvh_nodes": int(bvh.node_count),
             "bvh_max_depth": int(bvh.max_depth),
             "bvh_build_ms": round(bvh.build_ms, 1),
+            "sun_bvh": sun_bvh_info(bvh),
             "setup_s": round(setup_s, 2),
             "lib_sha16": lib_sha,
         },
@@ -296,15 +297,15 @@ def per_ray(cnt):
 
 
 # rocprofv3 kernel names -> the bench's kernel keys
-PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun"],
+PMC_KERNELS = {"k_trace": ["k_trace"], "k_shade": ["k_shade"], "k_shadow": ["k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun", "k_trace_shadow_sunw"],
                "k_probe_update": ["k_probe_update"]}
 # launched only for some scenes: the sun's light-space shadow traversal (a scene with a
 # sun), the world-BVH shadow traversal (other lights, or no sun BVH)
-PMC_OPTIONAL = {"k_trace_shadow", "k_trace_shadow_sun"}
+PMC_OPTIONAL = {"k_trace_shadow", "k_trace_shadow_sun", "k_trace_shadow_sunw"}
 
 
 # every kernel of one probe-path update (the whole-update counter figure)
-PMC_PATH_KERNELS = ("k_probe_slots", "k_trace", "k_probe_offsets", "k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun", "k_shade", "k_probe_update")
+PMC_PATH_KERNELS = ("k_probe_slots", "k_trace", "k_probe_offsets", "k_shadow_gen", "k_trace_shadow", "k_trace_shadow_sun", "k_trace_shadow_sunw", "k_shade", "k_probe_update")
 CLOCK_GHZ = 2.4      # MI355X max engine clock (MI355X_MICROARCH.md); the VALU fractions below use it
 SIMDS = 256 * 4      # 256 CUs x 4 SIMDs
 WAVE64_VALU_CYCLES = 2  # a wave64 VALU instruction issues over 2 cycles on the 32-wide CDNA4 SIMD
@@ -536,13 +537,21 @@ def config_line(name, torch, device, steps=10, warmup=3):
     c = node.ctx.counters()
     node.ctx.set_counting(False)
     a = [sum(k[i] for k in kt) / len(kt) for i in range(5)]
+    bvh = node.ctx.bvh_stats()
     node.ctx.close()
     rays = N * R
     return {"workload": workload, "triangles": sc.triangle_count, "mrays_per_s": round(rays / ms / 1e3, 1),
             "probes_updated_per_s": round(N / ms * 1e3, 1), "ms_per_step": round(ms, 4), "steps": steps,
             "kernels_ms": {"k_trace": round(a[1], 4), "k_shadow": round(a[4], 4), "k_shade": round(a[2], 4), "k_probe_update": round(a[3], 4)},
             "shadow_rays_per_ray": round(c.shadow_rays / rays, 4), "primary_nodes_per_ray": round(c.primary_node_visits / rays, 2),
-            "setup_s": round(setup, 1)}
+            "sun_bvh": sun_bvh_info(bvh), "setup_s": round(setup, 1)}
+
+
+def sun_bvh_info(bvh):
+    """set_scene's choice for the sun's shadow rays: the light-space BVH8 (its nodes) or
+    the world BVHs, with the sampled any-hit steps per sun shadow ray of both."""
+    return {"light_space": bool(bvh.sun_node_count), "sampled_steps_world": round(bvh.sun_cost_world, 2),
+            "sampled_steps_light": round(bvh.sun_cost_light, 2)}
 
 
 def cpu_cores():

@@ -410,6 +410,12 @@ typedef struct ArkDdgiBvhStats {
     float build_ms;
     uint64_t node_bytes;
     uint64_t triangle_bytes;
+    /* the sun's light-space BVH8: its node count (0 = the sun's shadow rays traverse the
+     * world BVHs), and the sampled any-hit steps per sun shadow ray of both structures
+     * that chose it (0 when not sampled: no sun, or ARK_SUN_BVH=0) */
+    uint64_t sun_node_count;
+    float sun_cost_world;
+    float sun_cost_light;
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 

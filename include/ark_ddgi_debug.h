@@ -73,6 +73,13 @@ int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const fl
 int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, const float* sun_dir, const float* origins, uint64_t n_rays, float tmax,
                                  uint64_t* out);
 
+/* set_scene's choice of structure for the sun's shadow rays (ark_ddgi.cpp, ARK_SUN_BVH
+ * unset): the world BVH8 and the light-space BVH8 of the triangles are built, sample
+ * sun shadow rays from sun-facing points traced any-hit through both on the host;
+ * out[4] = {world steps per ray, light-space steps per ray, 1 if the light-space BVH
+ * is chosen, samples}. No GPU. */
+int ark_ddgi_debug_sun_choice(const float* triangles, uint64_t n, const float* sun_dir, uint32_t n_samples, double* out);
+
 #ifdef __cplusplus
 }
 #endif

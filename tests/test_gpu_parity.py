@@ -130,3 +130,33 @@ def test_binned_shadow_list_sun_and_spots(monkeypatch, grid_cells):
     reps = run_pair(sc, grid, cfg, 3, 1000.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.02,
                                                    environment_brightness=1.0), check_each_frame=False)
     _assert_exact(reps, offsets_expected=True)
+
+
+@pytest.mark.parametrize("sun_bvh", ["0", "1"])
+def test_sun_structure_forced(monkeypatch, sun_bvh):
+    """The sun's shadow rays forced through the world BVHs (ARK_SUN_BVH=0) or the
+    light-space BVH (=1) whatever the sampled cost says: with spot lights beside the sun
+    (the features scene, the C5-like city block) the light-space case runs both lists
+    in one launch (k_trace_shadow<.., kShadowSunWorld>); sun only (the small soup) the
+    sun's list alone. Any-hit occlusion does not depend on the structure: bit-exact."""
+    monkeypatch.setenv("ARK_SUN_BVH", sun_bvh)
+    sc = scenes.features_scene()
+    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
+    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
+                       max_rays_per_probe=128, max_probe_updates=144)
+    reps = run_pair(sc, grid, cfg, 2, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
+                                                  environment_brightness=0.5))
+    _assert_exact(reps, offsets_expected=True)
+    sc = S.city_block(2000, extent=40.0)
+    grid = D.ProbeGrid((8, 4, 8), (40.0 / 8, 2.5, 40.0 / 8), (2.5, 0.5, 2.5))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=256, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=256)
+    reps = run_pair(sc, grid, cfg, 2, 1000.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.02,
+                                                   environment_brightness=1.0))
+    _assert_exact(reps, offsets_expected=True)
+    sc = S.soup(64_000, extent=7.0)
+    grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=512, compute_probe_offsets=False,
+                       max_rays_per_probe=256, max_probe_updates=512)
+    reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
+    _assert_exact(reps)

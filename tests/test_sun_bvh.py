@@ -75,3 +75,24 @@ def test_sun_bvh_far_from_origin():
     there (ulp 5e-4 m), the box inflation must cover them."""
     tris = _world_triangles(S.soup(5_000, extent=6.0)) + np.float32(5000.0)
     _check(np.ascontiguousarray(tris, np.float32), (0.5, -1.0, 0.2), n_rays=2000)
+
+
+def _choice(tris, sun):
+    lib = abi.load_library()
+    sd = np.asarray(sun, np.float32)
+    out = (C.c_double * 4)()
+    assert lib.ark_ddgi_debug_sun_choice(tris.ctypes.data, tris.shape[0], sd.ctypes.data, 2048, out) == 0
+    return list(out)
+
+
+def test_sun_choice_by_sampled_cost():
+    """set_scene keeps the light-space BVH only where sampled sun shadow rays take fewer
+    steps through it (sun_bvh_pays): the soup's scattered small triangles gain (rays
+    along +w skip the slab tests' misses), the city block's walls and ground - long
+    slanted boxes in light space - lose, and its sun rays stay on the world BVH."""
+    soup = _world_triangles(S.soup(200_000))
+    w, l, chosen, n = _choice(soup, (0.5, -1.0, 0.2))
+    assert n == 2048 and chosen == 1.0 and l < 0.9 * w, (w, l)
+    city = S.city_block(box_count=20_000)
+    w, l, chosen, n = _choice(_world_triangles(city), city.sun[1])
+    assert n == 2048 and chosen == 0.0 and l > w, (w, l)

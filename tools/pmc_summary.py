@@ -28,8 +28,10 @@ def short(name: str) -> str:
     if not m:
         return name
     base = m.group(1)
-    if base == "k_trace_shadow" and m.group(2) and m.group(2).rstrip(">").split(",")[-1].strip() == "true":
-        base = "k_trace_shadow_sun"  # <COUNT, WPE, SUN = true>: the sun's light-space traversal
+    if base == "k_trace_shadow" and m.group(2):
+        mode = m.group(2).rstrip(">").split(",")[-1].strip()
+        # <COUNT, WPE, MODE>: 1 the sun's light-space traversal, 2 the sun's then the other lights'
+        base = {"1": "k_trace_shadow_sun", "2": "k_trace_shadow_sunw"}.get(mode, base)
     if base == "k_trace" and "ListRays" in name:
         return "k_refl_trace"
     if base == "k_shadow_gen":

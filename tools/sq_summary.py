@@ -29,8 +29,10 @@ def base_name(name):
     m = re.match(r"(k_[a-z0-9_]+)(<([a-z]+)[^>]*>)?", name)
     if not m or m.group(3) == "true":
         return None
-    if m.group(1) == "k_trace_shadow" and m.group(2) and m.group(2).rstrip(">").split(",")[-1].strip() == "true":
-        return "k_trace_shadow_sun"  # <.., .., SUN = true>: the sun's light-space traversal
+    if m.group(1) == "k_trace_shadow" and m.group(2):
+        mode = m.group(2).rstrip(">").split(",")[-1].strip()
+        # <.., .., MODE>: 1 the sun's light-space traversal, 2 the sun's then the other lights'
+        return {"1": "k_trace_shadow_sun", "2": "k_trace_shadow_sunw"}.get(mode, m.group(1))
     return m.group(1)
 
 

@@ -48,14 +48,18 @@ def main():
     ap.add_argument("--rays", type=int, default=65536)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--weights", nargs="+", default=["1,1,1", "1,0.25,0.25", "1,0.1,0.1", "1,0.02,0.02"])
+    ap.add_argument("--scene", choices=["soup", "city", "sponza"], default="soup", help="soup (--triangles), the C5 city block or the C3 substitute")
+    ap.add_argument("--any-hit", action="store_true", help="shadow-ray statistics: tmin 0.025, first hit ends the ray (ARK_SIM_ANYHIT)")
     args = ap.parse_args()
     from arkoserenderer_amd import abi
     from arkoserenderer_amd import scene as S
     from bvh_stats import world_triangles
 
-    sc = S.soup(args.triangles)
+    sc = {"soup": lambda: S.soup(args.triangles), "city": S.city_block, "sponza": S.sponza_substitute}[args.scene]()
     tris = world_triangles(sc)
-    L, F = sun_frame((0.5, -1.0, 0.2))
+    L, F = sun_frame(sc.sun[1] if sc.sun is not None else (0.5, -1.0, 0.2))
+    if args.any_hit:
+        os.environ["ARK_SIM_ANYHIT"] = "1"
     rng = np.random.default_rng(3)
     pick = rng.integers(0, tris.shape[0], args.rays)
     t = tris[pick].reshape(-1, 3, 3).astype(np.float64)
