@@ -1121,6 +1121,22 @@ static double rn16(double x)
     return std::nearbyint(x / ulp) * ulp;
 }
 
+// Round to fp16 toward -inf (dir < 0) or +inf (dir > 0), as a double: the MODE
+// register's directed rounding of ARK_NODE_F16 == 2 (a finite value never rounds to
+// the infinity on the other side; beyond the largest finite value toward it, inf).
+static double rd16(double x, int dir)
+{
+    if (x == 0.0 || std::isinf(x) || std::isnan(x)) return x;
+    const double ax = std::fabs(x);
+    int e = std::ilogb(ax);
+    if (e < -14) e = -14;
+    const double ulp = std::ldexp(1.0, e - 10);
+    double r = (dir < 0 ? std::floor(x / ulp) : std::ceil(x / ulp)) * ulp;
+    if (r > 65504.0) r = dir > 0 ? INFINITY : 65504.0;
+    if (r < -65504.0) r = dir < 0 ? -INFINITY : -65504.0;
+    return r;
+}
+
 // ark_ddgi_debug.h: traversal statistics of the BVH8 that set_scene would upload
 // (host simulation of k_trace's closest-hit order: per node the hit children,
 // those whose box holds the origin first, then octant order; a node's leaf
@@ -1168,7 +1184,14 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     // non-exact modes, a child that the exact test accepts and the chosen form rejects
     // is counted in out[8] (must stay 0: the form must be conservative).
     const char* boxEnv = std::getenv("ARK_SIM_BOX");
-    const int boxMode = !boxEnv ? 0 : std::strcmp(boxEnv, "kernel32") == 0 ? 1 : std::strcmp(boxEnv, "f16") == 0 ? 2 : std::strcmp(boxEnv, "f16s") == 0 ? 3 : 0;
+    // f16d: ARK_NODE_F16 == 2 - the f16s scales with the near planes' A, B and
+    // distances rounded toward -inf and the far planes' toward +inf, no error bound
+    const int boxMode = !boxEnv                           ? 0
+                        : std::strcmp(boxEnv, "kernel32") == 0 ? 1
+                        : std::strcmp(boxEnv, "f16") == 0      ? 2
+                        : std::strcmp(boxEnv, "f16s") == 0     ? 3
+                        : std::strcmp(boxEnv, "f16d") == 0     ? 4
+                                                               : 0;
     // f16s: q as the fp16 subnormal q * 2^-24 (no 1024 bias), A = a * 2^(24 - s) with a
     // per-node scale s (ARK_NODE_F16's visitNode8)
     // the f16 form's error bound e = EA |a| + EB |B'| + 2^-22 (sensitivity runs only:
@@ -1216,7 +1239,7 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                 int nh = 0;
                 // per-node terms of the kernel forms
                 float a32[3], b32[3];
-                double A16[3], Bn16[3], Bf16[3];
+                double A16[3], Bn16[3], Bf16[3], An16[3], Af16[3];
                 double tmin16 = 0.0, tmax16 = 0.0;
                 for (int a = 0; a < 3; ++a) {
                     a32[a] = std::ldexp(idir[a], static_cast<int>(nd.e[a]) - 127);
@@ -1261,6 +1284,22 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                     tmin16 = 0.0;  // the kernel does not apply tmin (conservative)
                     tmax16 = rn16(static_cast<double>(std::ldexp(tmax, -sN) * (1.0f + 0x1p-9f)));
                 }
+                if (boxMode == 4) {
+                    int L = 0;
+                    (void)std::frexp(std::max({ std::fabs(idir[0]), std::fabs(idir[1]), std::fabs(idir[2]) }), &L);
+                    const int emax = std::max({ static_cast<int>(nd.e[0]), static_cast<int>(nd.e[1]), static_cast<int>(nd.e[2]) });
+                    const int sN = std::max(0, emax - 127 + L + 9);
+                    for (int a = 0; a < 3; ++a) {
+                        const float Aa = std::ldexp(idir[a], static_cast<int>(nd.e[a]) - 103 - sN);
+                        const float bs = std::ldexp(b32[a], -sN);
+                        An16[a] = rd16(Aa, -1);
+                        Af16[a] = rd16(Aa, 1);
+                        Bn16[a] = rd16(bs, -1);
+                        Bf16[a] = rd16(bs, 1);
+                    }
+                    tmin16 = 0.0;
+                    tmax16 = rd16(static_cast<double>(std::ldexp(tmax, -sN) * (1.0f + 0x1p-16f)), 1);
+                }
                 for (int s = 0; s < 8; ++s) {
                     const bool internal = (nd.imask >> s) & 1u;
                     if (!internal && !((nd.leaf_mask >> s) & 1u)) continue;
@@ -1286,6 +1325,16 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
                             kf = std::min(kf, std::fma(qf, a32[a], b32[a]));
                         }
                         accept = kn <= std::fma(kf, 1.00001f, 1e-7f);
+                    } else if (boxMode == 4) {
+                        double kn = 0.0, kf = tmax16;
+                        for (int a = 0; a < 3; ++a) {
+                            const bool flip = idir[a] < 0.0f;
+                            const double qn = (flip ? nd.qhi[a][s] : nd.qlo[a][s]) * 0x1p-24;
+                            const double qf = (flip ? nd.qlo[a][s] : nd.qhi[a][s]) * 0x1p-24;
+                            kn = std::max(kn, rd16(qn * An16[a] + Bn16[a], -1));
+                            kf = std::min(kf, rd16(qf * Af16[a] + Bf16[a], 1));
+                        }
+                        accept = kn <= kf;
                     } else if (boxMode >= 2) {
                         double kn = -INFINITY, kf = INFINITY;
                         const double bias = boxMode == 2 ? 1024.0 : 0.0, qs = boxMode == 2 ? 1.0 : 0x1p-24;

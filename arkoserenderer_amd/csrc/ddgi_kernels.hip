@@ -399,12 +399,97 @@ __device__ __forceinline__ uint32_t cvtPkF16(float lo, float hi)
     asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
     return r;
 }
+
+// ARK_NODE_F16 == 2: directed rounding instead of error bounds. The near planes of
+// all four pairs are evaluated with the MODE register's rounding toward -inf (A and B
+// converted to fp16 downward, every packed fma rounded downward), the far planes toward
+// +inf, then round-to-nearest is restored - all inside one asm statement, so no
+// compiler-scheduled instruction runs under the directed modes. Near distances are
+// then never above, far distances never below, their values for the fp32 A and B
+// (q >= 0; either sign of A), so no child the exact-arithmetic test accepts is culled.
+// One pair's near half: (A_dn, B_dn) of each axis in NX / NY / NZ (lo = A, hi = B).
+#define ARK_F16D_NEAR(WX, WY, WZ, SEL, OUT)                                                                    \
+    "v_perm_b32 %[t0], %[" WX "], %[" WX "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t1], %[" WY "], %[" WY "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t2], %[" WZ "], %[" WZ "], %[" SEL "]\n\t"                                                  \
+    "v_pk_fma_f16 %[t0], %[t0], %[ax], %[ax] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_fma_f16 %[t1], %[t1], %[ay], %[ay] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_fma_f16 %[t2], %[t2], %[az], %[az] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_maximum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
+    "v_pk_max_f16 %[" OUT "], %[t0], 0\n\t"
+// One pair's far half (A_up, B_up per axis) and the compares: odd slot, then even
+// slot shifted into the mask (m = 2m + hit)
+#define ARK_F16D_FAR(WX, WY, WZ, SEL, NEAR)                                                                    \
+    "v_perm_b32 %[t0], %[" WX "], %[" WX "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t1], %[" WY "], %[" WY "], %[" SEL "]\n\t"                                                  \
+    "v_perm_b32 %[t2], %[" WZ "], %[" WZ "], %[" SEL "]\n\t"                                                  \
+    "v_pk_fma_f16 %[t0], %[t0], %[ax], %[ax] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_fma_f16 %[t1], %[t1], %[ay], %[ay] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_fma_f16 %[t2], %[t2], %[az], %[az] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
+    "v_pk_minimum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
+    "v_pk_min_f16 %[t0], %[t0], %[tm] op_sel:[0,0] op_sel_hi:[1,0]\n\t"                                       \
+    "v_cmp_le_f16_sdwa vcc, %[" NEAR "], %[t0] src0_sel:WORD_1 src1_sel:WORD_1\n\t"                          \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"                                                  \
+    "v_cmp_le_f16_e32 vcc, %[" NEAR "], %[t0]\n\t"                                                            \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
 #endif
 
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
-#if ARK_NODE_F16
+#if ARK_NODE_F16 == 2
+    // Packed-fp16 child tests with directed rounding (ARK_F16D_*). Per node a scale
+    // 2^-s keeps the node's largest A = step * idir * 2^(24 - s) below 2^15 (q enters
+    // as the fp16 subnormal q * 2^-24), B = (anchor - o) * idir * 2^-s in fp32 as the
+    // fp32 form computes it (its rounding is covered by the build's box inflation, as
+    // there); A and B are rounded to fp16 downward for the near planes and upward for
+    // the far planes, and so is every distance. tmin is not applied (0: a box within
+    // tmin of the origin is visited); tmax gets the fp32 form's relative margin for
+    // the reciprocal's error. Host restatement: ark_ddgi_debug_bvh8_trace_stats
+    // ARK_SIM_BOX=f16d (counts culled children: none).
+    (void)tmin;
+    const int ex = static_cast<int>(w0.w & 0xffu), ey = static_cast<int>((w0.w >> 8) & 0xffu), ez = static_cast<int>((w0.w >> 16) & 0xffu);
+    const int emax = max(max(ex, ey), ez);
+    const int L = __builtin_amdgcn_frexp_expf(fmaxf(fmaxf(fabsf(idir.x), fabsf(idir.y)), fabsf(idir.z)));
+    const int sN = max(0, emax - 127 + L + 9);
+    const int k = 103 + sN;
+    const float Ax = __builtin_amdgcn_ldexpf(idir.x, ex - k), Ay = __builtin_amdgcn_ldexpf(idir.y, ey - k), Az = __builtin_amdgcn_ldexpf(idir.z, ez - k);
+    const float bx = __builtin_amdgcn_ldexpf((__uint_as_float(w0.x) - o.x) * idir.x, -sN);
+    const float by = __builtin_amdgcn_ldexpf((__uint_as_float(w0.y) - o.y) * idir.y, -sN);
+    const float bz = __builtin_amdgcn_ldexpf((__uint_as_float(w0.z) - o.z) * idir.z, -sN);
+    const float tms = __builtin_amdgcn_ldexpf(tmax, -sN) * (1.0f + 0x1p-16f);
+    const uint32_t imask = w0.w >> 24;
+    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
+    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
+    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
+    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
+    uint32_t hitSlots = 0, t0, t1, t2, ax, ay, az, tm, n0, n1, n2, n3;
+    const uint32_t selLo = 0x0c010c00u, selHi = 0x0c030c02u; // bytes (0, 1) / (2, 3) as fp16 subnormals
+    // MODE bits 3:0 = FP_ROUND (f32 in 1:0, f16/f64 in 3:2): 0xa toward -inf, 0x5 toward
+    // +inf, 0 nearest even; s_nop 1 covers the write-to-use wait states
+    asm volatile(
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0xa\n\ts_nop 1\n\t"
+        "v_cvt_pk_f16_f32 %[ax], %[Ax], %[bx]\n\t"
+        "v_cvt_pk_f16_f32 %[ay], %[Ay], %[by]\n\t"
+        "v_cvt_pk_f16_f32 %[az], %[Az], %[bz]\n\t"
+        ARK_F16D_NEAR("nx1", "ny1", "nz1", "shi", "n3") ARK_F16D_NEAR("nx1", "ny1", "nz1", "slo", "n2")
+        ARK_F16D_NEAR("nx0", "ny0", "nz0", "shi", "n1") ARK_F16D_NEAR("nx0", "ny0", "nz0", "slo", "n0")
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0x5\n\ts_nop 1\n\t"
+        "v_cvt_pk_f16_f32 %[ax], %[Ax], %[bx]\n\t"
+        "v_cvt_pk_f16_f32 %[ay], %[Ay], %[by]\n\t"
+        "v_cvt_pk_f16_f32 %[az], %[Az], %[bz]\n\t"
+        "v_cvt_pk_f16_f32 %[tm], %[tms], %[tms]\n\t"
+        ARK_F16D_FAR("fx1", "fy1", "fz1", "shi", "n3") ARK_F16D_FAR("fx1", "fy1", "fz1", "slo", "n2")
+        ARK_F16D_FAR("fx0", "fy0", "fz0", "shi", "n1") ARK_F16D_FAR("fx0", "fy0", "fz0", "slo", "n0")
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0\n\ts_nop 1"
+        : [acc] "+v"(hitSlots), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [ax] "=&v"(ax), [ay] "=&v"(ay), [az] "=&v"(az), [tm] "=&v"(tm),
+          [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3)
+        : [nx0] "v"(nX0), [nx1] "v"(nX1), [ny0] "v"(nY0), [ny1] "v"(nY1), [nz0] "v"(nZ0), [nz1] "v"(nZ1), [fx0] "v"(fX0), [fx1] "v"(fX1),
+          [fy0] "v"(fY0), [fy1] "v"(fY1), [fz0] "v"(fZ0), [fz1] "v"(fZ1), [Ax] "v"(Ax), [Ay] "v"(Ay), [Az] "v"(Az), [bx] "v"(bx), [by] "v"(by),
+          [bz] "v"(bz), [tms] "v"(tms), [slo] "s"(selLo), [shi] "s"(selHi)
+        : "vcc");
+    const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
+#elif ARK_NODE_F16
     // Packed-fp16 child tests. Per node: a scale 2^-s that keeps the node's largest
     // A = step * idir * 2^(24 - s) below 2^15 (fp16 range), A per axis (the q factor:
     // q enters as the fp16 subnormal q * 2^-24), B = (anchor - o) * idir * 2^-s, and
