@@ -1170,6 +1170,19 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     for (int k = 0; k < 3; ++k) copt.area_w[k] = opt.area_w[k];
     const Bvh8BuildResult r8 = collapse_bvh8(r2, 0u, 0u, copt);
+    if (std::getenv("ARK_SIM_FILL")) {
+        // children per node (internal + leaf slots) and leaf triangles per leaf child
+        uint64_t hist[9] = {}, leafTris = 0, leaves = 0;
+        for (const GpuBvh8Node& nd : r8.nodes) {
+            hist[__builtin_popcount(static_cast<uint32_t>(nd.imask | nd.leaf_mask))]++;
+            leaves += static_cast<uint64_t>(__builtin_popcount(nd.leaf_mask));
+            leafTris += static_cast<uint64_t>(__builtin_popcount(nd.leaf_tris));
+        }
+        std::fprintf(stderr, "bvh8 fill: nodes %zu, children per node", r8.nodes.size());
+        for (int k = 0; k <= 8; ++k) std::fprintf(stderr, " %d:%llu", k, static_cast<unsigned long long>(hist[k]));
+        std::fprintf(stderr, ", leaves %llu, triangles per leaf %.3f\n", static_cast<unsigned long long>(leaves),
+                     leaves ? static_cast<double>(leafTris) / static_cast<double>(leaves) : 0.0);
+    }
     std::atomic<uint64_t> nodes { 0 }, triTests { 0 }, hits { 0 }, maxSteps { 0 }, boxViolations { 0 };
     // ARK_SIM_ORDER=distance: exact front-to-back child order (what octant order approximates)
     const bool sortByDistance = std::getenv("ARK_SIM_ORDER") && std::strcmp(std::getenv("ARK_SIM_ORDER"), "distance") == 0;

@@ -346,6 +346,12 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_NODE_INSIDE
 #define ARK_NODE_INSIDE 0 // 1: origin-containing children first, else plain octant order (40 VALU per node for +0.8 % node visits)
 #endif
+#ifndef ARK_NODE_SEL
+#define ARK_NODE_SEL 1 // octant selects of the plane words as v_bitop3_b32 on sign masks (2-cycle) instead of VCC v_cndmask (4+)
+#endif
+#ifndef ARK_NODE_CMP3
+#define ARK_NODE_CMP3 1 // child accept as three compares (tn <= lim, tn <= lim(tmax), tmin <= lim) instead of v_max + v_min (4-cycle each)
+#endif
 #ifndef ARK_NODE_F16
 #define ARK_NODE_F16 0 // 1: the child box tests in packed fp16 (visitNode8: two children per instruction, outward margins)
 #endif
@@ -554,9 +560,38 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const float bz = (__uint_as_float(w0.z) - o.z) * idir.z;
     const uint32_t imask = w0.w >> 24;
     const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
+#if ARK_NODE_SEL
+    // gfx950 issues v_bitop3_b32 and v_ashrrev_i32 in about half the cycles of a
+    // v_cndmask_b32 (tools/probe/valu_table*.hip): the near/far plane words of each axis
+    // are selected bitwise under the lane mask of its direction sign (all ones when the
+    // component is negative - the octant bit; idir is never -0, safeInv)
+    auto signMask = [](float v) { return static_cast<uint32_t>(static_cast<int32_t>(__float_as_uint(v)) >> 31); };
+    auto pick = [](uint32_t m, uint32_t a, uint32_t b) {
+        uint32_t r;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(a), "v"(b)); // m ? a : b, bitwise
+        return r;
+    };
+    const uint32_t mx = signMask(idir.x), my = signMask(idir.y), mz = signMask(idir.z);
+    const uint32_t nX0 = pick(mx, w3.z, w2.x), nX1 = pick(mx, w3.w, w2.y), fX0 = pick(mx, w2.x, w3.z), fX1 = pick(mx, w2.y, w3.w);
+    const uint32_t nY0 = pick(my, w4.x, w2.z), nY1 = pick(my, w4.y, w2.w), fY0 = pick(my, w2.z, w4.x), fY1 = pick(my, w2.w, w4.y);
+    const uint32_t nZ0 = pick(mz, w4.z, w3.x), nZ1 = pick(mz, w4.w, w3.y), fZ0 = pick(mz, w3.x, w4.z), fZ1 = pick(mz, w3.y, w4.w);
+#else
     const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
     const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
     const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
+#endif
+#if ARK_NODE_CMP3
+    // max(tn, tmin) <= f(min(tf, tmax)) with the monotone f(x) = fma(x, 1.00001, 1e-7) is
+    // tn <= f(tf) && tn <= f(tmax) && tmin <= f(tf) (tmin <= f(tmax) holds for any ray
+    // the traversal runs): the same accepted set as the max/min form (no NaN reaches
+    // it: A, B and q are finite), three 2-cycle compares instead of two 4-cycle v_max /
+    // v_min
+    // (tmin is an SGPR operand: every caller passes a wave-uniform constant)
+    const float limT = fmaf(tmax, 1.00001f, 1e-7f);
+    (void)fx;
+    (void)fy;
+    (void)fz;
+#endif
     uint32_t hitSlots = 0, insideLo = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -566,10 +601,28 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
         auto q = [&](uint32_t w0_, uint32_t w1_) { return static_cast<float>(((hiWord ? w1_ : w0_) >> sh) & 0xffu); };
         const float tnx = fmaf(q(nX0, nX1), ax, bx), tny = fmaf(q(nY0, nY1), ay, by), tnz = fmaf(q(nZ0, nZ1), az, bz);
         const float tfx = fmaf(q(fX0, fX1), ax, bx), tfy = fmaf(q(fY0, fY1), ay, by), tfz = fmaf(q(fZ0, fZ1), az, bz);
+#if ARK_NODE_CMP3 && ARK_MASK_ADDC && !ARK_NODE_INSIDE
+        const float tn = fmaxf(fmaxf(tnx, tny), tnz);
+        const float lim = fmaf(fminf(fminf(tfx, tfy), tfz), 1.00001f, 1e-7f);
+        {
+            uint64_t c0, c1;
+            asm("v_cmp_le_f32_e64 %[c0], %[tn], %[lim]\n\t"
+                "v_cmp_le_f32_e64 %[c1], %[tn], %[lt]\n\t"
+                "s_and_b64 %[c0], %[c0], %[c1]\n\t"
+                "v_cmp_le_f32_e64 %[c1], %[tmin], %[lim]\n\t"
+                "s_and_b64 vcc, %[c0], %[c1]\n\t"
+                "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc"
+                : [acc] "+v"(hitSlots), [c0] "=&s"(c0), [c1] "=&s"(c1)
+                : [tn] "v"(tn), [lim] "v"(lim), [lt] "v"(limT), [tmin] "s"(tmin)
+                : "vcc");
+        }
+#else
         const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
         const float lim = fmaf(tf, 1.00001f, 1e-7f);
-#if ARK_MASK_ADDC
+#endif
+#if ARK_NODE_CMP3 && ARK_MASK_ADDC && !ARK_NODE_INSIDE
+#elif ARK_MASK_ADDC
         hitSlots = shiftInLe(hitSlots, tn, lim);
         if (ARK_NODE_INSIDE) insideLo = shiftInLe(insideLo, tn, tmin);
 #else
