@@ -8,9 +8,9 @@ TAG=${1:-prof}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-windows --no-ao-bake --no-compose $*"
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-windows --no-ao-bake --no-compose --no-configs $*"
 # the byte passes also run the consumer lines (lighting compose, RT reflections)
-BENCH_ALL="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-windows --no-ao-bake $*"
+BENCH_ALL="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-windows --no-ao-bake --no-configs $*"
 run() { # name, then rocprofv3 options
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o run --output-format csv -- python3 $BENCH > $OUT/$name.log 2>&1 || { echo "$name pass failed rc=$?"; tail -5 $OUT/$name.log; exit 1; }
