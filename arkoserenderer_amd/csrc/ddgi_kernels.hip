@@ -352,6 +352,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_NODE_CMP3
 #define ARK_NODE_CMP3 1 // child accept as three compares (tn <= lim, tn <= lim(tmax), tmin <= lim) instead of v_max + v_min (4-cycle each)
 #endif
+#ifndef ARK_TAIL_PREFETCH
+#define ARK_TAIL_PREFETCH 1 // k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
+#endif
 #ifndef ARK_NODE_F16
 #define ARK_NODE_F16 0 // 1: the child box tests in packed fp16 (visitNode8: two children per instruction, outward margins)
 #endif
@@ -776,6 +779,41 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
     cNodes++;
     visitNode8(fx.w0, fx.w1, fx.w2, fx.w3, fx.w4, o, idir, oct, tmin, tmax, ts.gBase, ts.gBits, ts.tBase, ts.tBits);
     return false;
+}
+
+// Cache warming in the drain (ARK_TAIL_PREFETCH). After its queue is exhausted a wave
+// is latency-bound: each step waits for the node it picked at the previous step's end
+// (~1-2 us from L2 / HBM) with few co-resident waves to hide it. These loads fetch the
+// first children of the group the next steps will pop (the lane's current group, or
+// its stack top when that is empty), so the steps that reach them find the lines in
+// L2 / the vector cache. They are register-free (global_load_lds_dword into a
+// per-wave scratch line of LDS that nothing reads), so no VGPR stays bound to a load in
+// flight; vmcnt counts them, which can only make a later wait longer, never shorter
+// (loads return in order). Two dwords per node (its 80 B span at most two 128-B lines).
+// M0 (the LDS-DMA base, compiler-reserved) is saved and restored inside the statement;
+// the scratch line is kTailPfDwords dwords per wave, room for 64 lanes at either offset.
+constexpr uint32_t kTailPfDwords = 96;
+template<int BLOCK>
+__device__ __forceinline__ void tailPrefetch(const SceneArgs& sc, const TravState& ts, const Stack<BLOCK>& st, uint32_t oct, uint32_t ldsLine)
+{
+    uint32_t base = ts.gBase, bits = ts.gBits;
+    if ((bits & 0xffu) == 0 && st.depth > 0) {
+        const uint32_t* l = st.lds + ((st.depth - 1) & (kStackLds - 1)) * 2 * BLOCK;
+        base = l[0];
+        bits = l[BLOCK];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (bits & 0xffu) {
+            const uint32_t c = nextChild(base, bits, oct);
+            const char* a = reinterpret_cast<const char*>(sc.nodes + c);
+            uint32_t keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                         "global_load_lds_dword %1, off offset:64\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(a), "s"(ldsLine));
+        }
+    }
 }
 
 // Dual step (k_trace): one lane tests a pending leaf triangle AND visits the next
@@ -1210,6 +1248,12 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     constexpr bool kGF = ARK_TRACE_FETCH_GLOBAL != 0;
     __shared__ uint4 ldsNodes[(kGF ? 1 : kLdsNodes) * 5];
     const NodeCache nc = loadNodeCache<kTraceBlock, kGF ? 0 : kLdsNodes>(sc, ldsNodes);
+#if ARK_TAIL_PREFETCH
+    // the wave's LDS-DMA scratch line (tailPrefetch): written, never read
+    __shared__ uint32_t ldsPf[(kTraceBlock / 64) * kTailPfDwords];
+    const uint32_t pfLine = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ldsPf + (threadIdx.x >> 6) * kTailPfDwords)));
+#endif
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
@@ -1289,6 +1333,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // (an active lane is never done here: the check after the step retires or
         // restarts it, and a step of a done lane would change nothing anyway)
         if (active) travStepDual<kTraceBlock, false, kGF>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
+#if ARK_TAIL_PREFETCH
+        if (exhausted && active) tailPrefetch<kTraceBlock>(sc, ts, st, oct, pfLine);
+#endif
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
@@ -1333,6 +1380,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
     }
+#if ARK_TAIL_PREFETCH
+    // no LDS-DMA of tailPrefetch may land after the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #ifdef ARK_TAIL_PROBE
     {
         const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
