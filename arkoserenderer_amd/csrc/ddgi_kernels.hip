@@ -353,7 +353,7 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #define ARK_NODE_CMP3 1 // child accept as three compares (tn <= lim, tn <= lim(tmax), tmin <= lim) instead of v_max + v_min (4-cycle each)
 #endif
 #ifndef ARK_TAIL_PREFETCH
-#define ARK_TAIL_PREFETCH 1 // k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
+#define ARK_TAIL_PREFETCH 0 // 1: k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
 #endif
 #ifndef ARK_NODE_F16
 #define ARK_NODE_F16 0 // 1: the child box tests in packed fp16 (visitNode8: two children per instruction, outward margins)
