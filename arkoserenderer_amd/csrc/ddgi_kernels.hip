@@ -352,6 +352,9 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_NODE_CMP3
 #define ARK_NODE_CMP3 1 // child accept as three compares (tn <= lim, tn <= lim(tmax), tmin <= lim) instead of v_max + v_min (4-cycle each)
 #endif
+#ifndef ARK_LONG_RAY_STEPS
+#define ARK_LONG_RAY_STEPS 0 // k_trace: a wave holding a ray older than this many steps runs at raised priority (0: off)
+#endif
 #ifndef ARK_TAIL_PREFETCH
 #define ARK_TAIL_PREFETCH 0 // 1: k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
 #endif
@@ -906,7 +909,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
             const uint32_t inst = c.y, prim = c.z;
             if (ANY) anyHit = true;
             else if (!(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
-                !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
+                !((pass & 1) && !alphaAccept(sc, inst, prim, uu, vv))) {
                 h.t = tt;
                 h.u = uu;
                 h.v = vv;
@@ -1267,6 +1270,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     bool exhausted = false;
     bool active = false;
     uint32_t ray = 0;
+    // bit 0: the pass (0 opaque, 1 masked); bits 1+: the ray's age in steps
+    // (ARK_LONG_RAY_STEPS)
     int pass = 0;
     TravState ts { 0u, 0u, 0u, 0u };
     uint32_t nBase = 0, nBits = 0; // the next triangle group (dual step)
@@ -1332,6 +1337,14 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- one step: a pending leaf triangle and the next node -------------------
         // (an active lane is never done here: the check after the step retires or
         // restarts it, and a step of a done lane would change nothing anyway)
+#if ARK_LONG_RAY_STEPS
+        // Long rays set a small window's launch time (its longest ray's steps times the
+        // step latency, which grows with the waves sharing the SIMD): a wave holding a
+        // ray past ARK_LONG_RAY_STEPS steps is issued first
+        if (__ballot(active && pass >= 2 * ARK_LONG_RAY_STEPS)) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+        if (active) pass += 2;
+#endif
         if (active) travStepDual<kTraceBlock, false, kGF>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
 #if ARK_TAIL_PREFETCH
         if (exhausted && active) tailPrefetch<kTraceBlock>(sc, ts, st, oct, pfLine);
@@ -1339,13 +1352,13 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
-            if (Src::kMaskedPass && pass == 0) {
+            if (Src::kMaskedPass && (pass & 1) == 0) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
                 // cullMask 0x02, tmax = previous hit T (:64-92); a negative tmax
                 // (backface) is an empty interval.
                 opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
                 if (sc.root_masked >= 0 && opaqueT >= tmin) {
-                    pass = 1;
+                    pass |= 1;
                     finished = false;
                     ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
                     st.depth = 0;
@@ -1356,7 +1369,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
             if (finished) {
                 GpuHit out;
-                if (pass == 1 && h.tri == kNoHit) {
+                if ((pass & 1) && h.tri == kNoHit) {
                     // masked pass found nothing: the opaque result (already stored) stands
                     out = f.hits[ray];
                     if (COUNT && out.tri != kNoHit) cHits++;
