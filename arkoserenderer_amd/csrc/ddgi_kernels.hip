@@ -355,6 +355,13 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 #ifndef ARK_LONG_RAY_STEPS
 #define ARK_LONG_RAY_STEPS 0 // k_trace: a wave holding a ray older than this many steps runs at raised priority (0: off)
 #endif
+// k_trace's pass word: with ARK_LONG_RAY_STEPS bit 0 is the pass and the ray's age sits
+// above it; without, it is the pass itself
+#if ARK_LONG_RAY_STEPS
+#define ARK_PASS_IS(p, v) (((p) & 1) == (v))
+#else
+#define ARK_PASS_IS(p, v) ((p) == (v))
+#endif
 #ifndef ARK_TAIL_PREFETCH
 #define ARK_TAIL_PREFETCH 0 // 1: k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
 #endif
@@ -909,7 +916,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
             const uint32_t inst = c.y, prim = c.z;
             if (ANY) anyHit = true;
             else if (!(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
-                !((pass & 1) && !alphaAccept(sc, inst, prim, uu, vv))) {
+                !(ARK_PASS_IS(pass, 1) && !alphaAccept(sc, inst, prim, uu, vv))) {
                 h.t = tt;
                 h.u = uu;
                 h.v = vv;
@@ -1352,13 +1359,17 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
-            if (Src::kMaskedPass && (pass & 1) == 0) {
+            if (Src::kMaskedPass && ARK_PASS_IS(pass, 0)) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
                 // cullMask 0x02, tmax = previous hit T (:64-92); a negative tmax
                 // (backface) is an empty interval.
                 opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
                 if (sc.root_masked >= 0 && opaqueT >= tmin) {
+#if ARK_LONG_RAY_STEPS
                     pass |= 1;
+#else
+                    pass = 1;
+#endif
                     finished = false;
                     ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
                     st.depth = 0;
@@ -1369,7 +1380,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
             if (finished) {
                 GpuHit out;
-                if ((pass & 1) && h.tri == kNoHit) {
+                if (ARK_PASS_IS(pass, 1) && h.tri == kNoHit) {
                     // masked pass found nothing: the opaque result (already stored) stands
                     out = f.hits[ray];
                     if (COUNT && out.tri != kNoHit) cHits++;
