@@ -976,6 +976,24 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
     "s_and_b64 vcc, %[m], vcc\n\t"                                                         \
     "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
 
+// ARK_SUN_PAR: the five compares of a child into four SGPR pairs and VCC first, then the
+// ANDs - two levels of VALU -> SALU dependence per child instead of four (the wave
+// otherwise stalls on every compare's lane mask before the next compare issues)
+#ifndef ARK_SUN_PAR
+#define ARK_SUN_PAR 0
+#endif
+#define ARK_SUN_CHILD_PAR(LU, HU, LV, HV, HW, B)                                           \
+    "v_cmp_le_i32_sdwa %[m0], %[" LU "], %[fu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
+    "v_cmp_ge_i32_sdwa %[m1], %[" HU "], %[cu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
+    "v_cmp_le_i32_sdwa %[m2], %[" LV "], %[fv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
+    "v_cmp_ge_i32_sdwa %[m3], %[" HV "], %[cv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
+    "v_cmp_ge_i32_sdwa vcc, %[" HW "], %[cw] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"     \
+    "s_and_b64 %[m0], %[m0], %[m1]\n\t"                                                  \
+    "s_and_b64 %[m2], %[m2], %[m3]\n\t"                                                  \
+    "s_and_b64 %[m0], %[m0], %[m2]\n\t"                                                  \
+    "s_and_b64 vcc, %[m0], vcc\n\t"                                                      \
+    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
+
 // Node visit of a ray along +w from light-space point pl (k_trace_shadow<SUN>). With
 // the direction exactly +w the slab test of u and v degenerates to "pl's coordinate
 // lies in the child's interval" and that of w to "the box reaches above pl": in the
@@ -997,6 +1015,17 @@ __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4
     const int fv = static_cast<int>(floorf(qv)), cv = static_cast<int>(ceilf(qv));
     const int cw = static_cast<int>(ceilf(qw));
     uint32_t hit = 0;
+#if ARK_SUN_PAR
+    uint64_t m0, m1, m2, m3;
+    asm(ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "3") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "2")
+        ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "1") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "0")
+        ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "3") ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "2")
+        ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "1") ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "0")
+        : [acc] "+v"(hit), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
+        : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
+          [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
+        : "vcc");
+#else
     uint64_t m;
     // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
     // qhi w = w4.z|w (children 0-3 | 4-7); slots 7 .. 0 shifted in
@@ -1008,6 +1037,7 @@ __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4
         : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
           [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
         : "vcc");
+#endif
     const uint32_t imask = w0.w >> 24;
     gBase = w1.x;
     gBits = (hit & imask) | (imask << 8);
