@@ -744,6 +744,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
     // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
+    // early split clipping of the build's triangle references: ARK_BVH_PRESPLIT="levels,ratio"
+    if (const char* e = std::getenv("ARK_BVH_PRESPLIT")) std::sscanf(e, "%d,%f", &opt.presplit_levels, &opt.presplit_ratio);
     // BVH2 -> BVH8 child selection: SAH-optimal (Ylitie et al. 2017 DP; the default) or
     // ARK_BVH8_COLLAPSE=greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's
     // SAH terms

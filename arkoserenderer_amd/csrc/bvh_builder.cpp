@@ -52,7 +52,73 @@ struct Aabb {
 struct Ref {
     Aabb box;
     float c[3];
+    uint32_t tri; // the BuildTriangle this reference stands for
 };
+
+// --- early split clipping (BvhBuildOptions::presplit_levels) -----------------------
+struct Poly {
+    double p[9][3]; // a triangle clipped by up to 6 planes has at most 9 vertices
+    int n = 0;
+};
+
+// The part of `in` on one side of the plane x[axis] = at (keepLow: <=), exactly in
+// double but for the interpolated crossing points.
+Poly clipPoly(const Poly& in, int axis, double at, bool keepLow)
+{
+    Poly out;
+    for (int i = 0; i < in.n; ++i) {
+        const double* a = in.p[i];
+        const double* b = in.p[(i + 1) % in.n];
+        const double da = keepLow ? at - a[axis] : a[axis] - at, db = keepLow ? at - b[axis] : b[axis] - at;
+        if (da >= 0.0 && out.n < 9) std::memcpy(out.p[out.n++], a, sizeof(double) * 3);
+        if ((da >= 0.0) != (db >= 0.0) && out.n < 9) {
+            const double t = da / (da - db);
+            for (int k = 0; k < 3; ++k) out.p[out.n][k] = a[k] + (b[k] - a[k]) * t;
+            out.p[out.n][axis] = at; // on the plane
+            out.n++;
+        }
+    }
+    return out;
+}
+
+// float bounds of a double polygon, rounded outward (plus a relative hair for the
+// crossing points' interpolation error), so the box contains the exact piece
+Aabb polyBox(const Poly& P)
+{
+    Aabb b;
+    for (int i = 0; i < P.n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const double v = P.p[i][a], e = std::fabs(v) * 1e-12 + 1e-30;
+            b.lo[a] = std::min(b.lo[a], std::nextafter(static_cast<float>(v - e), -INFINITY));
+            b.hi[a] = std::max(b.hi[a], std::nextafter(static_cast<float>(v + e), INFINITY));
+        }
+    return b;
+}
+
+void splitRefs(const Poly& P, const Aabb& box, uint32_t tri, int level, double stopArea, std::vector<Ref>& out)
+{
+    const float e0 = box.hi[0] - box.lo[0], e1 = box.hi[1] - box.lo[1], e2 = box.hi[2] - box.lo[2];
+    if (level == 0 || box.area() <= stopArea) {
+        Ref r;
+        r.box = box;
+        for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (box.lo[a] + box.hi[a]);
+        r.tri = tri;
+        out.push_back(r);
+        return;
+    }
+    const int axis = (e0 >= e1 && e0 >= e2) ? 0 : (e1 >= e2 ? 1 : 2);
+    const double at = 0.5 * (static_cast<double>(box.lo[axis]) + static_cast<double>(box.hi[axis]));
+    for (int side = 0; side < 2; ++side) {
+        const Poly Q = clipPoly(P, axis, at, side == 0);
+        if (Q.n < 3) continue;
+        Aabb qb = polyBox(Q);
+        for (int a = 0; a < 3; ++a) { // never outside the parent's (already conservative) box
+            qb.lo[a] = std::max(qb.lo[a], box.lo[a]);
+            qb.hi[a] = std::min(qb.hi[a], box.hi[a]);
+        }
+        splitRefs(Q, qb, tri, level - 1, stopArea, out);
+    }
+}
 
 struct Range {
     int32_t code; // >= 0 node index, < 0 leaf code
@@ -64,17 +130,49 @@ public:
     Builder(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t nodeBase, uint32_t triBase)
         : m_opt(opt), m_nodeBase(nodeBase), m_triBase(triBase)
     {
-        const size_t n = tris.size();
-        m_refs.resize(n);
-        m_idx.resize(n);
-        for (size_t i = 0; i < n; ++i) {
+        const size_t nt = tris.size();
+        m_refs.resize(nt);
+        for (size_t i = 0; i < nt; ++i) {
             Ref& r = m_refs[i];
             r.box.grow(tris[i].v0);
             r.box.grow(tris[i].v1);
             r.box.grow(tris[i].v2);
             for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (r.box.lo[a] + r.box.hi[a]);
-            m_idx[i] = static_cast<uint32_t>(i);
+            r.tri = static_cast<uint32_t>(i);
         }
+        if (opt.presplit_levels > 0) {
+            std::vector<Ref> refs;
+            refs.reserve(nt + nt / 2);
+            for (size_t i = 0; i < nt; ++i) {
+                const BuildTriangle& t = tris[i];
+                double e1[3], e2[3];
+                for (int a = 0; a < 3; ++a) {
+                    e1[a] = static_cast<double>(t.v1[a]) - t.v0[a];
+                    e2[a] = static_cast<double>(t.v2[a]) - t.v0[a];
+                }
+                const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+                const double area2 = std::sqrt(cx * cx + cy * cy + cz * cz); // twice the area
+                const double stop = opt.presplit_ratio * area2;
+                if (!(m_refs[i].box.area() > stop)) {
+                    refs.push_back(m_refs[i]);
+                    continue;
+                }
+                Poly P;
+                P.n = 3;
+                for (int a = 0; a < 3; ++a) {
+                    P.p[0][a] = t.v0[a];
+                    P.p[1][a] = t.v1[a];
+                    P.p[2][a] = t.v2[a];
+                }
+                const size_t before = refs.size();
+                splitRefs(P, m_refs[i].box, static_cast<uint32_t>(i), opt.presplit_levels, stop, refs);
+                if (refs.size() == before) refs.push_back(m_refs[i]); // degenerate clip: keep the whole
+            }
+            m_refs.swap(refs);
+        }
+        const size_t n = m_refs.size();
+        m_idx.resize(n);
+        for (size_t i = 0; i < n; ++i) m_idx[i] = static_cast<uint32_t>(i);
         m_nodes.resize(2 * n + 2);
         int hw = opt.threads > 0 ? opt.threads : static_cast<int>(std::thread::hardware_concurrency());
         m_threadsAvail = std::max(0, hw - 1);
@@ -96,7 +194,7 @@ public:
         m_nodes.resize(m_nodeCount);
         res.nodes = std::move(m_nodes);
         res.tris.resize(n);
-        for (uint32_t i = 0; i < n; ++i) res.tris[i] = make_gpu_triangle(tris[m_idx[i]]);
+        for (uint32_t i = 0; i < n; ++i) res.tris[i] = make_gpu_triangle(tris[m_refs[m_idx[i]].tri]);
         res.max_depth = m_maxDepth.load();
         res.max_leaf = m_maxLeaf.load();
         res.sah_cost = sahCost(res.nodes, root.box);
@@ -277,6 +375,17 @@ private:
 
     Range makeLeaf(uint32_t first, uint32_t count, const Aabb& box)
     {
+        // split references of one triangle: the leaf tests it once (the rest of the
+        // range stays unreferenced; the collapse copies only referenced records)
+        if (count > 1) {
+            uint32_t k = 1;
+            for (uint32_t i = 1; i < count; ++i) {
+                bool dup = false;
+                for (uint32_t j = 0; j < k; ++j) dup |= m_refs[m_idx[first + j]].tri == m_refs[m_idx[first + i]].tri;
+                if (!dup) std::swap(m_idx[first + k++], m_idx[first + i]);
+            }
+            count = k;
+        }
         uint32_t ml = m_maxLeaf.load();
         while (count > ml && !m_maxLeaf.compare_exchange_weak(ml, count)) {}
         return Range { leafCode(first, count), box };
@@ -1161,6 +1270,8 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
     opt.inflate_abs = bvh8_inflation(triangles, n);
     opt.threads = threads > 0 ? threads : 8;
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
+    // ARK_BVH_PRESPLIT="levels,ratio": early split clipping (BvhBuildOptions::presplit_levels)
+    if (const char* e = std::getenv("ARK_BVH_PRESPLIT")) std::sscanf(e, "%d,%f", &opt.presplit_levels, &opt.presplit_ratio);
     // ARK_BVH_AREA_W="xy,yz,zx": SAH face weights of both the BVH2 build and the collapse
     if (const char* e = std::getenv("ARK_BVH_AREA_W"))
         std::sscanf(e, "%f,%f,%f", &opt.area_w[0], &opt.area_w[1], &opt.area_w[2]);

@@ -802,7 +802,7 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
 // (loads return in order). Two dwords per node (its 80 B span at most two 128-B lines).
 // M0 (the LDS-DMA base, compiler-reserved) is saved and restored inside the statement;
 // the scratch line is kTailPfDwords dwords per wave, room for 64 lanes at either offset.
-constexpr uint32_t kTailPfDwords = 96;
+[[maybe_unused]] constexpr uint32_t kTailPfDwords = 96;
 template<int BLOCK>
 __device__ __forceinline__ void tailPrefetch(const SceneArgs& sc, const TravState& ts, const Stack<BLOCK>& st, uint32_t oct, uint32_t ldsLine)
 {
