@@ -375,17 +375,9 @@ private:
 
     Range makeLeaf(uint32_t first, uint32_t count, const Aabb& box)
     {
-        // split references of one triangle: the leaf tests it once (the rest of the
-        // range stays unreferenced; the collapse copies only referenced records)
-        if (count > 1) {
-            uint32_t k = 1;
-            for (uint32_t i = 1; i < count; ++i) {
-                bool dup = false;
-                for (uint32_t j = 0; j < k; ++j) dup |= m_refs[m_idx[first + j]].tri == m_refs[m_idx[first + i]].tri;
-                if (!dup) std::swap(m_idx[first + k++], m_idx[first + i]);
-            }
-            count = k;
-        }
+        // (two split references of one triangle in one leaf stay two records: the
+        // collapse merges leaves as contiguous ranges of the leaf order, so a leaf
+        // range must not leave a gap)
         uint32_t ml = m_maxLeaf.load();
         while (count > ml && !m_maxLeaf.compare_exchange_weak(ml, count)) {}
         return Range { leafCode(first, count), box };

@@ -30,7 +30,7 @@ struct BvhBuildOptions {
     // Early split clipping (Ernst & Greiner 2007): a triangle whose box surface exceeds
     // presplit_ratio x twice its area enters the build as up to 2^presplit_levels
     // references, the bounds of its pieces clipped at the box's longest-axis midpoints
-    // (rounded outward); leaves hold each triangle once (0: off)
+    // (rounded outward) (0: off)
     int presplit_levels = 0;
     float presplit_ratio = 8.0f;
 };

@@ -77,3 +77,25 @@ def test_box_check_has_power(monkeypatch):
     out = (C.c_uint64 * 9)()
     assert lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], 4, out, None) == 0
     assert out[8] > 0
+
+
+def test_presplit_references_keep_every_hit(monkeypatch):
+    """Early split clipping of the BVH2 build (ARK_BVH_PRESPLIT, off by default): the
+    clipped references' boxes cover their triangles, so the host traversal finds the
+    same number of hits as the plain build."""
+    lib = abi.load_library()
+    tris = _triangles(S.soup(60_000))
+    lo, hi = tris.reshape(-1, 3).min(0), tris.reshape(-1, 3).max(0)
+    rays = _rays(4000, lo, hi, np.random.default_rng(5))
+    res = {}
+    for ps in (None, "2,4"):
+        if ps is None:
+            monkeypatch.delenv("ARK_BVH_PRESPLIT", raising=False)
+        else:
+            monkeypatch.setenv("ARK_BVH_PRESPLIT", ps)
+        out = (C.c_uint64 * 9)()
+        assert lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], 4, out, None) == 0
+        res[ps] = list(out)
+    assert res["2,4"][2] == res[None][2] and res[None][2] > 0  # hits
+    assert res["2,4"][8] == 0
+    assert res["2,4"][7] > res[None][7]  # more triangle records: references were split
