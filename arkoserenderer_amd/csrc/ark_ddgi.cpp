@@ -30,7 +30,10 @@ using namespace ark;
 namespace {
 
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
-constexpr uint32_t kPipeHalfRays = 5u << 20;
+#ifndef ARK_PIPE_HALF_RAYS
+#define ARK_PIPE_HALF_RAYS (5u << 20)
+#endif
+constexpr uint32_t kPipeHalfRays = ARK_PIPE_HALF_RAYS;
 #ifndef ARK_PIPE_TRACE_PER_CU
 #define ARK_PIPE_TRACE_PER_CU 3 // traversal workgroups per CU of such a window (ctx->pipeTraceBlocks)
 #endif
