@@ -1120,6 +1120,17 @@ __device__ __forceinline__ bool travStepSun(const SceneArgs& sc, TravState& ts, 
 // opaque.rchit:118-131: world-space shading normal of a front hit. The trace
 // kernel's shadow phase and the shading kernel both evaluate exactly this
 // expression, so they agree on N (and on which lights need a shadow ray).
+// hitShadingNormal from the triangle's shading record (a, b, c: n0 n1 n2) and its
+// instance's normal matrix rows (m0, m1, m2), already read
+__device__ __forceinline__ V3 shadingNormalOf(float4 a, float4 b, float4 c, float4 m0, float4 m1, float4 m2, float hu, float hv)
+{
+    const float bx = 1.0f - hu - hv, by = hu, bz = hv;
+    // same operation sequence as k_shade (opaque.rchit:118-131)
+    V3 N = normalize(v3(a.x, a.y, a.z) * bx + v3(a.w, b.x, b.y) * by + v3(b.z, b.w, c.x) * bz);
+    V3 Nw = { m0.x * N.x + m0.y * N.y + m0.z * N.z, m1.x * N.x + m1.y * N.y + m1.z * N.z, m2.x * N.x + m2.y * N.y + m2.z * N.z };
+    return normalize(Nw);
+}
+
 __device__ __forceinline__ V3 hitShadingNormal(const SceneArgs& sc, uint32_t tri, float hu, float hv)
 {
     const float4* tn = sc.tri_normals + 4u * static_cast<size_t>(tri);
@@ -1127,7 +1138,7 @@ __device__ __forceinline__ V3 hitShadingNormal(const SceneArgs& sc, uint32_t tri
     const uint32_t inst = __float_as_uint(c.y);
     const float* M = sc.instances[inst].normal_matrix;
     const float bx = 1.0f - hu - hv, by = hu, bz = hv;
-    // same operation sequence as k_shade (opaque.rchit:118-131)
+    // same operation sequence as k_shade (opaque.rchit:118-131) and shadingNormalOf
     V3 N = normalize(v3(a.x, a.y, a.z) * bx + v3(a.w, b.x, b.y) * by + v3(b.z, b.w, c.x) * bz);
     V3 Nw = { M[0] * N.x + M[1] * N.y + M[2] * N.z, M[4] * N.x + M[5] * N.y + M[6] * N.z, M[8] * N.x + M[9] * N.y + M[10] * N.z };
     return normalize(Nw);
@@ -2202,6 +2213,9 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 #define ARK_GEN_STEPS 4 // queue positions per block = 256 x this (16: 0.185 ms, 4: 0.163, 2: 0.215 at C4)
 #endif
 constexpr uint32_t kGenSteps = ARK_GEN_STEPS, kGenSpan = kGenSteps * 256u;
+#ifndef ARK_GEN_V2
+#define ARK_GEN_V2 0
+#endif
 
 __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 {
@@ -2258,6 +2272,28 @@ __device__ __forceinline__ uint32_t shadowBinKey(const SceneArgs& sc, const Fram
     return l * G * G + morton2(x, y);
 }
 
+#if ARK_GEN_V2
+// shadowBinKey with the spot's position already read (P; unused for the sun)
+__device__ __forceinline__ uint32_t shadowBinKeyAt(const SceneArgs& sc, const FrameArgs& f, uint32_t l, V3 X, V3 P)
+{
+    const uint32_t G = f.shadow_bin_grid;
+    const float gmax = static_cast<float>(G) - 0.5f;
+    float cu, cv;
+    if (sc.has_sun && l == 0) {
+        cu = X.x * f.sun_bin_axes[0][0] + X.y * f.sun_bin_axes[0][1] + X.z * f.sun_bin_axes[0][2] + f.sun_bin_axes[0][3];
+        cv = X.x * f.sun_bin_axes[1][0] + X.y * f.sun_bin_axes[1][1] + X.z * f.sun_bin_axes[1][2] + f.sun_bin_axes[1][3];
+    } else {
+        float ox, oy;
+        octahedralEncode(normalize(X - P), &ox, &oy);
+        cu = (ox * 0.5f + 0.5f) * static_cast<float>(G);
+        cv = (oy * 0.5f + 0.5f) * static_cast<float>(G);
+    }
+    // NaN (a degenerate origin) lands in cell 0
+    const uint32_t x = static_cast<uint32_t>(fminf(fmaxf(cu, 0.0f), gmax)), y = static_cast<uint32_t>(fminf(fmaxf(cv, 0.0f), gmax));
+    return l * G * G + morton2(x, y);
+}
+#endif
+
 template<bool REFL = false>
 __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 {
@@ -2265,6 +2301,34 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     __shared__ uint32_t bitsL[kGenSpan];
     __shared__ uint32_t waveOff[kGenSteps][4];
     __shared__ uint32_t blockBase, sunBlockBase;
+#if ARK_GEN_V2
+    // the lit test direction -normalize(direction) of light l (litLightMask) and its
+    // position (shadowRayOf), read once per workgroup: per ray they were dependent reads
+    __shared__ float4 lightDirL[kMaxLights], lightPosL[kMaxLights];
+    const uint32_t nSun = sc.has_sun ? 1u : 0u, nLights = nSun + static_cast<uint32_t>(sc.spot_count);
+    if (threadIdx.x < nLights) {
+        const uint32_t l = threadIdx.x;
+        V3 Ld, P = splat(0.0f);
+        if (l < nSun) {
+            Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
+        } else {
+            const GpuSpotLight& sl = sc.spots[l - nSun];
+            Ld = -normalize(v3(sl.direction[0], sl.direction[1], sl.direction[2]));
+            P = v3(sl.position[0], sl.position[1], sl.position[2]);
+        }
+        lightDirL[l] = make_float4(Ld.x, Ld.y, Ld.z, 0.0f);
+        lightPosL[l] = make_float4(P.x, P.y, P.z, 0.0f);
+    }
+    __syncthreads();
+    auto litMaskL = [&](V3 N) {
+        uint32_t need = 0;
+        for (uint32_t l = 0; l < nLights; ++l) {
+            const float4 d = lightDirL[l];
+            if (dot(v3(d.x, d.y, d.z), N) > 0.0f) need |= 1u << l;
+        }
+        return need;
+    };
+#endif
     // the sun's rays (light 0) to their own list when the scene has a light-space BVH
     const bool splitSun = !REFL && f.sun_rays != nullptr;
     const uint32_t total = REFL ? *f.list_count : f.window_rays;
@@ -2275,6 +2339,72 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     // dependent loads (slot order -> hit -> triangle normals -> instance) are in
     // flight for all of them at once (the kernel is latency bound)
     uint32_t rays[kGenSteps];
+#if ARK_GEN_V2
+    // probe rays in four stages, each stage's reads issued for all kGenSteps rays of
+    // the thread before any is waited for (straight-line code, clamped indices: a
+    // position past the window or a ray without a front hit reads index 0 and is
+    // dropped): slot -> hit + slot record + direction -> shading record -> instance.
+    // The hit point is formed here, so pass 2 reads nothing per ray.
+    V3 hitPt[kGenSteps];
+    if (!REFL) {
+        uint32_t slotv[kGenSteps];
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            const uint32_t pos = first + k * 256u + threadIdx.x;
+            slotv[k] = slotAt(f, pos < total ? pos / f.R : 0u);
+        }
+        float4 hv[kGenSteps], sp[kGenSteps], sa[kGenSteps], fbv[kGenSteps];
+        float sc_[kGenSteps];
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            const uint32_t pos = first + k * 256u + threadIdx.x;
+            const bool valid = pos < total;
+            const uint32_t q = pos / f.R, sample = valid ? pos - q * f.R : 0u;
+            const uint32_t ray = valid ? slotv[k] * f.R + sample : 0u;
+            rays[k] = valid ? ray : kNoHit;
+            hv[k] = *reinterpret_cast<const float4*>(f.hits + ray);
+            const GpuProbeSlot* ps = f.slots + (valid ? slotv[k] : 0u);
+            sp[k] = *reinterpret_cast<const float4*>(ps->pos);
+            sa[k] = *reinterpret_cast<const float4*>(ps->axis); // axis xyz + angle_sin
+            sc_[k] = ps->angle_cos;
+            fbv[k] = f.fib[sample];
+        }
+        float4 ta[kGenSteps], tb[kGenSteps], tc[kGenSteps];
+        bool front[kGenSteps];
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            const uint32_t tri = __float_as_uint(hv[k].w);
+            front[k] = rays[k] != kNoHit && tri != kNoHit && !(hv[k].x < 0.0f); // backface: no shading, no shadow ray
+            const float4* tn = sc.tri_normals + 4u * static_cast<size_t>(front[k] ? tri : 0u);
+            ta[k] = tn[0];
+            tb[k] = tn[1];
+            tc[k] = tn[2];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            const V3 dir = rotate(v3(fbv[k].x, fbv[k].y, fbv[k].z), v3(sa[k].x, sa[k].y, sa[k].z), sa[k].w, sc_[k]);
+            hitPt[k] = v3(sp[k].x, sp[k].y, sp[k].z) + hv[k].x * dir;
+        }
+        float4 m0[kGenSteps], m1[kGenSteps], m2[kGenSteps];
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            const float4* M = reinterpret_cast<const float4*>(sc.instances[__float_as_uint(tc[k].y)].normal_matrix);
+            m0[k] = M[0];
+            m1[k] = M[1];
+            m2[k] = M[2];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kGenSteps; ++k) {
+            uint32_t bits = 0;
+            if (front[k]) {
+                bits = litMaskL(shadingNormalOf(ta[k], tb[k], tc[k], m0[k], m1[k], m2[k], hv[k].y, hv[k].z));
+                f.shadow_bits[rays[k]] = bits;
+            }
+            bitsL[k * 256u + threadIdx.x] = bits;
+        }
+    } else
+#endif
+    {
     GpuHit hits[kGenSteps];
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
@@ -2302,6 +2432,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         }
         bitsL[k * 256u + threadIdx.x] = bits;
     }
+    }
     // counts packed: world-list rays in bits 0-15, sun-list rays in bits 16-31 (a
     // block has at most kGenSpan x kMaxLights = 11,264 of either, no carry)
     auto packedCount = [&](uint32_t bits) {
@@ -2326,6 +2457,9 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         sunBlockBase = (run >> 16) ? atomicAdd(f.sun_count, run >> 16) : 0u;
     }
     __syncthreads();
+#if ARK_GEN_V2
+#pragma unroll
+#endif
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         const uint32_t bits = bitsL[k * 256u + threadIdx.x];
         const uint32_t c = packedCount(bits);
@@ -2335,32 +2469,56 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         if (bits == 0) continue;
         const uint32_t pos = first + k * 256u + threadIdx.x;
         uint32_t ray;
-        V3 origin, dir;
-        float t;
+        V3 hitPoint;
         if (REFL) {
             ray = pos;
             const float4 a = f.ray_list[2u * pos], b = f.ray_list[2u * pos + 1u];
-            origin = v3(a.x, a.y, a.z);
-            dir = v3(b.x, b.y, b.z);
-            t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
+            const V3 origin = v3(a.x, a.y, a.z), dir = v3(b.x, b.y, b.z);
+            const float t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
+            hitPoint = origin + t * dir;
         } else {
+#if ARK_GEN_V2
+            ray = rays[k];
+            hitPoint = hitPt[k];
+#else
             const uint32_t q = pos / f.R;
             ray = slotAt(f, q) * f.R + (pos - q * f.R);
-            t = f.hits[ray].t;
+            const float t = f.hits[ray].t;
+            V3 origin, dir;
             rayOf(f, ray, &origin, &dir);
+            hitPoint = origin + t * dir;
+#endif
         }
-        const V3 hitPoint = origin + t * dir;
         const bool binned = !REFL && f.shadow_bin_grid != 0;
         for (uint32_t b = bits; b; b &= b - 1) {
             const uint32_t l = static_cast<uint32_t>(__builtin_ctz(b));
             V3 ld;
             float tmax;
+#if ARK_GEN_V2
+            if (l < nSun) { // shadowRayOf from the staged light
+                const float4 d = lightDirL[0];
+                ld = v3(d.x, d.y, d.z);
+                tmax = 2.0f * f.z_far;
+            } else {
+                const float4 P = lightPosL[l];
+                const V3 toLight = v3(P.x, P.y, P.z) - hitPoint;
+                const float distanceToLight = length(toLight);
+                ld = toLight / distanceToLight;
+                tmax = distanceToLight - 0.001f;
+            }
+#else
             shadowRayOf(sc, f.z_far, l, hitPoint, &ld, &tmax);
+#endif
             const ShadowRay sr { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax), make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
             if (splitSun && l == 0u) {
                 f.sun_rays[sunj++] = sr;
             } else if (binned) {
+#if ARK_GEN_V2
+                const float4 P = lightPosL[l];
+                const uint32_t key = shadowBinKeyAt(sc, f, l, hitPoint, v3(P.x, P.y, P.z));
+#else
                 const uint32_t key = shadowBinKey(sc, f, l, hitPoint);
+#endif
                 f.shadow_bin_key[sj] = key;
                 f.shadow_bin_rank[sj] = atomicAdd(f.shadow_bin_count + key * kBinStride, 1u);
                 f.shadow_rays_gen[sj++] = sr;
