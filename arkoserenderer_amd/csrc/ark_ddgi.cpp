@@ -384,9 +384,12 @@ int ensureShadeWork(ArkDdgiCtx* ctx)
 // there are few, and fewer co-resident waves shorten each one's iterations
 // (measured on C4: K = 2048 windows 0.228 -> 0.180 ms at 3 workgroups per CU,
 // K = 4096 0.246 -> 0.225, the full grid (8.4 M rays) unchanged from 5 to 6).
+#ifndef ARK_SHADOW_MIN_PER_CU
+#define ARK_SHADOW_MIN_PER_CU 3
+#endif
 uint32_t shadowBlocksFor(const ArkDdgiCtx* ctx, uint64_t rays)
 {
-    const uint64_t perCu = std::min<uint64_t>(ctx->shadowBlocksPerCu, std::max<uint64_t>(3, rays >> 20));
+    const uint64_t perCu = std::min<uint64_t>(ctx->shadowBlocksPerCu, std::max<uint64_t>(ARK_SHADOW_MIN_PER_CU, rays >> 20));
     return static_cast<uint32_t>(perCu * ctx->cuCount);
 }
 
