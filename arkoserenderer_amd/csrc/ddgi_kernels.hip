@@ -1740,6 +1740,9 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
     *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
 }
 
+#ifndef ARK_SHADE_SPOTS_LDS
+#define ARK_SHADE_SPOTS_LDS 0
+#endif
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
@@ -1747,6 +1750,17 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
     __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
     uint32_t cFront = 0;
+#if ARK_SHADE_SPOTS_LDS
+    // the spot lights, read once per workgroup: per front hit and lit spot they were a
+    // dependent 96-B read ahead of the IES lookup (C5: 4 spots)
+    __shared__ GpuSpotLight spotsL[kMaxLights - 1];
+    {
+        const uint32_t words = static_cast<uint32_t>(sc.spot_count) * static_cast<uint32_t>(sizeof(GpuSpotLight) / 4u);
+        for (uint32_t i = threadIdx.x; i < words; i += kShadeBlock)
+            reinterpret_cast<uint32_t*>(spotsL)[i] = reinterpret_cast<const uint32_t*>(sc.spots)[i];
+        __syncthreads();
+    }
+#endif
 
     // chunks come from the second set of per-XCD partition heads (see grabRays)
     uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
@@ -1834,7 +1848,11 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     l++;
                 }
                 for (int li = 0; li < sc.spot_count; ++li, ++l) {
+#if ARK_SHADE_SPOTS_LDS
+                    const V3 Ld = -normalize(v3(spotsL[li].direction[0], spotsL[li].direction[1], spotsL[li].direction[2]));
+#else
                     const V3 Ld = -normalize(v3(sc.spots[li].direction[0], sc.spots[li].direction[1], sc.spots[li].direction[2]));
+#endif
                     if (dot(Ld, N) > 0.0f) need |= 1u << l;
                 }
             }
@@ -1858,7 +1876,11 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             }
             for (int li = 0; li < sc.spot_count; ++li, ++l) { // opaque.rchit:75-103
                 if (!((need >> l) & 1u)) continue;
+#if ARK_SHADE_SPOTS_LDS
+                const GpuSpotLight sl = spotsL[li];
+#else
                 const GpuSpotLight sl = sc.spots[li];
+#endif
                 V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
                 V3 Ld = -normalize(sdir);
                 float LdotN = dot(Ld, N);
