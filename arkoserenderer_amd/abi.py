@@ -174,6 +174,21 @@ class ArkDdgiScene(C.Structure):
     ]
 
 
+ARK_DDGI_MAX_SPOT_LIGHTS = 10
+
+
+class ArkDdgiLights(C.Structure):
+    """include/ark_ddgi.h ArkDdgiLights: the per-frame light set (GpuScene.cpp:790-858)."""
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("has_directional_light", C.c_int32),
+        ("directional_light", ArkDirectionalLight),
+        ("spot_lights", C.c_void_p),
+        ("spot_light_count", C.c_uint32),
+        ("reserved", C.c_int32 * 4),
+    ]
+
+
 class ArkDdgiFrameParams(C.Structure):
     _fields_ = [
         ("struct_size", C.c_uint32),
@@ -239,6 +254,8 @@ class ArkDdgiBvhStats(C.Structure):
         ("sun_node_count", C.c_uint64),
         ("sun_cost_world", C.c_float),
         ("sun_cost_light", C.c_float),
+        ("sun_build_ms", C.c_float),
+        ("refit_ms", C.c_float),
     ]
 
 
@@ -402,6 +419,8 @@ EXPORTS = {
     "ark_ddgi_last_error": (C.c_char_p, [C.c_void_p]),
     "ark_ddgi_set_scene": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiScene)]),
     "ark_ddgi_share_scene": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ark_ddgi_set_lights": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ark_ddgi_set_instances": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "ark_ddgi_mark_external_write": (C.c_int, [C.c_void_p]),
     "ark_ddgi_get_next_probe_index": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ark_ddgi_update": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),

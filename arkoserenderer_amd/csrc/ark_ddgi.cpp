@@ -30,15 +30,8 @@ using namespace ark;
 namespace {
 
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
-#ifndef ARK_PIPE_HALF_RAYS
-#define ARK_PIPE_HALF_RAYS (5u << 20)
-#endif
-constexpr uint32_t kPipeHalfRays = ARK_PIPE_HALF_RAYS;
-#ifndef ARK_PIPE_TRACE_PER_CU
-#define ARK_PIPE_TRACE_PER_CU 3 // traversal workgroups per CU of such a window (ctx->pipeTraceBlocks)
-#endif
-// u32 words per shadow-ray bin counter (ddgi_kernels.hip kBinStride)
-constexpr uint64_t kShadowBinStride = 32;
+constexpr uint32_t kPipeHalfRays = 5u << 20;
+constexpr int kPipeTracePerCu = 3; // traversal workgroups per CU of such a window (ctx->pipeTraceBlocks; 2, 4, 5 measured slower)
 
 // roctx range over a scope (host-side enqueue markers, named after the reference's
 // ScopedDebugZone labels, DDGINode.cpp:152-247); end() closes it early.
@@ -132,24 +125,37 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 // ark_ddgi_share_scene lets the Z-slab contexts of one GPU use one copy.
 struct SceneStore {
     int device = 0;
-    DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels, spots;
+    DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels;
     DeviceBuffer sunNodes; // light-space BVH8 of the sun's shadow rays + its world-space triangle records
     uint64_t sunBvhNodes = 0;
     float sunCostWorld = 0.0f, sunCostLight = 0.0f; // sampled sun shadow-ray steps per ray (sun_shadow_cost)
-    std::vector<ArkRTInstance> instHost;     // for the AO bake (instance -> mesh segment)
+    std::vector<ArkRTInstance> instHost;     // the AO bake (instance -> mesh segment), set_instances' topology check
     std::vector<ArkRTTriangleMesh> meshHost;
-    SceneArgs args {};
+    SceneArgs args {};    // the world BVHs, pools, materials, textures (lights: per context, deriveSceneArgs)
+    SceneArgs sunArgs {}; // sun_nodes / sun_tris / sun_root / sun_frame of the light-space BVH (sun_root -1: none)
+    float sunDirBuilt[3] { 0, 0, 0 }; // the sun direction the light-space BVH was built for
+    // the scene's lights as set_scene got them: a context's lights until ark_ddgi_set_lights
+    int32_t hasSunScene = 0;
+    ArkDirectionalLight sunScene {};
+    std::vector<GpuSpotLight> spotsScene;
     ArkDdgiBvhStats bvhStats {};
-    uint32_t bvhMaxDepth = 0;
-    uint32_t lightCount = 0;
+    uint32_t bvhMaxDepth = 0; // deepest of the world BVHs and the sun's (traversal spill)
     float boundsLo[3] { 0, 0, 0 }, boundsHi[3] { 0, 0, 0 }; // world AABB of all triangles
+    // ark_ddgi_set_instances: bumped by every refit (a sharing context re-derives its
+    // SceneArgs); the builder's absolute inflation; the refit's buffers, built on first use
+    uint32_t version = 0;
+    float inflateAbs = 0.0f;
+    uint64_t triRecords = 0; // triangle records of the world BVHs (holes included)
+    DeviceBuffer refitInst, refitBoxes, refitOrder, refitBounds;
+    std::vector<uint32_t> levelOffsets; // refitOrder[levelOffsets[i] .. [i + 1]): the nodes of one depth, deepest first
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
     SceneStore& operator=(const SceneStore&) = delete;
     ~SceneStore()
     {
         (void)hipSetDevice(device);
-        for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &spots, &sunNodes })
+        for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
+                                 &refitBoxes, &refitOrder, &refitBounds })
             b->release();
     }
 };
@@ -181,11 +187,6 @@ struct ArkDdgiCtx {
     uint32_t lightCount = 0;
     uint32_t spillEntries = 0;
     uint32_t traceBlocks = 0, shadeBlocks = 0, shadowBlocks = 0, shadowBlocksPerCu = 1;
-    // light-space binning of the shadow-ray list (FrameArgs::shadow_bin_grid); the sun's
-    // cell axes follow from the scene (adoptScene)
-    uint32_t shadowBinGrid = 0; // ARK_SHADOW_BIN_GRID (off: measured slower)
-    uint32_t shadowBinMinRays = 1u << 16; // windows below this many probe rays keep the queue order
-    float sunBinAxes[2][4] = {};
     // Frames in flight (updateImpl): the per-frame buffers the traversal writes come in
     // two sets (slot table, slot order, sample directions, hit records, work counters);
     // frame n uses set n & 1. Frame n's slot table, primary traversal and probe offsets
@@ -239,6 +240,16 @@ struct ArkDdgiCtx {
     // scene
     bool hasScene = false;
     std::shared_ptr<SceneStore> sceneStore; // device scene (possibly shared with other contexts)
+    uint32_t sceneVersion = 0;              // sceneStore->version that `scene` was derived at
+    // Per-frame lights (ark_ddgi_set_lights; set_scene / share_scene start them with the
+    // scene's): the sun travels in `scene` (kernel arguments), the spots in `lights` on
+    // the device, stored there in stream order ahead of the next operation that reads
+    // them (flushLights) when lightsDirty
+    DeviceBuffer lights; // GpuSpotLight[kMaxLights - 1]
+    std::vector<GpuSpotLight> spotHost;
+    int32_t hasSun = 0;
+    float sunColor[3] { 0, 0, 0 }, sunDir[3] { 0, 0, 0 };
+    bool lightsDirty = false;
     // AO bake results (ark_ddgi_bake_ao)
     DeviceBuffer bakeTri, bakeBary, bakeOut, bakePixels, bakeCounters;
     uint32_t bakeW = 0, bakeH = 0;
@@ -337,10 +348,8 @@ hipError_t orderEnd(ArkDdgiCtx* ctx, hipStream_t s)
 
 // Shading work set for the largest window: per-ray light bits, then k_shadow_gen's
 // shadow-ray list (at most one ray per probe ray and light).
-// With binning (shadowBinGrid > 0) also the generator's unsorted list, the per-entry
-// bin key and rank, and the bin counts / starts.
 struct ShadeWorkLayout {
-    uint64_t bits, list, gen, key, rank, count, start, total;
+    uint64_t bits, list, total;
 };
 
 ShadeWorkLayout shadeWorkLayout(const ArkDdgiCtx* ctx)
@@ -348,17 +357,10 @@ ShadeWorkLayout shadeWorkLayout(const ArkDdgiCtx* ctx)
     auto al = [](uint64_t b) { return (b + 255) & ~static_cast<uint64_t>(255); };
     const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
     const uint64_t entries = rays * ctx->lightCount;
-    const uint64_t bins = ctx->shadowBinGrid ? static_cast<uint64_t>(ctx->lightCount) * ctx->shadowBinGrid * ctx->shadowBinGrid : 0;
     ShadeWorkLayout w {};
     w.bits = 0;
     w.list = al(rays * 4);
-    w.gen = w.list + al(entries * sizeof(ShadowRay));
-    const uint64_t binned = bins ? 1 : 0;
-    w.key = w.gen + binned * al(entries * sizeof(ShadowRay));
-    w.rank = w.key + binned * al(entries * 4);
-    w.count = w.rank + binned * al(entries * 4);
-    w.start = w.count + al(bins * 4 * kShadowBinStride);
-    w.total = w.start + al(bins * 4);
+    w.total = w.list + al(entries * sizeof(ShadowRay));
     return w;
 }
 
@@ -368,13 +370,7 @@ int ensureShadeWork(ArkDdgiCtx* ctx)
     if (rays >= (1ull << 28) && ctx->lightCount > 0)
         return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "%llu rays per update: shadow-ray owners pack (ray << 4) | light in 32 bits", static_cast<unsigned long long>(rays));
     const ShadeWorkLayout w = shadeWorkLayout(ctx);
-    if (ctx->shadeWork.bytes < w.total) {
-        ARK_HIP(ctx->shadeWork.alloc(w.total));
-        // the bin counts start at zero; the bin scan zeroes them again after each frame
-        if (w.start > w.count) ARK_HIP(hipMemset(static_cast<char*>(ctx->shadeWork.ptr) + w.count, 0, w.start - w.count));
-    } else if (w.start > w.count) {
-        ARK_HIP(hipMemset(static_cast<char*>(ctx->shadeWork.ptr) + w.count, 0, w.start - w.count));
-    }
+    if (ctx->shadeWork.bytes < w.total) ARK_HIP(ctx->shadeWork.alloc(w.total));
     return ARK_DDGI_OK;
 }
 
@@ -384,12 +380,10 @@ int ensureShadeWork(ArkDdgiCtx* ctx)
 // there are few, and fewer co-resident waves shorten each one's iterations
 // (measured on C4: K = 2048 windows 0.228 -> 0.180 ms at 3 workgroups per CU,
 // K = 4096 0.246 -> 0.225, the full grid (8.4 M rays) unchanged from 5 to 6).
-#ifndef ARK_SHADOW_MIN_PER_CU
-#define ARK_SHADOW_MIN_PER_CU 3
-#endif
+constexpr uint64_t kShadowMinPerCu = 3; // 1 and 2 measured slower or within noise (profiles/r04_p)
 uint32_t shadowBlocksFor(const ArkDdgiCtx* ctx, uint64_t rays)
 {
-    const uint64_t perCu = std::min<uint64_t>(ctx->shadowBlocksPerCu, std::max<uint64_t>(ARK_SHADOW_MIN_PER_CU, rays >> 20));
+    const uint64_t perCu = std::min<uint64_t>(ctx->shadowBlocksPerCu, std::max<uint64_t>(kShadowMinPerCu, rays >> 20));
     return static_cast<uint32_t>(perCu * ctx->cuCount);
 }
 
@@ -413,49 +407,95 @@ int upload(ArkDdgiCtx* ctx, DeviceBuffer& buf, const T* data, size_t count)
     return ARK_DDGI_OK;
 }
 
+static_assert(ARK_DDGI_MAX_SPOT_LIGHTS == kMaxLights - 1, "spot light capacity");
+
+// SpotLightData as the closest hit reads it (GpuScene.cpp:844-858: the fields of
+// LightData.h:19-40 the DDGI path uses)
+GpuSpotLight gpuSpotLight(const ArkSpotLight& sl)
+{
+    GpuSpotLight g;
+    std::memset(&g, 0, sizeof(g));
+    for (int k = 0; k < 3; ++k) {
+        g.color[k] = sl.color[k];
+        g.direction[k] = sl.world_space_direction[k];
+        g.right[k] = sl.world_space_right[k];
+        g.up[k] = sl.world_space_up[k];
+        g.position[k] = sl.world_space_position[k];
+    }
+    g.position[3] = sl.outer_cone_half_angle;
+    g.ies_texture = sl.ies_profile_index;
+    return g;
+}
+
 // sRGB EOTF applied per texel before filtering (Vulkan sRGB formats).
 float srgbToLinear(float c)
 {
     return c <= 0.04045f ? c / 12.92f : powf_((c + 0.055f) / 1.055f, 2.4f);
 }
 
-// Makes `st` the context's scene: the per-context work sets follow its light count
-// and BVH depth.
+// The context's kernel view of its scene: the store's world BVHs, pools and tables with
+// the context's own lights (sun by value, spots in its light buffer); the light-space
+// sun BVH only while it is valid and the sun points the way it was built for (any other
+// direction traces the sun's shadow rays through the world BVHs: same results).
+void deriveSceneArgs(ArkDdgiCtx* ctx)
+{
+    const SceneStore& st = *ctx->sceneStore;
+    SceneArgs sc = st.args;
+    sc.has_sun = ctx->hasSun;
+    for (int k = 0; k < 3; ++k) {
+        sc.sun_color[k] = ctx->sunColor[k];
+        sc.sun_dir[k] = ctx->sunDir[k];
+    }
+    sc.spot_count = static_cast<int32_t>(ctx->spotHost.size());
+    sc.spots = ctx->lights.as<GpuSpotLight>();
+    const bool sunOk = ctx->hasSun && st.sunArgs.sun_root >= 0 && std::memcmp(ctx->sunDir, st.sunDirBuilt, sizeof(ctx->sunDir)) == 0;
+    sc.sun_nodes = sunOk ? st.sunArgs.sun_nodes : nullptr;
+    sc.sun_tris = sunOk ? st.sunArgs.sun_tris : nullptr;
+    sc.sun_root = sunOk ? st.sunArgs.sun_root : -1;
+    std::memcpy(sc.sun_frame, st.sunArgs.sun_frame, sizeof(sc.sun_frame));
+    ctx->scene = sc;
+    ctx->lightCount = (ctx->hasSun ? 1u : 0u) + static_cast<uint32_t>(ctx->spotHost.size());
+    ctx->bvhStats = st.bvhStats;
+    ctx->bvhMaxDepth = st.bvhMaxDepth;
+    ctx->sceneVersion = st.version;
+}
+
+// The context's spot lights reach the device in stream order on `s`, ahead of the
+// operation that reads them (a by-value kernel argument: no host buffer to keep alive).
+hipError_t flushLights(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (!ctx->lightsDirty) return hipSuccess;
+    LightBlock b {};
+    b.count = static_cast<uint32_t>(ctx->spotHost.size());
+    std::copy(ctx->spotHost.begin(), ctx->spotHost.end(), b.spots);
+    const hipError_t e = launch_store_lights(b, ctx->lights.as<GpuSpotLight>(), s);
+    if (e == hipSuccess) ctx->lightsDirty = false;
+    return e;
+}
+
+// Waits for every operation of the context enqueued so far (both of its streams).
+hipError_t drainContext(ArkDdgiCtx* ctx)
+{
+    hipError_t e = hipStreamSynchronize(ctx->traceStream);
+    if (e == hipSuccess && ctx->orderValid) e = hipEventSynchronize(ctx->evOrder);
+    return e;
+}
+
+// Makes `st` the context's scene with the scene's lights: the per-context work sets
+// follow its light count and BVH depth.
 int adoptScene(ArkDdgiCtx* ctx, std::shared_ptr<SceneStore> st)
 {
-    ctx->scene = st->args;
-    ctx->bvhStats = st->bvhStats;
-    ctx->bvhMaxDepth = st->bvhMaxDepth;
-    ctx->lightCount = st->lightCount;
-    // Sun cells: an orthonormal pair (e1, e2) perpendicular to the sun direction, the
-    // scene AABB's projection onto it mapped to [0, G) (shadowBinKey)
-    if (st->args.has_sun && ctx->shadowBinGrid) {
-        const float* d = st->args.sun_dir;
-        const double n = std::sqrt(double(d[0]) * d[0] + double(d[1]) * d[1] + double(d[2]) * d[2]);
-        const double L[3] = { n > 0 ? d[0] / n : 0.0, n > 0 ? d[1] / n : 1.0, n > 0 ? d[2] / n : 0.0 };
-        const int least = std::fabs(L[0]) <= std::fabs(L[1]) && std::fabs(L[0]) <= std::fabs(L[2]) ? 0 : (std::fabs(L[1]) <= std::fabs(L[2]) ? 1 : 2);
-        double a[3] = { 0, 0, 0 };
-        a[least] = 1.0;
-        double e1[3] = { L[1] * a[2] - L[2] * a[1], L[2] * a[0] - L[0] * a[2], L[0] * a[1] - L[1] * a[0] };
-        const double n1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
-        for (double& c : e1) c /= n1;
-        const double e2[3] = { L[1] * e1[2] - L[2] * e1[1], L[2] * e1[0] - L[0] * e1[2], L[0] * e1[1] - L[1] * e1[0] };
-        const double* E[2] = { e1, e2 };
-        for (int k = 0; k < 2; ++k) {
-            double lo = INFINITY, hi = -INFINITY;
-            for (int c = 0; c < 8; ++c) {
-                const double P[3] = { (c & 1) ? st->boundsHi[0] : st->boundsLo[0], (c & 2) ? st->boundsHi[1] : st->boundsLo[1],
-                                      (c & 4) ? st->boundsHi[2] : st->boundsLo[2] };
-                const double u = P[0] * E[k][0] + P[1] * E[k][1] + P[2] * E[k][2];
-                lo = std::min(lo, u);
-                hi = std::max(hi, u);
-            }
-            const double scale = ctx->shadowBinGrid / std::max(hi - lo, 1e-6);
-            for (int c = 0; c < 3; ++c) ctx->sunBinAxes[k][c] = static_cast<float>(E[k][c] * scale);
-            ctx->sunBinAxes[k][3] = static_cast<float>(-lo * scale);
-        }
+    ctx->hasSun = st->hasSunScene;
+    for (int k = 0; k < 3; ++k) {
+        ctx->sunColor[k] = st->sunScene.color[k];
+        ctx->sunDir[k] = st->sunScene.world_space_direction[k];
     }
+    ctx->spotHost = st->spotsScene;
     ctx->sceneStore = std::move(st);
+    if (!ctx->lights.ptr) ARK_HIP(ctx->lights.alloc((kMaxLights - 1) * sizeof(GpuSpotLight)));
+    if (!ctx->spotHost.empty()) ARK_HIP(hipMemcpy(ctx->lights.ptr, ctx->spotHost.data(), ctx->spotHost.size() * sizeof(GpuSpotLight), hipMemcpyHostToDevice));
+    ctx->lightsDirty = false;
+    deriveSceneArgs(ctx);
     int rc;
     if ((rc = ensureShadeWork(ctx)) != 0) return rc;
     if ((rc = ensureSpill(ctx)) != 0) return rc;
@@ -530,19 +570,10 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // (checkSequencing), dropping frames; such a context starts with events instead
         if (const char* pc = std::getenv("ROCPROF_COUNTER_COLLECTION"))
             if (*pc && std::strcmp(pc, "0") != 0 && std::strcmp(pc, "false") != 0) ctx->seqSync = false;
-        // ARK_SHADOW_BIN_GRID: light-space cells per axis of the shadow-ray binning
-        // (a power of 2 up to 256), 0 = the list in queue order
-        if (const char* g = std::getenv("ARK_SHADOW_BIN_GRID")) {
-            const int v = std::atoi(g);
-            ctx->shadowBinGrid = v <= 0 ? 0u : static_cast<uint32_t>(std::min(256, 1 << static_cast<int>(std::ceil(std::log2(std::max(1, v))))));
-        }
-        if (const char* m = std::getenv("ARK_SHADOW_BIN_MIN_RAYS")) ctx->shadowBinMinRays = static_cast<uint32_t>(std::max(0, std::atoi(m)));
     }
     if ((e = hipStreamCreateWithFlags(&ctx->traceStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-    // stream-order events of the frames in flight (ARK_SYNC_EVENT_FLAGS: extra
-    // hipEventCreateWithFlags flags, for A/B runs of the release scope)
-    unsigned syncFlags = hipEventDisableTiming;
-    if (const char* ef = std::getenv("ARK_SYNC_EVENT_FLAGS")) syncFlags |= static_cast<unsigned>(std::strtoul(ef, nullptr, 0));
+    // stream-order events of the frames in flight
+    const unsigned syncFlags = hipEventDisableTiming;
     if ((e = hipEventCreateWithFlags(&ctx->evTraced, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeSrc, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeDone, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
@@ -590,7 +621,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     // P = 4 1.21 -> 1.11, P = 2 2.22 -> 2.10; K = 4096 windows 0.72 -> 0.65, K = 2048
     // 0.43 unchanged; 2 per CU: P = 8 0.72, 4 per CU: 0.69). The whole C4 grid (8.4 M
     // rays) keeps the full grid: 4.059 vs 4.067 ms per step at 3 (profiles/r02_m17_ab).
-    ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(ARK_PIPE_TRACE_PER_CU, std::max(1, occT)) * ctx->cuCount);
+    ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(kPipeTracePerCu, std::max(1, occT)) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
     ctx->shadowBlocksPerCu = static_cast<uint32_t>(std::max(1, occW));
@@ -609,7 +640,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->seqWords, &ctx->shadeWork, &ctx->reflWork,
-                             &ctx->raySteps, &ctx->counters, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
+                             &ctx->raySteps, &ctx->counters, &ctx->lights, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
         b->release();
     ctx->sceneStore.reset();
     for (auto& ev : ctx->ev)
@@ -692,6 +723,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         if (static_cast<uint64_t>(m.first_index) + 3ull * inst.triangle_count > s->index_count)
             return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "instance %u: indices out of range", i);
     }
+    if (s->spot_light_count > ARK_DDGI_MAX_SPOT_LIGHTS || (s->spot_light_count && !s->spot_lights))
+        return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", ARK_DDGI_MAX_SPOT_LIGHTS);
     // World-space triangles per hit-mask class (GpuScene.cpp:883-929: one TLAS
     // instance per mesh segment; flattened here into one BVH per class).
     std::vector<BuildTriangle> cls[3];
@@ -750,8 +783,6 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
     // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
     if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
-    // early split clipping of the build's triangle references: ARK_BVH_PRESPLIT="levels,ratio"
-    if (const char* e = std::getenv("ARK_BVH_PRESPLIT")) std::sscanf(e, "%d,%f", &opt.presplit_levels, &opt.presplit_ratio);
     // BVH2 -> BVH8 child selection: SAH-optimal (Ylitie et al. 2017 DP; the default) or
     // ARK_BVH8_COLLAPSE=greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's
     // SAH terms
@@ -835,20 +866,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         infos.push_back(ti);
     }
     std::vector<GpuSpotLight> gspots(s->spot_light_count);
-    for (uint32_t i = 0; i < s->spot_light_count; ++i) {
-        const ArkSpotLight& sl = s->spot_lights[i];
-        GpuSpotLight& g = gspots[i];
-        std::memset(&g, 0, sizeof(g));
-        for (int k = 0; k < 3; ++k) {
-            g.color[k] = sl.color[k];
-            g.direction[k] = sl.world_space_direction[k];
-            g.right[k] = sl.world_space_right[k];
-            g.up[k] = sl.world_space_up[k];
-            g.position[k] = sl.world_space_position[k];
-        }
-        g.position[3] = sl.outer_cone_half_angle;
-        g.ies_texture = sl.ies_profile_index;
-    }
+    for (uint32_t i = 0; i < s->spot_light_count; ++i) gspots[i] = gpuSpotLight(s->spot_lights[i]);
     int rc;
     // nodes and triangles in ONE allocation (triangles after the nodes, 256-B aligned):
     // the traversal addresses both through one buffer resource with a per-lane
@@ -866,6 +884,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     size_t sunTriOffset = 0;
     Bvh8BuildResult r;
     bool sunBuilt = false;
+    const auto ts0 = std::chrono::steady_clock::now();
     if (sunBvh && !sunIn.tris.empty()) {
         sunBuilt = true;
         if (!build_sun_bvh(sunIn, opt, copt, r)) return ctx->fail(ARK_DDGI_E_DEVICE, "sun BVH2 leaf over %d triangles", kBvh8MaxLeafSize);
@@ -889,7 +908,10 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         ARK_HIP(hipMemcpy(st->sunNodes.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice));
         ARK_HIP(hipMemcpy(static_cast<char*>(st->sunNodes.ptr) + sunTriOffset, r.tris.data(), r.tris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
         sunNodeCount = r.nodes.size();
+        // the sun's traversal pushes onto the same spill area (its depth counts)
+        maxDepth = std::max(maxDepth, r.max_depth);
     }
+    const float sunBuildMs = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     std::vector<GpuTriangle>().swap(sunIn.world);
     if ((rc = upload(ctx, st->indices, s->indices, s->index_count)) != 0) return rc;
     if ((rc = upload(ctx, st->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
@@ -901,7 +923,6 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, st->instances, ginst.data(), ginst.size())) != 0) return rc;
     if ((rc = upload(ctx, st->texInfos, infos.data(), infos.size())) != 0) return rc;
     if ((rc = upload(ctx, st->texels, texels.data(), texels.size())) != 0) return rc;
-    if ((rc = upload(ctx, st->spots, gspots.data(), gspots.size())) != 0) return rc;
     {
         // per-triangle shading records (GpuTriangle order, 64 B): the three vertex
         // normals, the instance and the three UVs, copied from the vertex pool, so
@@ -946,25 +967,24 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     sc.texels = st->texels.as<float4>();
     sc.white_texture = static_cast<int32_t>(s->texture_count);
     sc.env_texture = (s->environment_texture >= 0 && static_cast<uint32_t>(s->environment_texture) < s->texture_count) ? s->environment_texture : sc.white_texture;
-    sc.has_sun = s->has_directional_light ? 1 : 0;
-    for (int k = 0; k < 3; ++k) {
-        sc.sun_color[k] = s->directional_light.color[k];
-        sc.sun_dir[k] = s->directional_light.world_space_direction[k];
-    }
-    sc.spot_count = static_cast<int32_t>(s->spot_light_count);
-    sc.spots = st->spots.as<GpuSpotLight>();
+    // lights: the scene's are each context's until ark_ddgi_set_lights (deriveSceneArgs)
+    st->hasSunScene = s->has_directional_light ? 1 : 0;
+    st->sunScene = s->directional_light;
+    st->spotsScene = std::move(gspots);
     sc.sun_root = -1;
+    st->sunArgs.sun_root = -1;
     if (sunNodeCount) {
-        sc.sun_nodes = st->sunNodes.as<GpuBvh8Node>();
-        sc.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st->sunNodes.ptr) + sunTriOffset);
-        sc.sun_root = 0;
+        st->sunArgs.sun_nodes = st->sunNodes.as<GpuBvh8Node>();
+        st->sunArgs.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st->sunNodes.ptr) + sunTriOffset);
+        st->sunArgs.sun_root = 0;
         for (int r = 0; r < 3; ++r)
-            for (int k = 0; k < 3; ++k) sc.sun_frame[r * 3 + k] = static_cast<float>(sunIn.frame[r][k]);
+            for (int k = 0; k < 3; ++k) st->sunArgs.sun_frame[r * 3 + k] = static_cast<float>(sunIn.frame[r][k]);
+        for (int k = 0; k < 3; ++k) st->sunDirBuilt[k] = s->directional_light.world_space_direction[k];
     }
     st->sunBvhNodes = sunNodeCount;
     st->bvhMaxDepth = maxDepth;
-    if (s->spot_light_count > kMaxLights - 1) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", kMaxLights - 1);
-    st->lightCount = (s->has_directional_light ? 1u : 0u) + s->spot_light_count;
+    st->inflateAbs = opt.inflate_abs;
+    st->triRecords = allTris.size();
     const auto t1 = std::chrono::steady_clock::now();
     st->bvhStats.node_count = allNodes.size();
     st->bvhStats.triangle_count = triangles;
@@ -977,6 +997,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     st->bvhStats.sun_node_count = sunNodeCount;
     st->bvhStats.sun_cost_world = st->sunCostWorld;
     st->bvhStats.sun_cost_light = st->sunCostLight;
+    st->bvhStats.sun_build_ms = sunBuildMs;
     return adoptScene(ctx, std::move(st));
 }
 
@@ -992,6 +1013,177 @@ int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src)
     ctx->hasScene = false;
     ctx->sceneStore.reset();
     return adoptScene(ctx, std::move(st));
+}
+
+int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* L)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!L || L->struct_size != sizeof(ArkDdgiLights)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiLights");
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_set_lights before ark_ddgi_set_scene");
+    if (L->spot_light_count > ARK_DDGI_MAX_SPOT_LIGHTS) return ctx->fail(ARK_DDGI_E_UNSUPPORTED, "at most %d spot lights (GpuScene.cpp:430)", ARK_DDGI_MAX_SPOT_LIGHTS);
+    if (L->spot_light_count && !L->spot_lights) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "set_lights: null spot_lights");
+    std::vector<GpuSpotLight> spots(L->spot_light_count);
+    for (uint32_t i = 0; i < L->spot_light_count; ++i) spots[i] = gpuSpotLight(L->spot_lights[i]);
+    const uint32_t count = (L->has_directional_light ? 1u : 0u) + L->spot_light_count;
+    ARK_HIP(hipSetDevice(ctx->device));
+    if (count > ctx->lightCount) {
+        // the shadow-ray list holds one ray per probe ray and light: grow it once the
+        // frames in flight (which use it) are done
+        const ShadeWorkLayout need = [&] {
+            const uint32_t keep = ctx->lightCount;
+            ctx->lightCount = count;
+            const ShadeWorkLayout w = shadeWorkLayout(ctx);
+            ctx->lightCount = keep;
+            return w;
+        }();
+        if (ctx->shadeWork.bytes < need.total) {
+            ARK_HIP(drainContext(ctx));
+            const uint32_t keep = ctx->lightCount;
+            ctx->lightCount = count;
+            const int rc = ensureShadeWork(ctx);
+            ctx->lightCount = keep;
+            if (rc) return rc;
+        }
+    }
+    ctx->hasSun = L->has_directional_light ? 1 : 0;
+    for (int k = 0; k < 3; ++k) {
+        ctx->sunColor[k] = ctx->hasSun ? L->directional_light.color[k] : 0.0f;
+        ctx->sunDir[k] = ctx->hasSun ? L->directional_light.world_space_direction[k] : 0.0f;
+    }
+    if (spots.size() != ctx->spotHost.size() || (!spots.empty() && std::memcmp(spots.data(), ctx->spotHost.data(), spots.size() * sizeof(GpuSpotLight)) != 0)) {
+        ctx->spotHost = std::move(spots);
+        ctx->lightsDirty = true;
+    }
+    deriveSceneArgs(ctx);
+    return ARK_DDGI_OK;
+}
+
+namespace {
+// ark_ddgi_set_instances' first use of a scene: the world BVHs' nodes by depth, deepest
+// first (a node's internal children are one level deeper), its work buffers.
+int prepareRefit(ArkDdgiCtx* ctx, SceneStore& st)
+{
+    const uint64_t n = st.bvhStats.node_count;
+    std::vector<GpuBvh8Node> h(n);
+    if (n) ARK_HIP(hipMemcpy(h.data(), st.nodes.ptr, n * sizeof(GpuBvh8Node), hipMemcpyDeviceToHost));
+    std::vector<std::vector<uint32_t>> byDepth;
+    std::vector<std::pair<uint32_t, uint32_t>> work; // (node, depth)
+    for (int32_t root : { st.args.root_opaque, st.args.root_masked, st.args.root_blend })
+        if (root >= 0) work.push_back({ static_cast<uint32_t>(root), 0u });
+    while (!work.empty()) {
+        const auto [node, d] = work.back();
+        work.pop_back();
+        if (node >= n) return ctx->fail(ARK_DDGI_E_DEVICE, "refit: node %u outside the BVH", node);
+        if (byDepth.size() <= d) byDepth.resize(d + 1);
+        byDepth[d].push_back(node);
+        const uint32_t internal = static_cast<uint32_t>(__builtin_popcount(h[node].imask));
+        for (uint32_t k = 0; k < internal; ++k) work.push_back({ h[node].child_base + k, d + 1 });
+    }
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    st.levelOffsets.assign(1, 0u);
+    for (size_t d = byDepth.size(); d-- > 0;) {
+        std::sort(byDepth[d].begin(), byDepth[d].end());
+        order.insert(order.end(), byDepth[d].begin(), byDepth[d].end());
+        st.levelOffsets.push_back(static_cast<uint32_t>(order.size()));
+    }
+    int rc;
+    if ((rc = upload(ctx, st.refitOrder, order.data(), order.size())) != 0) return rc;
+    ARK_HIP(st.refitBoxes.alloc(std::max<size_t>(16, n * 6 * sizeof(float))));
+    ARK_HIP(st.refitInst.alloc(std::max<size_t>(16, st.instHost.size() * sizeof(RefitInstance))));
+    ARK_HIP(st.refitBounds.alloc(6 * sizeof(uint32_t)));
+    return ARK_DDGI_OK;
+}
+
+float fromOrderedBits(uint32_t u) { return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+} // namespace
+
+int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_set_instances before ark_ddgi_set_scene");
+    SceneStore& st = *ctx->sceneStore;
+    if (count != st.instHost.size() || (count && !instances))
+        return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "set_instances: %u instances, the scene has %zu", count, st.instHost.size());
+    for (uint32_t i = 0; i < count; ++i) {
+        const ArkRTInstance &a = instances[i], &b = st.instHost[i];
+        if (a.rt_mesh_index != b.rt_mesh_index || a.triangle_count != b.triangle_count || a.hit_mask != b.hit_mask)
+            return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "set_instances: instance %u changed its mesh, triangle count or hit mask (a set_scene builds a new scene)", i);
+        for (float v : a.object_to_world)
+            if (!std::isfinite(v)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "set_instances: instance %u: non-finite transform", i);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    ARK_HIP(hipSetDevice(ctx->device));
+    // every launch in flight may read the scene: this context's, or with a shared scene
+    // every context's on the device
+    if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
+    else ARK_HIP(drainContext(ctx));
+    int rc;
+    if (st.levelOffsets.empty() && (rc = prepareRefit(ctx, st)) != 0) return rc;
+    // the instance table of the shading kernels and the refit's transforms
+    std::vector<GpuInstance> ginst(count);
+    std::vector<RefitInstance> rinst(count);
+    for (uint32_t ii = 0; ii < count; ++ii) {
+        const float* M = instances[ii].object_to_world;
+        // set_scene's determinant and normal-matrix rows
+        const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
+        const ArkRTTriangleMesh& mesh = st.meshHost[instances[ii].rt_mesh_index];
+        GpuInstance& g = ginst[ii];
+        std::memset(&g, 0, sizeof(g));
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) g.normal_matrix[r * 4 + c] = M[r * 4 + c];
+        g.rt_mesh_index = static_cast<int32_t>(instances[ii].rt_mesh_index);
+        g.flip_facing = det < 0.0f ? 1 : 0;
+        g.hit_mask = static_cast<int32_t>(instances[ii].hit_mask);
+        g.material_index = mesh.material_index;
+        RefitInstance& q = rinst[ii];
+        std::memset(&q, 0, sizeof(q));
+        std::memcpy(q.m, M, sizeof(q.m));
+        q.first_vertex = mesh.first_vertex;
+        q.first_index = static_cast<uint32_t>(mesh.first_index);
+        q.flip = g.flip_facing ? 1u : 0u;
+    }
+    if (count) {
+        ARK_HIP(hipMemcpy(st.instances.ptr, ginst.data(), count * sizeof(GpuInstance), hipMemcpyHostToDevice));
+        ARK_HIP(hipMemcpy(st.refitInst.ptr, rinst.data(), count * sizeof(RefitInstance), hipMemcpyHostToDevice));
+    }
+    const uint32_t initBounds[6] = { 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u };
+    ARK_HIP(hipMemcpy(st.refitBounds.ptr, initBounds, sizeof(initBounds), hipMemcpyHostToDevice));
+    GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(static_cast<char*>(st.nodes.ptr) + st.args.tri_byte_offset);
+    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(),
+                              st.refitBounds.as<uint32_t>(), ctx->stream));
+    uint32_t b[6];
+    ARK_HIP(hipMemcpyAsync(b, st.refitBounds.ptr, sizeof(b), hipMemcpyDeviceToHost, ctx->stream));
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    // the builder's absolute inflation (1e-6 of the scene diagonal), never below set_scene's
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = fromOrderedBits(b[a]);
+        hi[a] = fromOrderedBits(b[3 + a]);
+    }
+    const float inflate = std::max(st.inflateAbs, bvh8_inflation_box(lo, hi));
+    const uint32_t* order = st.refitOrder.as<uint32_t>();
+    for (size_t l = 0; l + 1 < st.levelOffsets.size(); ++l)
+        ARK_HIP(launch_refit_nodes(st.nodes.as<GpuBvh8Node>(), tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l],
+                                   st.levelOffsets[l + 1] - st.levelOffsets[l], inflate, ctx->stream));
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    for (uint32_t ii = 0; ii < count; ++ii) std::memcpy(st.instHost[ii].object_to_world, instances[ii].object_to_world, sizeof(float) * 12);
+    for (int a = 0; a < 3; ++a) {
+        st.boundsLo[a] = lo[a] <= hi[a] ? lo[a] : 0.0f;
+        st.boundsHi[a] = lo[a] <= hi[a] ? hi[a] : 0.0f;
+    }
+    // the light-space sun BVH holds the old world-space records: the sun's shadow rays
+    // traverse the world BVHs from now on (a set_scene builds a new one)
+    st.sunArgs.sun_root = -1;
+    st.sunArgs.sun_nodes = nullptr;
+    st.sunArgs.sun_tris = nullptr;
+    st.sunNodes.release();
+    st.sunBvhNodes = 0;
+    st.bvhStats.sun_node_count = 0;
+    st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ++st.version;
+    deriveSceneArgs(ctx);
+    return ARK_DDGI_OK;
 }
 
 
@@ -1116,6 +1308,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!p || p->struct_size != sizeof(ArkDdgiFrameParams)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiFrameParams");
     if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_update before ark_ddgi_set_scene");
+    if (ctx->sceneVersion != ctx->sceneStore->version) deriveSceneArgs(ctx); // another context refitted the shared scene
     const uint32_t N = static_cast<uint32_t>(ctx->N);
     const uint32_t K = std::min(p->probe_updates, N);
     const uint32_t R = p->rays_per_probe;
@@ -1168,6 +1361,9 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.fib = ctx->fib.as<float4>() + b * Rmax;
     RoctxRange ddgiZone("DDGI");
     ARK_HIP(orderBegin(ctx, s));
+    // lights changed since the last update: stored ahead of this frame's shadow rays and
+    // shading on s (the traversal on the traversal stream reads no light)
+    ARK_HIP(flushLights(ctx, s));
     if (ctx->orderR != R) {
         sampleTraversalOrder(R, ctx->orderHost);
         ARK_HIP(hipMemcpyAsync(ctx->order.ptr, ctx->orderHost.data(), R * 4, hipMemcpyHostToDevice, s));
@@ -1193,28 +1389,14 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
         char* w = static_cast<char*>(ctx->shadeWork.ptr);
         f.shadow_bits = reinterpret_cast<uint32_t*>(w + l.bits);
         f.shadow_rays = reinterpret_cast<ShadowRay*>(w + l.list);
-        f.shadow_rays_gen = f.shadow_rays;
-        f.shadow_bin_grid = 0;
-        // binning pays for itself on large lists only (a window of a few probes is
-        // one wave's work either way)
-        if (ctx->shadowBinGrid && f.window_rays >= ctx->shadowBinMinRays) {
-            f.shadow_bin_grid = ctx->shadowBinGrid;
-            f.shadow_rays_gen = reinterpret_cast<ShadowRay*>(w + l.gen);
-            f.shadow_bin_key = reinterpret_cast<uint32_t*>(w + l.key);
-            f.shadow_bin_rank = reinterpret_cast<uint32_t*>(w + l.rank);
-            f.shadow_bin_count = reinterpret_cast<uint32_t*>(w + l.count);
-            f.shadow_bin_start = reinterpret_cast<uint32_t*>(w + l.start);
-            std::memcpy(f.sun_bin_axes, ctx->sunBinAxes, sizeof(f.sun_bin_axes));
-        }
     }
     f.shadow_count = f.ray_counter + kShadowCountWord;
     f.shadow_heads = f.ray_counter + kShadowHeadWord;
     // the sun's shadow rays in their own list (the first Kmax x Rmax entries of the
     // list area, the other lights' after them) for the light-space BVH
-    if (ctx->scene.sun_root >= 0 && f.shadow_bin_grid == 0) {
+    if (ctx->scene.sun_root >= 0) {
         f.sun_rays = f.shadow_rays;
         f.shadow_rays += Kmax * Rmax;
-        f.shadow_rays_gen = f.shadow_rays;
         f.sun_count = f.ray_counter + kSunCountWord;
         f.sun_heads = f.ray_counter + kSunHeadWord;
     }
@@ -1713,7 +1895,9 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.refill_min = ctx->refillMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
+    if (ctx->sceneVersion != ctx->sceneStore->version) deriveSceneArgs(ctx);
     ARK_HIP(orderBegin(ctx, s));
+    ARK_HIP(flushLights(ctx, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, (kRayCounterWords + kRayCounterStride) * 4, s));
     ARK_HIP(launch_rt_reflections(ctx->scene, f, *desc, ctx->traceBlocks, shadowBlocksFor(ctx, pixels), s));
     ARK_HIP(orderEnd(ctx, s));

@@ -169,7 +169,7 @@ struct SceneArgs {
     // rays then traverse the world BVHs)
     const GpuBvh8Node* sun_nodes;
     const GpuTriangle* sun_tris;
-    int32_t sun_root;
+    int32_t sun_root = -1; // (a zero-initialised SceneArgs must not mean "sun BVH at node 0")
     float sun_frame[9]; // rows u, v, w
 
     __device__ __forceinline__ int resolveTexture(int idx) const
@@ -228,21 +228,6 @@ struct FrameArgs {
     ShadowRay* sun_rays;
     uint32_t* sun_count;     // = ray_counter + kSunCountWord
     uint32_t* sun_heads;     // = ray_counter + kSunHeadWord
-    // Light-space binning of the shadow-ray list (shadow_bin_grid = G > 0): k_shadow_gen
-    // writes shadow_rays_gen with a bin key (light, Morton cell of the G x G light-space
-    // grid) and its rank in the bin, k_shadow_bin_scan turns the bin counts into bin
-    // starts, k_shadow_scatter writes shadow_rays in bin order. Sun rays: the cell of
-    // the origin projected on the plane perpendicular to the sun (parallel rays of one
-    // cell walk one column of the scene); spot rays: the octahedral cell of the
-    // direction from the spot. Only the order of the list changes (any-hit results do
-    // not depend on it).
-    ShadowRay* shadow_rays_gen;
-    uint32_t* shadow_bin_key;   // [list entry] light * G^2 + Morton(cell)
-    uint32_t* shadow_bin_rank;  // [list entry] rank in its bin (atomic order)
-    uint32_t* shadow_bin_count; // [light_count * G^2] (zeroed again by the scan)
-    uint32_t* shadow_bin_start; // [light_count * G^2]
-    uint32_t shadow_bin_grid;   // G (power of 2, <= 256); 0 = list in queue order
-    float sun_bin_axes[2][4];   // cell coordinate = dot(X, axis.xyz) + axis.w, in [0, G)
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
     uint16_t* ray_steps;     // counting updates: traversal iterations of each probe ray (both passes) at its hit-record index
@@ -284,6 +269,28 @@ struct BakeArgs {
     uint32_t* spill;
 };
 
+// Per-frame scene inputs (ddgi_scene_update.hip)
+// the context's spot lights as a kernel argument (ark_ddgi_set_lights)
+struct LightBlock {
+    GpuSpotLight spots[kMaxLights - 1];
+    uint32_t count;
+};
+// one TLAS instance for the refit of its triangle records (ark_ddgi_set_instances)
+struct alignas(16) RefitInstance {
+    float m[12];           // object_to_world, 3 x 4 row-major
+    int32_t first_vertex;  // its RT mesh's vertex and index offsets
+    uint32_t first_index;
+    uint32_t flip;         // det(object_to_world) < 0
+    uint32_t _pad;
+};
+hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream_t s);
+// every triangle record re-transformed; bounds = 3 x atomicMin, 3 x atomicMax of the
+// order-preserving bits of the new world coordinates
+hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, uint32_t* bounds,
+                             hipStream_t s);
+// one level: nodes order[0 .. count), boxes [node][6] (lo, hi) of the deeper levels in, this level's out
+hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, float inflateAbs, hipStream_t s);
+
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 // stage 0: parameterization raster, 1: barycentrics + work list, 2: AO rays
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s);
@@ -296,7 +303,6 @@ hipError_t launch_probe_debug(const FrameArgs& f, const ArkProbeDebugDesc& d, hi
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
 hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s);
-// k_shadow_gen, then (f.shadow_bin_grid > 0) the bin scan and the scatter into bin order
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_update(const FrameArgs& f, hipStream_t s);
 hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s);

@@ -28,10 +28,6 @@
 #include <utility>
 #include <vector>
 
-#ifndef ARK_DDGI_GATHER_BATCH
-#define ARK_DDGI_GATHER_BATCH 1 // cage probes whose atlas taps are in flight together (sampleDDGI; 2 and 4 measured no faster on C4)
-#endif
-
 #include "../../include/ark_ddgi.h"
 #include "ddgi_device.h"
 #include "ddgi_kernels.h"
@@ -318,262 +314,34 @@ __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uin
 // operands (measured 3.02 vs 2.72 ms traversal at C4 in round 1).
 // Returns the hit internal children as a node group and the hit leaf children's
 // triangles as a bit mask over [tBase, tBase + 24) (2 VALU: triangle rows).
-// Node-visit instruction budget (tools/isa_budget.py): the defaults cut
-// k_trace's node block from 269 to 223 VALU (gfx950 ISA of this file)
-// GF dual steps (travStepDual<.., GF = true>) fetch every node from global memory, with
-// both sides' loads outside any branch (see travStepDual); per kernel:
-// k_trace: on (its LDS node cache is then not allocated: 22.3 -> 18.4 KB of LDS per
-// workgroup). C4 step 3.66 / 3.68 -> 3.57 / 3.54 ms, K = 4096 windows 0.606 -> 0.591 /
-// 0.585 ms, K = 2048 within 1 %, Z-slab proxy P = 8 0.578 -> 0.570 ms, although the
-// serial traversal itself is 1 % slower (1.975 -> 1.985 ms; profiles/r03_an, r03_ao).
-// k_trace_shadow: off (its any-hit rays gain from the cached top nodes: 0.704 -> 0.730
-// ms with global fetches).
-#ifndef ARK_SHADOW_LDS_NODES
-#define ARK_SHADOW_LDS_NODES (kLdsNodes - 8) // top nodes k_trace_shadow keeps in LDS
-#endif
-#ifndef ARK_TRACE_FETCH_GLOBAL
-#define ARK_TRACE_FETCH_GLOBAL 1
-#endif
-#ifndef ARK_SHADOW_FETCH_GLOBAL
-#define ARK_SHADOW_FETCH_GLOBAL 0
-#endif
-#ifndef ARK_NODE_LDEXP
-#define ARK_NODE_LDEXP 1 // per-axis step * idir as v_ldexp_f32 of the exponent byte instead of a float build + multiply
-#endif
-#ifndef ARK_MASK_ADDC
-#define ARK_MASK_ADDC 1 // hit / inside masks as m = 2m + bit (v_cmp to VCC + v_addc) over slots 7..0
-#endif
-#ifndef ARK_NODE_INSIDE
-#define ARK_NODE_INSIDE 0 // 1: origin-containing children first, else plain octant order (40 VALU per node for +0.8 % node visits)
-#endif
-#ifndef ARK_NODE_SEL
-#define ARK_NODE_SEL 1 // octant selects of the plane words as v_bitop3_b32 on sign masks (2-cycle) instead of VCC v_cndmask (4+)
-#endif
-#ifndef ARK_NODE_CMP3
-#define ARK_NODE_CMP3 1 // child accept as three compares (tn <= lim, tn <= lim(tmax), tmin <= lim) instead of v_max + v_min (4-cycle each)
-#endif
-#ifndef ARK_LONG_RAY_STEPS
-#define ARK_LONG_RAY_STEPS 0 // k_trace: a wave holding a ray older than this many steps runs at raised priority (0: off)
-#endif
-// k_trace's pass word: with ARK_LONG_RAY_STEPS bit 0 is the pass and the ray's age sits
-// above it; without, it is the pass itself
-#if ARK_LONG_RAY_STEPS
-#define ARK_PASS_IS(p, v) (((p) & 1) == (v))
-#else
-#define ARK_PASS_IS(p, v) ((p) == (v))
-#endif
-#ifndef ARK_TAIL_PREFETCH
-#define ARK_TAIL_PREFETCH 0 // 1: k_trace: once its wave's ray supply is exhausted, each step warms the caches with the next node group's first children (register-free loads into LDS)
-#endif
-#ifndef ARK_NODE_F16
-#define ARK_NODE_F16 0 // 1: the child box tests in packed fp16 (visitNode8: two children per instruction, outward margins)
-#endif
+// Node-visit instruction budget (tools/isa_budget.py). Dual steps of
+// k_trace (travStepDual<.., GF = true>) fetch every node from global memory, with both
+// sides' loads outside any branch (see travStepDual): its LDS node cache is then not
+// allocated (22.3 -> 18.4 KB of LDS per workgroup); C4 step 3.66 / 3.68 -> 3.57 / 3.54
+// ms, K = 4096 windows 0.606 -> 0.591 / 0.585 ms, Z-slab proxy P = 8 0.578 -> 0.570 ms
+// (profiles/r03_an, r03_ao). k_trace_shadow keeps its top nodes in LDS (GF = false):
+// its any-hit rays gain from them (0.704 -> 0.730 ms with global fetches).
+constexpr int kShadowLdsNodes = kLdsNodes - 8; // top nodes k_trace_shadow keeps in LDS
 // LDS octant permutation table of the node visit (loadNodeCache fills it; every
 // kernel that visits nodes calls loadNodeCache first)
 __shared__ uint8_t g_octPerm[8 * 256];
 
-#if ARK_MASK_ADDC
-// m << 1 | (a <= b) in two VALU: the compare writes VCC and v_addc adds it in as the
-// carry (m + m + carry); an unordered compare (NaN) shifts in 0, as `<=` does
-__device__ __forceinline__ uint32_t shiftInLe(uint32_t m, float a, float b)
-{
-    uint32_t r;
-    asm("v_cmp_le_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc" : "=v"(r) : "v"(a), "v"(b), "v"(m) : "vcc");
-    return r;
-}
-#endif
-
-#if ARK_NODE_F16
-// One pair of children (slots 2j + 1, 2j of a plane word) in packed fp16: the eight
-// plane bytes as fp16 subnormals q * 2^-24 (v_perm_b32 with a zero high byte, SEL),
-// t = fma(q * 2^-24, A, B) per plane, A and B broadcast from their register's half by
-// op_sel, near planes with B - e (the low half of the axis's B register), far planes
-// with B + e (its high half), max3 with 0 / min3 with tmax (the low half of TMX), the
-// odd slot's then the even slot's compare shifted in.
-#define ARK_F16_PAIR(NX, NY, NZ, FX, FY, FZ, SEL)                                                              \
-    "v_perm_b32 %[t0], %[" NX "], %[" NX "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t1], %[" NY "], %[" NY "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t2], %[" NZ "], %[" NZ "], %[" SEL "]\n\t"                                                  \
-    "v_pk_fma_f16 %[t0], %[t0], %[axy], %[bx] op_sel:[0,0,0] op_sel_hi:[1,0,0]\n\t"                          \
-    "v_pk_fma_f16 %[t1], %[t1], %[axy], %[by] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"                          \
-    "v_pk_fma_f16 %[t2], %[t2], %[az], %[bz] op_sel:[0,0,0] op_sel_hi:[1,0,0]\n\t"                           \
-    "v_pk_maximum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
-    "v_pk_max_f16 %[t0], %[t0], 0\n\t"                                                                        \
-    "v_perm_b32 %[t1], %[" FX "], %[" FX "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t2], %[" FY "], %[" FY "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t3], %[" FZ "], %[" FZ "], %[" SEL "]\n\t"                                                  \
-    "v_pk_fma_f16 %[t1], %[t1], %[axy], %[bx] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                          \
-    "v_pk_fma_f16 %[t2], %[t2], %[axy], %[by] op_sel:[0,1,1] op_sel_hi:[1,1,1]\n\t"                          \
-    "v_pk_fma_f16 %[t3], %[t3], %[az], %[bz] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_minimum3_f16 %[t1], %[t1], %[t2], %[t3]\n\t"                                                        \
-    "v_pk_min_f16 %[t1], %[t1], %[tmx] op_sel:[0,0] op_sel_hi:[1,0]\n\t"                                      \
-    "v_cmp_le_f16_sdwa vcc, %[t0], %[t1] src0_sel:WORD_1 src1_sel:WORD_1\n\t"                                \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"                                                  \
-    "v_cmp_le_f16_e32 vcc, %[t0], %[t1]\n\t"                                                                  \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
-
-__device__ __forceinline__ uint32_t cvtPkF16(float lo, float hi)
-{
-    uint32_t r;
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-    return r;
-}
-
-// ARK_NODE_F16 == 2: directed rounding instead of error bounds. The near planes of
-// all four pairs are evaluated with the MODE register's rounding toward -inf (A and B
-// converted to fp16 downward, every packed fma rounded downward), the far planes toward
-// +inf, then round-to-nearest is restored - all inside one asm statement, so no
-// compiler-scheduled instruction runs under the directed modes. Near distances are
-// then never above, far distances never below, their values for the fp32 A and B
-// (q >= 0; either sign of A), so no child the exact-arithmetic test accepts is culled.
-// One pair's near half: (A_dn, B_dn) of each axis in NX / NY / NZ (lo = A, hi = B).
-#define ARK_F16D_NEAR(WX, WY, WZ, SEL, OUT)                                                                    \
-    "v_perm_b32 %[t0], %[" WX "], %[" WX "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t1], %[" WY "], %[" WY "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t2], %[" WZ "], %[" WZ "], %[" SEL "]\n\t"                                                  \
-    "v_pk_fma_f16 %[t0], %[t0], %[ax], %[ax] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_fma_f16 %[t1], %[t1], %[ay], %[ay] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_fma_f16 %[t2], %[t2], %[az], %[az] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_maximum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
-    "v_pk_max_f16 %[" OUT "], %[t0], 0\n\t"
-// One pair's far half (A_up, B_up per axis) and the compares: odd slot, then even
-// slot shifted into the mask (m = 2m + hit)
-#define ARK_F16D_FAR(WX, WY, WZ, SEL, NEAR)                                                                    \
-    "v_perm_b32 %[t0], %[" WX "], %[" WX "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t1], %[" WY "], %[" WY "], %[" SEL "]\n\t"                                                  \
-    "v_perm_b32 %[t2], %[" WZ "], %[" WZ "], %[" SEL "]\n\t"                                                  \
-    "v_pk_fma_f16 %[t0], %[t0], %[ax], %[ax] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_fma_f16 %[t1], %[t1], %[ay], %[ay] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_fma_f16 %[t2], %[t2], %[az], %[az] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"                           \
-    "v_pk_minimum3_f16 %[t0], %[t0], %[t1], %[t2]\n\t"                                                        \
-    "v_pk_min_f16 %[t0], %[t0], %[tm] op_sel:[0,0] op_sel_hi:[1,0]\n\t"                                       \
-    "v_cmp_le_f16_sdwa vcc, %[" NEAR "], %[t0] src0_sel:WORD_1 src1_sel:WORD_1\n\t"                          \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"                                                  \
-    "v_cmp_le_f16_e32 vcc, %[" NEAR "], %[t0]\n\t"                                                            \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
-#endif
-
+// Rejected node-test forms (measured slower, removed in round 5): packed
+// fp16 child tests with error bounds or directed rounding (C4 traversal 1.95 -> 20-30
+// ms from near-axis-parallel rays), origin-containing children first (+40 VALU per node
+// for 0.8 % fewer visits), v_cndmask plane selects and v_max/v_min interval tests.
 __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 o, V3 idir, uint32_t oct, float tmin,
                                            float tmax, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase, uint32_t& tBits)
 {
-#if ARK_NODE_F16 == 2
-    // Packed-fp16 child tests with directed rounding (ARK_F16D_*). Per node a scale
-    // 2^-s keeps the node's largest A = step * idir * 2^(24 - s) below 2^15 (q enters
-    // as the fp16 subnormal q * 2^-24), B = (anchor - o) * idir * 2^-s in fp32 as the
-    // fp32 form computes it (its rounding is covered by the build's box inflation, as
-    // there); A and B are rounded to fp16 downward for the near planes and upward for
-    // the far planes, and so is every distance. tmin is not applied (0: a box within
-    // tmin of the origin is visited); tmax gets the fp32 form's relative margin for
-    // the reciprocal's error. Host restatement: ark_ddgi_debug_bvh8_trace_stats
-    // ARK_SIM_BOX=f16d (counts culled children: none).
-    (void)tmin;
-    const int ex = static_cast<int>(w0.w & 0xffu), ey = static_cast<int>((w0.w >> 8) & 0xffu), ez = static_cast<int>((w0.w >> 16) & 0xffu);
-    const int emax = max(max(ex, ey), ez);
-    const int L = __builtin_amdgcn_frexp_expf(fmaxf(fmaxf(fabsf(idir.x), fabsf(idir.y)), fabsf(idir.z)));
-    const int sN = max(0, emax - 127 + L + 9);
-    const int k = 103 + sN;
-    const float Ax = __builtin_amdgcn_ldexpf(idir.x, ex - k), Ay = __builtin_amdgcn_ldexpf(idir.y, ey - k), Az = __builtin_amdgcn_ldexpf(idir.z, ez - k);
-    const float bx = __builtin_amdgcn_ldexpf((__uint_as_float(w0.x) - o.x) * idir.x, -sN);
-    const float by = __builtin_amdgcn_ldexpf((__uint_as_float(w0.y) - o.y) * idir.y, -sN);
-    const float bz = __builtin_amdgcn_ldexpf((__uint_as_float(w0.z) - o.z) * idir.z, -sN);
-    const float tms = __builtin_amdgcn_ldexpf(tmax, -sN) * (1.0f + 0x1p-16f);
-    const uint32_t imask = w0.w >> 24;
-    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
-    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
-    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
-    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-    uint32_t hitSlots = 0, t0, t1, t2, ax, ay, az, tm, n0, n1, n2, n3;
-    const uint32_t selLo = 0x0c010c00u, selHi = 0x0c030c02u; // bytes (0, 1) / (2, 3) as fp16 subnormals
-    // MODE bits 3:0 = FP_ROUND (f32 in 1:0, f16/f64 in 3:2): 0xa toward -inf, 0x5 toward
-    // +inf, 0 nearest even; s_nop 1 covers the write-to-use wait states
-    asm volatile(
-        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0xa\n\ts_nop 1\n\t"
-        "v_cvt_pk_f16_f32 %[ax], %[Ax], %[bx]\n\t"
-        "v_cvt_pk_f16_f32 %[ay], %[Ay], %[by]\n\t"
-        "v_cvt_pk_f16_f32 %[az], %[Az], %[bz]\n\t"
-        ARK_F16D_NEAR("nx1", "ny1", "nz1", "shi", "n3") ARK_F16D_NEAR("nx1", "ny1", "nz1", "slo", "n2")
-        ARK_F16D_NEAR("nx0", "ny0", "nz0", "shi", "n1") ARK_F16D_NEAR("nx0", "ny0", "nz0", "slo", "n0")
-        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0x5\n\ts_nop 1\n\t"
-        "v_cvt_pk_f16_f32 %[ax], %[Ax], %[bx]\n\t"
-        "v_cvt_pk_f16_f32 %[ay], %[Ay], %[by]\n\t"
-        "v_cvt_pk_f16_f32 %[az], %[Az], %[bz]\n\t"
-        "v_cvt_pk_f16_f32 %[tm], %[tms], %[tms]\n\t"
-        ARK_F16D_FAR("fx1", "fy1", "fz1", "shi", "n3") ARK_F16D_FAR("fx1", "fy1", "fz1", "slo", "n2")
-        ARK_F16D_FAR("fx0", "fy0", "fz0", "shi", "n1") ARK_F16D_FAR("fx0", "fy0", "fz0", "slo", "n0")
-        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0\n\ts_nop 1"
-        : [acc] "+v"(hitSlots), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [ax] "=&v"(ax), [ay] "=&v"(ay), [az] "=&v"(az), [tm] "=&v"(tm),
-          [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3)
-        : [nx0] "v"(nX0), [nx1] "v"(nX1), [ny0] "v"(nY0), [ny1] "v"(nY1), [nz0] "v"(nZ0), [nz1] "v"(nZ1), [fx0] "v"(fX0), [fx1] "v"(fX1),
-          [fy0] "v"(fY0), [fy1] "v"(fY1), [fz0] "v"(fZ0), [fz1] "v"(fZ1), [Ax] "v"(Ax), [Ay] "v"(Ay), [Az] "v"(Az), [bx] "v"(bx), [by] "v"(by),
-          [bz] "v"(bz), [tms] "v"(tms), [slo] "s"(selLo), [shi] "s"(selHi)
-        : "vcc");
-    const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
-#elif ARK_NODE_F16
-    // Packed-fp16 child tests. Per node: a scale 2^-s that keeps the node's largest
-    // A = step * idir * 2^(24 - s) below 2^15 (fp16 range), A per axis (the q factor:
-    // q enters as the fp16 subnormal q * 2^-24), B = (anchor - o) * idir * 2^-s, and
-    // an error bound per axis e = 0.3 |A| 2^-24 + 2^-9 |B| + 2^-22 that covers the
-    // rounding of A to fp16 over q <= 255 steps (0.125 |a|), of the product-sum
-    // (0.125 |a| + 2^-11 |t|), of B and B -+ e (2^-11 each): near planes use B - e, far
-    // planes B + e, tmin rounds down and tmax up, so no box holding an exact hit is
-    // culled (the host simulation, ark_ddgi_debug_bvh8_trace_stats ARK_SIM_BOX=f16s,
-    // counts none; the hits themselves stay fp32 and bit-exact).
-    const int ex = static_cast<int>(w0.w & 0xffu), ey = static_cast<int>((w0.w >> 8) & 0xffu), ez = static_cast<int>((w0.w >> 16) & 0xffu);
-    const int emax = max(max(ex, ey), ez);
-    const int L = __builtin_amdgcn_frexp_expf(fmaxf(fmaxf(fabsf(idir.x), fabsf(idir.y)), fabsf(idir.z)));
-    const int sN = max(0, emax - 127 + L + 9);
-    const float Ax = __builtin_amdgcn_ldexpf(idir.x, ex - 103 - sN), Ay = __builtin_amdgcn_ldexpf(idir.y, ey - 103 - sN),
-                Az = __builtin_amdgcn_ldexpf(idir.z, ez - 103 - sN);
-    const float bx = __builtin_amdgcn_ldexpf((__uint_as_float(w0.x) - o.x) * idir.x, -sN);
-    const float by = __builtin_amdgcn_ldexpf((__uint_as_float(w0.y) - o.y) * idir.y, -sN);
-    const float bz = __builtin_amdgcn_ldexpf((__uint_as_float(w0.z) - o.z) * idir.z, -sN);
-    auto err = [](float A, float b) { return fmaf(fabsf(A), 0.3f * 0x1p-24f, fmaf(fabsf(b), 0x1p-9f, 0x1p-22f)); };
-    const uint32_t axy = cvtPkF16(Ax, Ay), az = cvtPkF16(Az, Az);
-    // per axis (B - e, B + e): (B, e) in fp16, then one packed add with the low lane's e
-    // negated; its rounding is in e's budget
-    auto biases = [](float b, float e) {
-        uint32_t r;
-        asm("v_cvt_pk_f16_f32 %0, %1, %2\n\tv_pk_add_f16 %0, %0, %0 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[0,1]" : "=&v"(r) : "v"(b), "v"(e));
-        return r;
-    };
-    const uint32_t bxp = biases(bx, err(Ax, bx)), byp = biases(by, err(Ay, by)), bzp = biases(bz, err(Az, bz));
-    // tmin is not applied (0 instead: a box within tmin of the origin is visited, which
-    // is conservative); tmax rounds up
-    (void)tmin;
-    const uint32_t tmx = cvtPkF16(__builtin_amdgcn_ldexpf(tmax, -sN) * (1.0f + 0x1p-9f), 0.0f);
-    const uint32_t imask = w0.w >> 24;
-    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
-    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
-    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
-    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-    uint32_t hitSlots = 0, t0, t1, t2, t3;
-    const uint32_t selLo = 0x0c010c00u, selHi = 0x0c030c02u; // bytes (0, 1) / (2, 3) as fp16 subnormals
-    asm(ARK_F16_PAIR("nx1", "ny1", "nz1", "fx1", "fy1", "fz1", "shi") ARK_F16_PAIR("nx1", "ny1", "nz1", "fx1", "fy1", "fz1", "slo")
-        ARK_F16_PAIR("nx0", "ny0", "nz0", "fx0", "fy0", "fz0", "shi") ARK_F16_PAIR("nx0", "ny0", "nz0", "fx0", "fy0", "fz0", "slo")
-        : [acc] "+v"(hitSlots), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
-        : [nx0] "v"(nX0), [nx1] "v"(nX1), [ny0] "v"(nY0), [ny1] "v"(nY1), [nz0] "v"(nZ0), [nz1] "v"(nZ1), [fx0] "v"(fX0), [fx1] "v"(fX1),
-          [fy0] "v"(fY0), [fy1] "v"(fY1), [fz0] "v"(fZ0), [fz1] "v"(fZ1), [axy] "v"(axy), [az] "v"(az), [bx] "v"(bxp), [by] "v"(byp),
-          [bz] "v"(bzp), [tmx] "v"(tmx), [slo] "s"(selLo), [shi] "s"(selHi)
-        : "vcc");
-    const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
-#else
-#if ARK_NODE_LDEXP
     // exponent byte e: the step is 2^(e - 127) (e = 0 never occurs for a used axis:
-    // the builder's steps are normal numbers)
+    // the builder's steps are normal numbers); step * idir as one v_ldexp_f32
     const float ax = __builtin_amdgcn_ldexpf(idir.x, static_cast<int>(w0.w & 0xffu) - 127);
     const float ay = __builtin_amdgcn_ldexpf(idir.y, static_cast<int>((w0.w >> 8) & 0xffu) - 127);
     const float az = __builtin_amdgcn_ldexpf(idir.z, static_cast<int>((w0.w >> 16) & 0xffu) - 127);
-#else
-    const float ax = __uint_as_float((w0.w & 0xffu) << 23) * idir.x;
-    const float ay = __uint_as_float(((w0.w >> 8) & 0xffu) << 23) * idir.y;
-    const float az = __uint_as_float(((w0.w >> 16) & 0xffu) << 23) * idir.z;
-#endif
     const float bx = (__uint_as_float(w0.x) - o.x) * idir.x;
     const float by = (__uint_as_float(w0.y) - o.y) * idir.y;
     const float bz = (__uint_as_float(w0.z) - o.z) * idir.z;
     const uint32_t imask = w0.w >> 24;
-    const bool fx = oct & 1u, fy = oct & 2u, fz = oct & 4u;
-#if ARK_NODE_SEL
     // gfx950 issues v_bitop3_b32 and v_ashrrev_i32 in about half the cycles of a
     // v_cndmask_b32 (tools/probe/valu_table*.hip): the near/far plane words of each axis
     // are selected bitwise under the lane mask of its direction sign (all ones when the
@@ -588,79 +356,38 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     const uint32_t nX0 = pick(mx, w3.z, w2.x), nX1 = pick(mx, w3.w, w2.y), fX0 = pick(mx, w2.x, w3.z), fX1 = pick(mx, w2.y, w3.w);
     const uint32_t nY0 = pick(my, w4.x, w2.z), nY1 = pick(my, w4.y, w2.w), fY0 = pick(my, w2.z, w4.x), fY1 = pick(my, w2.w, w4.y);
     const uint32_t nZ0 = pick(mz, w4.z, w3.x), nZ1 = pick(mz, w4.w, w3.y), fZ0 = pick(mz, w3.x, w4.z), fZ1 = pick(mz, w3.y, w4.w);
-#else
-    const uint32_t nX0 = fx ? w3.z : w2.x, nX1 = fx ? w3.w : w2.y, fX0 = fx ? w2.x : w3.z, fX1 = fx ? w2.y : w3.w;
-    const uint32_t nY0 = fy ? w4.x : w2.z, nY1 = fy ? w4.y : w2.w, fY0 = fy ? w2.z : w4.x, fY1 = fy ? w2.w : w4.y;
-    const uint32_t nZ0 = fz ? w4.z : w3.x, nZ1 = fz ? w4.w : w3.y, fZ0 = fz ? w3.x : w4.z, fZ1 = fz ? w3.y : w4.w;
-#endif
-#if ARK_NODE_CMP3
     // max(tn, tmin) <= f(min(tf, tmax)) with the monotone f(x) = fma(x, 1.00001, 1e-7) is
     // tn <= f(tf) && tn <= f(tmax) && tmin <= f(tf) (tmin <= f(tmax) holds for any ray
     // the traversal runs): the same accepted set as the max/min form (no NaN reaches
     // it: A, B and q are finite), three 2-cycle compares instead of two 4-cycle v_max /
-    // v_min
-    // (tmin is an SGPR operand: every caller passes a wave-uniform constant)
+    // v_min (tmin is an SGPR operand: every caller passes a wave-uniform constant)
     const float limT = fmaf(tmax, 1.00001f, 1e-7f);
-    (void)fx;
-    (void)fy;
-    (void)fz;
-#endif
-    uint32_t hitSlots = 0, insideLo = 0;
+    uint32_t hitSlots = 0;
+    // slots 7 .. 0, each compare shifted into the mask as v_addc's carry (m = 2m + hit)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const int s = ARK_MASK_ADDC ? 7 - k : k;
+        const int s = 7 - k;
         const uint32_t sh = static_cast<uint32_t>(s & 3) * 8u;
         const bool hiWord = s >= 4;
         auto q = [&](uint32_t w0_, uint32_t w1_) { return static_cast<float>(((hiWord ? w1_ : w0_) >> sh) & 0xffu); };
         const float tnx = fmaf(q(nX0, nX1), ax, bx), tny = fmaf(q(nY0, nY1), ay, by), tnz = fmaf(q(nZ0, nZ1), az, bz);
         const float tfx = fmaf(q(fX0, fX1), ax, bx), tfy = fmaf(q(fY0, fY1), ay, by), tfz = fmaf(q(fZ0, fZ1), az, bz);
-#if ARK_NODE_CMP3 && ARK_MASK_ADDC && !ARK_NODE_INSIDE
         const float tn = fmaxf(fmaxf(tnx, tny), tnz);
         const float lim = fmaf(fminf(fminf(tfx, tfy), tfz), 1.00001f, 1e-7f);
-        {
-            uint64_t c0, c1;
-            asm("v_cmp_le_f32_e64 %[c0], %[tn], %[lim]\n\t"
-                "v_cmp_le_f32_e64 %[c1], %[tn], %[lt]\n\t"
-                "s_and_b64 %[c0], %[c0], %[c1]\n\t"
-                "v_cmp_le_f32_e64 %[c1], %[tmin], %[lim]\n\t"
-                "s_and_b64 vcc, %[c0], %[c1]\n\t"
-                "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc"
-                : [acc] "+v"(hitSlots), [c0] "=&s"(c0), [c1] "=&s"(c1)
-                : [tn] "v"(tn), [lim] "v"(lim), [lt] "v"(limT), [tmin] "s"(tmin)
-                : "vcc");
-        }
-#else
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-        const float lim = fmaf(tf, 1.00001f, 1e-7f);
-#endif
-#if ARK_NODE_CMP3 && ARK_MASK_ADDC && !ARK_NODE_INSIDE
-#elif ARK_MASK_ADDC
-        hitSlots = shiftInLe(hitSlots, tn, lim);
-        if (ARK_NODE_INSIDE) insideLo = shiftInLe(insideLo, tn, tmin);
-#else
-        hitSlots |= (tn <= lim ? 1u : 0u) << s;
-        // origin inside the box: every near-plane distance <= tmin (bits 0-7 here:
-        // the select constants stay inline, no literal moves; shifted once below)
-        if (ARK_NODE_INSIDE) insideLo |= (tn <= tmin ? 1u : 0u) << s;
-#endif
+        uint64_t c0, c1;
+        asm("v_cmp_le_f32_e64 %[c0], %[tn], %[lim]\n\t"
+            "v_cmp_le_f32_e64 %[c1], %[tn], %[lt]\n\t"
+            "s_and_b64 %[c0], %[c0], %[c1]\n\t"
+            "v_cmp_le_f32_e64 %[c1], %[tmin], %[lim]\n\t"
+            "s_and_b64 vcc, %[c0], %[c1]\n\t"
+            "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc"
+            : [acc] "+v"(hitSlots), [c0] "=&s"(c0), [c1] "=&s"(c1)
+            : [tn] "v"(tn), [lim] "v"(lim), [lt] "v"(limT), [tmin] "s"(tmin)
+            : "vcc");
     }
-    // internal children: slot bits -> visiting order bits (k = slot ^ oct)
-#if ARK_NODE_INSIDE
-    // by swapping bit pairs / pairs of pairs / nibbles per octant bit (hit and
-    // inside masks permuted together: bits 0-7 and 16-23)
-    const uint32_t insideSlots = insideLo << 16;
-    uint32_t m = (hitSlots & imask) | (insideSlots & (hitSlots << 16) & (imask << 16));
-    m = fx ? (((m & 0x00550055u) << 1) | ((m >> 1) & 0x00550055u)) : m;
-    m = fy ? (((m & 0x00330033u) << 2) | ((m >> 2) & 0x00330033u)) : m;
-    m = fz ? (((m & 0x000f000fu) << 4) | ((m >> 4) & 0x000f000fu)) : m;
-#else
-    // one LDS byte (g_octPerm, filled by loadNodeCache) instead of the three
-    // conditional swap stages (15 VALU)
-    (void)insideLo;
+    // internal children: slot bits -> visiting order bits (k = slot ^ oct), one LDS byte
+    // (g_octPerm, filled by loadNodeCache) instead of three conditional swap stages
     const uint32_t m = g_octPerm[(oct << 8) | (hitSlots & imask & 0xffu)];
-#endif
-#endif // ARK_NODE_F16
     // leaf children: their triangle rows (GpuBvh8Node: bit s + stride i = triangle
     // i of leaf slot s), the hit leaf slots spread over the three rows and masked
     gBase = w1.x;
@@ -791,41 +518,6 @@ __device__ __forceinline__ bool travCompute(const Fetch& fx, TravState& ts, V3 o
     return false;
 }
 
-// Cache warming in the drain (ARK_TAIL_PREFETCH). After its queue is exhausted a wave
-// is latency-bound: each step waits for the node it picked at the previous step's end
-// (~1-2 us from L2 / HBM) with few co-resident waves to hide it. These loads fetch the
-// first children of the group the next steps will pop (the lane's current group, or
-// its stack top when that is empty), so the steps that reach them find the lines in
-// L2 / the vector cache. They are register-free (global_load_lds_dword into a
-// per-wave scratch line of LDS that nothing reads), so no VGPR stays bound to a load in
-// flight; vmcnt counts them, which can only make a later wait longer, never shorter
-// (loads return in order). Two dwords per node (its 80 B span at most two 128-B lines).
-// M0 (the LDS-DMA base, compiler-reserved) is saved and restored inside the statement;
-// the scratch line is kTailPfDwords dwords per wave, room for 64 lanes at either offset.
-[[maybe_unused]] constexpr uint32_t kTailPfDwords = 96;
-template<int BLOCK>
-__device__ __forceinline__ void tailPrefetch(const SceneArgs& sc, const TravState& ts, const Stack<BLOCK>& st, uint32_t oct, uint32_t ldsLine)
-{
-    uint32_t base = ts.gBase, bits = ts.gBits;
-    if ((bits & 0xffu) == 0 && st.depth > 0) {
-        const uint32_t* l = st.lds + ((st.depth - 1) & (kStackLds - 1)) * 2 * BLOCK;
-        base = l[0];
-        bits = l[BLOCK];
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        if (bits & 0xffu) {
-            const uint32_t c = nextChild(base, bits, oct);
-            const char* a = reinterpret_cast<const char*>(sc.nodes + c);
-            uint32_t keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
-                         "global_load_lds_dword %1, off offset:64\n\ts_mov_b32 m0, %0"
-                         : "=&s"(keep)
-                         : "v"(a), "s"(ldsLine));
-        }
-    }
-}
-
 // Dual step (k_trace): one lane tests a pending leaf triangle AND visits the next
 // node in the same iteration. A divergent wave runs the node and the triangle code
 // every iteration anyway (28 % of the steps are triangle steps, spread over its
@@ -916,7 +608,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
             const uint32_t inst = c.y, prim = c.z;
             if (ANY) anyHit = true;
             else if (!(h.tri != kNoHit && tt == h.t && (inst > h.inst || (inst == h.inst && prim > h.prim))) &&
-                !(ARK_PASS_IS(pass, 1) && !alphaAccept(sc, inst, prim, uu, vv))) {
+                !(pass == 1 && !alphaAccept(sc, inst, prim, uu, vv))) {
                 h.t = tt;
                 h.u = uu;
                 h.v = vv;
@@ -962,28 +654,11 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
 
 // Child s of slot byte B (word LO / HI of the plane pairs): crossed iff
 // qlo_u <= Fu, qhi_u >= Cu, qlo_v <= Fv, qhi_v >= Cv and qhi_w >= Cw - five SDWA byte
-// compares (unsigned byte vs a signed lane value), ANDed in an SGPR pair, the result
-// shifted into the lane's slot mask as v_addc's carry (m = 2m + hit).
-#define ARK_SUN_CHILD(LU, HU, LV, HV, HW, B)                                               \
-    "v_cmp_le_i32_sdwa %[m], %[" LU "], %[fu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"     \
-    "v_cmp_ge_i32_sdwa vcc, %[" HU "], %[cu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
-    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
-    "v_cmp_le_i32_sdwa vcc, %[" LV "], %[fv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
-    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
-    "v_cmp_ge_i32_sdwa vcc, %[" HV "], %[cv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
-    "s_and_b64 %[m], %[m], vcc\n\t"                                                        \
-    "v_cmp_ge_i32_sdwa vcc, %[" HW "], %[cw] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"      \
-    "s_and_b64 vcc, %[m], vcc\n\t"                                                         \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
-
-// ARK_SUN_PAR: the five compares of a child into four SGPR pairs and VCC first, then the
-// ANDs - two levels of VALU -> SALU dependence per child instead of four (the wave
-// otherwise stalls on every compare's lane mask before the next compare issues).
-// Measured (profiles/r04_j_*): K = 4096 windows 1,901 -> 1,924 Mrays/s, P = 8 slab
-// shadow 0.198 -> 0.184 ms, slab step 0.577 -> 0.569 ms, whole grid flat
-#ifndef ARK_SUN_PAR
-#define ARK_SUN_PAR 1
-#endif
+// compares (unsigned byte vs a signed lane value) into four SGPR pairs and VCC first,
+// then the ANDs - two levels of VALU -> SALU dependence per child instead of four (the
+// wave otherwise stalls on every compare's lane mask before the next compare issues;
+// profiles/r04_j_*: K = 4096 windows 1,901 -> 1,924 Mrays/s, P = 8 slab shadow 0.198 ->
+// 0.184 ms) - the result shifted into the lane's slot mask as v_addc's carry (m = 2m + hit).
 #define ARK_SUN_CHILD_PAR(LU, HU, LV, HV, HW, B)                                           \
     "v_cmp_le_i32_sdwa %[m0], %[" LU "], %[fu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
     "v_cmp_ge_i32_sdwa %[m1], %[" HU "], %[cu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
@@ -1017,7 +692,8 @@ __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4
     const int fv = static_cast<int>(floorf(qv)), cv = static_cast<int>(ceilf(qv));
     const int cw = static_cast<int>(ceilf(qw));
     uint32_t hit = 0;
-#if ARK_SUN_PAR
+    // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
+    // qhi w = w4.z|w (children 0-3 | 4-7); slots 7 .. 0 shifted in
     uint64_t m0, m1, m2, m3;
     asm(ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "3") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "2")
         ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "1") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "0")
@@ -1027,19 +703,6 @@ __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4
         : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
           [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
         : "vcc");
-#else
-    uint64_t m;
-    // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
-    // qhi w = w4.z|w (children 0-3 | 4-7); slots 7 .. 0 shifted in
-    asm(ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "3") ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "2")
-        ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "1") ARK_SUN_CHILD("lu1", "hu1", "lv1", "hv1", "hw1", "0")
-        ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "3") ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "2")
-        ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "1") ARK_SUN_CHILD("lu0", "hu0", "lv0", "hv0", "hw0", "0")
-        : [acc] "+v"(hit), [m] "=&s"(m)
-        : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
-          [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
-        : "vcc");
-#endif
     const uint32_t imask = w0.w >> 24;
     gBase = w1.x;
     gBits = (hit & imask) | (imask << 8);
@@ -1048,7 +711,7 @@ __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4
     const uint32_t x = (leafHits << stride) | leafHits;
     tBits = ((x << stride) | x) & w1.z;
 }
-#undef ARK_SUN_CHILD
+#undef ARK_SUN_CHILD_PAR
 
 // travStepDual for a sun shadow ray in the light-space BVH: both sides' loads issued
 // by every lane (a skipped side reads the resident record 0 / the root), the
@@ -1243,9 +906,6 @@ __device__ __forceinline__ void grabRays(const FrameArgs& f, uint32_t* heads, ui
 // ray finished are refilled at the top of the next iteration from a wave-private
 // pool of consecutive ray indices (ballot + mbcnt rank, one atomic per 64 rays), so
 // the SIMD stays full until the global ray counter runs out.
-#ifdef ARK_TAIL_PROBE
-__device__ unsigned long long g_tail[2][32768][6];
-#endif
 
 // Ray sources of the closest-hit traversal. ProbeRays: the window's probe rays from
 // the slot table (raygen.rgen:35-92: opaque pass then masked pass, tmin 1e-4, tmax
@@ -1293,20 +953,10 @@ template<bool COUNT, int WPE, class Src = ProbeRays>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace(SceneArgs sc, FrameArgs f)
 {
     if (frameAborted(f.abort_word)) return;
-#ifdef ARK_TAIL_PROBE
-    const unsigned long long tStart = wall_clock64();
-    unsigned long long tEx = 0, itAll = 0, itEx = 0;
-#endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
-    constexpr bool kGF = ARK_TRACE_FETCH_GLOBAL != 0;
-    __shared__ uint4 ldsNodes[(kGF ? 1 : kLdsNodes) * 5];
-    const NodeCache nc = loadNodeCache<kTraceBlock, kGF ? 0 : kLdsNodes>(sc, ldsNodes);
-#if ARK_TAIL_PREFETCH
-    // the wave's LDS-DMA scratch line (tailPrefetch): written, never read
-    __shared__ uint32_t ldsPf[(kTraceBlock / 64) * kTailPfDwords];
-    const uint32_t pfLine = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ldsPf + (threadIdx.x >> 6) * kTailPfDwords)));
-#endif
+    // nodes from global memory only (GF dual steps): no LDS node cache, the octant table
+    __shared__ uint4 ldsNodes[5];
+    const NodeCache nc = loadNodeCache<kTraceBlock, 0>(sc, ldsNodes);
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     const uint32_t nthreads = gridDim.x * kTraceBlock;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, nthreads, 0 };
@@ -1320,9 +970,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     bool exhausted = false;
     bool active = false;
     uint32_t ray = 0;
-    // bit 0: the pass (0 opaque, 1 masked); bits 1+: the ray's age in steps
-    // (ARK_LONG_RAY_STEPS)
-    int pass = 0;
+    int pass = 0; // 0 opaque, 1 masked
     TravState ts { 0u, 0u, 0u, 0u };
     uint32_t nBase = 0, nBits = 0; // the next triangle group (dual step)
     uint32_t oct = 0;
@@ -1380,39 +1028,20 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             cIter++;
             rSteps += active ? 1u : 0u;
         }
-#ifdef ARK_TAIL_PROBE
-        itAll++;
-        if (exhausted) { if (!tEx) tEx = wall_clock64(); itEx++; }
-#endif
         // ---- one step: a pending leaf triangle and the next node -------------------
         // (an active lane is never done here: the check after the step retires or
         // restarts it, and a step of a done lane would change nothing anyway)
-#if ARK_LONG_RAY_STEPS
-        // Long rays set a small window's launch time (its longest ray's steps times the
-        // step latency, which grows with the waves sharing the SIMD): a wave holding a
-        // ray past ARK_LONG_RAY_STEPS steps is issued first
-        if (__ballot(active && pass >= 2 * ARK_LONG_RAY_STEPS)) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
-        if (active) pass += 2;
-#endif
-        if (active) travStepDual<kTraceBlock, false, kGF>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
-#if ARK_TAIL_PREFETCH
-        if (exhausted && active) tailPrefetch<kTraceBlock>(sc, ts, st, oct, pfLine);
-#endif
+        if (active) travStepDual<kTraceBlock, false, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
         if (active && done()) {
             bool finished = true;
-            if (Src::kMaskedPass && ARK_PASS_IS(pass, 0)) {
+            if (Src::kMaskedPass && pass == 0) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
                 // cullMask 0x02, tmax = previous hit T (:64-92); a negative tmax
                 // (backface) is an empty interval.
                 opaqueT = (h.tri != kNoHit) ? (h.backface ? -h.t : h.t) : f.z_far;
                 if (sc.root_masked >= 0 && opaqueT >= tmin) {
-#if ARK_LONG_RAY_STEPS
-                    pass |= 1;
-#else
                     pass = 1;
-#endif
                     finished = false;
                     ts = TravState { static_cast<uint32_t>(sc.root_masked), rootGroupBits(), 0u, 0u };
                     st.depth = 0;
@@ -1423,7 +1052,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
             if (finished) {
                 GpuHit out;
-                if (ARK_PASS_IS(pass, 1) && h.tri == kNoHit) {
+                if (pass == 1 && h.tri == kNoHit) {
                     // masked pass found nothing: the opaque result (already stored) stands
                     out = f.hits[ray];
                     if (COUNT && out.tri != kNoHit) cHits++;
@@ -1447,19 +1076,6 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
             }
         }
     }
-#if ARK_TAIL_PREFETCH
-    // no LDS-DMA of tailPrefetch may land after the workgroup's LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#ifdef ARK_TAIL_PROBE
-    {
-        const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
-        if (lane == 0 && w < 32768) {
-            unsigned long long* r = g_tail[0][w];
-            r[0] = tStart; r[1] = tEx; r[2] = wall_clock64(); r[3] = itAll; r[4] = itEx; r[5] = 0;
-        }
-    }
-#endif
     if (COUNT) {
         atomicAdd(&f.counters[0], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[1], static_cast<unsigned long long>(cTris));
@@ -1614,10 +1230,11 @@ __device__ __forceinline__ void atlasFilter(const AtlasTap<CH>& t, float* out)
     }
 }
 
-// probeSampling.glsl:64-163. The 8 cage probes are gathered in three waves of loads
-// (visibility of all 8, then irradiance of probes 0-3 and 4-7) instead of one
-// dependent round trip per probe; every weight and sum is the same IEEE sequence
-// as the per-probe loop, and the irradiance sums still run in probe order.
+// probeSampling.glsl:64-163. The 8 cage probes in groups of GB whose visibility and
+// irradiance taps are issued together before their weights are formed; every weight
+// and sum is the same IEEE sequence as the per-probe loop, and the irradiance sums run
+// in probe order. GB = 1 (kGatherBatch): 2 and 4 measured no faster on C4.
+constexpr int kGatherBatch = 1;
 template<int GB>
 __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 {
@@ -1740,9 +1357,6 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
     *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
 }
 
-#ifndef ARK_SHADE_SPOTS_LDS
-#define ARK_SHADE_SPOTS_LDS 0
-#endif
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
@@ -1750,9 +1364,9 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
     __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
     uint32_t cFront = 0;
-#if ARK_SHADE_SPOTS_LDS
     // the spot lights, read once per workgroup: per front hit and lit spot they were a
-    // dependent 96-B read ahead of the IES lookup (C5: 4 spots)
+    // dependent 96-B read ahead of the IES lookup (C5: k_shade 2.06 -> 1.97 ms, +1.2 %;
+    // profiles/r04_s_shade_spots_lds.log)
     __shared__ GpuSpotLight spotsL[kMaxLights - 1];
     {
         const uint32_t words = static_cast<uint32_t>(sc.spot_count) * static_cast<uint32_t>(sizeof(GpuSpotLight) / 4u);
@@ -1760,7 +1374,6 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             reinterpret_cast<uint32_t*>(spotsL)[i] = reinterpret_cast<const uint32_t*>(sc.spots)[i];
         __syncthreads();
     }
-#endif
 
     // chunks come from the second set of per-XCD partition heads (see grabRays)
     uint32_t* heads = f.ray_counter + kRayParts * kRayCounterStride;
@@ -1848,11 +1461,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                     l++;
                 }
                 for (int li = 0; li < sc.spot_count; ++li, ++l) {
-#if ARK_SHADE_SPOTS_LDS
                     const V3 Ld = -normalize(v3(spotsL[li].direction[0], spotsL[li].direction[1], spotsL[li].direction[2]));
-#else
-                    const V3 Ld = -normalize(v3(sc.spots[li].direction[0], sc.spots[li].direction[1], sc.spots[li].direction[2]));
-#endif
                     if (dot(Ld, N) > 0.0f) need |= 1u << l;
                 }
             }
@@ -1876,11 +1485,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             }
             for (int li = 0; li < sc.spot_count; ++li, ++l) { // opaque.rchit:75-103
                 if (!((need >> l) & 1u)) continue;
-#if ARK_SHADE_SPOTS_LDS
                 const GpuSpotLight sl = spotsL[li];
-#else
-                const GpuSpotLight sl = sc.spots[li];
-#endif
                 V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
                 V3 Ld = -normalize(sdir);
                 float LdotN = dot(Ld, N);
@@ -1912,7 +1517,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const V3 Vi = -dir;
             const V3 F0 = mix3(splat(kDielectricReflectance), baseColor, metallic);
             const V3 F = F_Schlick3(fmaxf_(0.0f, dot(Vi, N)), F0);
-            const V3 irradiance = sampleDDGI<ARK_DDGI_GATHER_BATCH>(f, hitPoint, N, Vi);
+            const V3 irradiance = sampleDDGI<kGatherBatch>(f, hitPoint, N, Vi);
             const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
             storeSurfel(f, ray, color + bi, T);
@@ -2014,11 +1619,7 @@ constexpr int kShadowWorld = 0, kShadowSun = 1, kShadowSunWorld = 2;
 
 template<bool COUNT, bool SUN>
 __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs& f, const NodeCache& nc, Stack<kTraceBlock>& st, const TailLds& tl,
-                                            uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow
-#ifdef ARK_TAIL_PROBE
-                                            , unsigned long long* tp
-#endif
-)
+                                            uint32_t& cNodes, uint32_t& cTris, uint32_t& cShadow)
 {
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     if (lane < 16u) tl.bytes[(wbase >> 2) + lane] = 0u; // wave-private tail bytes
@@ -2093,10 +1694,6 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
             }
         }
         if (__ballot(active) == 0) break;
-#ifdef ARK_TAIL_PROBE
-        tp[1]++;
-        if (exhausted) { if (!tp[0]) tp[0] = wall_clock64(); tp[2]++; }
-#endif
         if (exhausted) {
             // ---- tail: resolved rays stop, idle lanes take stack bottoms --------------
             const uint32_t root = pass >= 256 ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
@@ -2141,7 +1738,7 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
                 occluded = travStepSun<kTraceBlock>(sc, ts, nBase, nBits, st, o, d, idir, tmin, tmax, cNodes, cTris);
             } else {
                 RayHit h { tmax, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
-                occluded = travStepDual<kTraceBlock, true, ARK_SHADOW_FETCH_GLOBAL != 0>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
+                occluded = travStepDual<kTraceBlock, true, false>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, 0, cNodes, cTris);
             }
             const bool helper = pass >= 256;
             const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
@@ -2176,14 +1773,10 @@ template<bool COUNT, int WPE, int MODE = kShadowWorld>
 __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace_shadow(SceneArgs sc, FrameArgs f)
 {
     if (frameAborted(f.abort_word)) return;
-#ifdef ARK_TAIL_PROBE
-    const unsigned long long tStart = wall_clock64();
-    unsigned long long tp[3] = { 0, 0, 0 }; // first exhausted clock, iterations, exhausted iterations
-#endif
     __shared__ uint32_t ldsStack[kStackLds * 2 * kTraceBlock];
     // 8 cached nodes fewer than k_trace: the tail tables then fit 6 workgroups per CU
     // (the light-space traversal caches none)
-    constexpr int kNodes = MODE == kShadowSun ? 1 : ARK_SHADOW_LDS_NODES;
+    constexpr int kNodes = MODE == kShadowSun ? 1 : kShadowLdsNodes;
     __shared__ uint4 ldsNodes[kNodes * 5];
     __shared__ uint8_t ldsTable[kTraceBlock];
     __shared__ uint32_t ldsBytes[kTraceBlock / 4];
@@ -2194,24 +1787,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     const uint32_t gtid = blockIdx.x * kTraceBlock + threadIdx.x;
     Stack<kTraceBlock> st { ldsStack + threadIdx.x, f.spill + gtid, gridDim.x * kTraceBlock, 0 };
     uint32_t cNodes = 0, cTris = 0, cShadow = 0;
-#ifdef ARK_TAIL_PROBE
-#define ARK_TP , tp
-#else
-#define ARK_TP
-#endif
-    if constexpr (MODE != kShadowWorld) shadowPhase<COUNT, true>(sc, f, nc, st, tl, cNodes, cTris, cShadow ARK_TP);
-    if constexpr (MODE != kShadowSun) shadowPhase<COUNT, false>(sc, f, nc, st, tl, cNodes, cTris, cShadow ARK_TP);
-#undef ARK_TP
-#ifdef ARK_TAIL_PROBE
-    {
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t w = blockIdx.x * (kTraceBlock / 64) + (threadIdx.x >> 6);
-        if (lane == 0 && w < 32768) {
-            unsigned long long* r = g_tail[1][w];
-            r[0] = tStart; r[1] = tp[0]; r[2] = wall_clock64(); r[3] = tp[1]; r[4] = tp[2]; r[5] = 0;
-        }
-    }
-#endif
+    if constexpr (MODE != kShadowWorld) shadowPhase<COUNT, true>(sc, f, nc, st, tl, cNodes, cTris, cShadow);
+    if constexpr (MODE != kShadowSun) shadowPhase<COUNT, false>(sc, f, nc, st, tl, cNodes, cTris, cShadow);
     if (COUNT) {
         atomicAdd(&f.counters[4], static_cast<unsigned long long>(cNodes));
         atomicAdd(&f.counters[5], static_cast<unsigned long long>(cTris));
@@ -2230,14 +1807,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 // per block reserves the block's shadow rays (a per-wave atomic on the one list
 // counter serialises at L2: 1.45 ms for 131K waves on C4); pass 2 writes them in
 // position order (wave scans), so a shadow-kernel grab of 64 list entries holds the
-// neighbouring rays of one probe.
-#ifndef ARK_GEN_STEPS
-#define ARK_GEN_STEPS 4 // queue positions per block = 256 x this (16: 0.185 ms, 4: 0.163, 2: 0.215 at C4)
-#endif
-constexpr uint32_t kGenSteps = ARK_GEN_STEPS, kGenSpan = kGenSteps * 256u;
-#ifndef ARK_GEN_V2
-#define ARK_GEN_V2 0
-#endif
+// neighbouring rays of one probe. kGenSteps = 4 (16: 0.185 ms, 4: 0.163, 2: 0.215 at
+// C4). Measured and removed: the list binned by light-space cell (-15 %
+// shadow HBM, +34 % shadow phase) and a straight-line staged form (179 VGPRs, 0.416 ms).
+constexpr uint32_t kGenSteps = 4, kGenSpan = kGenSteps * 256u;
 
 __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 {
@@ -2254,68 +1827,6 @@ __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 // list index, and the closest hit shades back faces too, with the normal flipped
 // (opaque.rchit:121-125): N = -(shading normal), as negation commutes exactly with
 // the normal matrix product and the normalisation.
-#ifndef ARK_BIN_STRIDE
-#define ARK_BIN_STRIDE 32
-#endif
-// u32 words between two bin counters: each counter on its own 128-B line, so the
-// device-scope atomics of k_shadow_gen (which bypass the per-XCD L2s) do not queue
-// on a few shared lines (C4, G = 64, counters packed: shadow phase 0.75 -> 1.74 ms)
-constexpr uint32_t kBinStride = ARK_BIN_STRIDE;
-
-// 2-D Morton code of a cell (x, y < 256)
-__device__ __forceinline__ uint32_t morton2(uint32_t x, uint32_t y)
-{
-    auto spread = [](uint32_t v) {
-        v = (v | (v << 4)) & 0x0f0fu;
-        v = (v | (v << 2)) & 0x3333u;
-        return (v | (v << 1)) & 0x5555u;
-    };
-    return spread(x) | (spread(y) << 1);
-}
-
-// Light-space bin of shadow ray (light l, origin X): see FrameArgs::shadow_bin_grid.
-__device__ __forceinline__ uint32_t shadowBinKey(const SceneArgs& sc, const FrameArgs& f, uint32_t l, V3 X)
-{
-    const uint32_t G = f.shadow_bin_grid;
-    const float gmax = static_cast<float>(G) - 0.5f;
-    float cu, cv;
-    if (sc.has_sun && l == 0) {
-        cu = X.x * f.sun_bin_axes[0][0] + X.y * f.sun_bin_axes[0][1] + X.z * f.sun_bin_axes[0][2] + f.sun_bin_axes[0][3];
-        cv = X.x * f.sun_bin_axes[1][0] + X.y * f.sun_bin_axes[1][1] + X.z * f.sun_bin_axes[1][2] + f.sun_bin_axes[1][3];
-    } else {
-        const GpuSpotLight& sl = sc.spots[l - (sc.has_sun ? 1u : 0u)];
-        float ox, oy;
-        octahedralEncode(normalize(X - v3(sl.position[0], sl.position[1], sl.position[2])), &ox, &oy);
-        cu = (ox * 0.5f + 0.5f) * static_cast<float>(G);
-        cv = (oy * 0.5f + 0.5f) * static_cast<float>(G);
-    }
-    // NaN (a degenerate origin) lands in cell 0
-    const uint32_t x = static_cast<uint32_t>(fminf(fmaxf(cu, 0.0f), gmax)), y = static_cast<uint32_t>(fminf(fmaxf(cv, 0.0f), gmax));
-    return l * G * G + morton2(x, y);
-}
-
-#if ARK_GEN_V2
-// shadowBinKey with the spot's position already read (P; unused for the sun)
-__device__ __forceinline__ uint32_t shadowBinKeyAt(const SceneArgs& sc, const FrameArgs& f, uint32_t l, V3 X, V3 P)
-{
-    const uint32_t G = f.shadow_bin_grid;
-    const float gmax = static_cast<float>(G) - 0.5f;
-    float cu, cv;
-    if (sc.has_sun && l == 0) {
-        cu = X.x * f.sun_bin_axes[0][0] + X.y * f.sun_bin_axes[0][1] + X.z * f.sun_bin_axes[0][2] + f.sun_bin_axes[0][3];
-        cv = X.x * f.sun_bin_axes[1][0] + X.y * f.sun_bin_axes[1][1] + X.z * f.sun_bin_axes[1][2] + f.sun_bin_axes[1][3];
-    } else {
-        float ox, oy;
-        octahedralEncode(normalize(X - P), &ox, &oy);
-        cu = (ox * 0.5f + 0.5f) * static_cast<float>(G);
-        cv = (oy * 0.5f + 0.5f) * static_cast<float>(G);
-    }
-    // NaN (a degenerate origin) lands in cell 0
-    const uint32_t x = static_cast<uint32_t>(fminf(fmaxf(cu, 0.0f), gmax)), y = static_cast<uint32_t>(fminf(fmaxf(cv, 0.0f), gmax));
-    return l * G * G + morton2(x, y);
-}
-#endif
-
 template<bool REFL = false>
 __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
 {
@@ -2323,34 +1834,6 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     __shared__ uint32_t bitsL[kGenSpan];
     __shared__ uint32_t waveOff[kGenSteps][4];
     __shared__ uint32_t blockBase, sunBlockBase;
-#if ARK_GEN_V2
-    // the lit test direction -normalize(direction) of light l (litLightMask) and its
-    // position (shadowRayOf), read once per workgroup: per ray they were dependent reads
-    __shared__ float4 lightDirL[kMaxLights], lightPosL[kMaxLights];
-    const uint32_t nSun = sc.has_sun ? 1u : 0u, nLights = nSun + static_cast<uint32_t>(sc.spot_count);
-    if (threadIdx.x < nLights) {
-        const uint32_t l = threadIdx.x;
-        V3 Ld, P = splat(0.0f);
-        if (l < nSun) {
-            Ld = -normalize(v3(sc.sun_dir[0], sc.sun_dir[1], sc.sun_dir[2]));
-        } else {
-            const GpuSpotLight& sl = sc.spots[l - nSun];
-            Ld = -normalize(v3(sl.direction[0], sl.direction[1], sl.direction[2]));
-            P = v3(sl.position[0], sl.position[1], sl.position[2]);
-        }
-        lightDirL[l] = make_float4(Ld.x, Ld.y, Ld.z, 0.0f);
-        lightPosL[l] = make_float4(P.x, P.y, P.z, 0.0f);
-    }
-    __syncthreads();
-    auto litMaskL = [&](V3 N) {
-        uint32_t need = 0;
-        for (uint32_t l = 0; l < nLights; ++l) {
-            const float4 d = lightDirL[l];
-            if (dot(v3(d.x, d.y, d.z), N) > 0.0f) need |= 1u << l;
-        }
-        return need;
-    };
-#endif
     // the sun's rays (light 0) to their own list when the scene has a light-space BVH
     const bool splitSun = !REFL && f.sun_rays != nullptr;
     const uint32_t total = REFL ? *f.list_count : f.window_rays;
@@ -2361,72 +1844,6 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
     // dependent loads (slot order -> hit -> triangle normals -> instance) are in
     // flight for all of them at once (the kernel is latency bound)
     uint32_t rays[kGenSteps];
-#if ARK_GEN_V2
-    // probe rays in four stages, each stage's reads issued for all kGenSteps rays of
-    // the thread before any is waited for (straight-line code, clamped indices: a
-    // position past the window or a ray without a front hit reads index 0 and is
-    // dropped): slot -> hit + slot record + direction -> shading record -> instance.
-    // The hit point is formed here, so pass 2 reads nothing per ray.
-    V3 hitPt[kGenSteps];
-    if (!REFL) {
-        uint32_t slotv[kGenSteps];
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            const uint32_t pos = first + k * 256u + threadIdx.x;
-            slotv[k] = slotAt(f, pos < total ? pos / f.R : 0u);
-        }
-        float4 hv[kGenSteps], sp[kGenSteps], sa[kGenSteps], fbv[kGenSteps];
-        float sc_[kGenSteps];
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            const uint32_t pos = first + k * 256u + threadIdx.x;
-            const bool valid = pos < total;
-            const uint32_t q = pos / f.R, sample = valid ? pos - q * f.R : 0u;
-            const uint32_t ray = valid ? slotv[k] * f.R + sample : 0u;
-            rays[k] = valid ? ray : kNoHit;
-            hv[k] = *reinterpret_cast<const float4*>(f.hits + ray);
-            const GpuProbeSlot* ps = f.slots + (valid ? slotv[k] : 0u);
-            sp[k] = *reinterpret_cast<const float4*>(ps->pos);
-            sa[k] = *reinterpret_cast<const float4*>(ps->axis); // axis xyz + angle_sin
-            sc_[k] = ps->angle_cos;
-            fbv[k] = f.fib[sample];
-        }
-        float4 ta[kGenSteps], tb[kGenSteps], tc[kGenSteps];
-        bool front[kGenSteps];
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            const uint32_t tri = __float_as_uint(hv[k].w);
-            front[k] = rays[k] != kNoHit && tri != kNoHit && !(hv[k].x < 0.0f); // backface: no shading, no shadow ray
-            const float4* tn = sc.tri_normals + 4u * static_cast<size_t>(front[k] ? tri : 0u);
-            ta[k] = tn[0];
-            tb[k] = tn[1];
-            tc[k] = tn[2];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            const V3 dir = rotate(v3(fbv[k].x, fbv[k].y, fbv[k].z), v3(sa[k].x, sa[k].y, sa[k].z), sa[k].w, sc_[k]);
-            hitPt[k] = v3(sp[k].x, sp[k].y, sp[k].z) + hv[k].x * dir;
-        }
-        float4 m0[kGenSteps], m1[kGenSteps], m2[kGenSteps];
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            const float4* M = reinterpret_cast<const float4*>(sc.instances[__float_as_uint(tc[k].y)].normal_matrix);
-            m0[k] = M[0];
-            m1[k] = M[1];
-            m2[k] = M[2];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kGenSteps; ++k) {
-            uint32_t bits = 0;
-            if (front[k]) {
-                bits = litMaskL(shadingNormalOf(ta[k], tb[k], tc[k], m0[k], m1[k], m2[k], hv[k].y, hv[k].z));
-                f.shadow_bits[rays[k]] = bits;
-            }
-            bitsL[k * 256u + threadIdx.x] = bits;
-        }
-    } else
-#endif
-    {
     GpuHit hits[kGenSteps];
 #pragma unroll
     for (uint32_t k = 0; k < kGenSteps; ++k) {
@@ -2454,7 +1871,6 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         }
         bitsL[k * 256u + threadIdx.x] = bits;
     }
-    }
     // counts packed: world-list rays in bits 0-15, sun-list rays in bits 16-31 (a
     // block has at most kGenSpan x kMaxLights = 11,264 of either, no carry)
     auto packedCount = [&](uint32_t bits) {
@@ -2479,9 +1895,6 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         sunBlockBase = (run >> 16) ? atomicAdd(f.sun_count, run >> 16) : 0u;
     }
     __syncthreads();
-#if ARK_GEN_V2
-#pragma unroll
-#endif
     for (uint32_t k = 0; k < kGenSteps; ++k) {
         const uint32_t bits = bitsL[k * 256u + threadIdx.x];
         const uint32_t c = packedCount(bits);
@@ -2499,93 +1912,23 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             const float t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
             hitPoint = origin + t * dir;
         } else {
-#if ARK_GEN_V2
-            ray = rays[k];
-            hitPoint = hitPt[k];
-#else
             const uint32_t q = pos / f.R;
             ray = slotAt(f, q) * f.R + (pos - q * f.R);
             const float t = f.hits[ray].t;
             V3 origin, dir;
             rayOf(f, ray, &origin, &dir);
             hitPoint = origin + t * dir;
-#endif
         }
-        const bool binned = !REFL && f.shadow_bin_grid != 0;
         for (uint32_t b = bits; b; b &= b - 1) {
             const uint32_t l = static_cast<uint32_t>(__builtin_ctz(b));
             V3 ld;
             float tmax;
-#if ARK_GEN_V2
-            if (l < nSun) { // shadowRayOf from the staged light
-                const float4 d = lightDirL[0];
-                ld = v3(d.x, d.y, d.z);
-                tmax = 2.0f * f.z_far;
-            } else {
-                const float4 P = lightPosL[l];
-                const V3 toLight = v3(P.x, P.y, P.z) - hitPoint;
-                const float distanceToLight = length(toLight);
-                ld = toLight / distanceToLight;
-                tmax = distanceToLight - 0.001f;
-            }
-#else
             shadowRayOf(sc, f.z_far, l, hitPoint, &ld, &tmax);
-#endif
             const ShadowRay sr { make_float4(hitPoint.x, hitPoint.y, hitPoint.z, tmax), make_float4(ld.x, ld.y, ld.z, __uint_as_float((ray << 4) | l)) };
-            if (splitSun && l == 0u) {
-                f.sun_rays[sunj++] = sr;
-            } else if (binned) {
-#if ARK_GEN_V2
-                const float4 P = lightPosL[l];
-                const uint32_t key = shadowBinKeyAt(sc, f, l, hitPoint, v3(P.x, P.y, P.z));
-#else
-                const uint32_t key = shadowBinKey(sc, f, l, hitPoint);
-#endif
-                f.shadow_bin_key[sj] = key;
-                f.shadow_bin_rank[sj] = atomicAdd(f.shadow_bin_count + key * kBinStride, 1u);
-                f.shadow_rays_gen[sj++] = sr;
-            } else {
-                f.shadow_rays[sj++] = sr;
-            }
+            if (splitSun && l == 0u) f.sun_rays[sunj++] = sr;
+            else f.shadow_rays[sj++] = sr;
         }
     }
-}
-
-// Exclusive scan of the shadow-ray bin counts into bin starts, one workgroup of 1,024
-// threads (each a contiguous run of bins); the counts are zeroed for the next frame.
-constexpr uint32_t kBinScanBlock = 1024;
-__global__ void __launch_bounds__(kBinScanBlock) k_shadow_bin_scan(FrameArgs f)
-{
-    if (frameAborted(f.abort_word)) return;
-    __shared__ uint32_t waveSum[kBinScanBlock / 64];
-    const uint32_t bins = f.light_count * f.shadow_bin_grid * f.shadow_bin_grid;
-    const uint32_t per = (bins + kBinScanBlock - 1u) / kBinScanBlock;
-    const uint32_t b0 = min(bins, threadIdx.x * per), b1 = min(bins, b0 + per);
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += f.shadow_bin_count[b * kBinStride];
-    const uint32_t inc = waveInclusiveScan(sum);
-    const uint32_t wave = threadIdx.x >> 6;
-    if (__lane_id() == 63u) waveSum[wave] = inc;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < wave; ++w) base += waveSum[w];
-    uint32_t run = base + inc - sum;
-    for (uint32_t b = b0; b < b1; ++b) {
-        const uint32_t c = f.shadow_bin_count[b * kBinStride];
-        f.shadow_bin_start[b] = run;
-        f.shadow_bin_count[b * kBinStride] = 0u;
-        run += c;
-    }
-}
-
-// The shadow-ray list in bin order: entry i of k_shadow_gen's list goes to its bin's
-// start + its rank (grid-stride over the device-side count).
-__global__ void __launch_bounds__(256) k_shadow_scatter(FrameArgs f)
-{
-    if (frameAborted(f.abort_word)) return;
-    const uint32_t total = *f.shadow_count;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u)
-        f.shadow_rays[f.shadow_bin_start[f.shadow_bin_key[i]] + f.shadow_bin_rank[i]] = f.shadow_rays_gen[i];
 }
 
 // Frame sequencing between a context's two streams (ark_ddgi.cpp updateImpl): the
@@ -2919,15 +2262,10 @@ hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s)
 // Dual-step traversal at 6 waves/SIMD (80 VGPRs): the only spills (4 VGPRs) sit in
 // the masked pass's alpha test. C4: 2.39 ms, against 2.51 at 5 waves (96 VGPRs, no
 // spill) and 2.65 for one step per iteration at 6 waves.
-#ifndef ARK_TRACE_WPE
-#define ARK_TRACE_WPE 6
-#endif
-#ifndef ARK_SHADOW_WPE
-#define ARK_SHADOW_WPE 6
-#endif
+constexpr int kTraceWpe = 6, kShadowWpe = 6;
 const void* kernel_trace_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, ARK_TRACE_WPE>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace<false, kTraceWpe>);
 }
 
 hipError_t launch_trace(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
@@ -2953,16 +2291,14 @@ static uint32_t persistentBlocks(const void* fn, int block, uint32_t fallback)
 // One-pass shading at <= 128 VGPRs, 4 waves/SIMD, no spill (round 1: 0.57 -> 0.50 ms
 // at C4 against the compiler's 133 VGPRs, 3 waves). Round 3: 5 waves (96 VGPRs)
 // spills 30 and shades in 0.525 instead of 0.469 ms (profiles/r03_ak).
-#ifndef ARK_SHADE_WPE
-#define ARK_SHADE_WPE 4
-#endif
+constexpr int kShadeWpe = 4;
 hipError_t launch_shade(const SceneArgs& sc, const FrameArgs& f, uint32_t blocks, bool count, hipStream_t s)
 {
     if (count) {
         hipLaunchKernelGGL((dev::k_shade<true, 1>), dim3(blocks), dim3(kShadeBlock), 0, s, sc, f);
     } else {
-        const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, ARK_SHADE_WPE>);
-        hipLaunchKernelGGL((dev::k_shade<false, ARK_SHADE_WPE>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
+        const void* fn = reinterpret_cast<const void*>(&dev::k_shade<false, kShadeWpe>);
+        hipLaunchKernelGGL((dev::k_shade<false, kShadeWpe>), dim3(persistentBlocks(fn, kShadeBlock, blocks)), dim3(kShadeBlock), 0, s, sc, f);
     }
     return hipGetLastError();
 }
@@ -2976,10 +2312,10 @@ hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t
     const void* fn = kernel_trace_shadow_ptr(count);
     if (f.sun_rays && f.light_count <= 1u)
         fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, dev::kShadowSun>)
-                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, dev::kShadowSun>);
+                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, kShadowWpe, dev::kShadowSun>);
     else if (f.sun_rays)
         fn = count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1, dev::kShadowSunWorld>)
-                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE, dev::kShadowSunWorld>);
+                   : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, kShadowWpe, dev::kShadowSunWorld>);
     return hipLaunchKernel(fn, dim3(blocks), dim3(kTraceBlock), args, 0, s);
 }
 
@@ -2988,13 +2324,6 @@ hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_
     const uint32_t blocks = (f.window_rays + dev::kGenSpan - 1u) / dev::kGenSpan;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(dev::k_shadow_gen<false>, dim3(blocks), dim3(256), 0, s, sc, f);
-    if (f.shadow_bin_grid != 0) {
-        hipLaunchKernelGGL(dev::k_shadow_bin_scan, dim3(1), dim3(dev::kBinScanBlock), 0, s, f);
-        // at most one shadow ray per window ray and light; a few waves per CU
-        const uint64_t worst = static_cast<uint64_t>(f.window_rays) * f.light_count;
-        const uint32_t sblocks = static_cast<uint32_t>(std::min<uint64_t>((worst + 255u) / 256u, 2048u));
-        hipLaunchKernelGGL(dev::k_shadow_scatter, dim3(sblocks), dim3(256), 0, s, f);
-    }
     return hipGetLastError();
 }
 
@@ -3021,12 +2350,12 @@ hipError_t launch_fill_u32(void* p, uint64_t count, uint32_t value, hipStream_t 
 
 const void* kernel_shade_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, ARK_SHADE_WPE>);
+    return count ? reinterpret_cast<const void*>(&dev::k_shade<true, 1>) : reinterpret_cast<const void*>(&dev::k_shade<false, kShadeWpe>);
 }
 
 const void* kernel_trace_shadow_ptr(bool count)
 {
-    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, ARK_SHADOW_WPE>);
+    return count ? reinterpret_cast<const void*>(&dev::k_trace_shadow<true, 1>) : reinterpret_cast<const void*>(&dev::k_trace_shadow<false, kShadowWpe>);
 }
 
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s)
@@ -3074,9 +2403,3 @@ hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, 
 
 } // namespace ark
 
-#ifdef ARK_TAIL_PROBE
-extern "C" __attribute__((visibility("default"))) int ark_debug_tail(unsigned long long* out, size_t bytes)
-{
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(ark::dev::g_tail), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -382,142 +382,13 @@ __host__ __device__ __forceinline__ uint32_t offsetProbesPerBlock(uint32_t R)
     return p < 1u ? 1u : (p > 32u ? 32u : p);
 }
 
-#ifndef ARK_OFFSETS_V2
-#define ARK_OFFSETS_V2 0
-#endif
-#ifndef ARK_OFFSETS_WG_PER_CU
-#define ARK_OFFSETS_WG_PER_CU 8
-#endif
 
 // LDS bytes of one workgroup
 __host__ __device__ __forceinline__ size_t offsetLdsBytes(uint32_t P, uint32_t R)
 {
-#if ARK_OFFSETS_V2
-    return sizeof(float) * static_cast<size_t>(P) * (4u * R + 4u);
-#else
     return sizeof(float) * (static_cast<size_t>(P) * (6u * R + 8u) + 6u * P) + sizeof(uint32_t) * 2u * P;
-#endif
 }
 
-#if ARK_OFFSETS_V2
-// Same sums, same order. A persistent grid (a few workgroups per CU, the launcher's
-// grid) walks the groups of P probes: with one short workgroup per group the kernel
-// ran at ~1 TB/s with a handful of waves resident per CU (SQ counters, r04_final).
-// Per group: every load - hits, directions, the rays' slots - is issued together
-// (straight-line, so no read sinks into a branch), the next group's while this
-// group is summed; each ray stages (rotated direction, class) in LDS, 16 B. Sums:
-// lane 8q + c (c < 6) of probe q adds component c % 3 of the class-(1 + c / 3) rays
-// in ray order (`m ? v : 0`, the shader's loop), counting that class as it goes;
-// lanes 8q + 1..5 pass their sums to lane 8q by cross-lane reads (the 8 lanes of a
-// probe are in one wave), which blends the offset (probe index and current offset
-// read before the sums).
-__global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
-{
-    if (frameAborted(f.abort_word)) return;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t R = f.R;
-    const uint32_t P = offsetProbesPerBlock(R);
-    const uint32_t groups = (f.window_probes + P - 1u) / P;
-    const uint32_t pstride = 4u * R + 4u; // floats per probe: +4 puts the probes' rows on different LDS banks
-    float* recL = reinterpret_cast<float*>(smem); // [P][R] (d.x, d.y, d.z, class)
-    const uint32_t tid = threadIdx.x;
-    const float minAxialSpacing = fminf_(f.spacing[0], fminf_(f.spacing[1], f.spacing[2]));
-    const float maxOffset = minAxialSpacing / 2.0f;
-    // sum / blend lane of probe q = tid / 8
-    const uint32_t q = tid >> 3, c = tid & 7u;
-    // P * R <= 1,024 (offsetProbesPerBlock, R <= 512): 4 records per thread per group
-    constexpr uint32_t kBatch = 4;
-    float4 h[kBatch]; // GpuHit (t, u, v, tri) as one 16 B read
-    float4 fb[kBatch];
-    float4 ax[kBatch];
-    float ac[kBatch];
-    // a record outside the window reads record 0 of the group's first probe
-    // (window_probes > 0) and is not staged
-    auto load = [&](uint32_t g) {
-        const uint32_t slot0 = g * P;
-#pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t i = k * kOffsetBlock + tid;
-            const uint32_t p = i / R, s = i - p * R;
-            const bool ok = i < P * R && slot0 + p < f.window_probes;
-            const uint32_t pl = ok ? p : 0u, sl = ok ? s : 0u;
-            h[k] = *reinterpret_cast<const float4*>(f.hits + static_cast<size_t>(slot0 + pl) * R + sl);
-            fb[k] = f.fib[sl];
-            const GpuProbeSlot* ps = f.slots + slot0 + pl;
-            ax[k] = *reinterpret_cast<const float4*>(ps->axis); // axis xyz + angle_sin
-            ac[k] = ps->angle_cos;
-        }
-    };
-    uint32_t g = blockIdx.x;
-    if (g >= groups) return;
-    load(g);
-    for (;;) {
-        const uint32_t slot0 = g * P;
-        const bool blendLane = c == 0u && q < P && slot0 + q < f.window_probes;
-        const uint32_t probeIdx = f.slots[slot0 + (blendLane ? q : 0u)].probe_index;
-        const float4 cur = f.offsets[probeIdx];
-        // every lane classifies and rotates (no branch for the reads to sink into)
-#pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t i = k * kOffsetBlock + tid;
-            const uint32_t p = i / R, s = i - p * R;
-            // the surfel's distance (k_shade: miss, back face, front face)
-            const float t = h[k].x;
-            const float dist = __float_as_uint(h[k].w) == kNoHit ? f.z_far : (t < 0.0f ? t * 0.2f : t);
-            const float a = f16_to_f32(f32_to_f16(dist));
-            const uint32_t cls = (a > 0.0f && a < maxOffset) ? 1u : (a < 0.0f ? 2u : 0u);
-            const V3 d = rotate(v3(fb[k].x, fb[k].y, fb[k].z), v3(ax[k].x, ax[k].y, ax[k].z), ax[k].w, ac[k]);
-            if (i < P * R && slot0 + p < f.window_probes)
-                *reinterpret_cast<float4*>(recL + p * pstride + 4u * s) = make_float4(d.x, d.y, d.z, __uint_as_float(cls));
-        }
-        __syncthreads();
-        const uint32_t gn = g + gridDim.x;
-        if (gn < groups) load(gn); // in flight during the sums
-        float acc = 0.0f;
-        uint32_t cnt = 0;
-        if (c < 6u && q < P && slot0 + q < f.window_probes) {
-            const float* v = recL + q * pstride + (c % 3u);
-            const uint32_t* cl = reinterpret_cast<const uint32_t*>(recL + q * pstride + 3u);
-            const uint32_t want = c < 3u ? 1u : 2u;
-#pragma unroll 8
-            for (uint32_t s = 0; s < R; ++s) {
-                // m ? v : +0 as a bit mask: the compiler turns a select of the read into
-                // an exec-masked read, one LDS round trip per ray
-                const bool m = cl[4u * s] == want;
-                acc += __uint_as_float(__float_as_uint(v[4u * s]) & (m ? ~0u : 0u));
-                cnt += m ? 1u : 0u;
-            }
-        }
-        // the probe's six sums and two counts to its lane 8q (all lanes take part)
-        const int lane0 = static_cast<int>(__lane_id() & ~7u);
-        float sm[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) sm[k] = __shfl(acc, lane0 + k);
-        const uint32_t nc = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), lane0));
-        const uint32_t bc = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), lane0 + 3));
-        if (blendLane) {
-            const V3 accumNearFrontfaceDir = v3(sm[0], sm[1], sm[2]);
-            const V3 accumBackfaceDir = v3(sm[3], sm[4], sm[5]);
-            V3 currentOffset = v3(cur.x, cur.y, cur.z);
-            V3 offset = splat(0.0f);
-            const float stepSize = 0.125f, lerpSpeed = 10.0f;
-            if (static_cast<float>(bc) / static_cast<float>(R) >= 0.25f)
-                offset = offset + normalize(accumBackfaceDir) * stepSize;
-            else if (nc >= 1)
-                offset = offset - normalize(accumNearFrontfaceDir) * stepSize;
-            else
-                offset = offset - currentOffset * stepSize;
-            V3 newOffset = currentOffset + offset;
-            if (length(newOffset) > maxOffset) newOffset = maxOffset * normalize(newOffset);
-            newOffset = mix3(newOffset, currentOffset, exp2f_(-lerpSpeed * f.delta_time));
-            f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
-        }
-        if (gn >= groups) break;
-        g = gn;
-        __syncthreads(); // the group's records are read before the next group's are staged
-    }
-}
-#else
 __global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
 {
     if (frameAborted(f.abort_word)) return;
@@ -603,7 +474,6 @@ __global__ void __launch_bounds__(kOffsetBlock) k_probe_offsets(FrameArgs f)
         f.offsets[probeIdx] = make_float4(newOffset.x, newOffset.y, newOffset.z, 0.0f);
     }
 }
-#endif
 
 } // namespace dev
 
@@ -611,20 +481,7 @@ hipError_t launch_probe_offsets(const FrameArgs& f, hipStream_t s)
 {
     if (f.window_probes == 0 || !f.update_offsets) return hipSuccess;
     const uint32_t P = dev::offsetProbesPerBlock(f.R);
-#if ARK_OFFSETS_V2
-    if (static_cast<size_t>(P) * f.R > 4u * dev::kOffsetBlock) return hipErrorInvalidValue; // one batch per thread
-    // persistent: ARK_OFFSETS_WG_PER_CU workgroups per CU walk the groups of P probes
-    static thread_local int cus = 0;
-    if (cus <= 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    const uint32_t groups = (f.window_probes + P - 1) / P;
-    const uint32_t blocks = std::min<uint32_t>(groups, static_cast<uint32_t>(cus) * ARK_OFFSETS_WG_PER_CU);
-#else
     const uint32_t blocks = (f.window_probes + P - 1) / P;
-#endif
     const size_t lds = dev::offsetLdsBytes(P, f.R);
     static size_t lds_set = 0;
     if (lds > 65536 && lds > lds_set) {

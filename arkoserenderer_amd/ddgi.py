@@ -136,6 +136,22 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_set_scene(self.h, C.byref(s)), "ark_ddgi_set_scene")
         self._scene = scene
 
+    def set_lights(self, sun=None, spots=()):
+        """ark_ddgi_set_lights: the per-frame light set (GpuScene.cpp:790-858). sun =
+        (colour, direction) with the colour pre-exposed (colour x intensity x
+        lightPreExposure, :811) or None; spots = SpotLights, colours pre-exposed (:844)."""
+        from .scene import lights_abi
+
+        L, keep = lights_abi(sun, spots)
+        self.check(self.lib.ark_ddgi_set_lights(self.h, C.byref(L)), "ark_ddgi_set_lights")
+        del keep
+
+    def set_instances(self, instances: np.ndarray):
+        """ark_ddgi_set_instances: the per-frame TLAS instance update (GpuScene.cpp:872-1009),
+        a device refit. `instances` = the scene's INSTANCE_DTYPE array with new transforms."""
+        a = np.ascontiguousarray(instances)
+        self.check(self.lib.ark_ddgi_set_instances(self.h, C.c_void_p(a.ctypes.data), int(a.size)), "ark_ddgi_set_instances")
+
     def share_scene(self, src: "DDGIContext"):
         """ark_ddgi_share_scene: use src's device scene and BVH (same GPU), no copy."""
         self.check(self.lib.ark_ddgi_share_scene(self.h, src.h), "ark_ddgi_share_scene")

@@ -78,6 +78,37 @@ class SpotLight:
     ies_profile_index: int = -1
 
 
+def spot_array(spots) -> C.Array:
+    """ArkSpotLight[] of SpotLights (SpotLightData, GpuScene.cpp:844-858)."""
+    arr = (abi.ArkSpotLight * max(1, len(spots)))()
+    for i, sl in enumerate(spots):
+        for k in range(3):
+            arr[i].color[k] = sl.color[k]
+            arr[i].world_space_direction[k] = sl.direction[k]
+            arr[i].world_space_right[k] = sl.right[k]
+            arr[i].world_space_up[k] = sl.up[k]
+            arr[i].world_space_position[k] = sl.position[k]
+        arr[i].outer_cone_half_angle = sl.outer_cone_half_angle
+        arr[i].ies_profile_index = sl.ies_profile_index
+    return arr
+
+
+def lights_abi(sun, spots) -> tuple:
+    """ArkDdgiLights for ark_ddgi_set_lights: sun = (colour, direction) pre-exposed or
+    None, spots = SpotLights. Returns (struct, keep-alive array)."""
+    L = abi.ArkDdgiLights()
+    L.struct_size = C.sizeof(abi.ArkDdgiLights)
+    if sun is not None:
+        L.has_directional_light = 1
+        for k in range(3):
+            L.directional_light.color[k] = sun[0][k]
+            L.directional_light.world_space_direction[k] = sun[1][k]
+    arr = spot_array(list(spots))
+    L.spot_lights = C.addressof(arr)
+    L.spot_light_count = len(spots)
+    return L, arr
+
+
 @dataclass
 class SceneData:
     positions: np.ndarray            # (V, 3) float32
@@ -132,16 +163,7 @@ class SceneData:
             for k in range(3):
                 s.directional_light.color[k] = self.sun[0][k]
                 s.directional_light.world_space_direction[k] = self.sun[1][k]
-        spots = (abi.ArkSpotLight * max(1, len(self.spots)))()
-        for i, sl in enumerate(self.spots):
-            for k in range(3):
-                spots[i].color[k] = sl.color[k]
-                spots[i].world_space_direction[k] = sl.direction[k]
-                spots[i].world_space_right[k] = sl.right[k]
-                spots[i].world_space_up[k] = sl.up[k]
-                spots[i].world_space_position[k] = sl.position[k]
-            spots[i].outer_cone_half_angle = sl.outer_cone_half_angle
-            spots[i].ies_profile_index = sl.ies_profile_index
+        spots = spot_array(self.spots)
         keep.append(spots)
         s.spot_lights = C.addressof(spots)
         s.spot_light_count = len(self.spots)

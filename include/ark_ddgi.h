@@ -20,6 +20,10 @@
  *                           Vulkan driver builds is built here instead.
  *   ark_ddgi_share_scene <- one scene (TLAS + buffers) bound by several nodes of one
  *                           device: the Z-slab contexts of a GPU share it.
+ *   ark_ddgi_set_lights  <- the per-frame light upload of GpuScene::update
+ *                           (GpuScene.cpp:790-858, pre-exposure from :792).
+ *   ark_ddgi_set_instances <- the per-frame TLAS instance update + build
+ *                           (GpuScene.cpp:872-1009), as a device refit.
  *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:132-259):
  *                           traceRays -> irradiance update -> visibility update ->
  *                           border copies -> probe offsets.
@@ -297,6 +301,43 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
  * either context gives it a scene of its own. */
 int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src);
 
+/* The per-frame light set (GpuScene::update, GpuScene.cpp:790-858): the reference
+ * re-uploads every light every frame with colour x intensity x lightPreExposure (the
+ * camera's current exposure, :792, :811, :844) and its transform's forward / right / up
+ * / position. Replaces this context's lights (set_scene / share_scene start it with the
+ * scene's) for the updates and RT reflections called after it, without touching the
+ * BVHs: the spots reach the device in stream order ahead of the next operation that
+ * reads them, so frames already enqueued keep the lights they were enqueued with. At
+ * most one directional light (:797) and ARK_DDGI_MAX_SPOT_LIGHTS spot lights; a spot's
+ * ies_profile_index must name a texture of the scene (or be -1). A sun direction other
+ * than the one the scene's light-space sun BVH was built for makes the sun's shadow
+ * rays traverse the world BVHs (identical results), until the direction returns to it
+ * or ark_ddgi_set_scene builds a new one. Host arrays are not retained. */
+#define ARK_DDGI_MAX_SPOT_LIGHTS 10
+typedef struct ArkDdgiLights {
+    uint32_t struct_size;        /* sizeof(ArkDdgiLights) */
+    int32_t has_directional_light;
+    ArkDirectionalLight directional_light;
+    const ArkSpotLight* spot_lights; uint32_t spot_light_count;
+    int32_t reserved[4];
+} ArkDdgiLights;
+int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* lights);
+
+/* The per-frame TLAS instance update (GpuScene.cpp:872-1009: instance transforms
+ * re-uploaded, the TLAS updated most frames and fully rebuilt every 60). `instances`
+ * is the scene's instance list with new object_to_world transforms: the same count, RT
+ * meshes, triangle counts and hit masks as the last set_scene (else
+ * ARK_DDGI_E_INVALID_ARGUMENT and nothing changes). The flattened world-space BVHs are
+ * refitted on the device - every triangle record re-transformed in the fp32 operation
+ * order set_scene uses, every node box recomputed bottom-up and re-quantized outward -
+ * so the hits equal those of a set_scene with the same instances (they never depend on
+ * the BVH's shape); only the node boxes' tightness can degrade with large motions, which
+ * a set_scene (the full build) restores. The sun's light-space BVH is dropped (its
+ * shadow rays traverse the world BVHs). Blocking: waits for the context's (a shared
+ * scene: the device's) work in flight, refits, returns when the scene is updated; the
+ * cost is in ArkDdgiBvhStats.refit_ms. */
+int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count);
+
 /* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null
  * stream). Asynchronous: call ark_ddgi_synchronize or synchronize the stream before
  * reading.
@@ -416,6 +457,8 @@ typedef struct ArkDdgiBvhStats {
     uint64_t sun_node_count;
     float sun_cost_world;
     float sun_cost_light;
+    float sun_build_ms;  /* host time of the light-space BVH build and its cost sampling (part of build_ms) */
+    float refit_ms;      /* the last ark_ddgi_set_instances: wait + refit (0 = none since set_scene) */
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 

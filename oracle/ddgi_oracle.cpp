@@ -1263,6 +1263,40 @@ void bakeTexel(const Oracle& o, const ArkRTTriangleMesh& m, uint32_t p, uint32_t
 // ===========================================================================
 // Exported C API (for tests / bench cpu_baseline only)
 // ===========================================================================
+// World-space triangles of the instances (GpuScene.cpp:883-929: one instance per mesh
+// segment) and one BVH per hit-mask class.
+static void buildWorld(Oracle& o, int threads)
+{
+    o.tris.clear();
+    std::vector<uint32_t> opaque, masked, blend;
+    uint32_t gid = 0;
+    for (uint32_t ii = 0; ii < o.instances.size(); ++ii) {
+        const ArkRTInstance& inst = o.instances[ii];
+        const ArkRTTriangleMesh& m = o.meshes[inst.rt_mesh_index];
+        const float* M = inst.object_to_world;
+        float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
+        for (uint32_t p = 0; p < inst.triangle_count; ++p, ++gid) {
+            V3 w[3];
+            for (int k = 0; k < 3; ++k) {
+                uint32_t idx = o.indices[static_cast<size_t>(m.first_index) + 3u * p + k];
+                const float* P = &o.positions[(static_cast<size_t>(m.first_vertex) + idx) * 3];
+                w[k] = { M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3],
+                         M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7],
+                         M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11] };
+            }
+            WTri t { w[0], w[1] - w[0], w[2] - w[0], ii, p, gid, det < 0.0f ? 1u : 0u };
+            uint32_t ti = static_cast<uint32_t>(o.tris.size());
+            o.tris.push_back(t);
+            if (inst.hit_mask & ARK_RT_HIT_MASK_OPAQUE) opaque.push_back(ti);
+            else if (inst.hit_mask & ARK_RT_HIT_MASK_MASKED) masked.push_back(ti);
+            else blend.push_back(ti);
+        }
+    }
+    o.bvhOpaque = buildBvh(o.tris, opaque, threads);
+    o.bvhMasked = buildBvh(o.tris, masked, threads);
+    o.bvhBlend = buildBvh(o.tris, blend, threads);
+}
+
 extern "C" {
 
 struct OracleCtx;
@@ -1320,36 +1354,36 @@ int oracle_set_scene(void* ctx, const ArkDdgiScene* s, int threads)
     o.hasSun = s->has_directional_light != 0;
     o.sun = s->directional_light;
     o.spots.assign(s->spot_lights, s->spot_lights + s->spot_light_count);
-    // World-space triangles (GpuScene.cpp:883-929: one instance per mesh segment).
-    o.tris.clear();
-    std::vector<uint32_t> opaque, masked, blend;
-    uint32_t gid = 0;
-    for (uint32_t ii = 0; ii < s->instance_count; ++ii) {
-        const ArkRTInstance& inst = s->instances[ii];
-        const ArkRTTriangleMesh& m = s->meshes[inst.rt_mesh_index];
-        const float* M = inst.object_to_world;
-        float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
-        for (uint32_t p = 0; p < inst.triangle_count; ++p, ++gid) {
-            V3 w[3];
-            for (int k = 0; k < 3; ++k) {
-                uint32_t idx = s->indices[static_cast<size_t>(m.first_index) + 3u * p + k];
-                const float* P = &s->positions[(static_cast<size_t>(m.first_vertex) + idx) * 3];
-                w[k] = { M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3],
-                         M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7],
-                         M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11] };
-            }
-            WTri t { w[0], w[1] - w[0], w[2] - w[0], ii, p, gid, det < 0.0f ? 1u : 0u };
-            uint32_t ti = static_cast<uint32_t>(o.tris.size());
-            o.tris.push_back(t);
-            if (inst.hit_mask & ARK_RT_HIT_MASK_OPAQUE) opaque.push_back(ti);
-            else if (inst.hit_mask & ARK_RT_HIT_MASK_MASKED) masked.push_back(ti);
-            else blend.push_back(ti);
-        }
-    }
-    o.bvhOpaque = buildBvh(o.tris, opaque, threads);
-    o.bvhMasked = buildBvh(o.tris, masked, threads);
-    o.bvhBlend = buildBvh(o.tris, blend, threads);
+    buildWorld(o, threads);
     o.hasScene = true;
+    return 0;
+}
+
+// The per-frame light set (ark_ddgi_set_lights; GpuScene.cpp:790-858): the lights the
+// closest hit and the shadow rays of the next updates read.
+int oracle_set_lights(void* ctx, const ArkDdgiLights* L)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!L || !o.hasScene || L->spot_light_count > ARK_DDGI_MAX_SPOT_LIGHTS) return ARK_DDGI_E_INVALID_ARGUMENT;
+    o.hasSun = L->has_directional_light != 0;
+    o.sun = L->directional_light;
+    o.spots.assign(L->spot_lights, L->spot_lights + L->spot_light_count);
+    return 0;
+}
+
+// The per-frame instance transforms (ark_ddgi_set_instances; GpuScene.cpp:872-1009): the
+// world-space triangles recomputed and the BVHs rebuilt (the oracle has no refit: its
+// own BVH is rebuilt from scratch, which hits do not depend on).
+int oracle_set_instances(void* ctx, const ArkRTInstance* inst, uint32_t count, int threads)
+{
+    Oracle& o = *static_cast<Oracle*>(ctx);
+    if (!o.hasScene || count != o.instances.size() || (count && !inst)) return ARK_DDGI_E_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < count; ++i)
+        if (inst[i].rt_mesh_index != o.instances[i].rt_mesh_index || inst[i].triangle_count != o.instances[i].triangle_count ||
+            inst[i].hit_mask != o.instances[i].hit_mask)
+            return ARK_DDGI_E_INVALID_ARGUMENT;
+    o.instances.assign(inst, inst + count);
+    buildWorld(o, threads);
     return 0;
 }
 

@@ -1,9 +1,10 @@
 """The reduced-precision BVH8 child tests are conservative (host restatement, no GPU).
 
-visitNode8 (ddgi_kernels.hip) has three build-time forms: fp32 slabs (the default),
-packed fp16 with per-axis error bounds (ARK_NODE_F16=1) and packed fp16 with directed
-rounding (ARK_NODE_F16=2: near planes rounded toward -inf, far planes toward +inf).
-ark_ddgi_debug_bvh8_trace_stats restates each form on the host (ARK_SIM_BOX) and
+visitNode8 (ddgi_kernels.hip) tests children with fp32 slabs. Round 4 also built two
+packed-fp16 forms (per-axis error bounds, and directed rounding: near planes toward
+-inf, far planes toward +inf); they were measured 10x slower and removed from the
+kernels in round 5, and their host restatements stay as the record that
+they were conservative. ark_ddgi_debug_bvh8_trace_stats restates each form (ARK_SIM_BOX) and
 counts the children that the exact test accepts and the form culls (out[8]); a
 culled child could hide the closest hit, so the count must be 0. Rays: probe-like
 rays of a soup, plus near-axis-parallel directions (|idir| up to 1e6) and origins

@@ -107,31 +107,6 @@ def test_city_block_c5_like():
     _assert_exact(reps, offsets_expected=True)
 
 
-@pytest.mark.parametrize("grid_cells", ["8", "64", "256"])
-def test_binned_shadow_list_sun_and_spots(monkeypatch, grid_cells):
-    """The light-space binned shadow-ray list (k_shadow_gen keys -> k_shadow_bin_scan ->
-    k_shadow_scatter, FrameArgs::shadow_bin_grid) forced on for small windows: the
-    features scene (sun + 2 IES spots: octahedral cells around each spot) and the C5-like
-    city block (sun + 4 spots), at coarse, default and fine grids. Only the order of
-    the any-hit traversal changes: bit-exact against the oracle."""
-    monkeypatch.setenv("ARK_SHADOW_BIN_MIN_RAYS", "0")
-    monkeypatch.setenv("ARK_SHADOW_BIN_GRID", grid_cells)
-    sc = scenes.features_scene()
-    grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
-    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
-                       max_rays_per_probe=128, max_probe_updates=144)
-    reps = run_pair(sc, grid, cfg, 3, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
-                                                  environment_brightness=0.5))
-    _assert_exact(reps, offsets_expected=True)
-    sc = S.city_block(2000, extent=40.0)
-    grid = D.ProbeGrid((8, 4, 8), (40.0 / 8, 2.5, 40.0 / 8), (2.5, 0.5, 2.5))
-    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=200, compute_probe_offsets=True,
-                       max_rays_per_probe=64, max_probe_updates=256)
-    reps = run_pair(sc, grid, cfg, 3, 1000.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.02,
-                                                   environment_brightness=1.0), check_each_frame=False)
-    _assert_exact(reps, offsets_expected=True)
-
-
 @pytest.mark.parametrize("sun_bvh", ["0", "1"])
 def test_sun_structure_forced(monkeypatch, sun_bvh):
     """The sun's shadow rays forced through the world BVHs (ARK_SUN_BVH=0) or the
