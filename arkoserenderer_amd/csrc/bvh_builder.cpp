@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 namespace ark {
@@ -125,21 +126,35 @@ struct Range {
     Aabb box;
 };
 
+// f(begin, end) over [0, n) in `threads` contiguous chunks (one when n is small)
+template<class F>
+void parallelFor(size_t n, int threads, F f)
+{
+    const int T = std::max(1, std::min<int>(threads, static_cast<int>(n >> 16) + 1));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+    f(0, n / T);
+    for (std::thread& th : pool) th.join();
+}
+
 class Builder {
 public:
     Builder(const std::vector<BuildTriangle>& tris, const BvhBuildOptions& opt, uint32_t nodeBase, uint32_t triBase)
         : m_opt(opt), m_nodeBase(nodeBase), m_triBase(triBase)
     {
         const size_t nt = tris.size();
+        const int hw = opt.threads > 0 ? opt.threads : static_cast<int>(std::thread::hardware_concurrency());
         m_refs.resize(nt);
-        for (size_t i = 0; i < nt; ++i) {
-            Ref& r = m_refs[i];
-            r.box.grow(tris[i].v0);
-            r.box.grow(tris[i].v1);
-            r.box.grow(tris[i].v2);
-            for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (r.box.lo[a] + r.box.hi[a]);
-            r.tri = static_cast<uint32_t>(i);
-        }
+        parallelFor(nt, hw, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) {
+                Ref& r = m_refs[i];
+                r.box.grow(tris[i].v0);
+                r.box.grow(tris[i].v1);
+                r.box.grow(tris[i].v2);
+                for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (r.box.lo[a] + r.box.hi[a]);
+                r.tri = static_cast<uint32_t>(i);
+            }
+        });
         if (opt.presplit_levels > 0) {
             std::vector<Ref> refs;
             refs.reserve(nt + nt / 2);
@@ -171,10 +186,10 @@ public:
             m_refs.swap(refs);
         }
         const size_t n = m_refs.size();
-        m_idx.resize(n);
-        for (size_t i = 0; i < n; ++i) m_idx[i] = static_cast<uint32_t>(i);
-        m_nodes.resize(2 * n + 2);
-        int hw = opt.threads > 0 ? opt.threads : static_cast<int>(std::thread::hardware_concurrency());
+        // a binary tree over n leaves has at most n - 1 internal nodes (+ node 0's slot);
+        // written before read, so not zero-filled (1.3 GB at C4)
+        m_nodes.reset(new GpuBvhNode[n + 1]);
+        m_threads = std::max(1, hw);
         m_threadsAvail = std::max(0, hw - 1);
     }
 
@@ -183,7 +198,8 @@ public:
         BvhBuildResult res;
         const uint32_t n = static_cast<uint32_t>(m_refs.size());
         m_nodeCount = 1; // node 0 = root
-        Range root = buildRange(0, n, 1, 0);
+        Bin all = binRange(0, n, nullptr, nullptr);
+        Range root = buildRange(0, n, 1, all.b, all.c, 0);
         if (root.code < 0) {
             // whole set fits one leaf: root with the leaf + an unreachable far child
             Aabb far;
@@ -191,10 +207,12 @@ public:
             far.grow(p);
             writeNode(0, root.box, root.code, far, ~0);
         }
-        m_nodes.resize(m_nodeCount);
-        res.nodes = std::move(m_nodes);
+        res.nodes.assign(m_nodes.get(), m_nodes.get() + m_nodeCount.load());
+        m_nodes.reset();
         res.tris.resize(n);
-        for (uint32_t i = 0; i < n; ++i) res.tris[i] = make_gpu_triangle(tris[m_refs[m_idx[i]].tri]);
+        parallelFor(n, m_threads, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) res.tris[i] = make_gpu_triangle(tris[m_refs[i].tri]);
+        });
         res.max_depth = m_maxDepth.load();
         res.max_leaf = m_maxLeaf.load();
         res.sah_cost = sahCost(res.nodes, root.box);
@@ -255,17 +273,85 @@ private:
         return ~static_cast<int32_t>(v);
     }
 
-    Range buildRange(uint32_t first, uint32_t count, int depth, int forcedLocal = -1)
+    // Bounds of a run of references (box of their boxes, box of their centroids) and
+    // their count; with scale != null also their binning along all three axes at once
+    // (bins[a][k]: the references whose centroid falls in bin k of axis a of `cbox`).
+    // The references are the builder's own array, partitioned in place level by level,
+    // so every pass reads them sequentially.
+    struct Bin {
+        Aabb b, c;
+        uint32_t n = 0;
+        void add(const Ref& r)
+        {
+            b.grow(r.box);
+            c.grow(r.c);
+            ++n;
+        }
+        void add(const Bin& o)
+        {
+            b.grow(o.b);
+            c.grow(o.c);
+            n += o.n;
+        }
+    };
+    static constexpr int kMaxBins = 64;
+    struct Bins {
+        Bin k[3][kMaxBins];
+    };
+
+    Bin binRange(uint32_t first, uint32_t count, const Aabb* cbox, Bins* bins) const
+    {
+        const int B = std::max(4, std::min(m_opt.bins, kMaxBins));
+        float lo[3] = { 0, 0, 0 }, scale[3] = { 0, 0, 0 };
+        bool axis[3] = { false, false, false };
+        if (bins)
+            for (int a = 0; a < 3; ++a) {
+                const float ext = cbox->hi[a] - cbox->lo[a];
+                axis[a] = ext > 0.0f;
+                lo[a] = cbox->lo[a];
+                scale[a] = axis[a] ? static_cast<float>(B) / ext : 0.0f;
+            }
+        auto work = [&](uint32_t b, uint32_t e, Bin& all, Bins* out) {
+            for (uint32_t i = b; i < e; ++i) {
+                const Ref& r = m_refs[i];
+                all.add(r);
+                if (out)
+                    for (int a = 0; a < 3; ++a)
+                        if (axis[a]) out->k[a][std::min(B - 1, std::max(0, static_cast<int>((r.c[a] - lo[a]) * scale[a])))].add(r);
+            }
+        };
+        Bin all;
+        // the top levels in parallel: per-thread partial bins, merged (unions and counts
+        // do not depend on the order)
+        const int T = count >= (1u << 20) ? std::min(m_threads, static_cast<int>(count >> 18)) : 1;
+        if (T <= 1) {
+            work(first, first + count, all, bins);
+            return all;
+        }
+        std::vector<Bin> part(T);
+        std::vector<Bins> partBins(bins ? T : 0);
+        std::vector<std::thread> pool;
+        for (int t = 0; t < T; ++t) {
+            const uint32_t b = first + static_cast<uint32_t>(static_cast<uint64_t>(count) * t / T);
+            const uint32_t e = first + static_cast<uint32_t>(static_cast<uint64_t>(count) * (t + 1) / T);
+            pool.emplace_back([&, t, b, e] { work(b, e, part[t], bins ? &partBins[t] : nullptr); });
+        }
+        for (std::thread& th : pool) th.join();
+        for (int t = 0; t < T; ++t) {
+            all.add(part[t]);
+            if (bins)
+                for (int a = 0; a < 3; ++a)
+                    for (int k = 0; k < B; ++k) bins->k[a][k].add(partBins[t].k[a][k]);
+        }
+        return all;
+    }
+
+    // box / cbox: the bounds of the range (from the parent's bins)
+    Range buildRange(uint32_t first, uint32_t count, int depth, const Aabb& box, const Aabb& cbox, int forcedLocal = -1)
     {
         {
             int md = m_maxDepth.load();
             while (depth > md && !m_maxDepth.compare_exchange_weak(md, depth)) {}
-        }
-        Aabb box, cbox;
-        for (uint32_t i = first; i < first + count; ++i) {
-            const Ref& r = m_refs[m_idx[i]];
-            box.grow(r.box);
-            cbox.grow(r.c);
         }
         const int maxLeaf = std::min(m_opt.max_leaf_size, kMaxLeafSize);
         if (count == 1 || (count <= 2 && maxLeaf >= 2)) return makeLeaf(first, count, box);
@@ -274,38 +360,40 @@ private:
         const int log2n = static_cast<int>(std::ceil(std::log2(std::max(1.0, static_cast<double>(count) / maxLeaf))));
         const bool forceMedian = depth + log2n + 2 >= m_opt.max_depth;
         uint32_t mid = first + count / 2;
-        bool split = true;
+        bool split = true, childBounds = false;
+        Bin left, right;
         if (!forceMedian) {
-            const int B = std::max(4, std::min(m_opt.bins, 64));
+            const int B = std::max(4, std::min(m_opt.bins, kMaxBins));
             float bestCost = INFINITY;
             int bestAxis = -1, bestBin = -1;
-            for (int a = 0; a < 3; ++a) {
+            if (count <= kSmallCount) {
+                // few references: the same SAH sweep over the bins they occupy only (a
+                // split between two occupied bins equals the one at the upper bin, which
+                // the full sweep - descending, strict < - would keep), without
+                // initialising 3 x B bins per node
+                bestSmallSplit(first, count, cbox, B, bestCost, bestAxis, bestBin);
+            }
+            Bins bins;
+            if (count > kSmallCount) binRange(first, count, &cbox, &bins);
+            for (int a = 0; a < 3 && count > kSmallCount; ++a) {
                 const float ext = cbox.hi[a] - cbox.lo[a];
                 if (!(ext > 0.0f)) continue;
-                Aabb bb[64];
-                uint32_t bc[64] = {};
-                const float scale = static_cast<float>(B) / ext;
-                for (uint32_t i = first; i < first + count; ++i) {
-                    const Ref& r = m_refs[m_idx[i]];
-                    int k = std::min(B - 1, std::max(0, static_cast<int>((r.c[a] - cbox.lo[a]) * scale)));
-                    bc[k]++;
-                    bb[k].grow(r.box);
-                }
-                float leftArea[64];
-                uint32_t leftCount[64];
+                const Bin* bb = bins.k[a];
+                float leftArea[kMaxBins];
+                uint32_t leftCount[kMaxBins];
                 Aabb acc;
                 uint32_t n = 0;
                 for (int k = 0; k < B - 1; ++k) {
-                    acc.grow(bb[k]);
-                    n += bc[k];
+                    acc.grow(bb[k].b);
+                    n += bb[k].n;
                     leftArea[k] = acc.area(m_opt.area_w);
                     leftCount[k] = n;
                 }
                 Aabb accR;
                 uint32_t nr = 0;
                 for (int k = B - 1; k > 0; --k) {
-                    accR.grow(bb[k]);
-                    nr += bc[k];
+                    accR.grow(bb[k].b);
+                    nr += bb[k].n;
                     const uint32_t nl = leftCount[k - 1];
                     if (nl == 0 || nr == 0) continue;
                     const float cost = leftArea[k - 1] * nl + accR.area(m_opt.area_w) * nr;
@@ -325,15 +413,21 @@ private:
                 const float ext = cbox.hi[a] - cbox.lo[a];
                 const float scale = static_cast<float>(B) / ext;
                 const float lo = cbox.lo[a];
-                auto it = std::partition(m_idx.begin() + first, m_idx.begin() + first + count, [&](uint32_t id) {
-                    int k = std::min(B - 1, std::max(0, static_cast<int>((m_refs[id].c[a] - lo) * scale)));
+                auto it = std::partition(m_refs.begin() + first, m_refs.begin() + first + count, [&](const Ref& r) {
+                    int k = std::min(B - 1, std::max(0, static_cast<int>((r.c[a] - lo) * scale)));
                     return k < bestBin;
                 });
-                mid = static_cast<uint32_t>(it - m_idx.begin());
+                mid = static_cast<uint32_t>(it - m_refs.begin());
+                // the children's bounds are their bins' unions
+                if (count > kSmallCount) {
+                    for (int k = 0; k < B; ++k) (k < bestBin ? left : right).add(bins.k[a][k]);
+                    childBounds = true;
+                }
             }
             if (split && (bestAxis < 0 || mid == first || mid == first + count)) {
                 medianSplit(first, count, cbox);
                 mid = first + count / 2;
+                childBounds = false;
             }
         } else {
             if (static_cast<int>(count) <= maxLeaf) split = false;
@@ -344,23 +438,64 @@ private:
         const uint32_t local = forcedLocal >= 0 ? static_cast<uint32_t>(forcedLocal) : m_nodeCount.fetch_add(1);
         Range l, r;
         const uint32_t nl = mid - first, nr = first + count - mid;
+        if (!childBounds) {
+            left = binRange(first, nl, nullptr, nullptr);
+            right = binRange(mid, nr, nullptr, nullptr);
+        }
         bool spawned = false;
         if (count > 65536) {
             int avail = m_threadsAvail.fetch_sub(1);
             if (avail > 0) {
                 spawned = true;
-                std::thread t([&] { l = buildRange(first, nl, depth + 1); });
-                r = buildRange(mid, nr, depth + 1);
+                std::thread t([&] { l = buildRange(first, nl, depth + 1, left.b, left.c); });
+                r = buildRange(mid, nr, depth + 1, right.b, right.c);
                 t.join();
             }
             m_threadsAvail.fetch_add(1);
         }
         if (!spawned) {
-            l = buildRange(first, nl, depth + 1);
-            r = buildRange(mid, nr, depth + 1);
+            l = buildRange(first, nl, depth + 1, left.b, left.c);
+            r = buildRange(mid, nr, depth + 1, right.b, right.c);
         }
         writeNode(local, l.box, l.code, r.box, r.code);
         return Range { static_cast<int32_t>(m_nodeBase + local), box };
+    }
+
+    static constexpr uint32_t kSmallCount = 48;
+    void bestSmallSplit(uint32_t first, uint32_t count, const Aabb& cbox, int B, float& bestCost, int& bestAxis, int& bestBin) const
+    {
+        for (int a = 0; a < 3; ++a) {
+            const float ext = cbox.hi[a] - cbox.lo[a];
+            if (!(ext > 0.0f)) continue;
+            const float scale = static_cast<float>(B) / ext;
+            int key[kSmallCount];
+            uint32_t ord[kSmallCount];
+            for (uint32_t i = 0; i < count; ++i) {
+                key[i] = std::min(B - 1, std::max(0, static_cast<int>((m_refs[first + i].c[a] - cbox.lo[a]) * scale)));
+                ord[i] = i;
+            }
+            std::sort(ord, ord + count, [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+            // prefix boxes over the occupied bins in ascending order
+            Aabb pre[kSmallCount];
+            Aabb acc;
+            for (uint32_t j = 0; j < count; ++j) {
+                acc.grow(m_refs[first + ord[j]].box);
+                pre[j] = acc;
+            }
+            Aabb accR;
+            for (uint32_t j = count; j-- > 0;) {
+                accR.grow(m_refs[first + ord[j]].box);
+                // a candidate split at k = key of the first reference of a bin run
+                if (j == 0 || key[ord[j - 1]] == key[ord[j]]) continue;
+                const uint32_t nl = j, nr = count - j;
+                const float cost = pre[j - 1].area(m_opt.area_w) * nl + accR.area(m_opt.area_w) * nr;
+                if (cost < bestCost) {
+                    bestCost = cost;
+                    bestAxis = a;
+                    bestBin = key[ord[j]];
+                }
+            }
+        }
     }
 
     void medianSplit(uint32_t first, uint32_t count, const Aabb& cbox)
@@ -369,8 +504,8 @@ private:
         float e0 = cbox.hi[0] - cbox.lo[0], e1 = cbox.hi[1] - cbox.lo[1], e2 = cbox.hi[2] - cbox.lo[2];
         if (e1 > e0 && e1 >= e2) a = 1;
         else if (e2 > e0 && e2 > e1) a = 2;
-        std::nth_element(m_idx.begin() + first, m_idx.begin() + first + count / 2, m_idx.begin() + first + count,
-                         [&](uint32_t x, uint32_t y) { return m_refs[x].c[a] < m_refs[y].c[a]; });
+        std::nth_element(m_refs.begin() + first, m_refs.begin() + first + count / 2, m_refs.begin() + first + count,
+                         [&](const Ref& x, const Ref& y) { return x.c[a] < y.c[a]; });
     }
 
     Range makeLeaf(uint32_t first, uint32_t count, const Aabb& box)
@@ -385,9 +520,9 @@ private:
 
     const BvhBuildOptions m_opt;
     const uint32_t m_nodeBase, m_triBase;
-    std::vector<Ref> m_refs;
-    std::vector<uint32_t> m_idx;
-    std::vector<GpuBvhNode> m_nodes;
+    std::vector<Ref> m_refs; // partitioned in place: leaf order at the end
+    std::unique_ptr<GpuBvhNode[]> m_nodes;
+    int m_threads = 1;
     std::atomic<uint32_t> m_nodeCount { 0 };
     std::atomic<int> m_maxDepth { 0 };
     std::atomic<uint32_t> m_maxLeaf { 0 };
@@ -443,10 +578,16 @@ public:
     uint32_t place(uint32_t pattern)
     {
         static const uint32_t back = std::getenv("ARK_BVH8_ROW_WINDOW") ? static_cast<uint32_t>(std::atoi(std::getenv("ARK_BVH8_ROW_WINDOW"))) : kRowWindow;
-        const uint32_t lo = m_end > back ? m_end - back : 0u;
+        uint32_t lo = m_end > back ? m_end - back : 0u;
+        // every position below m_firstFree is taken, so no base whose lowest pattern
+        // position falls below it fits: the same first fit, without re-testing the
+        // filled front of the window for every node (C4 collapse 6.5 -> s)
+        const uint32_t low = static_cast<uint32_t>(__builtin_ctz(pattern));
+        if (m_firstFree > low) lo = std::max(lo, m_firstFree - low);
         for (uint32_t b = lo;; ++b)
             if ((window(b) & pattern) == 0) {
                 mark(b, pattern);
+                while (taken(m_firstFree)) ++m_firstFree;
                 return b;
             }
     }
@@ -470,8 +611,10 @@ private:
         if (sh > 40u) m_bits[i + 1] |= static_cast<uint64_t>(pattern) >> (64u - sh);
         m_end = std::max(m_end, b + 32u - static_cast<uint32_t>(__builtin_clz(pattern)));
     }
+    bool taken(uint32_t p) const { return (p >> 6) < m_bits.size() && ((m_bits[p >> 6] >> (p & 63u)) & 1u); }
     std::vector<uint64_t> m_bits;
     uint32_t m_end = 0;
+    uint32_t m_firstFree = 0; // lowest position not taken
 };
 
 // The smallest row stride (GpuBvh8Node) under which every position s + stride * i
@@ -592,19 +735,11 @@ float childCost(const CollapsePlan& P, const Child8& c, int i)
     return P.cTri * c.box.area(P.areaW) * static_cast<float>((static_cast<uint32_t>(~c.code) & (kMaxLeafSize - 1)) + 1);
 }
 
-CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri, const float* areaW)
+// The plan of BVH2 node k from its children's (planCollapse).
+void planNode(const BvhBuildResult& bvh2, CollapsePlan& P, size_t k)
 {
-    CollapsePlan P;
-    P.cNode = cNode;
-    P.cTri = cTri;
-    for (int k = 0; k < 3; ++k) P.areaW[k] = areaW[k];
-    const size_t N = bvh2.nodes.size();
-    P.cost.assign(8 * N, 0.0f);
-    P.pick.assign(8 * N, 0);
-    P.first.assign(N, 0);
-    P.count.assign(N, 0);
-    // children have larger indices than their parent (allocated at the parent's split)
-    for (size_t k = N; k-- > 0;) {
+    const float cNode = P.cNode, cTri = P.cTri;
+    {
         Child8 ch[2];
         int m = 0;
         childrenOf(bvh2.nodes[k], ch, m);
@@ -660,6 +795,45 @@ CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri, c
             }
         }
     }
+}
+
+// Children before parents: the subtrees of the top levels on their own threads (each
+// node's plan reads only its children's), identical to a sweep in decreasing index.
+void planSubtree(const BvhBuildResult& bvh2, CollapsePlan& P, size_t k, int spawnLevels)
+{
+    Child8 ch[2];
+    int m = 0;
+    childrenOf(bvh2.nodes[k], ch, m);
+    int32_t inner[2];
+    int ni = 0;
+    for (int c = 0; c < m; ++c)
+        if (ch[c].code >= 0) inner[ni++] = ch[c].code;
+    if (ni == 2 && spawnLevels > 0) {
+        std::thread t([&] { planSubtree(bvh2, P, static_cast<size_t>(inner[0]), spawnLevels - 1); });
+        planSubtree(bvh2, P, static_cast<size_t>(inner[1]), spawnLevels - 1);
+        t.join();
+    } else {
+        for (int c = 0; c < ni; ++c) planSubtree(bvh2, P, static_cast<size_t>(inner[c]), spawnLevels - 1);
+    }
+    planNode(bvh2, P, k);
+}
+
+CollapsePlan planCollapse(const BvhBuildResult& bvh2, float cNode, float cTri, const float* areaW, int threads)
+{
+    CollapsePlan P;
+    P.cNode = cNode;
+    P.cTri = cTri;
+    for (int k = 0; k < 3; ++k) P.areaW[k] = areaW[k];
+    const size_t N = bvh2.nodes.size();
+    P.cost.assign(8 * N, 0.0f);
+    P.pick.assign(8 * N, 0);
+    P.first.assign(N, 0);
+    P.count.assign(N, 0);
+    int levels = 0;
+    for (int t = threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency()); (1 << levels) < 2 * t && levels < 8; ++levels) {}
+    if (N > (1u << 16)) planSubtree(bvh2, P, 0, levels);
+    else
+        for (size_t k = N; k-- > 0;) planNode(bvh2, P, k); // children have larger indices
     return P;
 }
 
@@ -691,26 +865,38 @@ void emitChildren(const BvhBuildResult& bvh2, const CollapsePlan& P, const Child
     emitChildren(bvh2, P, two[1], i - kk, out, n);
 }
 
-Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& copt)
+namespace {
+struct CollapseItem {
+    uint32_t src;   // BVH2 node
+    uint32_t dst;   // BVH8 node (index in its part)
+    uint32_t depth;
+};
+
+// One part of a collapse: the BVH8 nodes of a subtree (or of the top levels) in BFS
+// order with part-local child and triangle indices, its triangle rows.
+struct CollapsePart {
+    std::vector<GpuBvh8Node> nodes;
+    std::vector<GpuTriangle> tris;
+    RowPlacer rows;
+    uint32_t max_depth = 0;
+    uint32_t leaf_children = 0;
+    uint64_t triangles = 0;
+    double sah = 0.0;
+};
+
+// Collapses the queue's items breadth first into `out`; items deeper than stopDepth go
+// to `frontier` unprocessed (their node slots are allocated).
+void collapseQueue(const BvhBuildResult& bvh2, const CollapsePlan& plan, const Bvh8CollapseOptions& copt, double& rootArea, CollapsePart& out,
+                   std::vector<CollapseItem> queue, uint32_t stopDepth, std::vector<CollapseItem>* frontier)
 {
-    Bvh8BuildResult res;
-    if (bvh2.nodes.empty()) return res;
-    CollapsePlan plan;
-    if (copt.sah_optimal) plan = planCollapse(bvh2, copt.node_cost, copt.tri_cost, copt.area_w);
-    struct Item {
-        uint32_t src;
-        uint32_t dst;
-        uint32_t depth;
-    };
-    std::vector<Item> queue;
-    queue.push_back({ 0u, 0u, 1u });
-    res.nodes.resize(1);
-    res.tris.reserve(bvh2.tris.size() + bvh2.tris.size() / 8);
-    RowPlacer rowPlacer;
-    double sah = 0.0, rootArea = 0.0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
-        const Item it = queue[qi];
-        res.max_depth = std::max(res.max_depth, it.depth);
+        const CollapseItem it = queue[qi];
+        if (it.depth > stopDepth) {
+            frontier->push_back(it);
+            continue;
+        }
+        const bool isRoot = frontier && qi == 0; // the top part's first item is the BVH's root
+        out.max_depth = std::max(out.max_depth, it.depth);
         Child8 ch[8];
         int n = 0;
         if (copt.sah_optimal) {
@@ -765,13 +951,13 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
         Aabb box;
         for (int c = 0; c < n; ++c) box.grow(ch[c].box);
         // SAH cost of the result (node cost 1, the plan's triangle cost), for reports
-        if (qi == 0) {
+        if (isRoot) {
             rootArea = std::max(1e-30, static_cast<double>(box.area()));
-            sah += 1.0;
+            out.sah += 1.0;
         }
         for (int c = 0; c < n; ++c) {
             const double a = ch[c].box.area() / rootArea;
-            sah += ch[c].code >= 0 ? a : a * copt.tri_cost * static_cast<double>((static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1);
+            out.sah += ch[c].code >= 0 ? a : a * copt.tri_cost * static_cast<double>((static_cast<uint32_t>(~ch[c].code) & (kMaxLeafSize - 1)) + 1);
         }
         float pc[3];
         for (int a = 0; a < 3; ++a) pc[a] = 0.5f * (box.lo[a] + box.hi[a]);
@@ -847,7 +1033,7 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
         // triangle i of slot s goes to position s + stride * i (GpuBvh8Node), the
         // rows placed at the first base in the tail of the array where all of their
         // positions are free
-        const uint32_t childBase = static_cast<uint32_t>(res.nodes.size());
+        const uint32_t childBase = static_cast<uint32_t>(out.nodes.size());
         uint32_t leafCnt[8] = {}, leafMask = 0;
         for (int s = 0; s < 8; ++s) {
             const int c = childIn[s];
@@ -859,10 +1045,10 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
         uint32_t rows = 0;
         for (uint32_t s = 0; s < 8; ++s)
             for (uint32_t i = 0; i < leafCnt[s]; ++i) rows |= 1u << (s + stride * i);
-        const uint32_t triStart = rows ? rowPlacer.place(rows) : 0u;
-        if (rows && res.tris.size() < triStart + 24u) res.tris.resize(triStart + 24u, holeTriangle());
-        nd.child_base = node_base + childBase;
-        nd.tri_base = tri_base + triStart;
+        const uint32_t triStart = rows ? out.rows.place(rows) : 0u;
+        if (rows && out.tris.size() < triStart + 24u) out.tris.resize(triStart + 24u, holeTriangle());
+        nd.child_base = childBase; // local: offset when the parts are joined
+        nd.tri_base = triStart;
         nd.leaf_tris = rows;
         nd.tri_stride = static_cast<uint8_t>(stride);
         nd.leaf_mask = static_cast<uint8_t>(leafMask);
@@ -889,17 +1075,91 @@ Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, ui
             } else {
                 const uint32_t code = static_cast<uint32_t>(~k.code);
                 const uint32_t first = code >> kLeafCountBits, cnt = (code & (kMaxLeafSize - 1)) + 1u;
-                for (uint32_t i = 0; i < cnt; ++i) res.tris[triStart + static_cast<uint32_t>(s) + stride * i] = bvh2.tris[first + i];
-                res.leaf_children++;
-                res.triangles += cnt;
+                for (uint32_t i = 0; i < cnt; ++i) out.tris[triStart + static_cast<uint32_t>(s) + stride * i] = bvh2.tris[first + i];
+                out.leaf_children++;
+                out.triangles += cnt;
             }
         }
-        res.nodes.resize(res.nodes.size() + nInternal);
-        res.nodes[it.dst] = nd;
+        out.nodes.resize(out.nodes.size() + nInternal);
+        out.nodes[it.dst] = nd;
     }
-    // drop trailing holes (the array keeps one padding record for the five-load fetch
-    // in the uploader)
-    while (!res.tris.empty() && isHoleTriangle(res.tris.back())) res.tris.pop_back();
+}
+} // namespace
+
+// The top levels (BVH8 depth <= kTopDepth) are collapsed first, then the subtrees below
+// them in parallel, each a part with its own node and triangle-row arrays, joined in
+// order: the top levels stay breadth first at the front (k_trace_shadow caches the
+// first nodes in LDS), every subtree is breadth first in its block. (One sequential
+// breadth-first pass took 6.2 s of a C4 build; the plan's DP is shared.)
+Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& copt)
+{
+    Bvh8BuildResult res;
+    if (bvh2.nodes.empty()) return res;
+    CollapsePlan plan;
+    if (copt.sah_optimal) plan = planCollapse(bvh2, copt.node_cost, copt.tri_cost, copt.area_w, copt.threads);
+    constexpr uint32_t kTopDepth = 3;
+    double rootArea = 0.0;
+    CollapsePart top;
+    top.nodes.resize(1);
+    std::vector<CollapseItem> frontier;
+    collapseQueue(bvh2, plan, copt, rootArea, top, { { 0u, 0u, 1u } }, kTopDepth, &frontier);
+    std::vector<CollapsePart> parts(frontier.size());
+    {
+        const int hw = copt.threads > 0 ? copt.threads : static_cast<int>(std::thread::hardware_concurrency());
+        const int T = std::max(1, std::min<int>(hw, static_cast<int>(frontier.size())));
+        std::atomic<size_t> next { 0 };
+        auto worker = [&] {
+            for (size_t f; (f = next.fetch_add(1)) < frontier.size();) {
+                parts[f].nodes.resize(1);
+                double ra = rootArea;
+                collapseQueue(bvh2, plan, copt, ra, parts[f], { { frontier[f].src, 0u, frontier[f].depth } }, UINT32_MAX, nullptr);
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < T; ++t) pool.emplace_back(worker);
+        worker();
+        for (std::thread& th : pool) th.join();
+    }
+    // join: subtree f's root fills its frontier slot of the top part, its other nodes
+    // follow the top part's nodes; its rows follow the top part's rows
+    auto trimHoles = [](std::vector<GpuTriangle>& t) {
+        while (!t.empty() && isHoleTriangle(t.back())) t.pop_back();
+    };
+    trimHoles(top.tris);
+    size_t nodeCount = top.nodes.size(), triCount = top.tris.size();
+    std::vector<size_t> nodeOff(parts.size()), triOff(parts.size());
+    for (size_t f = 0; f < parts.size(); ++f) {
+        trimHoles(parts[f].tris);
+        nodeOff[f] = nodeCount;
+        triOff[f] = triCount;
+        nodeCount += parts[f].nodes.size() - 1;
+        triCount += parts[f].tris.size();
+    }
+    res.nodes.resize(nodeCount);
+    res.tris.reserve(triCount);
+    auto place = [&](GpuBvh8Node nd, size_t nodeShift, size_t triShift) {
+        nd.child_base = node_base + static_cast<uint32_t>(nd.child_base + nodeShift);
+        nd.tri_base = tri_base + static_cast<uint32_t>(nd.leaf_tris ? nd.tri_base + triShift : 0u);
+        return nd;
+    };
+    for (size_t k = 0; k < top.nodes.size(); ++k) res.nodes[k] = place(top.nodes[k], 0, 0);
+    res.tris.insert(res.tris.end(), top.tris.begin(), top.tris.end());
+    res.max_depth = top.max_depth;
+    res.leaf_children = top.leaf_children;
+    res.triangles = top.triangles;
+    double sah = top.sah;
+    for (size_t f = 0; f < parts.size(); ++f) {
+        const CollapsePart& P = parts[f];
+        // part-local node k >= 1 -> nodeOff + k - 1 (its children are all >= 1)
+        const size_t shift = nodeOff[f] - 1;
+        res.nodes[frontier[f].dst] = place(P.nodes[0], shift, triOff[f]);
+        for (size_t k = 1; k < P.nodes.size(); ++k) res.nodes[shift + k] = place(P.nodes[k], shift, triOff[f]);
+        res.tris.insert(res.tris.end(), P.tris.begin(), P.tris.end());
+        res.max_depth = std::max(res.max_depth, P.max_depth);
+        res.leaf_children += P.leaf_children;
+        res.triangles += P.triangles;
+        sah += P.sah;
+    }
     res.sah_cost = static_cast<float>(sah);
     return res;
 }
@@ -1047,30 +1307,44 @@ void sun_frame(const float sunDir[3], double frame[3][3])
     }
 }
 
-void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris)
+void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, int threads)
 {
-    for (const BuildTriangle& t : tris) {
-        const GpuTriangle rec = make_gpu_triangle(t);
-        // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2 (exact, from the record)
-        double V[3][3];
-        for (int a = 0; a < 3; ++a) V[0][a] = rec.t0[a];
-        const double e1[3] = { rec.t0[3], rec.t1[0], rec.t1[1] }, e2[3] = { rec.t1[2], rec.t1[3], rec.t2[0] };
-        for (int a = 0; a < 3; ++a) {
-            V[1][a] = V[0][a] + e1[a];
-            V[2][a] = V[0][a] + e2[a];
-            in.maxAbs = std::max(in.maxAbs, static_cast<float>(std::max({ std::fabs(V[0][a]), std::fabs(V[1][a]), std::fabs(V[2][a]) })));
+    const size_t base = in.world.size(), n = tris.size();
+    in.tris.resize(base + n);
+    in.world.resize(base + n);
+    // independent per triangle: in chunks on `threads` threads, the largest |coordinate|
+    // reduced at the end (a max does not depend on the order)
+    const int T = std::max(1, std::min<int>(threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency()), static_cast<int>(n >> 16) + 1));
+    std::vector<float> maxAbs(T, 0.0f);
+    auto work = [&](int t) {
+        const size_t b = n * t / T, e = n * (t + 1) / T;
+        for (size_t i = b; i < e; ++i) {
+            const GpuTriangle rec = make_gpu_triangle(tris[i]);
+            // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2 (exact, from the record)
+            double V[3][3];
+            for (int a = 0; a < 3; ++a) V[0][a] = rec.t0[a];
+            const double e1[3] = { rec.t0[3], rec.t1[0], rec.t1[1] }, e2[3] = { rec.t1[2], rec.t1[3], rec.t2[0] };
+            for (int a = 0; a < 3; ++a) {
+                V[1][a] = V[0][a] + e1[a];
+                V[2][a] = V[0][a] + e2[a];
+                maxAbs[t] = std::max(maxAbs[t], static_cast<float>(std::max({ std::fabs(V[0][a]), std::fabs(V[1][a]), std::fabs(V[2][a]) })));
+            }
+            BuildTriangle& l = in.tris[base + i];
+            float* dst[3] = { l.v0, l.v1, l.v2 };
+            for (int k = 0; k < 3; ++k)
+                for (int r = 0; r < 3; ++r)
+                    dst[k][r] = static_cast<float>(in.frame[r][0] * V[k][0] + in.frame[r][1] * V[k][1] + in.frame[r][2] * V[k][2]);
+            l.instance = 0;
+            l.primitive = static_cast<uint32_t>(base + i);
+            l.flip_facing = 0;
+            in.world[base + i] = rec;
         }
-        BuildTriangle l;
-        float* dst[3] = { l.v0, l.v1, l.v2 };
-        for (int k = 0; k < 3; ++k)
-            for (int r = 0; r < 3; ++r)
-                dst[k][r] = static_cast<float>(in.frame[r][0] * V[k][0] + in.frame[r][1] * V[k][1] + in.frame[r][2] * V[k][2]);
-        l.instance = 0;
-        l.primitive = static_cast<uint32_t>(in.world.size());
-        l.flip_facing = 0;
-        in.tris.push_back(l);
-        in.world.push_back(rec);
-    }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (std::thread& th : pool) th.join();
+    for (float m : maxAbs) in.maxAbs = std::max(in.maxAbs, m);
 }
 
 bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8CollapseOptions& copt, Bvh8BuildResult& out)

@@ -76,6 +76,7 @@ struct Bvh8CollapseOptions {
     // 0-2: in slots 0, 1, ... by their box's lower bound along that axis (a BVH that
     // only rays along +axis traverse: the sun's light-space BVH, slot order = octant 0)
     int slot_sort_axis = -1;
+    int threads = 0; // subtrees collapsed in parallel (0 = hardware concurrency)
 };
 Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& opt);
 
@@ -109,7 +110,7 @@ struct SunBvhInput {
     float maxAbs = 0.0f;              // largest |world coordinate|
 };
 void sun_frame(const float sun_dir[3], double frame[3][3]);
-void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_tris);
+void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_tris, int threads = 0);
 // Builds the BVH2 (opt; its inflation replaced by the light-space bound), the BVH8
 // (copt, slots sorted by w) and swaps in the world records; consumes in.tris and
 // in.world. False when a BVH2 leaf exceeds kBvh8MaxLeafSize.

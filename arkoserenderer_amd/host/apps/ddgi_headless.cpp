@@ -19,6 +19,10 @@
 //                                                       they wait). S is required for P > 1 (one
 //                                                       value per launch, the same on every rank)
 //                 [--save-state FILE] [--load-state FILE] [--first-frame F]
+//                 [--frame-script FILE]                 per-frame scene changes (ARKFRM1): the
+//                                                       camera exposure, the managed lights and
+//                                                       the instance transforms of each frame,
+//                                                       applied before GpuScene::update()
 //                                                       checkpoint of the (unsharded) node after the
 //                                                       last frame / before the first; frame indices
 //                                                       start at F (DDGINode::saveState/loadState)
@@ -238,6 +242,71 @@ __global__ void k_stall(uint64_t ticks)
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// Per-frame scene changes (--frame-script): "ARKFRM1\0", u32 frames, u32 instances, then
+// per frame: f32 exposure; i32 has_sun, f32 colour[3], intensity, forward[3]; u32 spots,
+// per spot f32 colour[3], intensity, forward[3], right[3], up[3], position[3], outer
+// cone angle, i32 IES LUT texture; u32 moved, and when 1 the instances' object-to-world
+// rows (12 f32 each).
+struct FrameChange {
+    float exposure = 1.0f;
+    std::optional<ManagedDirectionalLight> sun;
+    std::vector<ManagedSpotLight> spots;
+    std::vector<float> transforms; // instances x 12, empty = unchanged
+};
+
+bool loadFrameScript(const char* path, std::vector<FrameChange>& out)
+{
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return false;
+    auto rd = [&](void* p, size_t n) { return std::fread(p, 1, n, f) == n; };
+    char magic[8];
+    uint32_t frames = 0, instances = 0;
+    bool ok = rd(magic, 8) && std::memcmp(magic, "ARKFRM1\0", 8) == 0 && rd(&frames, 4) && rd(&instances, 4);
+    for (uint32_t i = 0; ok && i < frames; ++i) {
+        FrameChange c;
+        int32_t hasSun = 0;
+        float sun[7];
+        ok = rd(&c.exposure, 4) && rd(&hasSun, 4) && rd(sun, sizeof(sun));
+        if (ok && hasSun) {
+            ManagedDirectionalLight d;
+            for (int k = 0; k < 3; ++k) {
+                d.color[k] = sun[k];
+                d.forward[k] = sun[4 + k];
+            }
+            d.intensity = sun[3];
+            c.sun = d;
+        }
+        uint32_t n = 0;
+        ok = ok && rd(&n, 4) && n <= ARK_DDGI_MAX_SPOT_LIGHTS;
+        for (uint32_t l = 0; ok && l < n; ++l) {
+            float v[17];
+            int32_t ies = -1;
+            ok = rd(v, sizeof(v)) && rd(&ies, 4);
+            ManagedSpotLight sl;
+            for (int k = 0; k < 3; ++k) {
+                sl.color[k] = v[k];
+                sl.forward[k] = v[4 + k];
+                sl.right[k] = v[7 + k];
+                sl.up[k] = v[10 + k];
+                sl.position[k] = v[13 + k];
+            }
+            sl.intensity = v[3];
+            sl.outerConeAngle = v[16];
+            sl.iesLut = ies;
+            c.spots.push_back(sl);
+        }
+        uint32_t moved = 0;
+        ok = ok && rd(&moved, 4);
+        if (ok && moved) {
+            c.transforms.resize(static_cast<size_t>(instances) * 12);
+            ok = rd(c.transforms.data(), c.transforms.size() * 4);
+        }
+        out.push_back(std::move(c));
+    }
+    std::fclose(f);
+    return ok;
+}
+
 bool dump(ArkDdgiCtx* ctx, int which, const std::string& path)
 {
     uint64_t bytes = 0;
@@ -262,7 +331,7 @@ int main(int argc, char** argv)
     int shards = 1, world = 1, rank = 0;
     std::string ncclIdPath, ncclNonce;
     double exchangeTimeout = 0.0;
-    std::string saveStatePath, loadStatePath;
+    std::string saveStatePath, loadStatePath, frameScriptPath;
     int firstFrame = 0;
     bool deadlineTest = false;
     const std::time_t startedAt = std::time(nullptr);
@@ -299,6 +368,7 @@ int main(int argc, char** argv)
         else if (a == "--save-state") saveStatePath = next();
         else if (a == "--load-state") loadStatePath = next();
         else if (a == "--first-frame") firstFrame = std::atoi(next());
+        else if (a == "--frame-script") frameScriptPath = next();
         else ARKOSE_LOG(Fatal, "unknown argument %s", a.c_str());
     }
     SceneFile file;
@@ -403,7 +473,22 @@ int main(int argc, char** argv)
         if (!nodeOf(*pipelines[0])->loadState(blob)) ARKOSE_LOG(Fatal, "DDGINode::loadState failed");
         std::printf("ddgi_headless: resumed at probe %d\n", nodeOf(*pipelines[0])->probeUpdateIdx());
     }
+    std::vector<FrameChange> script;
+    if (!frameScriptPath.empty() && !loadFrameScript(frameScriptPath.c_str(), script)) ARKOSE_LOG(Fatal, "cannot read frame script %s", frameScriptPath.c_str());
     for (int f = firstFrame; f < firstFrame + frames; ++f) {
+        if (static_cast<size_t>(f - firstFrame) < script.size()) {
+            // this frame's camera exposure, lights and instance transforms
+            const FrameChange& c = script[static_cast<size_t>(f - firstFrame)];
+            scene.camera().setExposure(c.exposure);
+            scene.setManagedLights(c.sun, c.spots);
+            for (size_t i = 0; i < c.transforms.size() / 12; ++i) {
+                float m[16];
+                for (int r = 0; r < 4; ++r)
+                    for (int col = 0; col < 4; ++col) m[col * 4 + r] = r < 3 ? c.transforms[i * 12 + r * 4 + col] : (col == 3 ? 1.0f : 0.0f);
+                scene.setInstanceTransform(i, m);
+            }
+        }
+        scene.update(); // GpuScene::update: the exposure and light data of this frame
         if (f == rebuildAt) {
             // pipeline rebuild (VulkanBackend::reconstructRenderPipelineResources,
             // VulkanBackend.cpp:2327-2347): same nodes, new Registry that adopts the

@@ -92,9 +92,30 @@ void GpuScene::setLightData(std::vector<DirectionalLightData> directional, std::
 {
     m_dirLightData = std::move(directional);
     m_spotLightData = std::move(spots);
+    m_lightsManaged = false;
 }
 
-const ArkDdgiScene& GpuScene::rtScene()
+void GpuScene::setManagedLights(std::optional<ManagedDirectionalLight> directional, std::vector<ManagedSpotLight> spots)
+{
+    m_directional = directional;
+    m_spots = std::move(spots);
+    m_lightsManaged = true;
+}
+
+void GpuScene::setInstanceTransform(size_t index, const float worldMatrix[16])
+{
+    if (index >= m_instances.size()) ARKOSE_LOG(Fatal, "GpuScene: no static mesh instance %zu", index);
+    std::memcpy(m_instances[index].worldMatrix, worldMatrix, sizeof(m_instances[index].worldMatrix));
+    ++m_instanceVersion;
+}
+
+void GpuScene::update()
+{
+    // m_lightPreExposure = camera().exposure() (:792), then the light buffers (:795-858)
+    if (m_lightsManaged) updateLightData();
+}
+
+void GpuScene::buildRtInstances()
 {
     // GpuScene.cpp:872-929 (the TLAS update): every LOD of every static mesh instance,
     // every segment whose BLAS exists, becomes one RT mesh (firstVertex, firstIndex,
@@ -131,6 +152,10 @@ const ArkDdgiScene& GpuScene::rtScene()
             }
         }
     }
+}
+
+void GpuScene::buildArkLights()
+{
     // SceneLightSet (lighting.glsl:8-17): at most one directional light (GpuScene.cpp:797)
     if (m_dirLightData.size() > 1) ARKOSE_LOG(Fatal, "GpuScene: we only support 0 or 1 directional lights in a scene");
     m_arkSpots.clear();
@@ -147,6 +172,35 @@ const ArkDdgiScene& GpuScene::rtScene()
         a.ies_profile_index = s.iesProfileIndex;
         m_arkSpots.push_back(a);
     }
+}
+
+const std::vector<ArkRTInstance>& GpuScene::rtInstances()
+{
+    buildRtInstances();
+    return m_rtInstances;
+}
+
+const ArkDdgiLights& GpuScene::rtLights()
+{
+    buildArkLights();
+    ArkDdgiLights& v = m_lightsView;
+    std::memset(&v, 0, sizeof(v));
+    v.struct_size = sizeof(ArkDdgiLights);
+    v.has_directional_light = m_dirLightData.empty() ? 0 : 1;
+    if (!m_dirLightData.empty())
+        for (int k = 0; k < 3; ++k) {
+            v.directional_light.color[k] = m_dirLightData[0].color[k];
+            v.directional_light.world_space_direction[k] = m_dirLightData[0].worldSpaceDirection[k];
+        }
+    v.spot_lights = m_arkSpots.data();
+    v.spot_light_count = static_cast<uint32_t>(m_arkSpots.size());
+    return v;
+}
+
+const ArkDdgiScene& GpuScene::rtScene()
+{
+    buildRtInstances();
+    buildArkLights();
     ArkDdgiScene& v = m_view;
     std::memset(&v, 0, sizeof(v));
     v.struct_size = sizeof(ArkDdgiScene);

@@ -138,16 +138,32 @@ public:
     void addStaticMeshInstance(const StaticMeshInstance& instance);
     void setEnvironmentMap(int32_t textureHandle) { m_environmentTexture = textureHandle; }  // -1: the 1x1 white default
 
-    void setDirectionalLight(const ManagedDirectionalLight& light) { m_directional = light; }
-    void addSpotLight(const ManagedSpotLight& light) { m_spots.push_back(light); }
+    void setDirectionalLight(const ManagedDirectionalLight& light) { m_directional = light; m_lightsManaged = true; }
+    void addSpotLight(const ManagedSpotLight& light) { m_spots.push_back(light); m_lightsManaged = true; }
+    // the scene's lights as they are this frame (a light that moved, turned or changed colour)
+    void setManagedLights(std::optional<ManagedDirectionalLight> directional, std::vector<ManagedSpotLight> spots);
     // GpuScene::update's light data from the managed lights (GpuScene.cpp:790-858)
     void updateLightData();
-    // light data recorded as uploaded (a loader of captured frames)
+    // light data recorded as uploaded (a loader of captured frames); replaces the managed lights
     void setLightData(std::vector<DirectionalLightData> directional, std::vector<SpotLightData> spots);
+    // Transform::setWorldMatrix of instance i (column-major ark::mat4): the TLAS instance
+    // data of the next frame changes (GpuScene.cpp:901-928)
+    void setInstanceTransform(size_t index, const float worldMatrix[16]);
+    uint32_t instanceVersion() const { return m_instanceVersion; }
+
+    // The per-frame part of GpuScene::update (GpuScene.cpp:790-1009): the exposure is read
+    // (:792) and the light data re-computed from the managed lights with it (recorded
+    // light data stays as recorded); the TLAS instance data follow the transforms
+    // (rtInstances()).
+    void update();
 
     // The adapter: the C-ABI scene view of this GpuScene (valid until the next change).
     const ArkDdgiScene& rtScene();
     uint32_t rtMeshCount() const { return static_cast<uint32_t>(m_rtMeshes.size()); }
+    // this frame's light set for ark_ddgi_set_lights (valid until the next call)
+    const ArkDdgiLights& rtLights();
+    // this frame's TLAS instances (GpuScene.cpp:901-928) for ark_ddgi_set_instances
+    const std::vector<ArkRTInstance>& rtInstances();
 
 private:
     HipBackend& m_backend;
@@ -166,9 +182,14 @@ private:
     std::vector<ManagedSpotLight> m_spots;
     std::vector<DirectionalLightData> m_dirLightData;
     std::vector<SpotLightData> m_spotLightData;
+    bool m_lightsManaged { false }; // update() recomputes the light data from the managed lights
+    uint32_t m_instanceVersion { 0 };
     // adapter output
+    void buildRtInstances(); // m_rtMeshes + m_rtInstances from the instances
+    void buildArkLights();   // m_arkSpots from the light data
     std::vector<ArkRTTriangleMesh> m_rtMeshes;
     std::vector<ArkRTInstance> m_rtInstances;
     std::vector<ArkSpotLight> m_arkSpots;
     ArkDdgiScene m_view {};
+    ArkDdgiLights m_lightsView {};
 };

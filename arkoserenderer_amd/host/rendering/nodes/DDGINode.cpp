@@ -97,6 +97,7 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
         ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_scene failed (%d): %s", rc, ark_ddgi_last_error(ctx));
         return RenderPipelineNode::NullExecuteCallback;
     }
+    m_instanceVersion = scene.instanceVersion(); // set_scene built the BVHs at these transforms
 
     ArkDdgiDeviceViews views {};
     ark_ddgi_get_device_views(ctx, &views);
@@ -133,6 +134,21 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
         p.environment_multiplier = scene.preExposedEnvironmentBrightnessFactor();
         p.delta_time = appState.deltaTime();
         p.update_offsets = (m_computeProbeOffsets && m_applyProbeOffsets) ? 1 : 0;
+        // GpuScene::update's per-frame uploads, which the reference's trace reads through
+        // the SceneLightSet and the TLAS: the light buffers with this frame's
+        // pre-exposure (GpuScene.cpp:792-858; the context keeps its device copy when
+        // nothing changed), and the TLAS instance data + build when a transform moved
+        // (:872-1009; here a device refit of the flattened BVHs - the reference's full
+        // build every 60 frames only restores tightness, which construct()'s set_scene
+        // does on a pipeline rebuild)
+        if (int rc = ark_ddgi_set_lights(ctx, &scene.rtLights()); rc != ARK_DDGI_OK)
+            ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_lights failed (%d): %s", rc, ark_ddgi_last_error(ctx));
+        if (scene.instanceVersion() != m_instanceVersion) {
+            const std::vector<ArkRTInstance>& instances = scene.rtInstances();
+            if (int rc = ark_ddgi_set_instances(ctx, instances.data(), static_cast<uint32_t>(instances.size())); rc != ARK_DDGI_OK)
+                ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_instances failed (%d): %s", rc, ark_ddgi_last_error(ctx));
+            m_instanceVersion = scene.instanceVersion();
+        }
         if (m_exchange) {
             // Z-slab rank: traversal goes ahead, shading waits for the previous exchange;
             // this update's bands are then exchanged on the exchange's side stream

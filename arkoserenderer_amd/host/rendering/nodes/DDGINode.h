@@ -67,6 +67,7 @@ private:
     int m_shardRank { 0 };
     int m_shardCount { 1 };
     ArkDdgiCtx* m_ctx { nullptr };
+    uint32_t m_instanceVersion { 0 }; // GpuScene::instanceVersion() the context's BVHs follow
     SlabExchange* m_exchange { nullptr };
     void* m_updateDone { nullptr };      // hipEvent_t recorded after each update
     void* m_exchangePending { nullptr }; // hipEvent_t of the last exchange

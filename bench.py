@@ -551,7 +551,8 @@ def sun_bvh_info(bvh):
     """set_scene's choice for the sun's shadow rays: the light-space BVH8 (its nodes) or
     the world BVHs, with the sampled any-hit steps per sun shadow ray of both."""
     return {"light_space": bool(bvh.sun_node_count), "sampled_steps_world": round(bvh.sun_cost_world, 2),
-            "sampled_steps_light": round(bvh.sun_cost_light, 2)}
+            "sampled_steps_light": round(bvh.sun_cost_light, 2),
+            "build_ms": round(bvh.sun_build_ms, 1)}
 
 
 def cpu_cores():

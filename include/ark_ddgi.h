@@ -372,9 +372,16 @@ int ark_ddgi_synchronize(ArkDdgiCtx* ctx);
  * default 10,000 ms). A wait that gives up FAILS CLOSED: every update kernel that
  * starts after it skips (atlases, surfels and offsets are left as they were; a
  * launch already running completes), and the next ark_ddgi_update,
- * ark_ddgi_exchange_begin or ark_ddgi_synchronize drains the device, returns
+ * ark_ddgi_exchange_begin or ark_ddgi_synchronize drains the device (all of it: the
+ * late producer may be on a caller's stream the context does not know), returns
  * ARK_DDGI_E_DEVICE and switches the context to events; the calls after it run
- * normally. ark_ddgi_get_sequencing reports the mode, the bound and the number of
+ * normally. The dropped frame's surfels and atlases are untouched; its primary
+ * traversal and probe offsets ran on the traversal stream before the failed wait, so
+ * its offsets stay applied and the rolling window has moved past it (the next
+ * first_probe_index the node passes is unchanged). A Z-slab rank that gets
+ * ARK_DDGI_E_DEVICE has dropped a frame the other ranks applied: a multi-rank caller
+ * treats it as fatal (or gets every rank to agree before going on), else the ranks'
+ * atlases diverge. ark_ddgi_get_sequencing reports the mode, the bound and the number of
  * timeouts reported so far. A context created under a counter-collecting profiler
  * (ROCPROF_COUNTER_COLLECTION set: kernels run one at a time across queues) starts
  * with events. */

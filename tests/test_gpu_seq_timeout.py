@@ -7,6 +7,13 @@ context's timed-out word at entry and leave their outputs untouched, the next
 context call reports ARK_DDGI_E_DEVICE and switches the context to events, and the
 frames after it are bit-exact again.
 
+What a dropped frame leaves behind (ark_ddgi_set_sequencing's contract):
+its traversal and probe offsets run on the traversal stream before the wait that
+gives up, so with offsets on its offsets are applied and the rolling window moves past
+it; its surfels and both atlases are untouched. The offsets case pins exactly that:
+the reference runs the dropped frame in full and then restores the atlases it had
+before it.
+
 The stall: the Z-slab exchange's stream (ark_ddgi_exchange_begin / _end) runs a
 bounded ~1.5 s kernel (torch.cuda._sleep) before exchange_end, so the next
 update's shading wait (bounded at 100 ms here) gives up. The exchange stream is a
@@ -26,12 +33,13 @@ pytestmark = pytest.mark.gpu
 READ = (abi.ARK_DDGI_SURFELS, abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS)
 
 
-def _setup():
+def _setup(offsets=False):
     sc, ex = S.cornell_box()
     grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
-    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, max_rays_per_probe=64, max_probe_updates=512,
-                       compute_probe_offsets=False)
-    params = [D.frame_params(cfg, grid, D.AppState(f), 0, light_pre_exposure=ex["light_pre_exposure"],
+    K = 200 if offsets else 512  # offsets: a rolling window K < N, as the node advances it
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=K, max_rays_per_probe=64, max_probe_updates=512,
+                       compute_probe_offsets=offsets)
+    params = [D.frame_params(cfg, grid, D.AppState(f), (f * K) % 512, light_pre_exposure=ex["light_pre_exposure"],
                              environment_brightness=ex["environment_brightness"]) for f in range(5)]
     ctx = D.DDGIContext(grid, ex["z_far"], cfg, device=0)
     ctx.set_scene(sc)
@@ -40,11 +48,11 @@ def _setup():
     return ctx, ref, params
 
 
-@pytest.mark.parametrize("observer", ["update", "synchronize"])
-def test_seq_wait_timeout_fails_closed(observer):
+@pytest.mark.parametrize("observer,offsets", [("update", False), ("synchronize", False), ("update", True)])
+def test_seq_wait_timeout_fails_closed(observer, offsets):
     import torch
 
-    ctx, ref, params = _setup()
+    ctx, ref, params = _setup(offsets)
     try:
         ctx.set_sequencing(True, 100)
         assert ctx.sequencing() == {"device_sequence_words": True, "timeout_ms": 100, "timeouts": 0}
@@ -81,8 +89,18 @@ def test_seq_wait_timeout_fails_closed(observer):
         frame(3)
         frame(4)
         ctx.synchronize()
-        # frame 2 dropped: the reference runs frames 0, 1, 3, 4
-        for f in (0, 1, 3, 4):
+        # frame 2 dropped: the reference runs frames 0, 1, 3, 4 - with offsets, frame 2
+        # too, followed by a restore of the atlases frame 1 left (its offsets stay)
+        for f in (0, 1):
+            ref.update(params[f])
+        if offsets:
+            ref.synchronize()
+            keep = {w: ref.read(w) for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY)}
+            ref.update(params[2])
+            ref.synchronize()
+            for w, a in keep.items():
+                ref.write(w, a)
+        for f in (3, 4):
             ref.update(params[f])
         ref.synchronize()
         for which in READ:
