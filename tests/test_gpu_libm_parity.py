@@ -30,7 +30,16 @@ ST = (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI
 
 
 def _report(name, frame, st):
+    """The full statistics, then one line with the clean-probe and all-probe atlas
+    figures side by side (the all-probe ones include the probes with a
+    flipped ray, where no tolerance is asserted)."""
     print(f"LIBM {name} frame {frame}: " + json.dumps(st), flush=True)
+    c, a = st["clean"], st["all"]
+    print(f"LIBM-SUMMARY {name} frame {frame}: flipped {st['flipped_rays']}/{st['rays']} rays; "
+          f"irradiance L-inf clean {c['irradiance']['linf']:.3g} / all {a['irradiance']['linf']:.3g}, "
+          f"within 1 ulp clean {c['irradiance']['within_1ulp_frac']:.5f} / all {a['irradiance']['within_1ulp_frac']:.5f}; "
+          f"visibility within 1e-3 clean {c['visibility']['within_rel_tol_frac']:.5f} / all {a['visibility']['within_rel_tol_frac']:.5f} "
+          f"(probes clean {c['probes']} / all {a['probes']})", flush=True)
 
 
 def _whole_grid(name, sc, grid, cfg, frames, z_far, exposure):
@@ -72,6 +81,53 @@ def test_cornell_c2_vs_libm_oracle():
                        max_rays_per_probe=64, max_probe_updates=512)
     _whole_grid("C2", sc, grid, cfg, 4, ex["z_far"], dict(light_pre_exposure=ex["light_pre_exposure"],
                                                            environment_brightness=ex["environment_brightness"]))
+
+
+# Drift bounds of the free-running C2 run (not SURVEY §8(d)'s one-frame tolerances,
+# which the frame-local cases above assert): measured 8-frame figures are quoted in
+# DESIGN.md §4; these only catch a divergence that grows without bound.
+DRIFT_IRR_LINF = 0.05
+DRIFT_WITHIN_1ULP = 0.9
+
+
+def test_cornell_c2_free_running_drift():
+    """C2, 8 frames, the libm oracle NOT re-seeded: both start from a
+    reset history and each runs from its own state, so a last-bit difference of one
+    frame is carried into the next frames through the indirect bounce (the surfels'
+    irradiance lookups read the previous frame's atlases, probeSampling.glsl:64-163).
+    Prints the drift per frame against SURVEY §8(d)'s tolerances (all probes)."""
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False,
+                       max_rays_per_probe=64, max_probe_updates=512)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    ctx = D.DDGIContext(grid, ex["z_far"], cfg)
+    ctx.set_scene(sc)
+    orc = O.Oracle(ctx.desc, libm=True)
+    orc.set_scene(sc, threads=16)
+    N, R = grid.probe_count(), cfg.rays_per_probe
+    rows = []
+    try:
+        for f in range(8):
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            ctx.update(p)
+            ctx.synchronize()
+            orc.update(p, threads=16)
+            shape = (cfg.max_probe_updates, cfg.max_rays_per_probe, 4)
+            sg = ctx.read(abi.ARK_DDGI_SURFELS).reshape(shape)[:N, :R]
+            so = orc.read(abi.ARK_DDGI_SURFELS).reshape(shape)[:N, :R]
+            st = L.compare_window(grid.grid_dimensions, np.arange(N), sg, so, ctx.read(ST[0]), orc.read(ST[0]), ctx.read(ST[1]), orc.read(ST[1]))
+            _report("C2-free", f, st)
+            a = st["all"]
+            rows.append((f, st["flipped_rays"], a["irradiance"]["linf"], a["irradiance"]["within_1ulp_frac"], a["visibility"]["within_rel_tol_frac"]))
+    finally:
+        ctx.close()
+        orc.close()
+    print("LIBM-DRIFT C2 (frame, flipped rays, irradiance L-inf, within 1 ulp, visibility within 1e-3; all probes; "
+          f"one-frame tolerances L-inf < {L.IRR_TOL_LINF}, >= {L.ULP_FRACTION}): " + json.dumps(rows), flush=True)
+    for f, _, linf, ulp, _ in rows:
+        assert np.isfinite(linf) and linf < DRIFT_IRR_LINF, rows
+        assert ulp >= DRIFT_WITHIN_1ULP, rows
 
 
 def test_features_scene_vs_libm_oracle():

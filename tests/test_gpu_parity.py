@@ -135,3 +135,49 @@ def test_sun_structure_forced(monkeypatch, sun_bvh):
                        max_rays_per_probe=256, max_probe_updates=512)
     reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
     _assert_exact(reps)
+
+
+def test_inf_radiance_surfels():
+    """Non-finite radiance through the probe update. One Cornell
+    material emits 1e9 x its colour, past fp16's range: its surfels store +inf
+    radiance. The irradiance blend adds every ray of a texel, weight max(0, dot)
+    (probeUpdateIrradiance.comp:41-50), so a texel facing away from such a ray adds
+    fma(+0, inf) = NaN, as the reference's sequential loop does, and that NaN reaches
+    the next frames through the indirect lookups. Nothing may skip a zero-weight ray:
+    bit-exact against the oracle (NaN == NaN), and the oracle's own outputs must hold
+    inf surfels (frame 0) and NaN irradiance texels (the case is not vacuous).
+    Offsets on: a back-face count or a distance sum over NaN must agree too."""
+    sc, ex = S.cornell_box()
+    sc.materials["emissive_factor"][0] = (1e9, 1e9, 1e9)
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=512)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    import oracle_lib as O
+    from parity import RESOURCES, diff_report
+
+    ctx = D.DDGIContext(grid, ex["z_far"], cfg)
+    ctx.set_scene(sc)
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(sc, 8)
+    try:
+        for f in range(3):
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            ctx.update(p)
+            ctx.synchronize()
+            orc.update(p, 8)
+            for k, w in RESOURCES.items():
+                r = diff_report(k, ctx.read(w), orc.read(w))
+                assert r["mismatch"] == 0, f"frame {f}: {r}"
+            surf = O.f16_to_f32(orc.read(abi.ARK_DDGI_SURFELS)).reshape(-1, 4)
+            irr = O.f16_to_f32(orc.read(abi.ARK_DDGI_ATLAS_IRRADIANCE))
+            # frame 0: 12 % of the surfels +inf, half the irradiance texels NaN; later
+            # frames: the NaN atlases make most surfels NaN through the indirect term
+            if f == 0:
+                assert np.isposinf(surf[:, :3]).any(), "no inf surfel"
+            else:
+                assert np.isnan(surf).any(), f"frame {f}: no NaN surfel"
+            assert np.isnan(irr).any(), f"frame {f}: no NaN irradiance texel"
+    finally:
+        ctx.close()
+        orc.close()

@@ -1,0 +1,82 @@
+"""Cost of the per-frame instance update (ark_ddgi_set_instances) at
+C4 (10 M-triangle soup, 16 instances, 32^3 x 256) and the C3 substitute: the refit's
+wall time and its device part (ArkDdgiBvhStats.refit_ms), and the update throughput
+before and after - one instance moved by 0.5 m, then every instance rotated by 2 deg
+about y (the refit keeps the topology, so the boxes loosen with the motion).
+
+    python tools/refit_cost.py [--config c4 c3] [--steps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def build(name):
+    from arkoserenderer_amd import ddgi as D
+    from arkoserenderer_amd import scene as S
+    if name == "c4":
+        return S.soup(10_000_000), D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0)), 256, 10000.0
+    return S.sponza_substitute(), D.ProbeGrid(*S.sponza_substitute_grid()), 256, 10000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", nargs="+", default=["c4", "c3"])
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from arkoserenderer_amd import ddgi as D
+
+    torch.cuda.set_device(0)
+    for name in args.config:
+        sc, grid, R, zf = build(name)
+        N = grid.probe_count()
+        cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+        node = D.DDGINode(cfg)
+        node.construct(sc, grid, zf, light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
+        app = [D.AppState(0)]
+
+        def rate():
+            for _ in range(2):
+                node.execute(app[0])
+                app[0] = D.AppState(app[0].frame_index + 1)
+            node.ctx.synchronize()
+            t = time.perf_counter()
+            for _ in range(args.steps):
+                node.execute(app[0])
+                app[0] = D.AppState(app[0].frame_index + 1)
+            node.ctx.synchronize()
+            return N * R * args.steps / (time.perf_counter() - t) / 1e6
+
+        out = {"config": name, "triangles": int(sc.triangle_count), "instances": int(sc.instances.size),
+               "build_ms": round(node.ctx.bvh_stats().build_ms, 1), "mrays_per_s_static": round(rate(), 1)}
+        inst = sc.instances.copy()
+        moves = []
+        inst["object_to_world"][0, 3] += 0.5
+        c, s_ = np.cos(np.radians(2.0)), np.sin(np.radians(2.0))
+        rot = np.array([[c, 0, s_], [0, 1, 0], [-s_, 0, c]], np.float32)
+        for label in ("one_moved", "all_rotated"):
+            if label == "all_rotated":
+                m = inst["object_to_world"].reshape(-1, 3, 4)
+                m[:] = np.einsum("ij,njk->nik", rot, m)
+                inst["object_to_world"] = m.reshape(-1, 12)
+            node.ctx.synchronize()
+            t = time.perf_counter()
+            node.ctx.set_instances(inst)
+            wall = (time.perf_counter() - t) * 1e3
+            st = node.ctx.bvh_stats()
+            moves.append({"move": label, "set_instances_ms": round(wall, 2), "refit_ms": round(st.refit_ms, 2), "mrays_per_s": round(rate(), 1)})
+        out["refits"] = moves
+        print(json.dumps(out), flush=True)
+        node.ctx.close()
+
+
+if __name__ == "__main__":
+    main()
