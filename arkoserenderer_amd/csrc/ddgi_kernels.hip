@@ -1357,42 +1357,6 @@ __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* orig
     *dir = rotate(v3(fb.x, fb.y, fb.z), v3(ps.axis[0], ps.axis[1], ps.axis[2]), ps.angle_sin, ps.angle_cos);
 }
 
-// The IES lookup of a spot light (evaluateIESLookupTable, lighting.glsl:20-39) split in
-// two: iesFetch issues the four texel loads (only the profile's red channel is used),
-// iesFilter blends them - so the loads of every lit spot of a group are in flight
-// before the first one is filtered. The texture's info comes from LDS (iesInfoL), its
-// _pad word set when the spot's profile resolves to the 1x1 white default.
-struct IesFetch {
-    float t00, t10, t01, t11, fx, fy;
-};
-
-__device__ __forceinline__ IesFetch iesFetch(const GpuTextureInfo& ti, const float4* __restrict__ texels, float u, float v)
-{
-    IesFetch r;
-    const float x = u * static_cast<float>(ti.width) - 0.5f;
-    const float y = v * static_cast<float>(ti.height) - 0.5f;
-    const float x0f = floorf_(x), y0f = floorf_(y);
-    r.fx = x - x0f;
-    r.fy = y - y0f;
-    const int x0 = static_cast<int>(x0f), y0 = static_cast<int>(y0f);
-    const int ws = ti.wrap & 0xf, wt = (ti.wrap >> 4) & 0xf;
-    const int xa = wrapCoord(x0, ti.width, ws), xb = wrapCoord(x0 + 1, ti.width, ws);
-    const int ya = wrapCoord(y0, ti.height, wt), yb = wrapCoord(y0 + 1, ti.height, wt);
-    const float* base = reinterpret_cast<const float*>(texels + ti.texel_offset);
-    r.t00 = base[4 * (static_cast<size_t>(ya) * ti.width + xa)];
-    r.t10 = base[4 * (static_cast<size_t>(ya) * ti.width + xb)];
-    r.t01 = base[4 * (static_cast<size_t>(yb) * ti.width + xa)];
-    r.t11 = base[4 * (static_cast<size_t>(yb) * ti.width + xb)];
-    return r;
-}
-
-__device__ __forceinline__ float iesFilter(const IesFetch& t) { return lerpf(lerpf(t.t00, t.t10, t.fx), lerpf(t.t01, t.t11, t.fx), t.fy); }
-
-#ifndef ARK_IES_GROUP
-#define ARK_IES_GROUP 2
-#endif
-constexpr int kIesGroup = ARK_IES_GROUP; // spot lights whose IES loads are issued together
-
 template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
@@ -1400,21 +1364,14 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
     __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
     __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
     uint32_t cFront = 0;
-    // the spot lights and their IES textures' infos, read once per workgroup: per front
-    // hit and lit spot they were a dependent 96-B read ahead of the IES lookup (C5:
-    // k_shade 2.06 -> 1.97 ms, +1.2 %; profiles/r04_s_shade_spots_lds.log)
+    // the spot lights, read once per workgroup: per front hit and lit spot they were a
+    // dependent 96-B read ahead of the IES lookup (C5: k_shade 2.06 -> 1.97 ms, +1.2 %;
+    // profiles/r04_s_shade_spots_lds.log)
     __shared__ GpuSpotLight spotsL[kMaxLights - 1];
-    __shared__ GpuTextureInfo iesInfoL[kMaxLights - 1];
     {
         const uint32_t words = static_cast<uint32_t>(sc.spot_count) * static_cast<uint32_t>(sizeof(GpuSpotLight) / 4u);
         for (uint32_t i = threadIdx.x; i < words; i += kShadeBlock)
             reinterpret_cast<uint32_t*>(spotsL)[i] = reinterpret_cast<const uint32_t*>(sc.spots)[i];
-        if (threadIdx.x < static_cast<uint32_t>(sc.spot_count)) {
-            const int r = sc.resolveTexture(sc.spots[threadIdx.x].ies_texture);
-            GpuTextureInfo ti = sc.tex_infos[r];
-            ti._pad = r == sc.white_texture ? 1 : 0;
-            iesInfoL[threadIdx.x] = ti;
-        }
         __syncthreads();
     }
 
@@ -1526,66 +1483,35 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
                 }
                 l++;
             }
-            for (int g = 0; g < sc.spot_count; g += kIesGroup) { // opaque.rchit:75-103
-                // the IES loads of the group's lit spots first, then each spot's term in
-                // light order
-                IesFetch tf[kIesGroup];
-                float atten[kIesGroup];
-                uint32_t iesState[kIesGroup]; // 0: angleV <= 0 (value 0), 1: fetched, 2: white default (value 1)
-#pragma unroll
-                for (int j = 0; j < kIesGroup; ++j) {
-                    const int li = g + j;
-                    iesState[j] = 0u;
-                    atten[j] = 0.0f;
-                    if (li >= sc.spot_count || !((need >> (l + j)) & 1u)) continue;
-                    const GpuSpotLight& sl = spotsL[li];
-                    const V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
-                    const V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
-                    const float distanceToLight = length(toLight);
-                    const V3 normalizedToLight = toLight / distanceToLight;
-                    atten[j] = 1.0f / square(distanceToLight);
-                    // evaluateIESLookupTable (lighting.glsl:20-39)
-                    const V3 lrd = -normalizedToLight;
-                    const float angleV = dot(lrd, sdir);
-                    if (!(angleV <= 0.0f)) {
-                        const float hx = dot(lrd, v3(sl.right[0], sl.right[1], sl.right[2]));
-                        const float hy = dot(lrd, v3(sl.up[0], sl.up[1], sl.up[2]));
-                        const float angleH = atan2f_(hy, hx) + kPi;
-                        const float lx = acosf_(angleV) / (2.0f * sl.position[3]);
-                        const float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
-                        const GpuTextureInfo& ti = iesInfoL[li];
-                        // SceneArgs::sample's white shortcut: exactly 1 for finite coordinates
-                        if (ti._pad && fabsf(lx) < INFINITY && fabsf(ly) < INFINITY) {
-                            iesState[j] = 2u;
-                        } else {
-                            tf[j] = iesFetch(ti, sc.texels, lx, ly);
-                            iesState[j] = 1u;
+            for (int li = 0; li < sc.spot_count; ++li, ++l) { // opaque.rchit:75-103
+                if (!((need >> l) & 1u)) continue;
+                const GpuSpotLight sl = spotsL[li];
+                V3 sdir = v3(sl.direction[0], sl.direction[1], sl.direction[2]);
+                V3 Ld = -normalize(sdir);
+                float LdotN = dot(Ld, N);
+                {
+                        V3 toLight = v3(sl.position[0], sl.position[1], sl.position[2]) - hitPoint;
+                        float distanceToLight = length(toLight);
+                        V3 normalizedToLight = toLight / distanceToLight;
+                        float distanceAttenuation = 1.0f / square(distanceToLight);
+                        // evaluateIESLookupTable (lighting.glsl:20-39)
+                        V3 lrd = -normalizedToLight;
+                        float iesValue = 0.0f;
+                        float angleV = dot(lrd, sdir);
+                        if (!(angleV <= 0.0f)) {
+                            float hx = dot(lrd, v3(sl.right[0], sl.right[1], sl.right[2]));
+                            float hy = dot(lrd, v3(sl.up[0], sl.up[1], sl.up[2]));
+                            float angleH = atan2f_(hy, hx) + kPi;
+                            float lx = acosf_(angleV) / (2.0f * sl.position[3]);
+                            float ly = clampf(angleH / kTwoPi, 0.0f, 1.0f);
+                            iesValue = sc.sample(sl.ies_texture, lx, ly).x;
                         }
-                    }
+                        V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
+                        V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
+                        V3 tT = brdf * LdotN * (lc * 1.0f * distanceAttenuation * iesValue);
+                        V3 tZ = brdf * LdotN * (lc * 0.0f * distanceAttenuation * iesValue);
+                    color = color + ((occ >> l) & 1u ? tZ : tT);
                 }
-                float ies[kIesGroup];
-#pragma unroll
-                for (int j = 0; j < kIesGroup; ++j)
-                    ies[j] = iesState[j] == 1u ? iesFilter(tf[j]) : (iesState[j] == 2u ? 1.0f : 0.0f);
-                // one BRDF body for the group (unrolled, four of them spill)
-#pragma unroll 1
-                for (int j = 0; j < kIesGroup; ++j) {
-                    const int li = g + j;
-                    if (li >= sc.spot_count || !((need >> (l + j)) & 1u)) continue;
-                    float iesValue = ies[0], at = atten[0];
-#pragma unroll
-                    for (int i = 1; i < kIesGroup; ++i)
-                        if (j == i) { iesValue = ies[i]; at = atten[i]; }
-                    const GpuSpotLight& sl = spotsL[li];
-                    const V3 Ld = -normalize(v3(sl.direction[0], sl.direction[1], sl.direction[2]));
-                    const float LdotN = dot(Ld, N);
-                    const V3 brdf = evaluateDefaultBRDF(Ld, V, N, baseColor, roughness, metallic, clearcoat, ccRough);
-                    const V3 lc = v3(sl.color[0], sl.color[1], sl.color[2]);
-                    const V3 tT = brdf * LdotN * (lc * 1.0f * at * iesValue);
-                    const V3 tZ = brdf * LdotN * (lc * 0.0f * at * iesValue);
-                    color = color + ((occ >> (l + j)) & 1u ? tZ : tT);
-                }
-                l += kIesGroup;
             }
             // raygen.rgen:125-127 + evaluateIndirectLightFromPreviousFrame (:94-106)
             const V3 Vi = -dir;
