@@ -102,12 +102,6 @@ __device__ __forceinline__ float visWeightAbs(float a, float sharp, int ns)
     return a > 0.0f ? powf_pos_(a, sharp) : 0.0f;
 }
 
-// ARK_UPDATE_ALIAS (A/B knob): 1 = the tiles alias the ray staging (written after a
-// barrier that ends every wave's loop), 2 = also no LDS copy of the squared distances
-// (the visibility loop squares r.w itself)
-#ifndef ARK_UPDATE_ALIAS
-#define ARK_UPDATE_ALIAS 0
-#endif
 struct UpdateLds {
     float4* ray;    // [P][R + pad]  rotated direction + clamped distance
     float* d2;      // [P][R + pad]  clamped distance squared
@@ -127,15 +121,10 @@ __device__ __forceinline__ UpdateLds updateLds(uint32_t R)
     p += sizeof(float4) * kUpdateProbes * L.stride;
     L.rad = reinterpret_cast<uint2*>(p);
     p += sizeof(uint2) * kUpdateProbes * L.stride;
-#if ARK_UPDATE_ALIAS
-    L.irr = reinterpret_cast<uint2*>(smem);
-    L.vis = reinterpret_cast<uint32_t*>(smem + sizeof(uint2) * kUpdateProbes * 100);
-#else
     L.irr = reinterpret_cast<uint2*>(p);
     p += sizeof(uint2) * kUpdateProbes * 100;
     L.vis = reinterpret_cast<uint32_t*>(p);
     p += sizeof(uint32_t) * kUpdateProbes * 324;
-#endif
     L.d2 = reinterpret_cast<float*>(p);
     return L;
 }
@@ -143,13 +132,7 @@ __device__ __forceinline__ UpdateLds updateLds(uint32_t R)
 size_t probe_update_lds_bytes(uint32_t R)
 {
     const size_t stride = R + 4;
-#if ARK_UPDATE_ALIAS == 2
-    return kUpdateProbes * stride * (16 + 8);
-#elif ARK_UPDATE_ALIAS == 1
-    return kUpdateProbes * stride * (16 + 8 + 4);
-#else
     return kUpdateProbes * (stride * (16 + 8 + 4) + 100 * 8 + 324 * 4); // 37.6 KB at R = 256: 4 workgroups per CU
-#endif
 }
 
 // the orbit of quadrant texel (qx, qy) of a res x res tile: t, x-mirror t', antipode -t, -t'
@@ -178,12 +161,7 @@ __device__ __forceinline__ void visibilityOrbit(const UpdateLds& L, int p, uint3
 #pragma unroll 2
     for (uint32_t s = 0; s < R; ++s) {
         const float4 r = ray[s];
-#if ARK_UPDATE_ALIAS == 2
-        const float dd2 = square(r.w);
-        (void)d2;
-#else
         const float dd2 = d2[s];
-#endif
         const float px = t.x * r.x, py = t.y * r.y;
         const float d1 = fmaf(t.z, r.z, px + py);
         const float d2v = fmaf(t.z, r.z, py - px);
@@ -240,18 +218,13 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             const float a = f16_to_f32(static_cast<uint16_t>(sv.y >> 16));
             const float dd = fminf_(fabsf_(a), maxDistance);
             L.ray[p * L.stride + s] = make_float4(d.x, d.y, d.z, dd);
-#if ARK_UPDATE_ALIAS != 2
             L.d2[p * L.stride + s] = square(dd);
-#endif
             L.rad[p * L.stride + s] = sv; // fp16 as stored: converted where used (exact)
         }
     }
     __syncthreads();
     const float epsilon = 1e-9f * static_cast<float>(R);
     const int wv = tid >> 6, ln = tid & 63;
-    // the lane's 4 tile texels (index into L.vis / L.irr, value), stored after the loops
-    int tIdx[4] = { -1, -1, -1, -1 };
-    uint2 tVal[4];
     if (wv < kUpdateProbes) {
         // --- visibility of probe wv: lane = orbit of quadrant texel (ln & 7, ln >> 3)
         const uint32_t slot = slot0 + wv;
@@ -291,13 +264,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 a1 = mixf(a1, f16_to_f32(static_cast<uint16_t>(old >> 16)), f.hysteresis_visibility);
                 const uint32_t nw = static_cast<uint32_t>(f32_to_f16(a0)) | (static_cast<uint32_t>(f32_to_f16(a1)) << 16);
                 *g = nw;
-#if ARK_UPDATE_ALIAS
-                tIdx[k] = static_cast<int>(wv * 324 + (ty[k] + 1) * (VR + 2) + tx[k] + 1);
-                tVal[k] = make_uint2(nw, 0u);
-                (void)tile;
-#else
                 tile[(ty[k] + 1) * (VR + 2) + tx[k] + 1] = nw;
-#endif
             }
         }
     } else {
@@ -355,29 +322,10 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                 nw.x = static_cast<uint32_t>(f32_to_f16(newIrr.x)) | (static_cast<uint32_t>(f32_to_f16(newIrr.y)) << 16);
                 nw.y = static_cast<uint32_t>(f32_to_f16(newIrr.z)) | (static_cast<uint32_t>(f32_to_f16(0.0f)) << 16);
                 *g = nw;
-#if ARK_UPDATE_ALIAS
-                tIdx[k] = static_cast<int>(p * 100 + (ty[k] + 1) * (IR + 2) + tx[k] + 1);
-                tVal[k] = nw;
-                (void)tile;
-#else
                 tile[(ty[k] + 1) * (IR + 2) + tx[k] + 1] = nw;
-#endif
             }
         }
     }
-#if ARK_UPDATE_ALIAS
-    // the tiles overlay the staged rays: written once every wave has left its loop
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (tIdx[k] < 0) continue;
-        if (wv < kUpdateProbes) L.vis[tIdx[k]] = tVal[k].x;
-        else L.irr[tIdx[k]] = tVal[k];
-    }
-#else
-    (void)tIdx;
-    (void)tVal;
-#endif
     __syncthreads();
     // --- border texels of the updated tiles ------------------------------------
     // Tiles not updated this frame already hold border == f(interior) since their
