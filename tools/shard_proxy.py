@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--triangles", type=int, default=10_000_000)
     ap.add_argument("--all-ranks", action="store_true")
     ap.add_argument("--exchange", action="store_true", help="exchange stand-in (device copy of the received bands)")
+    ap.add_argument("--no-sun", action="store_true", help="no light: no shadow rays (a bound on what a fused shadow phase could save)")
     args = ap.parse_args()
     import torch
 
@@ -47,6 +48,8 @@ def main():
         node = D.DDGINode(cfg)
         assert node.construct(scene, grid, 10000.0, device=0, shard_rank=rank, shard_count=s,
                               light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+        if args.no_sun:
+            node.ctx.set_lights(None, ())
         sptr = torch.cuda.current_stream(dev).cuda_stream
         run = node.execute
         if args.exchange and s > 1:

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--windows", type=int, nargs="+", default=[4096, 2048])
+    ap.add_argument("--no-sun", action="store_true", help="no light (ark_ddgi_set_lights): no shadow rays - the frame without any shadow work, a bound on what a fused shadow phase could save")
     args = ap.parse_args()
     import torch
 
@@ -35,6 +36,8 @@ def main():
                        max_probe_updates=max(args.windows), compute_probe_offsets=True)
     node = D.DDGINode(cfg)
     assert node.construct(scene, grid, 10000.0, device=0, light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    if args.no_sun:
+        node.ctx.set_lights(None, ())
     sptr = torch.cuda.current_stream(dev).cuda_stream
     frame = 0
     out = {}
