@@ -14,7 +14,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <map>
 #include <memory>
 #include <string>
 #include <thread>
@@ -195,7 +194,6 @@ struct ArkDdgiCtx {
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
     bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
-    bool sunOrdered = true;        // ARK_SUN_ORDER=0: the sun's list in k_shadow_gen's order (sunOrder)
     int sunBvh = -1;               // ARK_SUN_BVH: 0 the sun's shadow rays traverse the world BVHs, 1 the light-space BVH, unset: by cost (sun_bvh_pays)
     uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined window below kPipeHalfRays rays
     bool pipeReady = false;        // the previous context operation was an update
@@ -252,12 +250,6 @@ struct ArkDdgiCtx {
     int32_t hasSun = 0;
     float sunColor[3] { 0, 0, 0 }, sunDir[3] { 0, 0, 0 };
     bool lightsDirty = false;
-    // Light-space order of the sun's shadow rays (sunOrder): per window (first, K, R) the
-    // rank of each k_shadow_gen block, valid for the scene version and sun frame below
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, DeviceBuffer> sunOrders;
-    const SceneStore* sunOrderStore = nullptr;
-    uint32_t sunOrderVersion = 0;
-    float sunOrderFrame[9] {};
     // AO bake results (ark_ddgi_bake_ao)
     DeviceBuffer bakeTri, bakeBary, bakeOut, bakePixels, bakeCounters;
     uint32_t bakeW = 0, bakeH = 0;
@@ -356,25 +348,19 @@ hipError_t orderEnd(ArkDdgiCtx* ctx, hipStream_t s)
 
 // Shading work set for the largest window: per-ray light bits, then k_shadow_gen's
 // shadow-ray list (at most one ray per probe ray and light).
-// The list holds up to one ray per probe ray and light, each light's part rounded up
-// to whole k_shadow_gen blocks (the sun's part is indexed by block rank, sunOrder), then
-// the sun's per-rank ray counts.
 struct ShadeWorkLayout {
-    uint64_t bits, list, sunCounts, total;
-    uint64_t perLight; // list entries of one light
+    uint64_t bits, list, total;
 };
 
 ShadeWorkLayout shadeWorkLayout(const ArkDdgiCtx* ctx)
 {
     auto al = [](uint64_t b) { return (b + 255) & ~static_cast<uint64_t>(255); };
     const uint64_t rays = static_cast<uint64_t>(ctx->Kmax) * ctx->Rmax;
-    const uint64_t blocks = (rays + kGenSpan - 1) / kGenSpan;
+    const uint64_t entries = rays * ctx->lightCount;
     ShadeWorkLayout w {};
-    w.perLight = blocks * kGenSpan;
     w.bits = 0;
     w.list = al(rays * 4);
-    w.sunCounts = w.list + al(w.perLight * ctx->lightCount * sizeof(ShadowRay));
-    w.total = w.sunCounts + al(blocks * 8); // per rank: rays, rays handed out
+    w.total = w.list + al(entries * sizeof(ShadowRay));
     return w;
 }
 
@@ -588,7 +574,6 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
         if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0 ? 1 : 0;
-        if (const char* so = std::getenv("ARK_SUN_ORDER")) ctx->sunOrdered = std::atoi(so) != 0;
         if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
         // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
         // across queues: a polling wait could then hold the GPU while the kernel it
@@ -668,7 +653,6 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     for (DeviceBuffer* b : { &ctx->irr, &ctx->vis, &ctx->offsets, &ctx->slots, &ctx->slotOrder, &ctx->fib, &ctx->fibOrder, &ctx->order, &ctx->hits, &ctx->surfels, &ctx->spill, &ctx->rayCounter, &ctx->seqWords, &ctx->shadeWork, &ctx->reflWork,
                              &ctx->raySteps, &ctx->counters, &ctx->lights, &ctx->bakeTri, &ctx->bakeBary, &ctx->bakeOut, &ctx->bakePixels, &ctx->bakeCounters })
         b->release();
-    for (auto& kv : ctx->sunOrders) kv.second.release();
     ctx->sceneStore.reset();
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1230,82 +1214,6 @@ int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint
 }
 
 
-// Light-space order of the sun's shadow rays (k_trace_shadow<SUN>). The sun list is
-// written by k_shadow_gen blocks of kGenSpan queue positions (a few neighbouring probes
-// of one y-layer: the slot order sweeps each x-z block bottom to top for the probe rays'
-// locality, k_probe_slots). A shadow ray toward the sun crosses every layer above its
-// start, so concurrent waves that take blocks in that order share little of the
-// light-space BVH. Here the blocks are ranked by the Morton code of their first probe's
-// light-space (u, v): each of the kRayParts contiguous rank ranges is a compact region of
-// the plane perpendicular to the sun, and its waves walk it along the Morton curve.
-// Only the order of the any-hit work changes, never a result. The ranks depend on the
-// window (first, K, R), the slab and the sun's frame: computed on the host once per
-// window and kept on the device (a rolling window cycles through N / K of them).
-static const uint32_t* sunOrder(ArkDdgiCtx* ctx, const FrameArgs& f)
-{
-    const SceneStore* store = ctx->sceneStore.get();
-    if (store != ctx->sunOrderStore || ctx->sceneVersion != ctx->sunOrderVersion ||
-        std::memcmp(ctx->sunOrderFrame, ctx->scene.sun_frame, sizeof(ctx->sunOrderFrame)) != 0 || ctx->sunOrders.size() >= 64) {
-        if (!ctx->sunOrders.empty() && drainContext(ctx) != hipSuccess) return nullptr; // in-flight frames may read them
-        for (auto& kv : ctx->sunOrders) kv.second.release();
-        ctx->sunOrders.clear();
-        ctx->sunOrderStore = store;
-        ctx->sunOrderVersion = ctx->sceneVersion;
-        std::memcpy(ctx->sunOrderFrame, ctx->scene.sun_frame, sizeof(ctx->sunOrderFrame));
-    }
-    const auto key = std::make_tuple(f.first, f.window, f.R);
-    auto it = ctx->sunOrders.find(key);
-    if (it != ctx->sunOrders.end()) return it->second.as<uint32_t>();
-    const uint32_t X = static_cast<uint32_t>(f.X), Y = static_cast<uint32_t>(f.Y), Z = static_cast<uint32_t>(f.Z), N = X * Y * Z;
-    const uint32_t z0 = f.sharded ? static_cast<uint32_t>(f.slab_z0) : 0u, z1 = f.sharded ? static_cast<uint32_t>(f.slab_z1) : Z;
-    // queue position -> probe (k_probe_slots' closed form)
-    std::vector<uint32_t> qProbe(f.window_probes, 0u);
-    for (uint32_t w = 0; w < f.window; ++w) {
-        const uint32_t p = (f.first + w) % N;
-        const uint32_t z = (p % (X * Z)) / X;
-        if (f.sharded && (z < z0 || z >= z1)) continue;
-        const uint32_t q = slotQueuePos(X, Y, Z, z0, std::max(1u, z1 - z0), f.first, f.window, w, p);
-        if (q < qProbe.size()) qProbe[q] = p;
-    }
-    const uint32_t nb = f.sun_blocks;
-    std::vector<float> u(nb), v(nb);
-    float lo[2] = { INFINITY, INFINITY }, hi[2] = { -INFINITY, -INFINITY };
-    const float* F = ctx->scene.sun_frame;
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint32_t p = qProbe[std::min<uint64_t>(static_cast<uint64_t>(b) * kGenSpan / f.R, qProbe.size() - 1)];
-        const uint32_t y = p / (X * Z), z = (p % (X * Z)) / X, x = p % X;
-        const float P[3] = { f.origin[0] + f.spacing[0] * static_cast<float>(x), f.origin[1] + f.spacing[1] * static_cast<float>(y),
-                             f.origin[2] + f.spacing[2] * static_cast<float>(z) };
-        u[b] = F[0] * P[0] + F[1] * P[1] + F[2] * P[2];
-        v[b] = F[3] * P[0] + F[4] * P[1] + F[5] * P[2];
-        lo[0] = std::min(lo[0], u[b]); hi[0] = std::max(hi[0], u[b]);
-        lo[1] = std::min(lo[1], v[b]); hi[1] = std::max(hi[1], v[b]);
-    }
-    auto cell = [](float c, float l, float h) {
-        const float t = h > l ? (c - l) / (h - l) : 0.0f;
-        return static_cast<uint32_t>(std::min(65535.0f, std::max(0.0f, t * 65535.0f)));
-    };
-    auto spread = [](uint32_t a) { // 16 bits -> the even bits of 32
-        a = (a | (a << 8)) & 0x00ff00ffu;
-        a = (a | (a << 4)) & 0x0f0f0f0fu;
-        a = (a | (a << 2)) & 0x33333333u;
-        return (a | (a << 1)) & 0x55555555u;
-    };
-    std::vector<uint64_t> keyed(nb);
-    for (uint32_t b = 0; b < nb; ++b)
-        keyed[b] = (static_cast<uint64_t>(spread(cell(u[b], lo[0], hi[0])) | (spread(cell(v[b], lo[1], hi[1])) << 1)) << 32) | b;
-    std::sort(keyed.begin(), keyed.end());
-    std::vector<uint32_t> rank(nb);
-    for (uint32_t i = 0; i < nb; ++i) rank[static_cast<uint32_t>(keyed[i])] = i;
-    DeviceBuffer& buf = ctx->sunOrders[key];
-    if (buf.alloc(std::max<size_t>(16, nb * 4u)) != hipSuccess || hipMemcpy(buf.ptr, rank.data(), nb * 4u, hipMemcpyHostToDevice) != hipSuccess) {
-        buf.release();
-        ctx->sunOrders.erase(key);
-        return nullptr;
-    }
-    return buf.as<uint32_t>();
-}
-
 static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t K)
 {
     if (ctx->desc.shard_count <= 1) return K;
@@ -1518,17 +1426,10 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     // the sun's shadow rays in their own list (the first Kmax x Rmax entries of the
     // list area, the other lights' after them) for the light-space BVH
     if (ctx->scene.sun_root >= 0) {
-        const ShadeWorkLayout l = shadeWorkLayout(ctx);
         f.sun_rays = f.shadow_rays;
-        f.shadow_rays += l.perLight;
+        f.shadow_rays += Kmax * Rmax;
         f.sun_count = f.ray_counter + kSunCountWord;
         f.sun_heads = f.ray_counter + kSunHeadWord;
-        if (ctx->sunOrdered && f.window_probes > 0) {
-            f.sun_blocks = (f.window_rays + kGenSpan - 1) / kGenSpan;
-            f.sun_block_count = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->shadeWork.ptr) + l.sunCounts);
-            f.sun_rank = sunOrder(ctx, f);
-            if (!f.sun_rank) return ctx->fail(ARK_DDGI_E_DEVICE, "the sun's shadow-ray order: device allocation or upload failed");
-        }
     }
     // the slot table and the primary traversal: on traceStream after frame n - 2 (the
     // last user of buffer set b) when pipelined, else in line on the caller's stream

@@ -125,10 +125,6 @@ struct alignas(16) ShadowRay {
     float4 dir_owner;
 };
 
-// k_shadow_gen: each workgroup (256 threads) owns kGenSteps x 256 consecutive queue
-// positions of the window's probe rays
-constexpr uint32_t kGenSteps = 4, kGenSpan = kGenSteps * 256u;
-
 // Word offsets in the ray-counter buffer (each counter on its own 128-B line): the
 // probe-ray partition heads, the shading heads, the shadow list (count + partition heads).
 constexpr int kShadeHeadWord = kRayParts * kRayCounterStride;
@@ -232,14 +228,6 @@ struct FrameArgs {
     ShadowRay* sun_rays;
     uint32_t* sun_count;     // = ray_counter + kSunCountWord
     uint32_t* sun_heads;     // = ray_counter + kSunHeadWord
-    // light-space order of the sun's list (ark_ddgi.cpp sunOrder; null: list order):
-    // k_shadow_gen block b writes its sun rays at sun_rank[b] * kGenSpan and their count
-    // at sun_block_count[sun_rank[b]]; k_trace_shadow<SUN> hands them out in rank order,
-    // kRayParts contiguous rank ranges (grabSunBlock; sun_block_count[sun_blocks + r]:
-    // rays of rank r handed out)
-    const uint32_t* sun_rank;
-    uint32_t* sun_block_count;
-    uint32_t sun_blocks;     // k_shadow_gen blocks of this update
     uint32_t* ray_counter;
     unsigned long long* counters; // [0] nodes [1] tris [2] hits [3] shadow rays
     uint16_t* ray_steps;     // counting updates: traversal iterations of each probe ray (both passes) at its hit-record index

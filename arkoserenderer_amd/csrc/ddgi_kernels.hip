@@ -874,36 +874,6 @@ __device__ __forceinline__ void grabItems(uint32_t* heads, uint32_t total, uint3
     }
 }
 
-// The sun's list in light-space order (FrameArgs::sun_rank): chunks of at most CHUNK
-// rays of one k_shadow_gen block's span [r * kGenSpan, + count), the blocks of partition
-// p's contiguous rank range (a compact region of the light-space plane) in rank order.
-// sun_heads[p] holds partition p's current rank (relative), sun_block_count[nb + r] the
-// rays of block r handed out so far (zeroed by k_shadow_gen); a block is passed over
-// once its rays are gone (a CAS from r to r + 1, so no rank is skipped twice).
-__device__ __forceinline__ void grabSunBlock(const FrameArgs& f, uint32_t home, uint32_t& tried, uint32_t& b, uint32_t& e, uint32_t CHUNK)
-{
-    b = e = 0;
-    const uint32_t nb = f.sun_blocks;
-    for (; tried < kRayParts; ++tried) {
-        const uint32_t p = (home + tried) & (kRayParts - 1);
-        const uint32_t pb = nb * p / kRayParts, pe = nb * (p + 1) / kRayParts;
-        uint32_t* cur = f.sun_heads + p * kRayCounterStride;
-        for (;;) {
-            const uint32_t rel = __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (rel >= pe - pb) break;
-            const uint32_t r = pb + rel;
-            const uint32_t c = f.sun_block_count[r];
-            const uint32_t off = c ? atomicAdd(f.sun_block_count + nb + r, CHUNK) : c;
-            if (off < c) {
-                b = r * kGenSpan + off;
-                e = r * kGenSpan + min(off + CHUNK, c);
-                return;
-            }
-            atomicCAS(cur, rel, rel + 1u);
-        }
-    }
-}
-
 __device__ __forceinline__ uint32_t partRayBegin(const FrameArgs& f, uint32_t p)
 {
     return static_cast<uint32_t>(static_cast<uint64_t>(f.window_probes) * p / kRayParts) * f.R;
@@ -1654,8 +1624,7 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     if (lane < 16u) tl.bytes[(wbase >> 2) + lane] = 0u; // wave-private tail bytes
     const float tmin = 0.025f;
-    const bool sunBlocks = SUN && f.sun_rank != nullptr;
-    const uint32_t total = sunBlocks ? 0u : (SUN ? *f.sun_count : *f.shadow_count);
+    const uint32_t total = SUN ? *f.sun_count : *f.shadow_count;
     uint32_t* const heads = SUN ? f.sun_heads : f.shadow_heads;
     const ShadowRay* const list = SUN ? f.sun_rays : f.shadow_rays;
     const int32_t roots[3] = { SUN ? sc.sun_root : sc.root_opaque, SUN ? -1 : sc.root_masked, SUN ? -1 : sc.root_blend };
@@ -1682,10 +1651,7 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
             uint32_t fb = 0, fe = 0;
             if (avail < n) {
                 uint32_t b = 0, e = 0, t = tried;
-                if (lane == 0) {
-                    if (sunBlocks) grabSunBlock(f, home, t, b, e, f.grab_chunk);
-                    else grabItems(heads, total, home, t, b, e, f.grab_chunk);
-                }
+                if (lane == 0) grabItems(heads, total, home, t, b, e, f.grab_chunk);
                 fb = __shfl(b, 0);
                 fe = __shfl(e, 0);
                 tried = __shfl(t, 0);
@@ -1844,6 +1810,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 // neighbouring rays of one probe. kGenSteps = 4 (16: 0.185 ms, 4: 0.163, 2: 0.215 at
 // C4). Measured and removed: the list binned by light-space cell (-15 %
 // shadow HBM, +34 % shadow phase) and a straight-line staged form (179 VGPRs, 0.416 ms).
+constexpr uint32_t kGenSteps = 4, kGenSpan = kGenSteps * 256u;
 
 __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t x)
 {
@@ -1925,15 +1892,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
                 run += c;
             }
         blockBase = (run & 0xffffu) ? atomicAdd(f.shadow_count, run & 0xffffu) : 0u;
-        if (f.sun_rank) {
-            // the light-space order: this block's sun rays at its rank's span of the list
-            const uint32_t r = f.sun_rank[blockIdx.x];
-            sunBlockBase = r * kGenSpan;
-            f.sun_block_count[r] = run >> 16;
-            f.sun_block_count[f.sun_blocks + r] = 0u; // its rays handed out (grabSunBlock)
-        } else {
-            sunBlockBase = (run >> 16) ? atomicAdd(f.sun_count, run >> 16) : 0u;
-        }
+        sunBlockBase = (run >> 16) ? atomicAdd(f.sun_count, run >> 16) : 0u;
     }
     __syncthreads();
     for (uint32_t k = 0; k < kGenSteps; ++k) {
@@ -2362,7 +2321,7 @@ hipError_t launch_trace_shadow(const SceneArgs& sc, const FrameArgs& f, uint32_t
 
 hipError_t launch_shadow_gen(const SceneArgs& sc, const FrameArgs& f, hipStream_t s)
 {
-    const uint32_t blocks = (f.window_rays + kGenSpan - 1u) / kGenSpan;
+    const uint32_t blocks = (f.window_rays + dev::kGenSpan - 1u) / dev::kGenSpan;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(dev::k_shadow_gen<false>, dim3(blocks), dim3(256), 0, s, sc, f);
     return hipGetLastError();
@@ -2425,7 +2384,7 @@ hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const 
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(&dev::k_trace<false, 6, dev::ListRays>), dim3(traceBlocks), dim3(kTraceBlock), args, 0, s);
     if (e != hipSuccess) return e;
     if (f.light_count > 0) {
-        hipLaunchKernelGGL(dev::k_shadow_gen<true>, dim3(static_cast<uint32_t>((pixels + kGenSpan - 1) / kGenSpan)), dim3(256), 0, s, sc, f);
+        hipLaunchKernelGGL(dev::k_shadow_gen<true>, dim3(static_cast<uint32_t>((pixels + dev::kGenSpan - 1) / dev::kGenSpan)), dim3(256), 0, s, sc, f);
         e = launch_trace_shadow(sc, f, shadowBlocks, false, s);
         if (e != hipSuccess) return e;
     }
