@@ -1597,6 +1597,156 @@ extern "C" int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t 
             sceneHi[a] = root.p[a] + 255.0 * std::ldexp(1.0, static_cast<int>(root.e[a]) - 127);
         }
     }
+    // ARK_SIM_STEP=1: k_trace's dual step (one pending leaf triangle and one node per
+    // iteration, the node side paused while a second leaf group waits), per-ray
+    // iterations in perRay / out[5]; =2: the same with two nodes per iteration (the next
+    // two children of the group / stack, the second's children pushed below the first's
+    // group, up to two waiting leaf groups). Exact box test, k-order (slot ^ octant).
+    const int stepMode = std::getenv("ARK_SIM_STEP") ? std::atoi(std::getenv("ARK_SIM_STEP")) : 0;
+    if (stepMode) {
+        std::atomic<uint64_t> sumIter { 0 };
+        auto stepWorker = [&](uint64_t r0, uint64_t r1) {
+            uint64_t cn = 0, ct = 0, ch = 0, ms = 0, it = 0;
+            struct Group { uint32_t base; uint32_t bits; uint32_t imask; };
+            for (uint64_t r = r0; r < r1; ++r) {
+                const float* ry = rays + 7 * r;
+                const float o[3] = { ry[0], ry[1], ry[2] }, d[3] = { ry[3], ry[4], ry[5] };
+                float tmax = ry[6];
+                const float tmin = 1e-4f;
+                float idir[3];
+                for (int a = 0; a < 3; ++a) idir[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? (d[a] < 0.0f ? -1e-20f : 1e-20f) : d[a]);
+                const uint32_t oct = (idir[0] < 0 ? 1u : 0u) | (idir[1] < 0 ? 2u : 0u) | (idir[2] < 0 ? 4u : 0u);
+                bool hit = false;
+                auto nextChild = [&](Group& g) {
+                    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(g.bits));
+                    g.bits &= g.bits - 1u;
+                    const uint32_t slot = k ^ oct;
+                    return g.base + static_cast<uint32_t>(__builtin_popcount(g.imask & ((1u << slot) - 1u)));
+                };
+                // node visit: the group of hit internal children, the hit leaves' triangles
+                auto visit = [&](uint32_t ni, Group& g, std::vector<uint32_t>& leafTris) {
+                    const GpuBvh8Node& nd = r8.nodes[ni];
+                    cn++;
+                    g = Group { nd.child_base, 0u, nd.imask };
+                    leafTris.clear();
+                    for (int s = 0; s < 8; ++s) {
+                        const bool internal = (nd.imask >> s) & 1u;
+                        if (!internal && !((nd.leaf_mask >> s) & 1u)) continue;
+                        float tn = tmin, tf = tmax;
+                        for (int a = 0; a < 3; ++a) {
+                            const float step = std::ldexp(1.0f, static_cast<int>(nd.e[a]) - 127);
+                            const float lo = std::fma(static_cast<float>(nd.qlo[a][s]), step, nd.p[a]);
+                            const float hi = std::fma(static_cast<float>(nd.qhi[a][s]), step, nd.p[a]);
+                            float t0 = (lo - o[a]) * idir[a], t1 = (hi - o[a]) * idir[a];
+                            if (t0 > t1) std::swap(t0, t1);
+                            tn = std::max(tn, t0);
+                            tf = std::min(tf, t1);
+                        }
+                        if (!(tn <= tf * 1.00001f + 1e-7f)) continue;
+                        if (internal) g.bits |= 1u << (static_cast<uint32_t>(s) ^ oct);
+                        else {
+                            uint32_t st[kBvh8MaxLeafSize];
+                            const int c = bvh8SlotTriangles(nd, s, st);
+                            for (int i = 0; i < c; ++i) leafTris.push_back(st[i]);
+                        }
+                    }
+                };
+                auto testTri = [&](uint32_t t) {
+                    ct++;
+                    const GpuTriangle& g = r8.tris[t];
+                    const float v0[3] = { g.t0[0], g.t0[1], g.t0[2] }, e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+                    const float pv[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
+                    const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+                    if (det == 0.0f) return;
+                    const float inv = 1.0f / det;
+                    const float sv[3] = { o[0] - v0[0], o[1] - v0[1], o[2] - v0[2] };
+                    const float u = (sv[0] * pv[0] + sv[1] * pv[1] + sv[2] * pv[2]) * inv;
+                    if (!(u >= 0.0f && u <= 1.0f)) return;
+                    const float q[3] = { sv[1] * e1[2] - sv[2] * e1[1], sv[2] * e1[0] - sv[0] * e1[2], sv[0] * e1[1] - sv[1] * e1[0] };
+                    const float v = (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]) * inv;
+                    if (!(v >= 0.0f && u + v <= 1.0f)) return;
+                    const float tt = (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]) * inv;
+                    if (tt >= tmin && tt <= tmax) {
+                        tmax = tt;
+                        hit = true;
+                    }
+                };
+                Group G { 0u, 1u, 0u }; // the root alone (k = 0, no internal mask: base + 0)
+                std::vector<Group> S;
+                std::vector<uint32_t> triQ, q1, q2, leafA, leafB;
+                size_t triPos = 0;
+                uint64_t iters = 0;
+                auto addLeaves = [&](std::vector<uint32_t>& L) {
+                    if (L.empty()) return;
+                    if (triPos >= triQ.size()) { triQ.swap(L); triPos = 0; }
+                    else if (q1.empty()) q1.swap(L);
+                    else q2.swap(L);
+                };
+                for (;;) {
+                    const bool doTri = triPos < triQ.size();
+                    const bool room = stepMode == 2 ? (q1.empty() && q2.empty()) : q1.empty();
+                    const bool doNode = room && (G.bits != 0 || !S.empty());
+                    if (!doTri && !doNode) break;
+                    iters++;
+                    if (doTri) testTri(triQ[triPos++]);
+                    if (doNode) {
+                        if (G.bits == 0) { G = S.back(); S.pop_back(); }
+                        const uint32_t A = nextChild(G);
+                        bool haveB = false;
+                        uint32_t B = 0;
+                        if (stepMode == 2) {
+                            if (G.bits != 0) { B = nextChild(G); haveB = true; }
+                            else if (!S.empty()) {
+                                Group& H = S.back();
+                                B = nextChild(H);
+                                haveB = true;
+                                if (H.bits == 0) S.pop_back();
+                            }
+                        }
+                        if (G.bits != 0) S.push_back(G);
+                        Group GA {}, GB {};
+                        visit(A, GA, leafA);
+                        if (haveB) {
+                            visit(B, GB, leafB);
+                            if (GB.bits != 0) S.push_back(GB);
+                        }
+                        G = GA;
+                        addLeaves(leafA);
+                        if (haveB) addLeaves(leafB);
+                    }
+                    if (triPos >= triQ.size()) {
+                        if (!q1.empty()) { triQ.swap(q1); q1.clear(); triPos = 0; if (!q2.empty()) { q1.swap(q2); q2.clear(); } }
+                    }
+                }
+                ch += hit ? 1 : 0;
+                it += iters;
+                ms = std::max(ms, iters);
+                if (perRay) perRay[r] = static_cast<uint32_t>(iters);
+            }
+            nodes += cn;
+            triTests += ct;
+            hits += ch;
+            sumIter += it;
+            uint64_t m = maxSteps.load();
+            while (ms > m && !maxSteps.compare_exchange_weak(m, ms)) {}
+        };
+        const int T = std::max(1, threads);
+        std::vector<std::thread> pool;
+        for (int t = 0; t < T; ++t) pool.emplace_back(stepWorker, nRays * t / T, nRays * (t + 1) / T);
+        for (auto& th : pool) th.join();
+        if (out) {
+            out[0] = nodes.load();
+            out[1] = triTests.load();
+            out[2] = hits.load();
+            out[3] = r8.nodes.size();
+            out[4] = sumIter.load(); // iterations (in place of the SAH cost)
+            out[5] = maxSteps.load();
+            out[6] = r8.max_depth;
+            out[7] = r8.tris.size();
+            out[8] = 0;
+        }
+        return 0;
+    }
     auto worker = [&](uint64_t r0, uint64_t r1) {
         uint64_t cn = 0, ct = 0, ch = 0, ms = 0;
         for (uint64_t r = r0; r < r1; ++r) {
