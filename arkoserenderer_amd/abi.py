@@ -256,6 +256,8 @@ class ArkDdgiBvhStats(C.Structure):
         ("sun_cost_light", C.c_float),
         ("sun_build_ms", C.c_float),
         ("refit_ms", C.c_float),
+        ("sun_max_depth", C.c_uint32),
+        ("sun_rebuilds", C.c_uint32),
     ]
 
 

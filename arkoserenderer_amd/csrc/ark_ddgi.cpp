@@ -8,6 +8,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -123,6 +124,23 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 // The scene of a context on the device (ark_ddgi_set_scene): BVH nodes + triangles,
 // shading records, RT mesh data, materials, textures, lights. Reference-counted:
 // ark_ddgi_share_scene lets the Z-slab contexts of one GPU use one copy.
+// A background rebuild of the sun's light-space BVH (sunRebuildStep): a host thread
+// downloads the world BVHs' triangle records, builds the BVH for `dir` and uploads it
+// into `buf`; `done` set last (release).
+struct SunJob {
+    std::thread t;
+    std::atomic<bool> done { false };
+    float dir[3] {};
+    uint32_t version = 0; // SceneStore::version when started (a refit since: discarded)
+    DeviceBuffer buf;     // nodes, then the triangle records at triOffset
+    size_t triOffset = 0;
+    uint64_t nodes = 0;
+    uint32_t depth = 0;
+    float frame[9] {};
+    float ms = 0.0f;
+    bool ok = false;
+};
+
 struct SceneStore {
     int device = 0;
     DeviceBuffer nodes, triNormals, indices, vertices, positions, meshes, materials, instances, texInfos, texels;
@@ -148,12 +166,23 @@ struct SceneStore {
     uint64_t triRecords = 0; // triangle records of the world BVHs (holes included)
     DeviceBuffer refitInst, refitBoxes, refitOrder, refitBounds;
     std::vector<uint32_t> levelOffsets; // refitOrder[levelOffsets[i] .. [i + 1]): the nodes of one depth, deepest first
+    // the light-space BVH follows the sun: set_scene chose it (sunWanted), and after a
+    // sun-direction change or a refit it is rebuilt in the background (sunRebuildStep)
+    bool sunWanted = false;
+    int buildThreads = 16;
+    std::unique_ptr<SunJob> sunJob;
+    uint32_t sunRebuilds = 0;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
     SceneStore& operator=(const SceneStore&) = delete;
     ~SceneStore()
     {
         (void)hipSetDevice(device);
+        // the job reads the triangle records: done before they are freed
+        if (sunJob) {
+            if (sunJob->t.joinable()) sunJob->t.join();
+            sunJob->buf.release();
+        }
         for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
                                  &refitBoxes, &refitOrder, &refitBounds })
             b->release();
@@ -310,6 +339,8 @@ int clearHistory(ArkDdgiCtx* ctx)
     return ARK_DDGI_OK;
 }
 
+hipError_t drainContext(ArkDdgiCtx* ctx);
+
 int ensureSpill(ArkDdgiCtx* ctx)
 {
     // a node group is pushed at most once per BVH8 level: depth + 2 entries of 2 words
@@ -317,8 +348,12 @@ int ensureSpill(ArkDdgiCtx* ctx)
     uint32_t threads = std::max(ctx->traceBlocks, ctx->shadowBlocks) * kTraceBlock; // the traversal kernels
     const uint64_t words = static_cast<uint64_t>(need) * 2 * threads;
     const size_t bytes = 2 * words * sizeof(uint32_t); // region 0: all but the primary traversal
+    if (ctx->spill.bytes >= bytes) {
+        ctx->spillRegionWords = words;
+        return ARK_DDGI_OK;
+    }
+    if (ctx->spill.ptr) ARK_HIP(drainContext(ctx)); // a deeper BVH (a rebuilt sun BVH): frames in flight use it
     ctx->spillRegionWords = words;
-    if (ctx->spill.bytes >= bytes) return ARK_DDGI_OK;
     ARK_HIP(ctx->spill.alloc(bytes));
     ctx->spillEntries = need;
     return ARK_DDGI_OK;
@@ -490,6 +525,99 @@ hipError_t drainContext(ArkDdgiCtx* ctx)
     hipError_t e = hipStreamSynchronize(ctx->traceStream);
     if (e == hipSuccess && ctx->orderValid) e = hipEventSynchronize(ctx->evOrder);
     return e;
+}
+
+// The background rebuild's thread: the world records from the device, the light-space
+// BVH of job->dir on the host (as set_scene builds it, from the same records), the
+// result uploaded into job->buf on a stream of its own.
+void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t count, int threads)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    bool ok = hipSetDevice(device) == hipSuccess;
+    hipStream_t s = nullptr;
+    ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    std::vector<GpuTriangle> rec(ok ? count : 0);
+    ok = ok && hipMemcpyAsync(rec.data(), records, count * sizeof(GpuTriangle), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    Bvh8BuildResult r;
+    if (ok) {
+        SunBvhInput in;
+        sun_frame(job->dir, in.frame);
+        sun_add_records(in, rec, threads);
+        std::vector<GpuTriangle>().swap(rec);
+        BvhBuildOptions opt;
+        opt.threads = threads;
+        Bvh8CollapseOptions copt;
+        copt.threads = threads;
+        ok = build_sun_bvh(in, opt, copt, r) && !r.nodes.empty();
+        for (int i = 0; i < 3; ++i)
+            for (int k = 0; k < 3; ++k) job->frame[i * 3 + k] = static_cast<float>(in.frame[i][k]);
+    }
+    if (ok) {
+        const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
+        job->triOffset = (nb + 255) & ~static_cast<size_t>(255);
+        r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
+        ok = job->buf.alloc(job->triOffset + r.tris.size() * sizeof(GpuTriangle)) == hipSuccess &&
+             hipMemcpyAsync(job->buf.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(static_cast<char*>(job->buf.ptr) + job->triOffset, r.tris.data(), r.tris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+        job->nodes = r.nodes.size();
+        job->depth = r.max_depth;
+    }
+    if (s) (void)hipStreamDestroy(s);
+    job->ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    job->ok = ok;
+    job->done.store(true, std::memory_order_release);
+}
+
+// The light-space sun BVH follows the context's sun (called by every update and by
+// set_lights / set_instances): a finished rebuild is installed - once the frames that
+// may read the old one are done, and only if no refit came in between - and a new one
+// is started when the scene chose the light-space BVH at set_scene but holds none for
+// this direction (a direction change, or a refit dropped it). Until it is installed the
+// sun's shadow rays traverse the world BVHs (deriveSceneArgs), with the same results.
+// One rebuild at a time per scene; with contexts that share a scene under different
+// suns, the scene follows the context that asked last.
+int sunRebuildStep(ArkDdgiCtx* ctx)
+{
+    SceneStore& st = *ctx->sceneStore;
+    if (st.sunJob && st.sunJob->done.load(std::memory_order_acquire)) {
+        std::unique_ptr<SunJob> job = std::move(st.sunJob);
+        if (job->t.joinable()) job->t.join();
+        if (job->ok && job->version == st.version) {
+            // frames in flight may traverse the old one (any context, when shared)
+            if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
+            else ARK_HIP(drainContext(ctx));
+            st.sunNodes.release();
+            st.sunNodes = job->buf;
+            job->buf = DeviceBuffer {};
+            st.sunArgs.sun_nodes = st.sunNodes.as<GpuBvh8Node>();
+            st.sunArgs.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.sunNodes.ptr) + job->triOffset);
+            st.sunArgs.sun_root = 0;
+            std::memcpy(st.sunArgs.sun_frame, job->frame, sizeof(job->frame));
+            std::memcpy(st.sunDirBuilt, job->dir, sizeof(job->dir));
+            st.sunBvhNodes = job->nodes;
+            st.bvhMaxDepth = std::max(st.bvhMaxDepth, job->depth);
+            st.bvhStats.max_depth = st.bvhMaxDepth;
+            st.bvhStats.sun_node_count = job->nodes;
+            st.bvhStats.sun_max_depth = job->depth;
+            st.bvhStats.sun_rebuilds = ++st.sunRebuilds;
+            st.bvhStats.sun_build_ms = job->ms;
+            ++st.version;
+            deriveSceneArgs(ctx);
+            if (const int rc = ensureSpill(ctx)) return rc;
+        } else {
+            job->buf.release();
+        }
+    }
+    if (!st.sunWanted || !ctx->hasSun || st.sunJob) return ARK_DDGI_OK;
+    if (st.sunArgs.sun_root >= 0 && std::memcmp(ctx->sunDir, st.sunDirBuilt, sizeof(ctx->sunDir)) == 0) return ARK_DDGI_OK;
+    auto job = std::make_unique<SunJob>();
+    std::memcpy(job->dir, ctx->sunDir, sizeof(job->dir));
+    job->version = st.version;
+    const GpuTriangle* records = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.nodes.ptr) + st.args.tri_byte_offset);
+    job->t = std::thread(runSunJob, job.get(), st.device, records, st.triRecords, st.buildThreads);
+    st.sunJob = std::move(job);
+    return ARK_DDGI_OK;
 }
 
 // Makes `st` the context's scene with the scene's lights: the per-context work sets
@@ -908,6 +1036,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     ARK_HIP(hipMemcpy(static_cast<char*>(st->nodes.ptr) + triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice));
     allTris.pop_back();
     uint64_t sunNodeCount = 0;
+    uint32_t sunMaxDepth = 0;
     size_t sunTriOffset = 0;
     if (sunThread.t.joinable()) sunThread.t.join();
     const auto ts0 = std::chrono::steady_clock::now();
@@ -935,6 +1064,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         sunNodeCount = r.nodes.size();
         // the sun's traversal pushes onto the same spill area (its depth counts)
         maxDepth = std::max(maxDepth, r.max_depth);
+        sunMaxDepth = r.max_depth;
     }
     sunBuildMs += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     std::vector<GpuTriangle>().swap(sunIn.world);
@@ -1009,6 +1139,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         for (int k = 0; k < 3; ++k) st->sunDirBuilt[k] = s->directional_light.world_space_direction[k];
     }
     st->sunBvhNodes = sunNodeCount;
+    st->sunWanted = sunNodeCount > 0;
+    st->buildThreads = opt.threads;
     st->bvhMaxDepth = maxDepth;
     st->inflateAbs = opt.inflate_abs;
     st->triRecords = allTris.size();
@@ -1022,6 +1154,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     st->bvhStats.node_bytes = allNodes.size() * sizeof(GpuBvh8Node);
     st->bvhStats.triangle_bytes = allTris.size() * sizeof(GpuTriangle);
     st->bvhStats.sun_node_count = sunNodeCount;
+    st->bvhStats.sun_max_depth = sunMaxDepth;
     st->bvhStats.sun_cost_world = st->sunCostWorld;
     st->bvhStats.sun_cost_light = st->sunCostLight;
     st->bvhStats.sun_build_ms = sunBuildMs;
@@ -1082,7 +1215,7 @@ int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* L)
         ctx->lightsDirty = true;
     }
     deriveSceneArgs(ctx);
-    return ARK_DDGI_OK;
+    return sunRebuildStep(ctx);
 }
 
 namespace {
@@ -1207,10 +1340,11 @@ int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint
     st.sunNodes.release();
     st.sunBvhNodes = 0;
     st.bvhStats.sun_node_count = 0;
+    st.bvhStats.sun_max_depth = 0;
     st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     ++st.version;
     deriveSceneArgs(ctx);
-    return ARK_DDGI_OK;
+    return sunRebuildStep(ctx); // a new light-space BVH of the refitted records, in the background
 }
 
 
@@ -1339,7 +1473,6 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!p || p->struct_size != sizeof(ArkDdgiFrameParams)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "bad ArkDdgiFrameParams");
     if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_update before ark_ddgi_set_scene");
-    if (ctx->sceneVersion != ctx->sceneStore->version) deriveSceneArgs(ctx); // another context refitted the shared scene
     const uint32_t N = static_cast<uint32_t>(ctx->N);
     const uint32_t K = std::min(p->probe_updates, N);
     const uint32_t R = p->rays_per_probe;
@@ -1348,6 +1481,11 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     const hipStream_t s = streamOf(hipStream);
     if (const int r = checkSequencing(ctx)) return r;
     ARK_HIP(hipSetDevice(ctx->device));
+    if (ctx->sceneVersion != ctx->sceneStore->version) { // another context refitted the shared scene or installed a sun BVH
+        deriveSceneArgs(ctx);
+        if (const int rc = ensureSpill(ctx)) return rc;
+    }
+    if (const int rc = sunRebuildStep(ctx)) return rc;
     FrameArgs f {};
     f.abort_word = ctx->seqWords.as<uint32_t>() + 64;
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
@@ -1926,7 +2064,10 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.refill_min = ctx->refillMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
-    if (ctx->sceneVersion != ctx->sceneStore->version) deriveSceneArgs(ctx);
+    if (ctx->sceneVersion != ctx->sceneStore->version) {
+        deriveSceneArgs(ctx);
+        if (const int rc = ensureSpill(ctx)) return rc;
+    }
     ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(flushLights(ctx, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, (kRayCounterWords + kRayCounterStride) * 4, s));

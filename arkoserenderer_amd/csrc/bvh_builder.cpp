@@ -1307,9 +1307,11 @@ void sun_frame(const float sunDir[3], double frame[3][3])
     }
 }
 
-void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, int threads)
+// Light-space build triangles of world-space records: rec(i) gives triangle i's record.
+template<class RecordOf>
+static void sunAddRecords(SunBvhInput& in, size_t n, RecordOf rec, int threads)
 {
-    const size_t base = in.world.size(), n = tris.size();
+    const size_t base = in.world.size();
     in.tris.resize(base + n);
     in.world.resize(base + n);
     // independent per triangle: in chunks on `threads` threads, the largest |coordinate|
@@ -1319,11 +1321,11 @@ void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, 
     auto work = [&](int t) {
         const size_t b = n * t / T, e = n * (t + 1) / T;
         for (size_t i = b; i < e; ++i) {
-            const GpuTriangle rec = make_gpu_triangle(tris[i]);
+            const GpuTriangle rc = rec(i);
             // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2 (exact, from the record)
             double V[3][3];
-            for (int a = 0; a < 3; ++a) V[0][a] = rec.t0[a];
-            const double e1[3] = { rec.t0[3], rec.t1[0], rec.t1[1] }, e2[3] = { rec.t1[2], rec.t1[3], rec.t2[0] };
+            for (int a = 0; a < 3; ++a) V[0][a] = rc.t0[a];
+            const double e1[3] = { rc.t0[3], rc.t1[0], rc.t1[1] }, e2[3] = { rc.t1[2], rc.t1[3], rc.t2[0] };
             for (int a = 0; a < 3; ++a) {
                 V[1][a] = V[0][a] + e1[a];
                 V[2][a] = V[0][a] + e2[a];
@@ -1337,7 +1339,7 @@ void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, 
             l.instance = 0;
             l.primitive = static_cast<uint32_t>(base + i);
             l.flip_facing = 0;
-            in.world[base + i] = rec;
+            in.world[base + i] = rc;
         }
     };
     std::vector<std::thread> pool;
@@ -1345,6 +1347,20 @@ void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, 
     work(0);
     for (std::thread& th : pool) th.join();
     for (float m : maxAbs) in.maxAbs = std::max(in.maxAbs, m);
+}
+
+void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& tris, int threads)
+{
+    sunAddRecords(in, tris.size(), [&](size_t i) { return make_gpu_triangle(tris[i]); }, threads);
+}
+
+void sun_add_records(SunBvhInput& in, const std::vector<GpuTriangle>& records, int threads)
+{
+    std::vector<uint32_t> live;
+    live.reserve(records.size());
+    for (size_t i = 0; i < records.size(); ++i)
+        if (!isHoleTriangle(records[i])) live.push_back(static_cast<uint32_t>(i));
+    sunAddRecords(in, live.size(), [&](size_t i) { return records[live[i]]; }, threads);
 }
 
 bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8CollapseOptions& copt, Bvh8BuildResult& out)

@@ -111,6 +111,9 @@ struct SunBvhInput {
 };
 void sun_frame(const float sun_dir[3], double frame[3][3]);
 void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_tris, int threads = 0);
+// The same from world-space triangle records as the world BVHs hold them (holes skipped):
+// the background rebuild after a sun-direction change or a refit (ark_ddgi.cpp)
+void sun_add_records(SunBvhInput& in, const std::vector<GpuTriangle>& records, int threads = 0);
 // Builds the BVH2 (opt; its inflation replaced by the light-space bound), the BVH8
 // (copt, slots sorted by w) and swaps in the world records; consumes in.tris and
 // in.world. False when a BVH2 leaf exceeds kBvh8MaxLeafSize.

@@ -309,10 +309,13 @@ int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src);
  * BVHs: the spots reach the device in stream order ahead of the next operation that
  * reads them, so frames already enqueued keep the lights they were enqueued with. At
  * most one directional light (:797) and ARK_DDGI_MAX_SPOT_LIGHTS spot lights; a spot's
- * ies_profile_index must name a texture of the scene (or be -1). A sun direction other
- * than the one the scene's light-space sun BVH was built for makes the sun's shadow
- * rays traverse the world BVHs (identical results), until the direction returns to it
- * or ark_ddgi_set_scene builds a new one. Host arrays are not retained. */
+ * ies_profile_index outside the scene's textures samples the 1x1 white default, as in
+ * set_scene. A sun direction other than the one the scene's light-space sun BVH was
+ * built for makes the sun's shadow rays traverse the world BVHs at once (identical
+ * results); when set_scene chose a light-space BVH, a host thread builds one for the new
+ * direction from the device's triangle records, and the first update after it is done
+ * installs it (after the frames in flight; ArkDdgiBvhStats.sun_rebuilds). Host arrays
+ * are not retained. */
 #define ARK_DDGI_MAX_SPOT_LIGHTS 10
 typedef struct ArkDdgiLights {
     uint32_t struct_size;        /* sizeof(ArkDdgiLights) */
@@ -332,10 +335,12 @@ int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* lights);
  * order set_scene uses, every node box recomputed bottom-up and re-quantized outward -
  * so the hits equal those of a set_scene with the same instances (they never depend on
  * the BVH's shape); only the node boxes' tightness can degrade with large motions, which
- * a set_scene (the full build) restores. The sun's light-space BVH is dropped (its
- * shadow rays traverse the world BVHs). Blocking: waits for the context's (a shared
- * scene: the device's) work in flight, refits, returns when the scene is updated; the
- * cost is in ArkDdgiBvhStats.refit_ms. */
+ * a set_scene (the full build) restores. The sun's light-space BVH holds the old
+ * records: it is dropped (the sun's shadow rays traverse the world BVHs) and rebuilt in
+ * the background from the refitted records, as after a sun-direction change
+ * (ark_ddgi_set_lights). Blocking: waits for the context's (a shared scene: the
+ * device's) work in flight, refits, returns when the scene is updated; the cost is in
+ * ArkDdgiBvhStats.refit_ms. */
 int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count);
 
 /* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null
@@ -466,6 +471,11 @@ typedef struct ArkDdgiBvhStats {
     float sun_cost_light;
     float sun_build_ms;  /* host time of the light-space BVH build and its cost sampling (part of build_ms) */
     float refit_ms;      /* the last ark_ddgi_set_instances: wait + refit (0 = none since set_scene) */
+    uint32_t sun_max_depth; /* depth of the light-space BVH8 (0 = none); max_depth, which sizes the
+                             * traversal stacks' spill, covers it */
+    uint32_t sun_rebuilds;  /* light-space BVHs rebuilt in the background and installed since
+                             * set_scene (after sun-direction changes or refits; sun_build_ms is
+                             * then the last rebuild's time) */
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 

@@ -181,3 +181,31 @@ def test_inf_radiance_surfels():
     finally:
         ctx.close()
         orc.close()
+
+
+def test_sun_bvh_depth_sizes_the_spill(monkeypatch):
+    """the light-space sun BVH holds the triangles of all three
+    hit-mask classes in one tree, so it can be deeper than each class's world BVH, and
+    the shadow traversal's stack spills with its depth. A soup split evenly over the
+    opaque / masked / translucent classes (one sun BVH over all of them): the depth that
+    sizes the spill (ArkDdgiBvhStats.max_depth) covers the sun BVH's, and the update
+    stays bit-exact with the sun's rays forced through it."""
+    monkeypatch.setenv("ARK_SUN_BVH", "1")
+    sc = S.soup(96_000, extent=7.0)
+    classes = ((abi.ARK_RT_HIT_MASK_OPAQUE, abi.ARK_BLEND_MODE_OPAQUE), (abi.ARK_RT_HIT_MASK_MASKED, abi.ARK_BLEND_MODE_MASKED),
+               (abi.ARK_RT_HIT_MASK_BLEND, abi.ARK_BLEND_MODE_TRANSLUCENT))
+    for i in range(sc.instances.size):
+        mask, blend = classes[i % 3]
+        sc.instances["hit_mask"][i] = mask
+        sc.materials["blend_mode"][sc.meshes["material_index"][sc.instances["rt_mesh_index"][i]]] = blend
+    grid = D.ProbeGrid((6, 6, 6), (1.2, 1.2, 1.2), (0.5, 0.5, 0.5))
+    cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=216, compute_probe_offsets=False,
+                       max_rays_per_probe=128, max_probe_updates=216)
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
+    ctx.set_scene(sc)
+    st = ctx.bvh_stats()
+    ctx.close()
+    assert st.sun_node_count > 0 and st.sun_max_depth > 0
+    assert st.max_depth >= st.sun_max_depth, (st.max_depth, st.sun_max_depth)
+    reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
+    _assert_exact(reps)

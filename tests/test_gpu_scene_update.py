@@ -70,8 +70,9 @@ def _rot_y(a):
 def test_lights_per_frame_exposure_spots_sun(sun_bvh, sync):
     """Frame 1: camera exposure 1 -> 1.7 (every light colour and the ambient term
     re-pre-exposed); frame 2: a spot moves and turns; frame 3: the sun rotates (the
-    light-space sun BVH no longer serves it: the world BVHs do); frame 4: the sun back
-    (the light-space BVH again), one spot removed; frame 5: three spots (the shadow-ray
+    light-space sun BVH no longer serves it: the world BVHs do, while a new one is
+    built in the background); frame 4: the sun back (whichever light-space BVH is
+    installed by then, or the world BVHs), one spot removed; frame 5: three spots (the shadow-ray
     list grows); frame 6: no sun. Bit-exact against the oracle after every frame, or
     (sync = False) with all seven frames and their light changes queued back to back
     and the atlases compared at the end."""
@@ -258,3 +259,58 @@ def test_shared_scene_refit_reaches_every_context():
     assert np.array_equal(sb[: len(probes), :R], sr[probes, :R])
     for c in (a, b, ref):
         c.close()
+
+
+@pytest.mark.parametrize("cause", ["direction", "refit"])
+def test_sun_bvh_rebuilt_in_background(cause):
+    """The light-space sun BVH follows the sun: after a sun-direction change (or a refit,
+    whose records it no longer holds) the sun's shadow rays traverse the world BVHs
+    while a host thread builds a new light-space BVH from the device's triangle records;
+    the next update after it is done installs it (ArkDdgiBvhStats.sun_rebuilds). Every
+    frame bit-exact against the oracle, before, during and after the rebuild."""
+    import time
+
+    sc = S.soup(64_000, extent=7.0)
+    grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False,
+                       max_rays_per_probe=64, max_probe_updates=512)
+    with _Env("1"):
+        ctx = D.DDGIContext(grid, 10000.0, cfg)
+    ctx.set_scene(sc)
+    assert ctx.bvh_stats().sun_node_count > 0
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(sc)
+    exposure = dict(light_pre_exposure=1.0, environment_brightness=1.0)
+    try:
+        f, installed_at = 0, None
+        t0 = time.time()
+        while installed_at is None or f < installed_at + 2:
+            if f == 1:
+                if cause == "direction":
+                    d = np.array([0.3, -1.0, -0.4], np.float32)
+                    sun = (sc.sun[0], tuple(float(x) for x in d / np.linalg.norm(d)))
+                    ctx.set_lights(sun, ())
+                    orc.set_lights(sun, ())
+                else:
+                    inst = sc.instances.copy()
+                    inst["object_to_world"][3, 3] += 0.25
+                    ctx.set_instances(inst)
+                    orc.set_instances(inst)
+                    assert ctx.bvh_stats().sun_node_count == 0  # the stale one is dropped at once
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            ctx.update(p)
+            orc.update(p)
+            ctx.synchronize()
+            _compare(ctx, orc, f, f"sun BVH rebuild after a {cause}")
+            st = ctx.bvh_stats()
+            if installed_at is None and st.sun_rebuilds > 0:
+                installed_at = f
+                assert st.sun_node_count > 0 and st.max_depth >= st.sun_max_depth
+            f += 1
+            assert time.time() - t0 < 90, "no light-space BVH rebuilt within 90 s"
+            if installed_at is None:
+                time.sleep(0.05)
+        assert installed_at is not None and installed_at >= 1
+    finally:
+        ctx.close()
+        orc.close()

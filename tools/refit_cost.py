@@ -55,6 +55,7 @@ def main():
             node.ctx.synchronize()
             return N * R * args.steps / (time.perf_counter() - t) / 1e6
 
+        had_sun_bvh = node.ctx.bvh_stats().sun_node_count > 0
         out = {"config": name, "triangles": int(sc.triangle_count), "instances": int(sc.instances.size),
                "build_ms": round(node.ctx.bvh_stats().build_ms, 1), "mrays_per_s_static": round(rate(), 1)}
         inst = sc.instances.copy()
@@ -74,6 +75,18 @@ def main():
             st = node.ctx.bvh_stats()
             moves.append({"move": label, "set_instances_ms": round(wall, 2), "refit_ms": round(st.refit_ms, 2), "mrays_per_s": round(rate(), 1)})
         out["refits"] = moves
+        # the light-space sun BVH, dropped by the refit, comes back from the background
+        # rebuild (sunRebuildStep): frames until it is installed, then the rate again
+        st = node.ctx.bvh_stats()
+        if had_sun_bvh:
+            t = time.perf_counter()
+            while node.ctx.bvh_stats().sun_rebuilds == st.sun_rebuilds and time.perf_counter() - t < 60.0:
+                node.execute(app[0])
+                app[0] = D.AppState(app[0].frame_index + 1)
+                node.ctx.synchronize()
+            s2 = node.ctx.bvh_stats()
+            out["sun_rebuild"] = {"installed_after_s": round(time.perf_counter() - t, 2), "rebuild_ms": round(s2.sun_build_ms, 1),
+                                  "sun_nodes": int(s2.sun_node_count), "mrays_per_s": round(rate(), 1)}
         print(json.dumps(out), flush=True)
         node.ctx.close()
 
