@@ -89,6 +89,15 @@ int main(int argc, char** argv)
     const double cw = sun_shadow_cost(r8.nodes, r8.tris, roots, 3, nullptr, L, origins);
     const double cl = sun_shadow_cost(rs.nodes, rs.tris, &sroot, 1, sunIn.frame, L, origins);
     std::printf("sun cost sampling %.0f ms (world %.2f, light %.2f)\n", ms(t), cw, cl);
+    // the background rebuild's input: the world BVH's records in leaf order (holes skipped)
+    SunBvhInput recIn;
+    sun_frame(s->directional_light.world_space_direction, recIn.frame);
+    t = Clock::now();
+    sun_add_records(recIn, r8.tris, threads);
+    Bvh8BuildResult rr;
+    build_sun_bvh(recIn, opt, copt, rr);
+    const double cr = sun_shadow_cost(rr.nodes, rr.tris, &sroot, 1, recIn.frame, L, origins);
+    std::printf("sun BVH from the world records %.0f ms (%zu nodes, depth %u vs %u), light cost %.2f\n", ms(t), rr.nodes.size(), rr.max_depth, rs.max_depth, cr);
     ark_soup_free(soup);
     return 0;
 }

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", nargs="+", default=["c4", "c3"])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--sun-turn", action="store_true", help="instead of refits: turn the sun by 10 deg, wait for the background rebuild, turn it back, wait again")
     args = ap.parse_args()
     import torch
     from arkoserenderer_amd import ddgi as D
@@ -58,6 +59,27 @@ def main():
         had_sun_bvh = node.ctx.bvh_stats().sun_node_count > 0
         out = {"config": name, "triangles": int(sc.triangle_count), "instances": int(sc.instances.size),
                "build_ms": round(node.ctx.bvh_stats().build_ms, 1), "mrays_per_s_static": round(rate(), 1)}
+        if args.sun_turn:
+            turns = []
+            base = node.ctx.bvh_stats().sun_rebuilds
+            d0 = np.array(sc.sun[1], np.float64)
+            c, s_ = np.cos(np.radians(10.0)), np.sin(np.radians(10.0))
+            d1 = np.array([c * d0[0] + s_ * d0[2], d0[1], -s_ * d0[0] + c * d0[2]])
+            for label, d in (("turned", d1), ("back", d0)):
+                node.ctx.set_lights((sc.sun[0], tuple(float(x) for x in d)), ())
+                world = rate()  # the world BVHs carry the sun's rays meanwhile
+                t = time.perf_counter()
+                while node.ctx.bvh_stats().sun_rebuilds == base and time.perf_counter() - t < 60.0:
+                    node.execute(app[0])
+                    app[0] = D.AppState(app[0].frame_index + 1)
+                    node.ctx.synchronize()
+                base = node.ctx.bvh_stats().sun_rebuilds
+                turns.append({"sun": label, "mrays_per_s_world": round(world, 1), "installed_after_s": round(time.perf_counter() - t, 2),
+                              "rebuild_ms": round(node.ctx.bvh_stats().sun_build_ms, 1), "mrays_per_s_rebuilt": round(rate(), 1)})
+            out["sun_turns"] = turns
+            print(json.dumps(out), flush=True)
+            node.ctx.close()
+            continue
         inst = sc.instances.copy()
         moves = []
         inst["object_to_world"][0, 3] += 0.5
