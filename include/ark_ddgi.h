@@ -298,7 +298,9 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* scene);
  * src's last set_scene built are shared, not copied, and stay alive while any context
  * uses them. For the Z-slab contexts of one GPU (the reference binds one TLAS and one
  * set of scene buffers per device, GpuScene.cpp:872-1010); a later set_scene on
- * either context gives it a scene of its own. */
+ * either context gives it a scene of its own. Contexts that share a scene are driven
+ * from one host thread (a refit or a sun BVH rebuild of one reaches the others). The
+ * scene's last holder joins a background sun BVH rebuild still running (set_lights). */
 int ark_ddgi_share_scene(ArkDdgiCtx* ctx, const ArkDdgiCtx* src);
 
 /* The per-frame light set (GpuScene::update, GpuScene.cpp:790-858): the reference
