@@ -139,6 +139,11 @@ struct SunJob {
     float frame[9] {};
     float ms = 0.0f;
     bool ok = false;
+    ~SunJob()
+    {
+        if (t.joinable()) t.join();
+        buf.release(); // not installed (an installed buffer was moved to the scene)
+    }
 };
 
 struct SceneStore {
@@ -178,11 +183,7 @@ struct SceneStore {
     ~SceneStore()
     {
         (void)hipSetDevice(device);
-        // the job reads the triangle records: done before they are freed
-        if (sunJob) {
-            if (sunJob->t.joinable()) sunJob->t.join();
-            sunJob->buf.release();
-        }
+        sunJob.reset(); // joins it: the job reads the triangle records freed below
         for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
                                  &refitBoxes, &refitOrder, &refitBounds })
             b->release();
@@ -582,7 +583,7 @@ int sunRebuildStep(ArkDdgiCtx* ctx)
     SceneStore& st = *ctx->sceneStore;
     if (st.sunJob && st.sunJob->done.load(std::memory_order_acquire)) {
         std::unique_ptr<SunJob> job = std::move(st.sunJob);
-        if (job->t.joinable()) job->t.join();
+        job->t.join();
         if (job->ok && job->version == st.version) {
             // frames in flight may traverse the old one (any context, when shared)
             if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
@@ -605,8 +606,6 @@ int sunRebuildStep(ArkDdgiCtx* ctx)
             ++st.version;
             deriveSceneArgs(ctx);
             if (const int rc = ensureSpill(ctx)) return rc;
-        } else {
-            job->buf.release();
         }
     }
     if (!st.sunWanted || !ctx->hasSun || st.sunJob) return ARK_DDGI_OK;

@@ -314,3 +314,41 @@ def test_sun_bvh_rebuilt_in_background(cause):
     finally:
         ctx.close()
         orc.close()
+
+
+def test_close_during_sun_bvh_rebuild():
+    """A context closed while its scene's light-space BVH is being rebuilt in the
+    background: the scene's destructor joins the thread before it frees the triangle
+    records the thread reads (no crash, no hang); a context sharing the scene keeps it
+    and installs the rebuild at its next update."""
+    import time
+
+    sc = S.soup(256_000, extent=9.0)
+    grid = D.ProbeGrid((6, 6, 6), (1.5, 1.5, 1.5), (0.5, 0.5, 0.5))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=216, compute_probe_offsets=False,
+                       max_rays_per_probe=64, max_probe_updates=216)
+    with _Env("1"):
+        a = D.DDGIContext(grid, 10000.0, cfg)
+        b = D.DDGIContext(grid, 10000.0, cfg)
+    a.set_scene(sc)
+    b.share_scene(a)
+    d = np.array([0.2, -1.0, 0.5], np.float32)
+    sun = (sc.sun[0], tuple(float(x) for x in d / np.linalg.norm(d)))
+    a.set_lights(sun, ())  # starts the rebuild on the shared scene
+    b.set_lights(sun, ())
+    a.close()
+    p = D.frame_params(cfg, grid, D.AppState(0), 0, light_pre_exposure=1.0, environment_brightness=1.0)
+    t0 = time.time()
+    while b.bvh_stats().sun_rebuilds == 0:
+        assert time.time() - t0 < 90, "the shared scene's rebuild was never installed"
+        b.update(p)
+        b.synchronize()
+        time.sleep(0.05)
+    assert b.bvh_stats().sun_node_count > 0
+    b.close()
+    # and a context closed with its rebuild still running, nothing sharing it
+    with _Env("1"):
+        c = D.DDGIContext(grid, 10000.0, cfg)
+    c.set_scene(sc)
+    c.set_lights(sun, ())
+    c.close()
