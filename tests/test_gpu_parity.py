@@ -183,6 +183,40 @@ def test_inf_radiance_surfels():
         orc.close()
 
 
+@pytest.mark.parametrize("sharpness", [50.0, 8.0, 7.3, 2.5, 0.25, 80.0])
+def test_visibility_sharpness_modes(sharpness):
+    """Every visibility-weight path of k_probe_update against the oracle
+    (pow(max(0, dot), sharpness), probeUpdateVisibility.comp:43-56): 50 (the node's
+    default, the unrolled integer power), 8 (other small integers), 7.3 (the branch-free
+    exp2/log2 form), 2.5 and 0.25 (the square-root exponents) and 80 (past the integer
+    range) - the last three on the generic per-texel path. Two frames, offsets on."""
+    sc, ex = S.cornell_box()
+    grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=512, visibility_sharpness=sharpness)
+    exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
+    import oracle_lib as O
+    from parity import RESOURCES, diff_report
+
+    ctx = D.DDGIContext(grid, ex["z_far"], cfg)
+    ctx.set_scene(sc)
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(sc, 8)
+    try:
+        for f in range(2):
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            assert p.visibility_sharpness == sharpness
+            ctx.update(p)
+            ctx.synchronize()
+            orc.update(p, 8)
+            for k, w in RESOURCES.items():
+                r = diff_report(k, ctx.read(w), orc.read(w))
+                assert r["mismatch"] == 0, f"sharpness {sharpness}, frame {f}: {r}"
+    finally:
+        ctx.close()
+        orc.close()
+
+
 def test_sun_bvh_depth_sizes_the_spill(monkeypatch):
     """the light-space sun BVH holds the triangles of all three
     hit-mask classes in one tree, so it can be deeper than each class's world BVH, and
