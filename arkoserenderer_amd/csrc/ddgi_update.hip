@@ -152,29 +152,14 @@ __device__ __forceinline__ V3 texelDirection(int res, int tx, int ty)
     return octahedralDecode(2.0f * uvx - 1.0f, 2.0f * uvy - 1.0f);
 }
 
-// The weight w of a pair's texels t (dot d) and -t: pos = d > 0 ? w : 0, neg = d > 0 ? 0
-// : w, as bit masks of d's sign - an arithmetic shift and two bitwise ands, which gfx950
-// issues at full rate, where v_cmp and v_cndmask issue at half rate (2.3 against 4.2
-// cycles per wave-instruction, tools/probe/valu_table4.hip). Bit for bit the selects for
-// every d: at d = +0 or -0, w = pow(+0) = +0 goes to either side. The ands are asm so
-// that the compiler does not fold them back into compare + select.
-__device__ __forceinline__ void splitBySign(float d, float w, float& pos, float& neg)
-{
-    const uint32_t m = static_cast<uint32_t>(static_cast<int32_t>(__float_as_uint(d)) >> 31);
-    uint32_t p, n;
-    asm("v_bitop3_b32 %0, %1, %2, %2 bitop3:0x30" : "=v"(p) : "v"(__float_as_uint(w)), "v"(m)); // w & ~m
-    asm("v_and_b32 %0, %1, %2" : "=v"(n) : "v"(__float_as_uint(w)), "v"(m));
-    pos = __uint_as_float(p);
-    neg = __uint_as_float(n);
-}
-
 template<int MODE>
 __device__ __forceinline__ void visibilityOrbit(const UpdateLds& L, int p, uint32_t R, V3 t, float sharp, float* nv0, float* nv1, float* tw)
 {
     const float4* ray = L.ray + p * L.stride;
     const float* d2 = L.d2 + p * L.stride;
     const int ns = static_cast<int>(sharp);
-    auto step = [&](uint32_t s) {
+#pragma unroll 2
+    for (uint32_t s = 0; s < R; ++s) {
         const float4 r = ray[s];
         const float dd2 = d2[s];
         const float px = t.x * r.x, py = t.y * r.y;
@@ -182,23 +167,14 @@ __device__ __forceinline__ void visibilityOrbit(const UpdateLds& L, int p, uint3
         const float d2v = fmaf(t.z, r.z, py - px);
         const float w1 = visWeightAbs<MODE>(fabsf_(d1), sharp, ns);
         const float w2 = visWeightAbs<MODE>(fabsf_(d2v), sharp, ns);
-        float w0, w2n, w1p, w3;
-        splitBySign(d1, w1, w0, w2n);
-        splitBySign(d2v, w2, w1p, w3);
+        const float w0 = d1 > 0.0f ? w1 : 0.0f, w2n = d1 > 0.0f ? 0.0f : w1;
+        const float w1p = d2v > 0.0f ? w2 : 0.0f, w3 = d2v > 0.0f ? 0.0f : w2;
         // texel order: t, t', -t, -t'
         nv0[0] = fmaf(w0, r.w, nv0[0]);  nv1[0] = fmaf(w0, dd2, nv1[0]);  tw[0] += w0;
         nv0[1] = fmaf(w1p, r.w, nv0[1]); nv1[1] = fmaf(w1p, dd2, nv1[1]); tw[1] += w1p;
         nv0[2] = fmaf(w2n, r.w, nv0[2]); nv1[2] = fmaf(w2n, dd2, nv1[2]); tw[2] += w2n;
         nv0[3] = fmaf(w3, r.w, nv0[3]);  nv1[3] = fmaf(w3, dd2, nv1[3]);  tw[3] += w3;
-    };
-    // two rays per iteration, unrolled by hand: the compiler does not unroll a loop
-    // with inline asm (splitBySign) and a runtime trip count
-    uint32_t s = 0;
-    for (; s + 1 < R; s += 2) {
-        step(s);
-        step(s + 1);
     }
-    if (s < R) step(s);
 }
 
 // any sharpness: each texel's dot and pow evaluated as the reference does
@@ -304,15 +280,12 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
             const uint2* rad = L.rad + p * L.stride;
             V3 acc[4] = { splat(0.0f), splat(0.0f), splat(0.0f), splat(0.0f) };
             float tw[4] = { 0.0f, 0.0f, 0.0f, 0.0f };
-            auto step = [&](uint32_t s) {
+#pragma unroll 2
+            for (uint32_t s = 0; s < R; ++s) {
                 const float4 r = ray[s];
                 const uint2 cw = rad[s];
-                float4 c = make_float4(f16_to_f32(static_cast<uint16_t>(cw.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(cw.x >> 16)),
-                                       f16_to_f32(static_cast<uint16_t>(cw.y & 0xffffu)), 0.0f);
-                // converted once per ray: the compiler otherwise folds each conversion
-                // into its four fmas as v_fma_mix_f32, a half-rate instruction on gfx950
-                // (3 conversions + 12 full-rate fmas instead of 12 half-rate mixes)
-                asm("" : "+v"(c.x), "+v"(c.y), "+v"(c.z));
+                const float4 c = make_float4(f16_to_f32(static_cast<uint16_t>(cw.x & 0xffffu)), f16_to_f32(static_cast<uint16_t>(cw.x >> 16)),
+                                             f16_to_f32(static_cast<uint16_t>(cw.y & 0xffffu)), 0.0f);
                 const float px = t.x * r.x, py = t.y * r.y;
                 const float d1 = fmaf(t.z, r.z, px + py);
                 const float d2 = fmaf(t.z, r.z, py - px);
@@ -326,13 +299,7 @@ __global__ void __launch_bounds__(kUpdateBlock) k_probe_update(FrameArgs f)
                     acc[k] = v3(fmaf(w[k], c.x, acc[k].x), fmaf(w[k], c.y, acc[k].y), fmaf(w[k], c.z, acc[k].z));
                     tw[k] += w[k];
                 }
-            };
-            uint32_t s = 0; // two rays per iteration (by hand, as visibilityOrbit)
-            for (; s + 1 < R; s += 2) {
-                step(s);
-                step(s + 1);
             }
-            if (s < R) step(s);
             const uint32_t probeIdx = f.slots[slot].probe_index;
             const uint32_t tilesPerSheet = static_cast<uint32_t>(f.X * f.Z);
             const uint32_t sheetProbeIdx = probeIdx % tilesPerSheet;

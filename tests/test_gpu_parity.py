@@ -205,7 +205,7 @@ def test_visibility_sharpness_modes(sharpness):
     try:
         for f in range(2):
             p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
-            assert p.visibility_sharpness == sharpness
+            assert p.visibility_sharpness == np.float32(sharpness)
             ctx.update(p)
             ctx.synchronize()
             orc.update(p, 8)
