@@ -652,24 +652,17 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
     return { fmaf(p.x, F[0], fmaf(p.y, F[1], p.z * F[2])), fmaf(p.x, F[3], fmaf(p.y, F[4], p.z * F[5])), fmaf(p.x, F[6], fmaf(p.y, F[7], p.z * F[8])) };
 }
 
-// Child s of slot byte B (word LO / HI of the plane pairs): crossed iff
-// qlo_u <= Fu, qhi_u >= Cu, qlo_v <= Fv, qhi_v >= Cv and qhi_w >= Cw - five SDWA byte
-// compares (unsigned byte vs a signed lane value) into four SGPR pairs and VCC first,
-// then the ANDs - two levels of VALU -> SALU dependence per child instead of four (the
-// wave otherwise stalls on every compare's lane mask before the next compare issues;
-// profiles/r04_j_*: K = 4096 windows 1,901 -> 1,924 Mrays/s, P = 8 slab shadow 0.198 ->
-// 0.184 ms) - the result shifted into the lane's slot mask as v_addc's carry (m = 2m + hit).
-#define ARK_SUN_CHILD_PAR(LU, HU, LV, HV, HW, B)                                           \
-    "v_cmp_le_i32_sdwa %[m0], %[" LU "], %[fu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
-    "v_cmp_ge_i32_sdwa %[m1], %[" HU "], %[cu] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
-    "v_cmp_le_i32_sdwa %[m2], %[" LV "], %[fv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
-    "v_cmp_ge_i32_sdwa %[m3], %[" HV "], %[cv] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"   \
-    "v_cmp_ge_i32_sdwa vcc, %[" HW "], %[cw] src0_sel:BYTE_" B " src1_sel:DWORD\n\t"     \
-    "s_and_b64 %[m0], %[m0], %[m1]\n\t"                                                  \
-    "s_and_b64 %[m2], %[m2], %[m3]\n\t"                                                  \
-    "s_and_b64 %[m0], %[m0], %[m2]\n\t"                                                  \
-    "s_and_b64 vcc, %[m0], vcc\n\t"                                                      \
-    "v_addc_co_u32_e32 %[acc], vcc, %[acc], %[acc], vcc\n\t"
+// Bytewise unsigned x >= y of four packed bytes, the result in bit 7 of each byte, from
+// xh = x | 0x80808080 and yl = y & 0x7f7f7f7f: d = xh - yl borrows within no byte
+// (each byte of xh is >= 0x80 > each of yl), so bit 7 of a byte of d says x_lo7 >= y_lo7;
+// with the top bits, x >= y = (x7 & ~y7) | (~(x7 ^ y7) & d7) - one v_bitop3.
+__device__ __forceinline__ uint32_t geBytes(uint32_t x, uint32_t y, uint32_t xh, uint32_t yl)
+{
+    const uint32_t d = xh - yl;
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xb2" : "=v"(r) : "v"(x), "v"(y), "v"(d));
+    return r;
+}
 
 // Node visit of a ray along +w from light-space point pl (k_trace_shadow<SUN>). With
 // the direction exactly +w the slab test of u and v degenerates to "pl's coordinate
@@ -679,39 +672,46 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
 // tmin is not used (a box between pl and pl + tmin is visited, conservatively). The
 // children are visited in slot order: the builder sorted them by their lower w bound
 // (Bvh8CollapseOptions::slot_sort_axis), the order the ray meets them.
+// The five conditions are tested on four children at once, bytewise within the plane
+// words (geBytes), with no lane-mask compares (the per-child form: 40 SDWA v_cmp, 32
+// s_and and 8 v_addc). Q is clamped to [0, 255]
+// so that floor and ceil are bytes: that can only accept more children (qlo <= 0 for a
+// point below the node's anchor, qhi >= 255 above its far side), never fewer, and an
+// any-hit result does not depend on extra visits.
 __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 pl, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase,
                                              uint32_t& tBits)
 {
-    // quantized coordinate, clamped to [-2, 258] (outside [0, 255] no child holds it)
-    // so the conversions stay in range
     auto quant = [](float c, uint32_t p, uint32_t ebyte) {
-        return __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(c - __uint_as_float(p), 127 - static_cast<int>(ebyte)), -2.0f, 258.0f);
+        return __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(c - __uint_as_float(p), 127 - static_cast<int>(ebyte)), 0.0f, 255.0f);
     };
     const float qu = quant(pl.x, w0.x, w0.w & 0xffu), qv = quant(pl.y, w0.y, (w0.w >> 8) & 0xffu), qw = quant(pl.z, w0.z, (w0.w >> 16) & 0xffu);
-    const int fu = static_cast<int>(floorf(qu)), cu = static_cast<int>(ceilf(qu));
-    const int fv = static_cast<int>(floorf(qv)), cv = static_cast<int>(ceilf(qv));
-    const int cw = static_cast<int>(ceilf(qw));
-    uint32_t hit = 0;
+    constexpr uint32_t kH = 0x80808080u;
+    // floor (the truncating conversion: Q >= 0) and ceil of Q, in every byte (v_perm_b32
+    // with selector 0: byte 0 of the second operand four times)
+    auto bcast = [](float q) { return __builtin_amdgcn_perm(0u, static_cast<uint32_t>(q), 0u); };
+    const uint32_t Fu = bcast(qu), Cu = bcast(ceilf(qu)), Fv = bcast(qv), Cv = bcast(ceilf(qv)), Cw = bcast(ceilf(qw));
+    const uint32_t FuH = Fu | kH, FvH = Fv | kH, CuL = Cu & ~kH, CvL = Cv & ~kH, CwL = Cw & ~kH;
     // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
-    // qhi w = w4.z|w (children 0-3 | 4-7); slots 7 .. 0 shifted in
-    uint64_t m0, m1, m2, m3;
-    asm(ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "3") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "2")
-        ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "1") ARK_SUN_CHILD_PAR("lu1", "hu1", "lv1", "hv1", "hw1", "0")
-        ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "3") ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "2")
-        ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "1") ARK_SUN_CHILD_PAR("lu0", "hu0", "lv0", "hv0", "hw0", "0")
-        : [acc] "+v"(hit), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
-        : [lu0] "v"(w2.x), [lu1] "v"(w2.y), [lv0] "v"(w2.z), [lv1] "v"(w2.w), [hu0] "v"(w3.z), [hu1] "v"(w3.w), [hv0] "v"(w4.x), [hv1] "v"(w4.y),
-          [hw0] "v"(w4.z), [hw1] "v"(w4.w), [fu] "v"(fu), [cu] "v"(cu), [fv] "v"(fv), [cv] "v"(cv), [cw] "v"(cw)
-        : "vcc");
+    // qhi w = w4.z|w (children 0-3 | 4-7, child k in byte k & 3)
+    auto crossed = [&](uint32_t lu, uint32_t hu, uint32_t lv, uint32_t hv, uint32_t hw) {
+        return geBytes(Fu, lu, FuH, lu & ~kH) & geBytes(hu, Cu, hu | kH, CuL) & geBytes(Fv, lv, FvH, lv & ~kH) & geBytes(hv, Cv, hv | kH, CvL) &
+               geBytes(hw, Cw, hw | kH, CwL) & kH;
+    };
+    const uint32_t r0 = crossed(w2.x, w3.z, w2.z, w4.x, w4.z), r1 = crossed(w2.y, w3.w, w2.w, w4.y, w4.w);
+    // bit 7 of byte k of r0 / r1 -> bit k / k + 4 of the slot mask: the bits of x =
+    // (r0 >> 4) | r1 sit at 8k + 3 (child k) and 8k + 7 (child k + 4), and the high word
+    // of x * (2^29 + 2^22 + 2^15 + 2^8) holds them at bits k and k + 4 (no two partial
+    // products share a bit position, so nothing carries); its bits above 7 are cleared
+    // by the 8-bit masks below
+    const uint32_t hit = __umulhi((r0 >> 4) | r1, 0x20408100u);
     const uint32_t imask = w0.w >> 24;
     gBase = w1.x;
     gBits = (hit & imask) | (imask << 8);
     tBase = w1.y;
     const uint32_t stride = w1.w & 31u, leafHits = hit & (w1.w >> 8) & 0xffu;
-    const uint32_t x = (leafHits << stride) | leafHits;
-    tBits = ((x << stride) | x) & w1.z;
+    const uint32_t xl = (leafHits << stride) | leafHits;
+    tBits = ((xl << stride) | xl) & w1.z;
 }
-#undef ARK_SUN_CHILD_PAR
 
 // travStepDual for a sun shadow ray in the light-space BVH: both sides' loads issued
 // by every lane (a skipped side reads the resident record 0 / the root), the
