@@ -978,11 +978,39 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
     RayHit h { 0.0f, 0.0f, 0.0f, kNoHit, 0u, 0u, false };
     float opaqueT = 0.0f; // signed t of the opaque hit, kept for the masked pass
     auto done = [&]() { return travDoneDual(ts, nBits, st); };
+    // Deferred retirement: without a masked pass to continue into, a lane whose ray is
+    // done only goes idle, and its hit record is written at the next refill, just
+    // before the lane takes a new ray. A lane finishes a ray in nearly every step of a
+    // wave (one ray per lane every ~25 steps), so the exec-masked store path would
+    // otherwise run almost every step; at a refill it runs once per batch of idle
+    // lanes. Lanes that finish after the ray supply is exhausted retire at once.
+    bool pending = false;
+    auto storeHit = [&]() {
+        GpuHit out;
+        if (h.tri == kNoHit) {
+            out.t = __builtin_bit_cast(float, 0x7f800000u);
+            out.u = out.v = 0.0f;
+            out.tri = kNoHit;
+        } else {
+            out.t = h.backface ? -h.t : h.t;
+            out.u = h.u;
+            out.v = h.v;
+            out.tri = h.tri;
+            if (COUNT) cHits++;
+        }
+        f.hits[ray] = out;
+        if (COUNT && f.ray_steps) f.ray_steps[ray] = static_cast<uint16_t>(min(rSteps, 65535u));
+        if (COUNT) rSteps = 0;
+    };
 
     for (;;) {
         // ---- refill finished lanes --------------------------------------------
         const uint64_t need = __ballot(!active);
         if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
+            if (pending) {
+                storeHit();
+                pending = false;
+            }
             const uint32_t n = static_cast<uint32_t>(__popcll(need));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
             const uint32_t avail = poolEnd - poolNext;
@@ -1033,7 +1061,10 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // restarts it, and a step of a done lane would change nothing anyway)
         if (active) travStepDual<kTraceBlock, false, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
-        if (active && done()) {
+        if (active && done() && (!Src::kMaskedPass || sc.root_masked < 0) && !exhausted) {
+            active = false;
+            pending = true;
+        } else if (active && done()) {
             bool finished = true;
             if (Src::kMaskedPass && pass == 0) {
                 // opaque pass done (raygen.rgen:35-62); masked pass: RayFlags_NoOpaque,
@@ -1056,22 +1087,11 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
                     // masked pass found nothing: the opaque result (already stored) stands
                     out = f.hits[ray];
                     if (COUNT && out.tri != kNoHit) cHits++;
+                    if (COUNT && f.ray_steps) f.ray_steps[ray] = static_cast<uint16_t>(min(rSteps, 65535u));
+                    if (COUNT) rSteps = 0;
                 } else {
-                    if (h.tri == kNoHit) {
-                        out.t = __builtin_bit_cast(float, 0x7f800000u);
-                        out.u = out.v = 0.0f;
-                        out.tri = kNoHit;
-                    } else {
-                        out.t = h.backface ? -h.t : h.t;
-                        out.u = h.u;
-                        out.v = h.v;
-                        out.tri = h.tri;
-                        if (COUNT) cHits++;
-                    }
-                    f.hits[ray] = out;
+                    storeHit();
                 }
-                if (COUNT && f.ray_steps) f.ray_steps[ray] = static_cast<uint16_t>(min(rSteps, 65535u));
-                if (COUNT) rSteps = 0;
                 active = false;
             }
         }
