@@ -1662,17 +1662,9 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
     V3 o = { 0, 0, 0 }, d = { 0, 0, 1 }, idir = { 0, 0, 1 };
     auto done = [&]() { return travDoneDual(ts, nBits, st); };
     auto stop = [&]() { ts = TravState { 0u, 0u, 0u, 0u }; nBits = 0; st.depth = 0; };
-    // Deferred occlusion bit (as k_trace's deferred retirement): before the supply is
-    // exhausted an occluded ray only goes idle, and its bit is set at the next refill,
-    // so the exec-masked atomic runs once per refill instead of in nearly every step.
-    bool pendingOcc = false;
     for (;;) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.refill_min || need == ~0ull)) {
-            if (pendingOcc) {
-                atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
-                pendingOcc = false;
-            }
             const uint32_t n = static_cast<uint32_t>(__popcll(need));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
             const uint32_t avail = poolEnd - poolNext;
@@ -1770,17 +1762,13 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
             }
             const bool helper = pass >= 256;
             const uint32_t root = helper ? static_cast<uint32_t>(pass >> 8) - 1u : lane;
-            if (occluded && !exhausted) {
-                // (no helper lanes before the supply is exhausted)
-                pendingOcc = true;
-                active = false;
-            } else if (occluded) {
+            if (occluded) {
                 atomicOr(&f.shadow_bits[owner >> 4], 1u << (16u + (owner & 15u)));
                 if (exhausted) tailOr(tl, wbase + root, 0x80u);
                 stop();
                 if (!helper) pass = 3; // no further hit-mask classes
             }
-            if (active && done()) {
+            if (done()) {
                 if (helper) {
                     tailSub(tl, wbase + root, 1u);
                     active = false;
