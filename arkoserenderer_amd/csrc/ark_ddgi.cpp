@@ -200,7 +200,7 @@ struct ArkDdgiCtx {
     hipStream_t orderStream = nullptr;
     bool orderValid = false;
     // traversal knobs, fixed at create: refill batch, grab chunk
-    uint32_t refillMin = 16, grabChunk = 64;
+    uint32_t refillMin = 16, shadowRefillMin = 16, grabChunk = 64;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -698,6 +698,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // ARK_GRAB_CHUNK: rays per partition-head grab, 64 = a probe quarter of
         // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
+        if (const char* r = std::getenv("ARK_SHADOW_REFILL_MIN")) ctx->shadowRefillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
         if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0 ? 1 : 0;
@@ -1544,6 +1545,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.spill = ctx->spill.as<uint32_t>() + ctx->spillRegionWords; // region 1 (primary traversal)
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
+    f.shadow_refill_min = ctx->shadowRefillMin;
     // a half-occupancy window (below kPipeHalfRays) hands out 32 rays per partition-head
     // grab to the probe-ray and shadow-ray queues (K = 2048 windows 0.429 -> 0.420 ms;
     // the whole grid keeps 64: 4.13 vs 4.18 ms at 32, profiles/r02_m19)
@@ -2061,6 +2063,7 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.list_count = f.ray_counter + kRayCounterWords;
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
+    f.shadow_refill_min = ctx->shadowRefillMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
     if (ctx->sceneVersion != ctx->sceneStore->version) {
