@@ -200,7 +200,7 @@ struct ArkDdgiCtx {
     hipStream_t orderStream = nullptr;
     bool orderValid = false;
     // traversal knobs, fixed at create: refill batch, grab chunk
-    uint32_t refillMin = 16, shadowRefillMin = 16, grabChunk = 64;
+    uint32_t refillMin = 16, sunRefillMin = 32, grabChunk = 64;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -698,7 +698,12 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // ARK_GRAB_CHUNK: rays per partition-head grab, 64 = a probe quarter of
         // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
         if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
-        if (const char* r = std::getenv("ARK_SHADOW_REFILL_MIN")) ctx->shadowRefillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
+        // ARK_SUN_REFILL_MIN: the same for the sun's shadow rays in the light-space BVH,
+        // whose any-hit rays are short: 32 (profiles/r05_q): C4 shadow phase 0.648 ->
+        // 0.625-0.635 ms, K = 4096 0.529 -> 0.514 ms, K = 2048 0.327 -> 0.320 ms, P = 8
+        // slowest slab 0.573 -> 0.556 ms; the world BVHs' shadow rays (spots) keep 16
+        // (32 there: C5 shadow 1.92 -> 2.07 ms)
+        if (const char* r = std::getenv("ARK_SUN_REFILL_MIN")) ctx->sunRefillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
         if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0 ? 1 : 0;
@@ -1545,7 +1550,7 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.spill = ctx->spill.as<uint32_t>() + ctx->spillRegionWords; // region 1 (primary traversal)
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
-    f.shadow_refill_min = ctx->shadowRefillMin;
+    f.sun_refill_min = ctx->sunRefillMin;
     // a half-occupancy window (below kPipeHalfRays) hands out 32 rays per partition-head
     // grab to the probe-ray and shadow-ray queues (K = 2048 windows 0.429 -> 0.420 ms;
     // the whole grid keeps 64: 4.13 vs 4.18 ms at 32, profiles/r02_m19)
@@ -2063,7 +2068,7 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.list_count = f.ray_counter + kRayCounterWords;
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
-    f.shadow_refill_min = ctx->shadowRefillMin;
+    f.sun_refill_min = ctx->sunRefillMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
     if (ctx->sceneVersion != ctx->sceneStore->version) {

@@ -1664,7 +1664,7 @@ __device__ __forceinline__ void shadowPhase(const SceneArgs& sc, const FrameArgs
     auto stop = [&]() { ts = TravState { 0u, 0u, 0u, 0u }; nBits = 0; st.depth = 0; };
     for (;;) {
         const uint64_t need = __ballot(!active);
-        if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= f.shadow_refill_min || need == ~0ull)) {
+        if (need != 0 && !exhausted && (static_cast<uint32_t>(__popcll(need)) >= (SUN ? f.sun_refill_min : f.refill_min) || need == ~0ull)) {
             const uint32_t n = static_cast<uint32_t>(__popcll(need));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(need >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(need), 0u));
             const uint32_t avail = poolEnd - poolNext;
