@@ -1381,8 +1381,9 @@ template<bool COUNT, int WPE>
 __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(WPE))) k_shade(SceneArgs sc, FrameArgs f)
 {
     if (frameAborted(f.abort_word)) return;
-    __shared__ uint32_t listA[kShadeChunk]; // compacted front hits (ray index)
-    __shared__ uint32_t counts[4];          // [0] front hits, [2,3] chunk
+    // compacted front hits (ray index) from the start, misses from the end
+    __shared__ uint32_t listA[kShadeChunk];
+    __shared__ uint32_t counts[4];          // [0] front hits, [1] misses, [2,3] chunk
     uint32_t cFront = 0;
     // the spot lights, read once per workgroup: per front hit and lit spot they were a
     // dependent 96-B read ahead of the IES lookup (C5: k_shade 2.06 -> 1.97 ms, +1.2 %;
@@ -1404,26 +1405,24 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             uint32_t b, e;
             grabRays(f, heads, home, tried, b, e, static_cast<uint32_t>(kShadeChunk));
             counts[0] = 0;
+            counts[1] = 0;
             counts[2] = b;
             counts[3] = e;
         }
         __syncthreads();
         const uint32_t chunk = counts[2], chunkEnd = counts[3];
         if (chunk >= chunkEnd) break;
-        // ---- A. classify: misses and backfaces finish here ----------------------
+        // ---- A. classify: backfaces finish here; front hits and misses are listed -
+        // (a miss's environment lookup - atan2, acos, a texture sample - runs densely in
+        // C below: inline, the few misses of a chunk made most of its waves run it)
         for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
             if (chunk + r >= chunkEnd) break;
             const uint32_t q = (chunk + r) / f.R;
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
-                // miss (raygen.rgen:70-79)
-                V3 origin, dir;
-                rayOf(f, ray, &origin, &dir);
-                float u, v;
-                sphericalUvFromDirection(dir, &u, &v);
-                float4 c = sc.sample(sc.env_texture, u, v);
-                storeSurfel(f, ray, f.environment_multiplier * v3(c.x, c.y, c.z), f.z_far);
+                const uint32_t k = atomicAdd(&counts[1], 1u);
+                listA[kShadeChunk - 1u - k] = ray;
             } else if (hit.t < 0.0f) {
                 // backface: colour 0, depth x 0.2 (raygen.rgen:129-134); the closest-hit
                 // colour and the indirect term are overwritten, so they are not evaluated.
@@ -1541,6 +1540,17 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
             const V3 indirect = splat(1.0f - metallic) * (splat(1.0f) - F) * irradiance;
             const V3 bi = baseColor * indirect;
             storeSurfel(f, ray, color + bi, T);
+        }
+        // ---- C. misses (raygen.rgen:70-79) ------------------------------------------
+        const uint32_t nM = counts[1];
+        for (uint32_t k = threadIdx.x; k < nM; k += kShadeBlock) {
+            const uint32_t ray = listA[kShadeChunk - 1u - k];
+            V3 origin, dir;
+            rayOf(f, ray, &origin, &dir);
+            float u, v;
+            sphericalUvFromDirection(dir, &u, &v);
+            float4 c = sc.sample(sc.env_texture, u, v);
+            storeSurfel(f, ray, f.environment_multiplier * v3(c.x, c.y, c.z), f.z_far);
         }
         __syncthreads();
     }
