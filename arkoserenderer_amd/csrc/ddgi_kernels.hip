@@ -43,6 +43,14 @@ __device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) c
 
 namespace dev {
 
+// x / R for a queue position or ray index: a shift when R is a power of two (the
+// bench's and the reference's ray counts), the integer division (~15 VALU, among them
+// quarter-rate multiplies) otherwise; the branch is on a kernel argument (uniform)
+__device__ __forceinline__ uint32_t divRay(const FrameArgs& f, uint32_t x)
+{
+    return f.r_shift1 != 0u ? x >> (f.r_shift1 - 1u) : x / f.R;
+}
+
 // ---------------------------------------------------------------------------
 // 1. window -> slots
 // ---------------------------------------------------------------------------
@@ -921,7 +929,7 @@ struct ProbeRays {
     }
     __device__ static void load(const FrameArgs& f, uint32_t r, uint32_t& ray, V3& o, V3& d, float& tmax)
     {
-        const uint32_t qp = r / f.R;
+        const uint32_t qp = divRay(f, r);
         const uint32_t slot = slotAt(f, qp);
         const float4 fv = f.fib_order[r - qp * f.R]; // (direction, sample index)
         const GpuProbeSlot ps = f.slots[slot];
@@ -1361,7 +1369,7 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 // (opaque.rchit:105-176 with traceShadowRay's shadowFactor 1 or 0).
 __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3 color, float dist)
 {
-    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+    const uint32_t slot = divRay(f, ray), sample = ray - slot * f.R;
     uint2 packed;
     packed.x = static_cast<uint32_t>(f32_to_f16(color.x)) | (static_cast<uint32_t>(f32_to_f16(color.y)) << 16);
     packed.y = static_cast<uint32_t>(f32_to_f16(color.z)) | (static_cast<uint32_t>(f32_to_f16(dist)) << 16);
@@ -1370,7 +1378,7 @@ __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3
 
 __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* origin, V3* dir)
 {
-    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
+    const uint32_t slot = divRay(f, ray), sample = ray - slot * f.R;
     const GpuProbeSlot ps = f.slots[slot];
     const float4 fb = f.fib[sample];
     *origin = { ps.pos[0], ps.pos[1], ps.pos[2] };
@@ -1417,7 +1425,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
         // C below: inline, the few misses of a chunk made most of its waves run it)
         for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
             if (chunk + r >= chunkEnd) break;
-            const uint32_t q = (chunk + r) / f.R;
+            const uint32_t q = divRay(f, chunk + r);
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
@@ -1881,7 +1889,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         if (REFL) {
             rays[k] = pos < total ? pos : kNoHit;
         } else {
-            const uint32_t q = pos / f.R;
+            const uint32_t q = divRay(f, pos);
             rays[k] = pos < total ? slotAt(f, q) * f.R + (pos - q * f.R) : kNoHit;
         }
     }
@@ -1942,7 +1950,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             const float t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
             hitPoint = origin + t * dir;
         } else {
-            const uint32_t q = pos / f.R;
+            const uint32_t q = divRay(f, pos);
             ray = slotAt(f, q) * f.R + (pos - q * f.R);
             const float t = f.hits[ray].t;
             V3 origin, dir;
