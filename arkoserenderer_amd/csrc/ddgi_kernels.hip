@@ -1369,7 +1369,7 @@ __device__ V3 sampleDDGI(const FrameArgs& f, V3 P, V3 N, V3 Vw)
 // (opaque.rchit:105-176 with traceShadowRay's shadowFactor 1 or 0).
 __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3 color, float dist)
 {
-    const uint32_t slot = divRay(f, ray), sample = ray - slot * f.R;
+    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
     uint2 packed;
     packed.x = static_cast<uint32_t>(f32_to_f16(color.x)) | (static_cast<uint32_t>(f32_to_f16(color.y)) << 16);
     packed.y = static_cast<uint32_t>(f32_to_f16(color.z)) | (static_cast<uint32_t>(f32_to_f16(dist)) << 16);
@@ -1378,7 +1378,7 @@ __device__ __forceinline__ void storeSurfel(const FrameArgs& f, uint32_t ray, V3
 
 __device__ __forceinline__ void rayOf(const FrameArgs& f, uint32_t ray, V3* origin, V3* dir)
 {
-    const uint32_t slot = divRay(f, ray), sample = ray - slot * f.R;
+    const uint32_t slot = ray / f.R, sample = ray - slot * f.R;
     const GpuProbeSlot ps = f.slots[slot];
     const float4 fb = f.fib[sample];
     *origin = { ps.pos[0], ps.pos[1], ps.pos[2] };
@@ -1425,7 +1425,7 @@ __global__ void __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_e
         // C below: inline, the few misses of a chunk made most of its waves run it)
         for (uint32_t r = threadIdx.x; r < kShadeChunk; r += kShadeBlock) {
             if (chunk + r >= chunkEnd) break;
-            const uint32_t q = divRay(f, chunk + r);
+            const uint32_t q = (chunk + r) / f.R;
             const uint32_t ray = slotAt(f, q) * f.R + (chunk + r - q * f.R);
             const GpuHit hit = f.hits[ray];
             if (hit.tri == kNoHit) {
