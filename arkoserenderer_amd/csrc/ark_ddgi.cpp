@@ -1508,7 +1508,6 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.slab_z1 = ctx->slabZ1;
     f.window_probes = countSlabProbes(ctx, f.first, K);
     f.R = R;
-    f.r_shift1 = (R & (R - 1u)) == 0u ? static_cast<uint32_t>(__builtin_ctz(R)) + 1u : 0u;
     f.Rmax = static_cast<uint32_t>(ctx->Rmax);
     f.window_rays = f.window_probes * R;
     f.hysteresis_irradiance = p->hysteresis_irradiance;

@@ -194,7 +194,6 @@ struct FrameArgs {
     uint32_t window_probes;  // probes this context updates (K, or its Z-slab share)
     uint32_t window_rays;    // window_probes * R
     uint32_t R;
-    uint32_t r_shift1;       // log2(R) + 1 when R is a power of two, else 0 (divRay divides)
     uint32_t Rmax;
     int32_t sharded;
     int32_t slab_z0, slab_z1;

@@ -43,14 +43,6 @@ __device__ __forceinline__ float4 SceneArgs::sample(int idx, float u, float v) c
 
 namespace dev {
 
-// x / R for a queue position or ray index: a shift when R is a power of two (the
-// bench's and the reference's ray counts), the integer division (~15 VALU, among them
-// quarter-rate multiplies) otherwise; the branch is on a kernel argument (uniform)
-__device__ __forceinline__ uint32_t divRay(const FrameArgs& f, uint32_t x)
-{
-    return f.r_shift1 != 0u ? x >> (f.r_shift1 - 1u) : x / f.R;
-}
-
 // ---------------------------------------------------------------------------
 // 1. window -> slots
 // ---------------------------------------------------------------------------
@@ -929,7 +921,7 @@ struct ProbeRays {
     }
     __device__ static void load(const FrameArgs& f, uint32_t r, uint32_t& ray, V3& o, V3& d, float& tmax)
     {
-        const uint32_t qp = divRay(f, r);
+        const uint32_t qp = r / f.R;
         const uint32_t slot = slotAt(f, qp);
         const float4 fv = f.fib_order[r - qp * f.R]; // (direction, sample index)
         const GpuProbeSlot ps = f.slots[slot];
@@ -1889,7 +1881,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
         if (REFL) {
             rays[k] = pos < total ? pos : kNoHit;
         } else {
-            const uint32_t q = divRay(f, pos);
+            const uint32_t q = pos / f.R;
             rays[k] = pos < total ? slotAt(f, q) * f.R + (pos - q * f.R) : kNoHit;
         }
     }
@@ -1950,7 +1942,7 @@ __global__ void __launch_bounds__(256) k_shadow_gen(SceneArgs sc, FrameArgs f)
             const float t = fabsf_(f.hits[ray].t); // rt_RayHitT of a front or back face
             hitPoint = origin + t * dir;
         } else {
-            const uint32_t q = divRay(f, pos);
+            const uint32_t q = pos / f.R;
             ray = slotAt(f, q) * f.R + (pos - q * f.R);
             const float t = f.hits[ray].t;
             V3 origin, dir;
