@@ -200,7 +200,7 @@ struct ArkDdgiCtx {
     hipStream_t orderStream = nullptr;
     bool orderValid = false;
     // traversal knobs, fixed at create: refill batch, grab chunk
-    uint32_t refillMin = 16, sunRefillMin = 32, grabChunk = 64, triMin = 0;
+    uint32_t refillMin = 16, sunRefillMin = 32, grabChunk = 64;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -703,7 +703,6 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         // 0.625-0.635 ms, K = 4096 0.529 -> 0.514 ms, K = 2048 0.327 -> 0.320 ms, P = 8
         // slowest slab 0.573 -> 0.556 ms; the world BVHs' shadow rays (spots) keep 16
         // (32 there: C5 shadow 1.92 -> 2.07 ms)
-        if (const char* r = std::getenv("ARK_TRI_MIN")) ctx->triMin = static_cast<uint32_t>(std::max(0, std::min(64, std::atoi(r))));
         if (const char* r = std::getenv("ARK_SUN_REFILL_MIN")) ctx->sunRefillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
         if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
         if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
@@ -1552,7 +1551,6 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
     f.sun_refill_min = ctx->sunRefillMin;
-    f.tri_min = ctx->triMin;
     // a half-occupancy window (below kPipeHalfRays) hands out 32 rays per partition-head
     // grab to the probe-ray and shadow-ray queues (K = 2048 windows 0.429 -> 0.420 ms;
     // the whole grid keeps 64: 4.13 vs 4.18 ms at 32, profiles/r02_m19)
@@ -2071,7 +2069,6 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.light_count = ctx->lightCount;
     f.refill_min = ctx->refillMin;
     f.sun_refill_min = ctx->sunRefillMin;
-    f.tri_min = ctx->triMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
     if (ctx->sceneVersion != ctx->sceneStore->version) {

@@ -218,7 +218,6 @@ struct FrameArgs {
     uint32_t light_count;    // has_sun + spot lights
     uint32_t refill_min;     // trace: refill finished lanes once at least this many are idle
     uint32_t sun_refill_min; // the sun's light-space shadow traversal: the same for its lanes
-    uint32_t tri_min;        // EXPERIMENT: probe-ray triangle side batched (0 = every step)
     uint32_t grab_chunk;     // trace / shadow: rays a wave takes from its partition head at once (<= 64)
     uint32_t* shadow_bits;   // [window_rays] lit light bits 0-15, occluded bits 16-31 (front hits)
     ShadowRay* shadow_rays;  // k_shadow_gen's list: [window_rays * light_count] worst case

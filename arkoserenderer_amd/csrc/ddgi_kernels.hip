@@ -535,18 +535,11 @@ __device__ __forceinline__ bool travDoneDual(const TravState& ts, uint32_t nBits
 
 template<int BLOCK, bool ANY, bool GF = false>
 __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCache& nc, TravState& ts, uint32_t& nBase, uint32_t& nBits, Stack<BLOCK>& st,
-                                             V3 o, V3 d, V3 idir, uint32_t oct, float tmin, RayHit& h, int pass, uint32_t& cNodes, uint32_t& cTris,
-                                             uint32_t triMin = 0)
+                                             V3 o, V3 d, V3 idir, uint32_t oct, float tmin, RayHit& h, int pass, uint32_t& cNodes, uint32_t& cTris)
 {
     bool anyHit = false;
-    bool doTri = ts.tBits != 0;
+    const bool doTri = ts.tBits != 0;
     const bool doNode = nBits == 0 && ((ts.gBits & 0xffu) != 0 || st.depth != 0);
-    // EXPERIMENT (ARK_TRI_MIN): the triangle side runs only once triMin lanes hold a
-    // pending triangle, or a lane has no node work to do instead
-    if (triMin != 0) {
-        const uint32_t nTri = static_cast<uint32_t>(__popcll(__ballot(doTri)));
-        if (nTri < triMin && __ballot(doTri && !doNode) == 0) doTri = false;
-    }
     // fetch registers are left undefined on lanes that skip a side: zero-filling
     // them cost ~34 VALU per iteration (the compiler materialised the zeros)
     uint4 a, b, c;
@@ -1066,7 +1059,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
         // ---- one step: a pending leaf triangle and the next node -------------------
         // (an active lane is never done here: the check after the step retires or
         // restarts it, and a step of a done lane would change nothing anyway)
-        if (active) travStepDual<kTraceBlock, false, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris, f.tri_min);
+        if (active) travStepDual<kTraceBlock, false, true>(sc, nc, ts, nBase, nBits, st, o, d, idir, oct, tmin, h, pass, cNodes, cTris);
         // ---- pass finished -------------------------------------------------------------
         if (active && done() && (!Src::kMaskedPass || sc.root_masked < 0) && !exhausted) {
             active = false;
