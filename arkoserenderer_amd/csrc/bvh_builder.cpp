@@ -553,19 +553,18 @@ void childrenOf(const GpuBvhNode& nd, Child8 out[2], int& n)
 }
 
 // Grid for one axis of a node box [L, H]: step 2^e, anchor p = k * 2^e <= L with
-// p + qmax * 2^e >= H and |k| + 256 < 2^24 (every plane p + q * 2^e exact in fp32);
-// qmax = Bvh8CollapseOptions::quant_max (255, or 127 for 7-bit planes)
-void quantGrid(float L, float H, double qmax, int& e, double& p)
+// p + 255 * 2^e >= H and |k| + 256 < 2^24 (every plane p + q * 2^e exact in fp32).
+void quantGrid(float L, float H, int& e, double& p)
 {
     const double ext = static_cast<double>(H) - static_cast<double>(L);
-    e = ext > 0.0 ? static_cast<int>(std::ceil(std::log2(ext / qmax))) : -100;
+    e = ext > 0.0 ? static_cast<int>(std::ceil(std::log2(ext / 255.0))) : -100;
     e = std::max(-100, e);
     for (;; ++e) {
         const double step = std::ldexp(1.0, e);
         const double k = std::floor(static_cast<double>(L) / step);
         if (std::fabs(k) + 256.0 >= 16777216.0) continue;
         p = k * step;
-        if (p + qmax * step < static_cast<double>(H)) continue;
+        if (p + 255.0 * step < static_cast<double>(H)) continue;
         return;
     }
 }
@@ -1023,10 +1022,9 @@ void collapseQueue(const BvhBuildResult& bvh2, const CollapsePlan& plan, const B
         GpuBvh8Node nd;
         std::memset(&nd, 0, sizeof(nd));
         double step[3], p[3];
-        const double qmax = static_cast<double>(copt.quant_max);
         for (int a = 0; a < 3; ++a) {
             int e;
-            quantGrid(box.lo[a], box.hi[a], qmax, e, p[a]);
+            quantGrid(box.lo[a], box.hi[a], e, p[a]);
             step[a] = std::ldexp(1.0, e);
             nd.p[a] = static_cast<float>(p[a]);
             nd.e[a] = static_cast<uint8_t>(e + 127);
@@ -1062,11 +1060,11 @@ void collapseQueue(const BvhBuildResult& bvh2, const CollapsePlan& plan, const B
             for (int a = 0; a < 3; ++a) {
                 double ql = std::floor((static_cast<double>(k.box.lo[a]) - p[a]) / step[a]);
                 double qh = std::ceil((static_cast<double>(k.box.hi[a]) - p[a]) / step[a]);
-                ql = std::min(qmax, std::max(0.0, ql));
-                qh = std::min(qmax, std::max(0.0, qh));
+                ql = std::min(255.0, std::max(0.0, ql));
+                qh = std::min(255.0, std::max(0.0, qh));
                 // outward rounding, checked on the exact fp32 decode
                 while (ql > 0.0 && static_cast<double>(static_cast<float>(p[a] + ql * step[a])) > k.box.lo[a]) ql -= 1.0;
-                while (qh < qmax && static_cast<double>(static_cast<float>(p[a] + qh * step[a])) < k.box.hi[a]) qh += 1.0;
+                while (qh < 255.0 && static_cast<double>(static_cast<float>(p[a] + qh * step[a])) < k.box.hi[a]) qh += 1.0;
                 nd.qlo[a][s] = static_cast<uint8_t>(ql);
                 nd.qhi[a][s] = static_cast<uint8_t>(qh);
             }
@@ -1386,7 +1384,6 @@ bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8Collap
     if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return false;
     Bvh8CollapseOptions lc = copt;
     lc.slot_sort_axis = 2; // every ray goes along +w
-    lc.quant_max = 127;    // 7-bit planes: visitNodeSun compares four children per word
     out = collapse_bvh8(r2, 0u, 0u, lc);
     // the leaves' records become the world-space ones (primitive = world index)
     for (GpuTriangle& g : out.tris) {
@@ -2017,12 +2014,6 @@ extern "C" int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, 
     Bvh8CollapseOptions copt;
     Bvh8BuildResult r;
     if (n == 0 || !build_sun_bvh(in, opt, copt, r)) return 1;
-    // the light-space node test's guard bit: every used plane within 7 bits
-    for (const GpuBvh8Node& nd : r.nodes)
-        for (int sl = 0; sl < 8; ++sl)
-            if (((nd.imask | nd.leaf_mask) >> sl) & 1u)
-                for (int a = 0; a < 3; ++a)
-                    if (nd.qlo[a][sl] > 127u || nd.qhi[a][sl] > 127u) return 3;
     float F[9];
     for (int a = 0; a < 3; ++a)
         for (int k = 0; k < 3; ++k) F[a * 3 + k] = static_cast<float>(in.frame[a][k]);
@@ -2074,7 +2065,7 @@ extern "C" int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, 
                 float Q[3];
                 for (int a = 0; a < 3; ++a) {
                     const float q = std::ldexp(pl[a] - nd.p[a], 127 - static_cast<int>(nd.e[a]));
-                    Q[a] = std::min(127.0f, std::max(0.0f, q)); // as visitNodeSun (7-bit planes)
+                    Q[a] = std::min(258.0f, std::max(-2.0f, q));
                 }
                 F_[0] = static_cast<int>(std::floor(Q[0]));
                 F_[1] = static_cast<int>(std::floor(Q[1]));

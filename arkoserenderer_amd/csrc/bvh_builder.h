@@ -77,10 +77,6 @@ struct Bvh8CollapseOptions {
     // only rays along +axis traverse: the sun's light-space BVH, slot order = octant 0)
     int slot_sort_axis = -1;
     int threads = 0; // subtrees collapsed in parallel (0 = hardware concurrency)
-    // largest quantized plane index: 255 (8-bit planes), or 127 for the sun's
-    // light-space BVH, whose node test subtracts packed bytes with a guard bit
-    // (visitNodeSun) - boxes up to a grid step looser per side
-    int quant_max = 255;
 };
 Bvh8BuildResult collapse_bvh8(const BvhBuildResult& bvh2, uint32_t node_base, uint32_t tri_base, const Bvh8CollapseOptions& opt);
 

@@ -652,6 +652,18 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
     return { fmaf(p.x, F[0], fmaf(p.y, F[1], p.z * F[2])), fmaf(p.x, F[3], fmaf(p.y, F[4], p.z * F[5])), fmaf(p.x, F[6], fmaf(p.y, F[7], p.z * F[8])) };
 }
 
+// Bytewise unsigned x >= y of four packed bytes, the result in bit 7 of each byte, from
+// xh = x | 0x80808080 and yl = y & 0x7f7f7f7f: d = xh - yl borrows within no byte
+// (each byte of xh is >= 0x80 > each of yl), so bit 7 of a byte of d says x_lo7 >= y_lo7;
+// with the top bits, x >= y = (x7 & ~y7) | (~(x7 ^ y7) & d7) - one v_bitop3.
+__device__ __forceinline__ uint32_t geBytes(uint32_t x, uint32_t y, uint32_t xh, uint32_t yl)
+{
+    const uint32_t d = xh - yl;
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xb2" : "=v"(r) : "v"(x), "v"(y), "v"(d));
+    return r;
+}
+
 // Node visit of a ray along +w from light-space point pl (k_trace_shadow<SUN>). With
 // the direction exactly +w the slab test of u and v degenerates to "pl's coordinate
 // lies in the child's interval" and that of w to "the box reaches above pl": in the
@@ -661,30 +673,29 @@ __device__ __forceinline__ V3 sunCoords(const SceneArgs& sc, V3 p)
 // children are visited in slot order: the builder sorted them by their lower w bound
 // (Bvh8CollapseOptions::slot_sort_axis), the order the ray meets them.
 // The five conditions are tested on four children at once, bytewise within the plane
-// words: the light-space BVH's planes are 7-bit (Bvh8CollapseOptions::quant_max = 127)
-// and Q is clamped to [0, 127], so for bytes x, y <= 127, (x | 0x80) - y borrows within
-// no byte and its bit 7 says x >= y - one v_sub per condition and word (qlo <= floor
-// Q: F | 0x80 computed once per node; qhi >= ceil Q: qhi | 0x80 per word), and no
-// lane-mask compares (the per-child form: 40 SDWA v_cmp, 32 s_and and 8 v_addc).
-// Clamping Q can only accept more children (qlo <= 0 for a point below the node's
-// anchor, qhi >= 127 above its far side), never fewer, and an any-hit result does not
-// depend on extra visits (tests/test_sun_node_swar.py checks the arithmetic).
+// words (geBytes), with no lane-mask compares (the per-child form: 40 SDWA v_cmp, 32
+// s_and and 8 v_addc). Q is clamped to [0, 255]
+// so that floor and ceil are bytes: that can only accept more children (qlo <= 0 for a
+// point below the node's anchor, qhi >= 255 above its far side), never fewer, and an
+// any-hit result does not depend on extra visits.
 __device__ __forceinline__ void visitNodeSun(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, V3 pl, uint32_t& gBase, uint32_t& gBits, uint32_t& tBase,
                                              uint32_t& tBits)
 {
     auto quant = [](float c, uint32_t p, uint32_t ebyte) {
-        return __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(c - __uint_as_float(p), 127 - static_cast<int>(ebyte)), 0.0f, 127.0f);
+        return __builtin_amdgcn_fmed3f(__builtin_amdgcn_ldexpf(c - __uint_as_float(p), 127 - static_cast<int>(ebyte)), 0.0f, 255.0f);
     };
     const float qu = quant(pl.x, w0.x, w0.w & 0xffu), qv = quant(pl.y, w0.y, (w0.w >> 8) & 0xffu), qw = quant(pl.z, w0.z, (w0.w >> 16) & 0xffu);
     constexpr uint32_t kH = 0x80808080u;
     // floor (the truncating conversion: Q >= 0) and ceil of Q, in every byte (v_perm_b32
     // with selector 0: byte 0 of the second operand four times)
     auto bcast = [](float q) { return __builtin_amdgcn_perm(0u, static_cast<uint32_t>(q), 0u); };
-    const uint32_t FuH = bcast(qu) | kH, Cu = bcast(ceilf(qu)), FvH = bcast(qv) | kH, Cv = bcast(ceilf(qv)), Cw = bcast(ceilf(qw));
+    const uint32_t Fu = bcast(qu), Cu = bcast(ceilf(qu)), Fv = bcast(qv), Cv = bcast(ceilf(qv)), Cw = bcast(ceilf(qw));
+    const uint32_t FuH = Fu | kH, FvH = Fv | kH, CuL = Cu & ~kH, CvL = Cv & ~kH, CwL = Cw & ~kH;
     // planes (GpuBvh8Node): qlo u = w2.x|y, qlo v = w2.z|w, qhi u = w3.z|w, qhi v = w4.x|y,
     // qhi w = w4.z|w (children 0-3 | 4-7, child k in byte k & 3)
     auto crossed = [&](uint32_t lu, uint32_t hu, uint32_t lv, uint32_t hv, uint32_t hw) {
-        return (FuH - lu) & ((hu | kH) - Cu) & (FvH - lv) & ((hv | kH) - Cv) & ((hw | kH) - Cw) & kH;
+        return geBytes(Fu, lu, FuH, lu & ~kH) & geBytes(hu, Cu, hu | kH, CuL) & geBytes(Fv, lv, FvH, lv & ~kH) & geBytes(hv, Cv, hv | kH, CvL) &
+               geBytes(hw, Cw, hw | kH, CwL) & kH;
     };
     const uint32_t r0 = crossed(w2.x, w3.z, w2.z, w4.x, w4.z), r1 = crossed(w2.y, w3.w, w2.w, w4.y, w4.w);
     // bit 7 of byte k of r0 / r1 -> bit k / k + 4 of the slot mask: the bits of x =

@@ -69,8 +69,7 @@ int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const fl
  * [0.025, tmax], any hit through the BVH with a host restatement of the kernel's
  * light-space node test, and against every triangle. out[8] = {rays, occluded (brute
  * force), occluded (BVH), mismatches, node visits, triangle tests, BVH8 nodes, max
- * stack depth}. Returns 0 when no ray differs, 2 on a mismatch, 1 on a build error,
- * 3 when a used child plane exceeds the 7 bits the light-space node test needs. */
+ * stack depth}. Returns 0 when no ray differs, 2 on a mismatch, 1 on a build error. */
 int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, const float* sun_dir, const float* origins, uint64_t n_rays, float tmax,
                                  uint64_t* out);
 
