@@ -281,23 +281,20 @@ __device__ __forceinline__ uint32_t rayOctant(V3 idir)
     return (idir.x < 0.0f ? 1u : 0u) | (idir.y < 0.0f ? 2u : 0u) | (idir.z < 0.0f ? 4u : 0u);
 }
 
-// Node group holding only the root: one hit child (k = 0) in the "origin inside"
-// set of a virtual parent with no internal-children mask, so nextChild returns the
-// group base (the root) whatever the ray octant - a fresh lane can fetch the root
-// before its ray direction is known.
-__device__ __forceinline__ uint32_t rootGroupBits() { return 1u | (1u << 16); }
+// Node group holding only the root: one hit child (k = 0) of a virtual parent with no
+// internal-children mask, so nextChild returns the group base (the root) whatever the
+// ray octant - a fresh lane can fetch the root before its ray direction is known.
+__device__ __forceinline__ uint32_t rootGroupBits() { return 1u; }
 
 // Next child of a non-empty node group; removes it from the group. Group bits:
 // 0-7 hit internal children in visiting order (k = slot ^ oct), 8-15 imask (slot
-// order), 16-23 the hit children whose box contains the ray origin (k order).
-// Those go first: their entry distance is zero, so they lead any front-to-back
-// order, and rays leaving the same probe then share their first node fetches.
+// order). (An "origin inside" set that went first was measured and removed in round 3;
+// its bits 16-23 stayed zero and their test ran in every node step until round 5.)
 __device__ __forceinline__ uint32_t nextChild(uint32_t base, uint32_t& bits, uint32_t oct)
 {
-    const uint32_t inside = (bits >> 16) & 0xffu;
-    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(inside ? inside : (bits & 0xffu)));
+    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(bits & 0xffu));
     const uint32_t slot = k ^ oct;
-    bits &= ~((1u << k) | (1u << (k + 16)));
+    bits &= ~(1u << k);
     return base + static_cast<uint32_t>(__builtin_popcount((bits >> 8) & ((1u << slot) - 1u)));
 }
 
@@ -391,7 +388,7 @@ __device__ __forceinline__ void visitNode8(uint4 w0, uint4 w1, uint4 w2, uint4 w
     // leaf children: their triangle rows (GpuBvh8Node: bit s + stride i = triangle
     // i of leaf slot s), the hit leaf slots spread over the three rows and masked
     gBase = w1.x;
-    gBits = (m & 0x00ff00ffu) | (imask << 8);
+    gBits = m | (imask << 8);
     tBase = w1.y;
     const uint32_t stride = w1.w & 31u, leafHits = hitSlots & (w1.w >> 8) & 0xffu;
     const uint32_t x = (leafHits << stride) | leafHits;
