@@ -557,10 +557,7 @@ void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t cou
         const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
         job->triOffset = (nb + 255) & ~static_cast<size_t>(255);
         r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
-        // (32-bit record offsets, recordAt: a light-space BVH of 4 GiB or more is not
-        // installed; the sun's shadow rays keep the world BVHs)
-        ok = job->triOffset + r.tris.size() * sizeof(GpuTriangle) < (1ull << 32) &&
-             job->buf.alloc(job->triOffset + r.tris.size() * sizeof(GpuTriangle)) == hipSuccess &&
+        ok = job->buf.alloc(job->triOffset + r.tris.size() * sizeof(GpuTriangle)) == hipSuccess &&
              hipMemcpyAsync(job->buf.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice, s) == hipSuccess &&
              hipMemcpyAsync(static_cast<char*>(job->buf.ptr) + job->triOffset, r.tris.data(), r.tris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -1032,8 +1029,8 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     for (uint32_t i = 0; i < s->spot_light_count; ++i) gspots[i] = gpuSpotLight(s->spot_lights[i]);
     int rc;
     // nodes and triangles in ONE allocation (triangles after the nodes, 256-B aligned):
-    // the traversal addresses records by a 32-bit byte offset from the array base
-    // (recordAt): the pair must stay below 4 GiB
+    // the traversal addresses both through one buffer resource with a per-lane
+    // byte offset (32 bits: the pair must stay below 4 GiB)
     const size_t nodeBytes = allNodes.size() * sizeof(GpuBvh8Node);
     const size_t triOffset = (nodeBytes + 255) & ~static_cast<size_t>(255);
     const size_t triBytes = (allTris.size() + 1) * sizeof(GpuTriangle); // + padding record
@@ -1062,9 +1059,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         st->sunCostWorld = static_cast<float>(sun_shadow_cost(allNodes, allTris, roots, 3, nullptr, L, origins));
         st->sunCostLight = static_cast<float>(sun_shadow_cost(r.nodes, r.tris, &sroot, 1, sunIn.frame, L, origins));
     }
-    // the light-space arrays below 4 GiB as the world ones (32-bit record offsets)
-    const bool sunFits = ((r.nodes.size() * sizeof(GpuBvh8Node) + 255) & ~static_cast<size_t>(255)) + (r.tris.size() + 1) * sizeof(GpuTriangle) < (1ull << 32);
-    if (sunBuilt && sunFits && (ctx->sunBvh == 1 || sun_bvh_pays(st->sunCostWorld, st->sunCostLight))) {
+    if (sunBuilt && (ctx->sunBvh == 1 || sun_bvh_pays(st->sunCostWorld, st->sunCostLight))) {
         const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
         sunTriOffset = (nb + 255) & ~static_cast<size_t>(255);
         r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)

@@ -409,15 +409,6 @@ __device__ __forceinline__ GpuTriangle triFromWords(uint4 a, uint4 b, uint4 c)
 // a group when it is empty). Triangles and nodes are fetched by the same five
 // 16-B loads, so a wave whose lanes mix both kinds of step waits for memory
 // once per step instead of once per node plus once per triangle.
-// Record addresses as a 32-bit byte offset from the array base: the base stays in
-// SGPRs and the loads take the saddr + 32-bit voffset form (no 64-bit VGPR address
-// arithmetic per fetch). set_scene keeps the node and triangle arrays below 4 GB.
-template<class T>
-__device__ __forceinline__ const uint4* recordAt(const T* base, uint32_t i)
-{
-    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + i * static_cast<uint32_t>(sizeof(T)));
-}
-
 struct TravState {
     uint32_t gBase, gBits; // node group: hits (k-space) | imask << 8
     uint32_t tBase, tBits; // triangle group
@@ -564,7 +555,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
         ts.tBits &= ts.tBits - 1u;
     }
     {
-        const uint4* src = recordAt(sc.tris, ti);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.tris + ti);
         a = src[0];
         b = src[1];
         c = src[2];
@@ -576,7 +567,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
         if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
     }
     {
-        const uint4* src = recordAt(sc.nodes, child);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.nodes + child);
         w0 = src[0];
         w1 = src[1];
         w2 = src[2];
@@ -587,7 +578,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
     if (doTri) {
         ti = ts.tBase + static_cast<uint32_t>(__builtin_ctz(ts.tBits));
         ts.tBits &= ts.tBits - 1u;
-        const uint4* src = recordAt(sc.tris, ti);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.tris + ti);
         a = src[0];
         b = src[1];
         c = src[2];
@@ -597,7 +588,7 @@ __device__ __forceinline__ bool travStepDual(const SceneArgs& sc, const NodeCach
         const uint32_t child = nextChild(ts.gBase, ts.gBits, oct);
         if (ts.gBits & 0xffu) st.push(ts.gBase, ts.gBits);
         const uint32_t rel = child - nc.base;
-        const uint4* src = rel < nc.count ? nc.lds + rel * 5u : recordAt(sc.nodes, child);
+        const uint4* src = rel < nc.count ? nc.lds + rel * 5u : reinterpret_cast<const uint4*>(sc.nodes + child);
         w0 = src[0];
         w1 = src[1];
         w2 = src[2];
@@ -737,7 +728,7 @@ __device__ __forceinline__ bool travStepSun(const SceneArgs& sc, TravState& ts, 
     }
     uint4 a, b, c;
     {
-        const uint4* src = recordAt(sc.sun_tris, ti);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.sun_tris + ti);
         a = src[0];
         b = src[1];
         c = src[2];
@@ -750,7 +741,7 @@ __device__ __forceinline__ bool travStepSun(const SceneArgs& sc, TravState& ts, 
     }
     uint4 w0, w1, w2, w3, w4;
     {
-        const uint4* src = recordAt(sc.sun_nodes, child);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.sun_nodes + child);
         w0 = src[0];
         w1 = src[1];
         w2 = src[2];
