@@ -765,9 +765,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     // P = 4 1.21 -> 1.11, P = 2 2.22 -> 2.10; K = 4096 windows 0.72 -> 0.65, K = 2048
     // 0.43 unchanged; 2 per CU: P = 8 0.72, 4 per CU: 0.69). The whole C4 grid (8.4 M
     // rays) keeps the full grid: 4.059 vs 4.067 ms per step at 3 (profiles/r02_m17_ab).
-    int pipePerCu = kPipeTracePerCu;
-    if (const char* e = std::getenv("ARK_PIPE_TRACE_PER_CU")) pipePerCu = std::max(1, std::atoi(e)); // EXPERIMENT
-    ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(pipePerCu, std::max(1, occT)) * ctx->cuCount);
+    ctx->pipeTraceBlocks = static_cast<uint32_t>(std::min(kPipeTracePerCu, std::max(1, occT)) * ctx->cuCount);
     ctx->shadeBlocks = static_cast<uint32_t>(std::max(1, occS) * ctx->cuCount);
     ctx->shadowBlocks = static_cast<uint32_t>(std::max(1, occW) * ctx->cuCount);
     ctx->shadowBlocksPerCu = static_cast<uint32_t>(std::max(1, occW));
