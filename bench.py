@@ -23,6 +23,11 @@ whole-update figures (roofline()).
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE starts the N ranks itself
+(torch.distributed.run as a child process, launch_decision()); it exits non-zero
+when fewer than N GPUs are visible. `--dry-run` prints that decision without any
+GPU call.
+
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -53,7 +58,7 @@ MISS_BYTES = 16        # environment texel
 SHADOW_RAY_BYTES = 32  # ShadowRay record (written by k_shadow_gen, read by k_trace_shadow)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -78,19 +83,70 @@ def parse():
                     help="PMC traffic summary (tools/pmc_summary.py --latest); used only if its library hash matches")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "latest_sq.json"),
                     help="SQ counter summary (tools/sq_summary.py --json); used only if its library hash matches")
-    return ap.parse_args()
+    ap.add_argument("--master-port", type=int, default=29517,
+                    help="rendezvous port of the ranks bench.py starts itself (--gpus N > 1 without WORLD_SIZE)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the launch decision (run in this process / start N ranks / refuse) as JSON and exit; no GPU call")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def launch_decision(gpus, env, visible_gpus, argv, master_port=29517):
+    """How `bench.py --gpus N` runs (VERDICT r05 "do this" #1), decided before any GPU
+    call: ("run", N) in this process when the world size already matches (N = 1, or a
+    rank of the driver's `torch.distributed.run --nproc-per-node N`); ("spawn", cmd)
+    when N > 1 ranks were asked for and this process is not one of them: bench.py
+    starts `torch.distributed.run` as a CHILD process (never an exec: this process has
+    not touched the GPU and forwards the child's output and exit status); ("error",
+    why) when the request cannot be met (more GPUs than are visible, or a WORLD_SIZE
+    that disagrees with --gpus). A 1-GPU line is never printed for an N-GPU request."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: at least one GPU"
+    world_env = env.get("WORLD_SIZE")
+    if world_env is not None:
+        world = int(world_env)
+        if world != gpus:
+            return "error", f"WORLD_SIZE={world} but --gpus {gpus}: launch {gpus} ranks (torch.distributed.run --nproc-per-node {gpus})"
+        return "run", world
+    if gpus == 1:
+        return "run", 1
+    if visible_gpus < gpus:
+        return "error", f"--gpus {gpus} but {visible_gpus} GPU(s) visible: no {gpus}-GPU line can be measured here"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={master_port}", os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
+
+
+def _visible_gpus():
+    """GPUs this process could use, counted without initialising the GPU (on this image
+    torch.cuda.device_count() does not create a HIP context)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env = os.environ
+    # the launch decision first: a spawning parent must not have touched the GPU
+    visible = _visible_gpus() if (args.gpus > 1 and "WORLD_SIZE" not in env) else args.gpus
+    kind, what = launch_decision(args.gpus, env, visible, [a for a in argv if a != "--dry-run"], args.master_port)
+    if args.dry_run:
+        print(json.dumps({"decision": kind, "world_size": args.gpus if kind != "error" else None,
+                          "command": what if kind == "spawn" else None, "error": what if kind == "error" else None}))
+        return 0 if kind != "error" else 2
+    if kind == "error":
+        print(f"bench.py: {what}", file=sys.stderr)
+        return 2
+    if kind == "spawn":
+        # stdout of rank 0 (the JSON line) and every rank's stderr pass straight through
+        return subprocess.run(what, env=dict(env, HSA_ENABLE_IPC_MODE_LEGACY=env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))).returncode
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local_rank = int(env.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     if world > 1:
@@ -257,6 +313,7 @@ def main():
     node.ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def library_sha16() -> str:
@@ -790,4 +847,4 @@ def ao_bake_c1(args, torch, device):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
