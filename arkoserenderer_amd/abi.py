@@ -47,6 +47,10 @@ ARK_DDGI_DEBUG_RAY_STEPS = 101
 
 ARK_DDGI_CLEAR_OVERFLOW_INF = 0
 ARK_DDGI_CLEAR_OVERFLOW_MAX_FINITE = 1
+ARK_DDGI_SUN_BVH_AUTO = 0
+ARK_DDGI_SUN_BVH_WORLD = 1
+ARK_DDGI_SUN_BVH_LIGHT_SPACE = 2
+ARK_DDGI_FLAG_SERIAL_FRAMES = 0x1
 
 ARK_TEX_RGBA8_UNORM = 0
 ARK_TEX_RGBA8_SRGB = 1
@@ -78,7 +82,10 @@ class ArkDdgiDesc(C.Structure):
         ("clear_overflow_mode", C.c_int32),
         ("shard_rank", C.c_int32),
         ("shard_count", C.c_int32),
-        ("reserved", C.c_int32 * 4),
+        ("sun_bvh", C.c_int32),
+        ("flags", C.c_uint32),
+        ("build_threads", C.c_int32),
+        ("reserved", C.c_int32 * 1),
     ]
 
 
@@ -258,6 +265,10 @@ class ArkDdgiBvhStats(C.Structure):
         ("refit_ms", C.c_float),
         ("sun_max_depth", C.c_uint32),
         ("sun_rebuilds", C.c_uint32),
+        ("sun_rebuild_failures", C.c_uint32),
+        ("bvh_rebuilds", C.c_uint32),
+        ("bvh_rebuild_ms", C.c_float),
+        ("refit_version", C.c_uint32),
     ]
 
 
@@ -466,7 +477,7 @@ EXPORTS = {
     "ark_ddgi_debug_fmath_host": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     "ark_ddgi_debug_struct_sizes": (C.c_int, [C.POINTER(C.c_uint32), C.c_int]),
     "ark_ddgi_debug_bvh8_check": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
-    "ark_ddgi_debug_bvh8_trace_stats": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
+    "ark_ddgi_debug_bvh8_check_opts": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int, C.c_float, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_sun_bvh_check": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_float, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_sun_choice": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
 }

@@ -293,7 +293,7 @@ class OverlappedSlabExchange:
 
     def __init__(self, node, exchange, device, watchdog: ExchangeWatchdog | None = None, device_seq: bool | None = None):
         """exchange: a callable that enqueues the all-gather on the current stream.
-        device_seq (default: on unless ARK_DDGI_SEQ_SYNC=0): the handovers between the
+        device_seq (default: on): the handovers between the
         update stream and the exchange stream are the context's device-side sequence
         words (ark_ddgi_update_exchanged / ark_ddgi_exchange_begin / _end) instead of
         torch events; the events below then only bound the host."""
@@ -303,7 +303,7 @@ class OverlappedSlabExchange:
 
         self.node, self.exchange = node, exchange
         if device_seq is None:
-            device_seq = os.environ.get("ARK_DDGI_SEQ_SYNC", "1") != "0"
+            device_seq = True
         self.device_seq = device_seq
         owner = getattr(exchange, "__self__", None)  # a bound RcclBandExchange.exchange: watch its communicator
         self.watchdog = watchdog or ExchangeWatchdog(rccl=owner if isinstance(owner, RcclBandExchange) else None)

@@ -33,6 +33,16 @@ namespace {
 // pipelined windows below this many probe rays trace at half occupancy (ctx->pipeTraceBlocks)
 constexpr uint32_t kPipeHalfRays = 5u << 20;
 constexpr int kPipeTracePerCu = 3; // traversal workgroups per CU of such a window (ctx->pipeTraceBlocks; 2, 4, 5 measured slower)
+// Idle traversal lanes are refilled in batches of >= kRefillMin (the refill then stalls
+// a wave once per 16 finished rays, and the rays it starts descend from the root
+// together: C4 2.98 vs 3.30 ms at 1 in round 1; with the fetches outside branches 16
+// is the best: step 3.53 -> 3.46 ms against 4, 24 and 32, profiles/r03_as, r03_at). The
+// sun's any-hit rays in the light-space BVH are short: 32 (profiles/r05_q: C4 shadow
+// phase 0.648 -> 0.630 ms, K = 2048 0.327 -> 0.320 ms; the world BVHs' shadow rays keep
+// 16: 32 there made C5's shadow phase 1.92 -> 2.07 ms). kGrabChunk: rays per
+// partition-head grab, 64 = a probe quarter of direction-clustered rays per wave pool
+// (16 and 8 measured slower on 1/8 slabs).
+constexpr uint32_t kRefillMin = 16, kSunRefillMin = 32, kGrabChunk = 64;
 
 // roctx range over a scope (host-side enqueue markers, named after the reference's
 // ScopedDebugZone labels, DDGINode.cpp:152-247); end() closes it early.
@@ -85,14 +95,13 @@ uint16_t f32_to_f16_host(float f)
 // Balanced greedy clustering around ceil(R/64) spherical-Fibonacci centres.
 // Only the lane -> sample assignment changes; every sample is traced exactly
 // once and its hit record is stored at its own index, so results do not depend
-// on the order. ARK_RAY_ORDER=0 selects the identity (sample order).
+// on the order.
 void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 {
     order.resize(R);
     for (uint32_t i = 0; i < R; ++i) order[i] = i;
-    const char* env = std::getenv("ARK_RAY_ORDER");
     const uint32_t G = (R + 63) / 64;
-    if (G <= 1 || (env && std::atoi(env) == 0)) return;
+    if (G <= 1) return;
     auto fib = [](uint32_t i, uint32_t n, double* d) { // same point set as sphericalFibonacci (math accuracy irrelevant here)
         const double phi = 2.0 * M_PI * std::fmod(i * 0.6180339887498949, 1.0);
         const double z = 1.0 - (2.0 * i + 1.0) / n, r = std::sqrt(std::max(0.0, 1.0 - z * z));
@@ -177,6 +186,17 @@ struct SceneStore {
     int buildThreads = 16;
     std::unique_ptr<SunJob> sunJob;
     uint32_t sunRebuilds = 0;
+    // rebuild requests (sunRebuildStep): the sun direction the contexts sharing this scene
+    // asked for last and how many calls in a row asked for it; a rebuild starts only on a
+    // stable request (>= 2), so contexts under different suns never start rebuilds that
+    // undo each other. A failed build is remembered (direction and
+    // scene version) and not retried until either changes.
+    float sunReqDir[3] { 0, 0, 0 };
+    uint32_t sunReqStreak = 0;
+    bool sunFailed = false;
+    float sunFailedDir[3] { 0, 0, 0 };
+    uint32_t sunFailedVersion = 0;
+    uint32_t sunFailures = 0;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
     SceneStore& operator=(const SceneStore&) = delete;
@@ -199,8 +219,8 @@ struct ArkDdgiCtx {
     hipEvent_t evOrder = nullptr;
     hipStream_t orderStream = nullptr;
     bool orderValid = false;
-    // traversal knobs, fixed at create: refill batch, grab chunk
-    uint32_t refillMin = 16, sunRefillMin = 32, grabChunk = 64;
+    // traversal refill batch (probe and shadow rays, the sun's), rays per partition-head grab
+    uint32_t refillMin = kRefillMin, sunRefillMin = kSunRefillMin, grabChunk = kGrabChunk;
     int device = 0;
     int cuCount = 0;
     int X = 0, Y = 0, Z = 0, N = 0;
@@ -223,8 +243,8 @@ struct ArkDdgiCtx {
     // run on traceStream as soon as frame n - 2 (the previous user of the set) is done,
     // after frame n - 1's offsets (same stream), overlapping frame n - 1's shadow
     // rays, shading and probe update on the caller's stream.
-    bool pipelining = true;        // ARK_DDGI_PIPELINE=0: every update runs serially
-    int sunBvh = -1;               // ARK_SUN_BVH: 0 the sun's shadow rays traverse the world BVHs, 1 the light-space BVH, unset: by cost (sun_bvh_pays)
+    bool pipelining = true;        // ARK_DDGI_FLAG_SERIAL_FRAMES: every update runs serially
+    int sunBvh = -1;               // ArkDdgiDesc.sun_bvh: 0 the sun's shadow rays traverse the world BVHs, 1 the light-space BVH, -1: by cost (sun_bvh_pays)
     uint32_t pipeTraceBlocks = 0; // primary-traversal grid of a pipelined window below kPipeHalfRays rays
     bool pipeReady = false;        // the previous context operation was an update
     uint32_t parity = 0;           // buffer set of the next update
@@ -241,7 +261,7 @@ struct ArkDdgiCtx {
     // fence per workgroup - measured slower: the fences write back L2, K = 2048 frames
     // 0.371 -> 0.387 ms, profiles/r03_y). setSeq[b] = the
     // frame that last used buffer set b, when that frame was sequenced this way
-    // (else its evFrameDone[b] is recorded). ARK_DDGI_SEQ_SYNC=0: events throughout.
+    // (else its evFrameDone[b] is recorded). ark_ddgi_set_sequencing(ctx, 0, ...): events throughout.
     bool seqSync = true;
     DeviceBuffer seqWords;
     uint32_t frameSeq = 0;
@@ -507,6 +527,16 @@ void deriveSceneArgs(ArkDdgiCtx* ctx)
     ctx->sceneVersion = st.version;
 }
 
+// deriveSceneArgs plus a traversal spill area deep enough for every BVH the derived
+// args reach. Every caller goes through here: a sharing context may
+// have installed a deeper sun BVH, and marking the store's version as seen without
+// growing the spill area would let the next traversal overrun it.
+int refreshScene(ArkDdgiCtx* ctx)
+{
+    deriveSceneArgs(ctx);
+    return ensureSpill(ctx);
+}
+
 // The context's spot lights reach the device in stream order on `s`, ahead of the
 // operation that reads them (a by-value kernel argument: no host buffer to keep alive).
 hipError_t flushLights(ArkDdgiCtx* ctx, hipStream_t s)
@@ -581,10 +611,32 @@ void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t cou
 int sunRebuildStep(ArkDdgiCtx* ctx)
 {
     SceneStore& st = *ctx->sceneStore;
+    auto sameDir = [](const float* a, const float* b) { return std::memcmp(a, b, 3 * sizeof(float)) == 0; };
+    if (ctx->hasSun) {
+        if (st.sunReqStreak && sameDir(st.sunReqDir, ctx->sunDir)) {
+            st.sunReqStreak = std::min<uint32_t>(st.sunReqStreak + 1u, 1u << 30);
+        } else {
+            std::memcpy(st.sunReqDir, ctx->sunDir, sizeof(st.sunReqDir));
+            st.sunReqStreak = 1;
+        }
+    }
     if (st.sunJob && st.sunJob->done.load(std::memory_order_acquire)) {
-        std::unique_ptr<SunJob> job = std::move(st.sunJob);
-        job->t.join();
-        if (job->ok && job->version == st.version) {
+        SunJob& j = *st.sunJob;
+        if (!j.ok) {
+            // remembered: not started again for this direction and scene version
+            st.sunFailed = true;
+            std::memcpy(st.sunFailedDir, j.dir, sizeof(j.dir));
+            st.sunFailedVersion = j.version;
+            st.bvhStats.sun_rebuild_failures = ++st.sunFailures;
+            j.t.join();
+            st.sunJob.reset();
+        } else if (j.version != st.version || (st.sunReqStreak >= 2 && !sameDir(j.dir, st.sunReqDir))) {
+            // stale: a refit came in between, or the scene's contexts settled on another sun
+            j.t.join();
+            st.sunJob.reset();
+        } else if (ctx->hasSun && sameDir(j.dir, ctx->sunDir)) {
+            std::unique_ptr<SunJob> job = std::move(st.sunJob);
+            job->t.join();
             // frames in flight may traverse the old one (any context, when shared)
             if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
             else ARK_HIP(drainContext(ctx));
@@ -604,12 +656,13 @@ int sunRebuildStep(ArkDdgiCtx* ctx)
             st.bvhStats.sun_rebuilds = ++st.sunRebuilds;
             st.bvhStats.sun_build_ms = job->ms;
             ++st.version;
-            deriveSceneArgs(ctx);
-            if (const int rc = ensureSpill(ctx)) return rc;
+            if (const int rc = refreshScene(ctx)) return rc;
         }
+        // else: built for another context's sun; that context installs it
     }
-    if (!st.sunWanted || !ctx->hasSun || st.sunJob) return ARK_DDGI_OK;
-    if (st.sunArgs.sun_root >= 0 && std::memcmp(ctx->sunDir, st.sunDirBuilt, sizeof(ctx->sunDir)) == 0) return ARK_DDGI_OK;
+    if (!st.sunWanted || !ctx->hasSun || st.sunJob || st.sunReqStreak < 2 || !sameDir(st.sunReqDir, ctx->sunDir)) return ARK_DDGI_OK;
+    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt)) return ARK_DDGI_OK;
+    if (st.sunFailed && st.sunFailedVersion == st.version && sameDir(st.sunFailedDir, ctx->sunDir)) return ARK_DDGI_OK;
     auto job = std::make_unique<SunJob>();
     std::memcpy(job->dir, ctx->sunDir, sizeof(job->dir));
     job->version = st.version;
@@ -661,7 +714,9 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     ctx->Rmax = desc->max_rays_per_probe > 0 ? desc->max_rays_per_probe : ARK_DDGI_MAX_RAYS_PER_PROBE;
     ctx->Kmax = desc->max_probe_updates > 0 ? desc->max_probe_updates : ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES;
     const int shards = desc->shard_count > 0 ? desc->shard_count : 1;
-    if (ctx->Rmax > ARK_DDGI_MAX_RAYS_PER_PROBE || ctx->Z % shards != 0 || desc->shard_rank < 0 || desc->shard_rank >= shards) {
+    if (ctx->Rmax > ARK_DDGI_MAX_RAYS_PER_PROBE || ctx->Z % shards != 0 || desc->shard_rank < 0 || desc->shard_rank >= shards ||
+        desc->sun_bvh < ARK_DDGI_SUN_BVH_AUTO || desc->sun_bvh > ARK_DDGI_SUN_BVH_LIGHT_SPACE || (desc->flags & ~ARK_DDGI_FLAG_SERIAL_FRAMES) ||
+        desc->build_threads < 0) {
         delete ctx;
         return ARK_DDGI_E_INVALID_ARGUMENT;
     }
@@ -688,33 +743,17 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     ctx->cuCount = prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evOrder, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-    {
-        // tuning knobs, read once: ARK_REFILL_MIN: refill idle trace lanes in batches
-        // of >= 16 (the refill then stalls a wave once per 16 finished rays, and the rays
-        // it starts descend from the root together: 2.98 vs 3.30 ms at 1 on C4, 16 was
-        // 3.03 in round 1; with the traversal's fetches outside branches (round 3) 16 is
-        // the best: C4 step 3.53 -> 3.46 ms, K = 4096 +2 %, K = 2048 +1 %, 4: 3.67, 24:
-        // 3.47-3.49, 32: 3.64; profiles/r03_as, r03_at);
-        // ARK_GRAB_CHUNK: rays per partition-head grab, 64 = a probe quarter of
-        // direction-clustered rays per wave pool (16 and 8 measured slower on 1/8 slabs)
-        if (const char* r = std::getenv("ARK_REFILL_MIN")) ctx->refillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
-        // ARK_SUN_REFILL_MIN: the same for the sun's shadow rays in the light-space BVH,
-        // whose any-hit rays are short: 32 (profiles/r05_q): C4 shadow phase 0.648 ->
-        // 0.625-0.635 ms, K = 4096 0.529 -> 0.514 ms, K = 2048 0.327 -> 0.320 ms, P = 8
-        // slowest slab 0.573 -> 0.556 ms; the world BVHs' shadow rays (spots) keep 16
-        // (32 there: C5 shadow 1.92 -> 2.07 ms)
-        if (const char* r = std::getenv("ARK_SUN_REFILL_MIN")) ctx->sunRefillMin = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(r))));
-        if (const char* g = std::getenv("ARK_GRAB_CHUNK")) ctx->grabChunk = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(g))));
-        if (const char* pl = std::getenv("ARK_DDGI_PIPELINE")) ctx->pipelining = std::atoi(pl) != 0;
-        if (const char* sb = std::getenv("ARK_SUN_BVH")) ctx->sunBvh = std::atoi(sb) != 0 ? 1 : 0;
-        if (const char* ss = std::getenv("ARK_DDGI_SEQ_SYNC")) ctx->seqSync = std::atoi(ss) != 0;
-        // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time
-        // across queues: a polling wait could then hold the GPU while the kernel it
-        // waits for queues behind it: it would give up after its bound and fail closed
-        // (checkSequencing), dropping frames; such a context starts with events instead
-        if (const char* pc = std::getenv("ROCPROF_COUNTER_COLLECTION"))
-            if (*pc && std::strcmp(pc, "0") != 0 && std::strcmp(pc, "false") != 0) ctx->seqSync = false;
-    }
+    // the desc's options (ArkDdgiDesc.sun_bvh / flags); the traversal's refill and grab
+    // sizes are the constants kRefillMin / kSunRefillMin / kGrabChunk
+    ctx->pipelining = (desc->flags & ARK_DDGI_FLAG_SERIAL_FRAMES) == 0;
+    ctx->sunBvh = desc->sun_bvh == ARK_DDGI_SUN_BVH_WORLD ? 0 : desc->sun_bvh == ARK_DDGI_SUN_BVH_LIGHT_SPACE ? 1 : -1;
+    // a counter-collecting profiler (rocprofv3 --pmc) runs one kernel at a time across
+    // queues: a polling wait could then hold the GPU while the kernel it waits for queues
+    // behind it: it would give up after its bound and fail closed (checkSequencing),
+    // dropping frames; such a context starts with events instead (the profiler's own
+    // environment, not a tuning knob; ark_ddgi_set_sequencing overrides it)
+    if (const char* pc = std::getenv("ROCPROF_COUNTER_COLLECTION"))
+        if (*pc && std::strcmp(pc, "0") != 0 && std::strcmp(pc, "false") != 0) ctx->seqSync = false;
     if ((e = hipStreamCreateWithFlags(&ctx->traceStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     // stream-order events of the frames in flight
     const unsigned syncFlags = hipEventDisableTiming;
@@ -922,18 +961,13 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
             st->boundsHi[a] = lo[a] <= hi[a] ? hi[a] : 0.0f;
         }
     }
-    // host threads for the build: the box's CPU share per GPU is 16 cores
-    opt.threads = 16;
-    if (const char* e = std::getenv("ARK_BUILD_THREADS")) opt.threads = std::max(1, std::atoi(e));
-    // SAH triangle-test cost relative to a BVH2 node step (tuning experiments)
-    if (const char* e = std::getenv("ARK_BVH_INTERSECTION_COST")) opt.intersection_cost = std::max(0.05f, static_cast<float>(std::atof(e)));
-    // BVH2 -> BVH8 child selection: SAH-optimal (Ylitie et al. 2017 DP; the default) or
-    // ARK_BVH8_COLLAPSE=greedy; ARK_BVH8_NODE_COST / ARK_BVH8_TRI_COST weigh the DP's
-    // SAH terms
+    // host threads for the build (ArkDdgiDesc.build_threads; 0: the box's CPU share per
+    // GPU, 16 cores)
+    opt.threads = ctx->desc.build_threads > 0 ? ctx->desc.build_threads : 16;
+    // BVH2 -> BVH8 child selection: SAH-optimal (Ylitie et al. 2017 DP) with the default
+    // node / triangle costs (a lower triangle cost and the greedy collapse measured no
+    // better)
     Bvh8CollapseOptions copt;
-    if (const char* e = std::getenv("ARK_BVH8_COLLAPSE")) copt.sah_optimal = std::strcmp(e, "sah") == 0;
-    if (const char* e = std::getenv("ARK_BVH8_NODE_COST")) copt.node_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
-    if (const char* e = std::getenv("ARK_BVH8_TRI_COST")) copt.tri_cost = std::max(0.01f, static_cast<float>(std::atof(e)));
     copt.threads = opt.threads;
     // the sun's light-space BVH input, before the class builds free their triangles; the
     // build itself on its own thread beside the class builds (each build's top levels
@@ -1219,7 +1253,7 @@ int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* L)
         ctx->spotHost = std::move(spots);
         ctx->lightsDirty = true;
     }
-    deriveSceneArgs(ctx);
+    if (const int rc = refreshScene(ctx)) return rc;
     return sunRebuildStep(ctx);
 }
 
@@ -1348,7 +1382,7 @@ int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint
     st.bvhStats.sun_max_depth = 0;
     st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     ++st.version;
-    deriveSceneArgs(ctx);
+    if (const int rc2 = refreshScene(ctx)) return rc2;
     return sunRebuildStep(ctx); // a new light-space BVH of the refitted records, in the background
 }
 
@@ -1486,10 +1520,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     const hipStream_t s = streamOf(hipStream);
     if (const int r = checkSequencing(ctx)) return r;
     ARK_HIP(hipSetDevice(ctx->device));
-    if (ctx->sceneVersion != ctx->sceneStore->version) { // another context refitted the shared scene or installed a sun BVH
-        deriveSceneArgs(ctx);
-        if (const int rc = ensureSpill(ctx)) return rc;
-    }
+    if (ctx->sceneVersion != ctx->sceneStore->version) // another context refitted the shared scene or installed a sun BVH
+        if (const int rc = refreshScene(ctx)) return rc;
     if (const int rc = sunRebuildStep(ctx)) return rc;
     FrameArgs f {};
     f.abort_word = ctx->seqWords.as<uint32_t>() + 64;
@@ -1938,6 +1970,8 @@ int ark_ddgi_bake_ao(ArkDdgiCtx* ctx, const ArkBakeAoDesc* d, void* hipStream)
     const ArkRTTriangleMesh& mesh = ctx->sceneStore->meshHost[inst.rt_mesh_index];
     const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
+    if (ctx->sceneVersion != ctx->sceneStore->version) // a sharing context refitted the scene or installed a deeper sun BVH
+        if (const int rc = refreshScene(ctx)) return rc;
     ARK_HIP(orderBegin(ctx, s));
     const size_t texels = static_cast<size_t>(d->width) * d->height;
     const size_t outBytes = texels * (d->bent_normals ? 4 : 1);
@@ -2032,7 +2066,13 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     int rc;
-    if ((rc = ensureSpill(ctx)) != 0) return rc;
+    // the scene first: a sharing context's deeper sun BVH may grow,
+    // i.e. reallocate, the spill area that f.spill points into below
+    if (ctx->sceneVersion != ctx->sceneStore->version) {
+        if ((rc = refreshScene(ctx)) != 0) return rc;
+    } else if ((rc = ensureSpill(ctx)) != 0) {
+        return rc;
+    }
     FrameArgs f {};
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
     f.Wi = ctx->Wi; f.Hi = ctx->Hi; f.Wv = ctx->Wv; f.Hv = ctx->Hv;
@@ -2071,10 +2111,6 @@ int ark_ddgi_rt_reflections(ArkDdgiCtx* ctx, const ArkReflectionsDesc* desc, voi
     f.sun_refill_min = ctx->sunRefillMin;
     f.grab_chunk = ctx->grabChunk;
     f.counters = ctx->counters.as<unsigned long long>();
-    if (ctx->sceneVersion != ctx->sceneStore->version) {
-        deriveSceneArgs(ctx);
-        if (const int rc = ensureSpill(ctx)) return rc;
-    }
     ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(flushLights(ctx, s));
     ARK_HIP(hipMemsetAsync(f.ray_counter, 0, (kRayCounterWords + kRayCounterStride) * 4, s));

@@ -66,6 +66,11 @@ class DDGIConfig:
     max_rays_per_probe: int = abi.ARK_DDGI_MAX_RAYS_PER_PROBE        # DDGINode.h:22
     max_probe_updates: int = abi.ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES  # DDGINode.h:23
     clear_overflow_mode: int = abi.ARK_DDGI_CLEAR_OVERFLOW_INF
+    # context options beyond the reference node's (ArkDdgiDesc): the sun's shadow-ray
+    # structure, serial frames (no frames in flight), host threads of the BVH builds
+    sun_bvh: int = abi.ARK_DDGI_SUN_BVH_AUTO
+    serial_frames: bool = False
+    build_threads: int = 0
 
 
 @dataclass
@@ -100,6 +105,9 @@ def desc_for(grid: ProbeGrid, z_far: float, config: DDGIConfig, device: int = 0,
     d.clear_overflow_mode = int(config.clear_overflow_mode)
     d.shard_rank = int(shard_rank)
     d.shard_count = int(shard_count)
+    d.sun_bvh = int(config.sun_bvh)
+    d.flags = abi.ARK_DDGI_FLAG_SERIAL_FRAMES if config.serial_frames else 0
+    d.build_threads = int(config.build_threads)
     return d
 
 

@@ -145,9 +145,17 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
             ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_lights failed (%d): %s", rc, ark_ddgi_last_error(ctx));
         if (scene.instanceVersion() != m_instanceVersion) {
             const std::vector<ArkRTInstance>& instances = scene.rtInstances();
-            if (int rc = ark_ddgi_set_instances(ctx, instances.data(), static_cast<uint32_t>(instances.size())); rc != ARK_DDGI_OK)
-                ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_instances failed (%d): %s", rc, ark_ddgi_last_error(ctx));
-            m_instanceVersion = scene.instanceVersion();
+            int rc = ark_ddgi_set_instances(ctx, instances.data(), static_cast<uint32_t>(instances.size()));
+            if (rc != ARK_DDGI_OK) {
+                // a refit cannot follow this change (the topology changed: another mesh,
+                // triangle count or hit mask): build the scene anew, as construct() does
+                // (never keep the old transforms for good)
+                ARKOSE_LOG(Warning, "DDGINode: ark_ddgi_set_instances failed (%d): %s; rebuilding the scene", rc, ark_ddgi_last_error(ctx));
+                rc = ark_ddgi_set_scene(ctx, &scene.rtScene());
+                if (rc != ARK_DDGI_OK) ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_scene failed (%d): %s", rc, ark_ddgi_last_error(ctx));
+            }
+            // the context follows this version only once it holds it (else: retried next frame)
+            if (rc == ARK_DDGI_OK) m_instanceVersion = scene.instanceVersion();
         }
         if (m_exchange) {
             // Z-slab rank: traversal goes ahead, shading waits for the previous exchange;

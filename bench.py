@@ -83,6 +83,10 @@ def parse(argv=None):
                     help="PMC traffic summary (tools/pmc_summary.py --latest); used only if its library hash matches")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "latest_sq.json"),
                     help="SQ counter summary (tools/sq_summary.py --json); used only if its library hash matches")
+    ap.add_argument("--sun-bvh", choices=("auto", "world", "light"), default="auto",
+                    help="the sun's shadow-ray structure (ArkDdgiDesc.sun_bvh); auto = set_scene's sampled choice")
+    ap.add_argument("--serial-frames", action="store_true",
+                    help="no frames in flight (ARK_DDGI_FLAG_SERIAL_FRAMES): kernels do not overlap (profiling A/B)")
     ap.add_argument("--master-port", type=int, default=29517,
                     help="rendezvous port of the ranks bench.py starts itself (--gpus N > 1 without WORLD_SIZE)")
     ap.add_argument("--dry-run", action="store_true",
@@ -164,8 +168,9 @@ def main(argv=None):
     t_setup = time.time()
     scene = S.soup(args.triangles)
     grid = D.ProbeGrid((G, G, G), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    sun_mode = {"auto": abi.ARK_DDGI_SUN_BVH_AUTO, "world": abi.ARK_DDGI_SUN_BVH_WORLD, "light": abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE}[args.sun_bvh]
     cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=K, max_rays_per_probe=R, max_probe_updates=K,
-                       compute_probe_offsets=True)
+                       compute_probe_offsets=True, sun_bvh=sun_mode, serial_frames=args.serial_frames)
     exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
     node = D.DDGINode(cfg)
     assert node.construct(scene, grid, 10000.0, device=local_rank, shard_rank=rank, shard_count=world, **exposure)

@@ -145,8 +145,23 @@ typedef struct ArkDdgiDesc {
     int32_t clear_overflow_mode; /* ARK_DDGI_CLEAR_OVERFLOW_* */
     int32_t shard_rank;          /* Z-slab owned by this context (0 when unsharded) */
     int32_t shard_count;         /* number of Z-slabs (1 when unsharded); must divide grid_dims[2] */
-    int32_t reserved[4];
+    int32_t sun_bvh;             /* ARK_DDGI_SUN_BVH_*: the structure the sun's shadow rays traverse */
+    uint32_t flags;              /* ARK_DDGI_FLAG_* */
+    int32_t build_threads;       /* host threads of the BVH builds; 0 = 16 (the GPU box's per-GPU CPU share) */
+    int32_t reserved[1];
 } ArkDdgiDesc;
+
+/* ArkDdgiDesc.sun_bvh. AUTO: when the scene has a sun, set_scene builds a BVH8 of all
+ * triangles in the sun's light space beside the world BVHs, samples 4,096 sun shadow
+ * rays through both on the host (any-hit steps per ray) and keeps it only when it is
+ * cheaper; WORLD: never built; LIGHT_SPACE: built and kept whenever there is a sun.
+ * Results do not depend on the choice (any-hit visibility). */
+#define ARK_DDGI_SUN_BVH_AUTO 0
+#define ARK_DDGI_SUN_BVH_WORLD 1
+#define ARK_DDGI_SUN_BVH_LIGHT_SPACE 2
+/* ArkDdgiDesc.flags. SERIAL_FRAMES: every update runs in line on the caller's stream
+ * (no traversal stream, no frames in flight); results are the same. */
+#define ARK_DDGI_FLAG_SERIAL_FRAMES 0x1u
 
 /* RTVertex, scalar layout, 36 B (RTData.h:9-13 / NonPositionVertex SceneData.h). */
 typedef struct ArkRTVertex {
@@ -478,6 +493,11 @@ typedef struct ArkDdgiBvhStats {
     uint32_t sun_rebuilds;  /* light-space BVHs rebuilt in the background and installed since
                              * set_scene (after sun-direction changes or refits; sun_build_ms is
                              * then the last rebuild's time) */
+    uint32_t sun_rebuild_failures; /* background sun rebuilds that failed (not retried for the same
+                                    * direction and scene version) */
+    uint32_t bvh_rebuilds;  /* world BVHs rebuilt in the background after refits and installed */
+    float bvh_rebuild_ms;   /* host time of the last such rebuild (0 = none) */
+    uint32_t refit_version; /* refits (ark_ddgi_set_instances) since set_scene */
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 

@@ -44,24 +44,15 @@ int ark_ddgi_debug_struct_sizes(uint32_t* out, int n);
  * every quantized plane exactly representable, every triangle vertex inside the
  * decoded boxes of its leaf and of all its ancestors. out[8] = {nodes, leaf
  * children, max depth, violations, triangles, bvh2 nodes, internal children, BVH8
- * SAH cost x 1e6 (node cost 1)}. The BVH8 child selection follows ARK_BVH8_COLLAPSE
- * (unset or "sah" = SAH-optimal, any other value = greedy) and ARK_BVH8_TRI_COST, as
- * set_scene does.
+ * SAH cost x 1e6 (node cost 1)}. The BVH8 child selection is set_scene's (SAH-optimal
+ * collapse, default triangle cost); _opts selects the greedy collapse (sah_optimal 0)
+ * or another triangle cost (tri_cost > 0), for comparing builds.
  * Returns 0 when the check passes, 1 when it found violations. No GPU. */
 int ark_ddgi_debug_bvh8_check(const float* triangles, uint64_t n, uint64_t* out);
+int ark_ddgi_debug_bvh8_check_opts(const float* triangles, uint64_t n, int sah_optimal, float tri_cost, uint64_t* out);
 
-/* Traversal statistics of that BVH8 on the host (a scalar simulation of k_trace's
- * closest-hit order: hit children, origin-containing first, then octant order; the
- * leaf triangles of a node right after it): nRays rays of 7 floats (origin,
- * direction, tmax) over `threads` host threads. out[9] = {node visits, triangle
- * tests, hits, BVH8 nodes, SAH cost x 1e6, max steps of one ray, max depth,
- * triangle records (leaf triangle rows, holes included), children the exact box
- * test accepts and the ARK_SIM_BOX form (kernel32 | f16) rejects (must be 0)};
- * per_ray_steps (if not NULL) gets each ray's node visits + triangle tests.
- * For comparing BVH builds (ARK_BVH8_COLLAPSE, ARK_BVH8_TRI_COST,
- * ARK_BVH_INTERSECTION_COST) without a GPU: tools/bvh_stats.py. */
-int ark_ddgi_debug_bvh8_trace_stats(const float* triangles, uint64_t n, const float* rays, uint64_t n_rays, int threads, uint64_t* out,
-                                    uint32_t* per_ray_steps /* nullable: node visits + triangle tests of each ray */);
+/* The host traversal simulator (ark_ddgi_debug_bvh8_trace_stats) is a tool, not part
+ * of this library: tools/sim/bvh_trace_sim.h, tools/lib/libark_bvhsim.so. */
 
 /* The sun's light-space BVH (the one set_scene builds for k_trace_shadow<SUN>) built
  * on the host from n world triangles (9 floats each) and checked without a GPU: a sun

@@ -16,8 +16,12 @@ import os
 import numpy as np
 import pytest
 
-from arkoserenderer_amd import abi
+import sys
+
 from arkoserenderer_amd import scene as S
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "sim"))
+import bvhsim  # noqa: E402  (the simulator is a tool library, not libark_ddgi.so)
 
 
 def _triangles(sc):
@@ -50,7 +54,7 @@ def _rays(n, lo, hi, rng):
 
 @pytest.mark.parametrize("mode", ["kernel32", "f16s", "f16d"])
 def test_box_forms_cull_no_exact_hit(mode, monkeypatch):
-    lib = abi.load_library()
+    lib = bvhsim.load()
     tris = _triangles(S.soup(120_000))
     lo, hi = tris.reshape(-1, 3).min(0), tris.reshape(-1, 3).max(0)
     rng = np.random.default_rng(11)
@@ -68,7 +72,7 @@ def test_box_forms_cull_no_exact_hit(mode, monkeypatch):
 def test_box_check_has_power(monkeypatch):
     """Negative control: the fp16 form without its error bound culls exact hits, and
     the check sees it."""
-    lib = abi.load_library()
+    lib = bvhsim.load()
     tris = _triangles(S.soup(120_000))
     lo, hi = tris.reshape(-1, 3).min(0), tris.reshape(-1, 3).max(0)
     rays = _rays(6000, lo, hi, np.random.default_rng(11))
@@ -84,7 +88,7 @@ def test_presplit_references_keep_every_hit(monkeypatch):
     """Early split clipping of the BVH2 build (ARK_BVH_PRESPLIT, off by default): the
     clipped references' boxes cover their triangles, so the host traversal finds the
     same number of hits as the plain build."""
-    lib = abi.load_library()
+    lib = bvhsim.load()
     tris = _triangles(S.soup(60_000))
     lo, hi = tris.reshape(-1, 3).min(0), tris.reshape(-1, 3).max(0)
     rays = _rays(4000, lo, hi, np.random.default_rng(5))

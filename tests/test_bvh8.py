@@ -9,11 +9,15 @@ import pytest
 from arkoserenderer_amd import abi
 
 
-def check(tris):
+def check(tris, sah_optimal=None, tri_cost=0.0):
+    """set_scene's build (sah_optimal None), or the _opts build for comparing collapses."""
     lib = abi.load_library()
     tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
     out = (C.c_uint64 * 8)()
-    rc = lib.ark_ddgi_debug_bvh8_check(tris.ctypes.data, tris.shape[0], out)
+    if sah_optimal is None:
+        rc = lib.ark_ddgi_debug_bvh8_check(tris.ctypes.data, tris.shape[0], out)
+    else:
+        rc = lib.ark_ddgi_debug_bvh8_check_opts(tris.ctypes.data, tris.shape[0], int(sah_optimal), float(tri_cost), out)
     return rc, list(out)
 
 
@@ -56,21 +60,18 @@ def test_bvh8_edge_cases(case):
 
 
 
-@pytest.mark.parametrize("tri_cost", ["1.0", "0.3"])
-def test_sah_optimal_collapse(monkeypatch, tri_cost):
+@pytest.mark.parametrize("tri_cost", [1.0, 0.3])
+def test_sah_optimal_collapse(tri_cost):
     """The SAH-optimal BVH2 -> BVH8 child selection (Ylitie et al. 2017 dynamic
-    programming, ARK_BVH8_COLLAPSE=sah, bvh_builder.cpp planCollapse) keeps every
+    programming, set_scene's choice, bvh_builder.cpp planCollapse) keeps every
     structural invariant and never costs more SAH than the greedy largest-area
     opening on the same BVH2 (it also fills nodes: fewer of them)."""
     rng = np.random.default_rng(11)
     n = 30000
     v0 = rng.uniform(-20, 20, (n, 3)).astype(np.float32)
     tris = np.concatenate([v0, v0 + rng.uniform(-0.4, 0.4, (n, 3)), v0 + rng.uniform(-0.4, 0.4, (n, 3))], axis=1)
-    monkeypatch.setenv("ARK_BVH8_TRI_COST", tri_cost)
-    monkeypatch.setenv("ARK_BVH8_COLLAPSE", "greedy")
-    rc_g, g = check(tris)
-    monkeypatch.setenv("ARK_BVH8_COLLAPSE", "sah")
-    rc_s, s = check(tris)
+    rc_g, g = check(tris, sah_optimal=False, tri_cost=tri_cost)
+    rc_s, s = check(tris, sah_optimal=True, tri_cost=tri_cost)
     assert rc_g == 0 and rc_s == 0 and g[3] == 0 and s[3] == 0
     assert s[4] == n and s[6] == s[0] - 1
     assert s[7] <= g[7], (s[7], g[7])   # SAH cost x 1e6

@@ -108,31 +108,31 @@ def test_city_block_c5_like():
 
 
 @pytest.mark.parametrize("sun_bvh", ["0", "1"])
-def test_sun_structure_forced(monkeypatch, sun_bvh):
-    """The sun's shadow rays forced through the world BVHs (ARK_SUN_BVH=0) or the
-    light-space BVH (=1) whatever the sampled cost says: with spot lights beside the sun
+def test_sun_structure_forced(sun_bvh):
+    """The sun's shadow rays forced through the world BVHs (ArkDdgiDesc.sun_bvh WORLD) or
+    the light-space BVH (LIGHT_SPACE) whatever the sampled cost says: with spot lights beside the sun
     (the features scene, the C5-like city block) the light-space case runs both lists
     in one launch (k_trace_shadow<.., kShadowSunWorld>); sun only (the small soup) the
     sun's list alone. Any-hit occlusion does not depend on the structure: bit-exact."""
-    monkeypatch.setenv("ARK_SUN_BVH", sun_bvh)
+    mode = abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE if sun_bvh == "1" else abi.ARK_DDGI_SUN_BVH_WORLD
     sc = scenes.features_scene()
     grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
     cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
-                       max_rays_per_probe=128, max_probe_updates=144)
+                       max_rays_per_probe=128, max_probe_updates=144, sun_bvh=mode)
     reps = run_pair(sc, grid, cfg, 2, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05,
                                                   environment_brightness=0.5))
     _assert_exact(reps, offsets_expected=True)
     sc = S.city_block(2000, extent=40.0)
     grid = D.ProbeGrid((8, 4, 8), (40.0 / 8, 2.5, 40.0 / 8), (2.5, 0.5, 2.5))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=256, compute_probe_offsets=True,
-                       max_rays_per_probe=64, max_probe_updates=256)
+                       max_rays_per_probe=64, max_probe_updates=256, sun_bvh=mode)
     reps = run_pair(sc, grid, cfg, 2, 1000.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.02,
                                                    environment_brightness=1.0))
     _assert_exact(reps, offsets_expected=True)
     sc = S.soup(64_000, extent=7.0)
     grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
     cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=512, compute_probe_offsets=False,
-                       max_rays_per_probe=256, max_probe_updates=512)
+                       max_rays_per_probe=256, max_probe_updates=512, sun_bvh=mode)
     reps = run_pair(sc, grid, cfg, 2, 10000.0, dict(light_pre_exposure=1.0, environment_brightness=1.0))
     _assert_exact(reps)
 
@@ -217,14 +217,13 @@ def test_visibility_sharpness_modes(sharpness):
         orc.close()
 
 
-def test_sun_bvh_depth_sizes_the_spill(monkeypatch):
+def test_sun_bvh_depth_sizes_the_spill():
     """the light-space sun BVH holds the triangles of all three
     hit-mask classes in one tree, so it can be deeper than each class's world BVH, and
     the shadow traversal's stack spills with its depth. A soup split evenly over the
     opaque / masked / translucent classes (one sun BVH over all of them): the depth that
     sizes the spill (ArkDdgiBvhStats.max_depth) covers the sun BVH's, and the update
     stays bit-exact with the sun's rays forced through it."""
-    monkeypatch.setenv("ARK_SUN_BVH", "1")
     sc = S.soup(96_000, extent=7.0)
     classes = ((abi.ARK_RT_HIT_MASK_OPAQUE, abi.ARK_BLEND_MODE_OPAQUE), (abi.ARK_RT_HIT_MASK_MASKED, abi.ARK_BLEND_MODE_MASKED),
                (abi.ARK_RT_HIT_MASK_BLEND, abi.ARK_BLEND_MODE_TRANSLUCENT))
@@ -234,7 +233,8 @@ def test_sun_bvh_depth_sizes_the_spill(monkeypatch):
         sc.materials["blend_mode"][sc.meshes["material_index"][sc.instances["rt_mesh_index"][i]]] = blend
     grid = D.ProbeGrid((6, 6, 6), (1.2, 1.2, 1.2), (0.5, 0.5, 0.5))
     cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=216, compute_probe_offsets=False,
-                       max_rays_per_probe=128, max_probe_updates=216)
+                       max_rays_per_probe=128, max_probe_updates=216,
+                       sun_bvh=abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE)
     ctx = D.DDGIContext(grid, 10000.0, cfg)
     ctx.set_scene(sc)
     st = ctx.bvh_stats()

@@ -1,12 +1,11 @@
 """Frames in flight (ark_ddgi.h, ark_ddgi_update): a rolling window's slot table and
 primary traversal overlap the previous frame's shadow rays, shading and update. The
-dependence rule must leave every result equal to the serial run (ARK_DDGI_PIPELINE=0):
+dependence rule must leave every result equal to the serial run (ARK_DDGI_FLAG_SERIAL_FRAMES):
 disjoint windows with probes moving, windows that intersect (they pipeline too: the
 offsets of update n run on the traversal stream before update n+1's slot table, so
 the next traversal reads them in order), an offsets write through ark_ddgi_write
 between two updates, and one through the device views on the update stream flagged
 with ark_ddgi_mark_external_write (the next traversal must see either)."""
-import os
 
 import numpy as np
 import pytest
@@ -23,17 +22,9 @@ WHICH = (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_D
 
 def _node(sc, K, pipelined):
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=K, max_rays_per_probe=64, max_probe_updates=K,
-                       compute_probe_offsets=True)
-    old = os.environ.get("ARK_DDGI_PIPELINE")
-    os.environ["ARK_DDGI_PIPELINE"] = "1" if pipelined else "0"
-    try:
-        n = D.DDGINode(cfg)
-        assert n.construct(sc, GRID, 100.0, **EXPOSURE)
-    finally:
-        if old is None:
-            del os.environ["ARK_DDGI_PIPELINE"]
-        else:
-            os.environ["ARK_DDGI_PIPELINE"] = old
+                       compute_probe_offsets=True, serial_frames=not pipelined)
+    n = D.DDGINode(cfg)
+    assert n.construct(sc, GRID, 100.0, **EXPOSURE)
     return n
 
 

@@ -36,21 +36,10 @@ def _compare(ctx, orc, frame, what):
         assert r["mismatch"] == 0, f"frame {frame} ({what}): {r}"
 
 
-class _Env:
-    """Sets ARK_SUN_BVH for contexts created inside the block (read at ark_ddgi_create)."""
-
-    def __init__(self, value):
-        self.value, self.old = value, None
-
-    def __enter__(self):
-        self.old = os.environ.get("ARK_SUN_BVH")
-        os.environ["ARK_SUN_BVH"] = self.value
-
-    def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop("ARK_SUN_BVH", None)
-        else:
-            os.environ["ARK_SUN_BVH"] = self.old
+def _sun_mode(value):
+    """ArkDdgiDesc.sun_bvh of a test's contexts: "1" the light-space BVH whenever there is
+    a sun, "0" the world BVHs."""
+    return abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE if value == "1" else abi.ARK_DDGI_SUN_BVH_WORLD
 
 
 def _scaled_lights(sc, pre, spots=None):
@@ -78,8 +67,8 @@ def test_lights_per_frame_exposure_spots_sun(sun_bvh, sync):
     and the atlases compared at the end."""
     sc = scenes.features_scene()
     cfg = _cfg()
-    with _Env(sun_bvh):
-        ctx = D.DDGIContext(GRID, 100.0, cfg)
+    cfg.sun_bvh = _sun_mode(sun_bvh)
+    ctx = D.DDGIContext(GRID, 100.0, cfg)
     ctx.set_scene(sc)
     stats = ctx.bvh_stats()
     if sun_bvh == "1":
@@ -137,8 +126,8 @@ def test_instances_per_frame_refit(sun_bvh):
     rebuilds its own BVH from the same transforms)."""
     sc = scenes.features_scene()
     cfg = _cfg()
-    with _Env(sun_bvh):
-        ctx = D.DDGIContext(GRID, 100.0, cfg)
+    cfg.sun_bvh = _sun_mode(sun_bvh)
+    ctx = D.DDGIContext(GRID, 100.0, cfg)
     ctx.set_scene(sc)
     orc = O.Oracle(ctx.desc)
     orc.set_scene(sc)
@@ -195,8 +184,8 @@ def test_soup_lights_and_instances_every_frame():
     grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
     cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=300, compute_probe_offsets=True,
                        max_rays_per_probe=128, max_probe_updates=512)
-    with _Env("1"):
-        ctx = D.DDGIContext(grid, 10000.0, cfg)
+    cfg.sun_bvh = _sun_mode("1")
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
     ctx.set_scene(sc)
     orc = O.Oracle(ctx.desc)
     orc.set_scene(sc)
@@ -231,9 +220,9 @@ def test_shared_scene_refit_reaches_every_context():
     light-space sun BVH never dereferenced)."""
     sc = scenes.features_scene()
     cfg = _cfg(64, 144)
-    with _Env("1"):
-        a = D.DDGIContext(GRID, 100.0, cfg, shard_rank=0, shard_count=2)
-        b = D.DDGIContext(GRID, 100.0, cfg, shard_rank=1, shard_count=2)
+    cfg.sun_bvh = _sun_mode("1")
+    a = D.DDGIContext(GRID, 100.0, cfg, shard_rank=0, shard_count=2)
+    b = D.DDGIContext(GRID, 100.0, cfg, shard_rank=1, shard_count=2)
     a.set_scene(sc)
     b.share_scene(a)
     ref = D.DDGIContext(GRID, 100.0, cfg)
@@ -274,8 +263,8 @@ def test_sun_bvh_rebuilt_in_background(cause):
     grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False,
                        max_rays_per_probe=64, max_probe_updates=512)
-    with _Env("1"):
-        ctx = D.DDGIContext(grid, 10000.0, cfg)
+    cfg.sun_bvh = _sun_mode("1")
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
     ctx.set_scene(sc)
     assert ctx.bvh_stats().sun_node_count > 0
     orc = O.Oracle(ctx.desc)
@@ -327,9 +316,9 @@ def test_close_during_sun_bvh_rebuild():
     grid = D.ProbeGrid((6, 6, 6), (1.5, 1.5, 1.5), (0.5, 0.5, 0.5))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=216, compute_probe_offsets=False,
                        max_rays_per_probe=64, max_probe_updates=216)
-    with _Env("1"):
-        a = D.DDGIContext(grid, 10000.0, cfg)
-        b = D.DDGIContext(grid, 10000.0, cfg)
+    cfg.sun_bvh = _sun_mode("1")
+    a = D.DDGIContext(grid, 10000.0, cfg)
+    b = D.DDGIContext(grid, 10000.0, cfg)
     a.set_scene(sc)
     b.share_scene(a)
     d = np.array([0.2, -1.0, 0.5], np.float32)
@@ -347,8 +336,8 @@ def test_close_during_sun_bvh_rebuild():
     assert b.bvh_stats().sun_node_count > 0
     b.close()
     # and a context closed with its rebuild still running, nothing sharing it
-    with _Env("1"):
-        c = D.DDGIContext(grid, 10000.0, cfg)
+    cfg.sun_bvh = _sun_mode("1")
+    c = D.DDGIContext(grid, 10000.0, cfg)
     c.set_scene(sc)
     c.set_lights(sun, ())
     c.close()

@@ -3,7 +3,7 @@ geBytes / visitNodeSun), restated in numpy and checked exhaustively on the CPU: 
 unsigned compare of four packed bytes with one subtraction and one three-input boolean
 function, and the gather of the eight per-child results into the 8-bit slot mask by the
 high word of one multiply. The device path itself is covered by the GPU parity suite
-(ARK_SUN_BVH=1 cases), where a wrong compare would cull an occluder."""
+(ARK_DDGI_SUN_BVH_LIGHT_SPACE cases), where a wrong compare would cull an occluder."""
 import numpy as np
 
 H = np.uint32(0x80808080)

@@ -19,6 +19,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools", "sim"))
 
 
 def world_triangles(sc):
@@ -67,6 +68,9 @@ def main():
             rays[k] = [x, y, z, d[0], d[1], d[2], 10000.0]
             k += 1
     lib = abi.load_library()
+    import bvhsim  # tools/sim: the simulator library
+
+    sim = bvhsim.load()
     res = {}
     for v in args.variants:
         parts = v.split()
@@ -78,7 +82,7 @@ def main():
         out = (C.c_uint64 * 9)()
         t = time.time()
         steps = np.zeros(rays.shape[0], np.uint32)
-        lib.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out, steps.ctypes.data)
+        sim.ark_ddgi_debug_bvh8_trace_stats(tris.ctypes.data, tris.shape[0], rays.ctypes.data, rays.shape[0], args.threads, out, steps.ctypes.data)
         if args.save_steps:
             np.savez_compressed(f"{args.save_steps}_{v.replace(' ', '_')}.npz", steps=steps, probes=probes, rays=rays)
         n = rays.shape[0]

@@ -23,6 +23,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools", "sim"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
@@ -76,13 +77,16 @@ def main():
     rays_l[:, 3:6] = (0.0, 0.0, 1.0)
     rays_l[:, 6] = 20000.0
     lib = abi.load_library()
+    import bvhsim  # tools/sim: the simulator library
+
+    sim = bvhsim.load()
     res = {}
     for name, tr, ry, ws in [("world", tris, rays_w, ["1,1,1"])] + [("light", tris_l, rays_l, args.weights)]:
         for w in ws:
             os.environ["ARK_BVH_AREA_W"] = w
             out = (C.c_uint64 * 9)()
             t0 = time.time()
-            lib.ark_ddgi_debug_bvh8_trace_stats(tr.ctypes.data, tr.shape[0], ry.ctypes.data, ry.shape[0], args.threads, out, None)
+            sim.ark_ddgi_debug_bvh8_trace_stats(tr.ctypes.data, tr.shape[0], ry.ctypes.data, ry.shape[0], args.threads, out, None)
             n = ry.shape[0]
             key = f"{name} {w}"
             res[key] = {"nodes_per_ray": round(out[0] / n, 3), "tris_per_ray": round(out[1] / n, 3), "hit_frac": round(out[2] / n, 4),
