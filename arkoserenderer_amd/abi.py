@@ -248,6 +248,21 @@ class ArkDdgiDeviceViews(C.Structure):
     ]
 
 
+ARK_DDGI_WINDOW_PACKET_BYTES = 2096
+
+
+class ArkDdgiWindowExchange(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("full_bands", C.c_uint32),
+        ("probes_per_rank", C.c_uint32),
+        ("my_probes", C.c_uint32),
+        ("first_probe", C.c_uint32),
+        ("probe_updates", C.c_uint32),
+        ("bytes_per_rank", C.c_uint64),
+    ]
+
+
 class ArkDdgiBvhStats(C.Structure):
     _fields_ = [
         ("node_count", C.c_uint64),
@@ -443,6 +458,9 @@ EXPORTS = {
     "ark_ddgi_update_overlapped": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p, C.c_void_p, C.c_void_p]),
     "ark_ddgi_update_exchanged": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),
     "ark_ddgi_exchange_begin": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ark_ddgi_window_exchange_info": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiWindowExchange)]),
+    "ark_ddgi_pack_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "ark_ddgi_unpack_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "ark_ddgi_exchange_end": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ark_ddgi_resource_size": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "ark_ddgi_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),

@@ -131,6 +131,17 @@ class RcclBandExchange:
             _nccl_check(lib.ncclAllGather(C.c_void_p(mine), C.c_void_p(full), C.c_size_t(n), self.NCCL_UINT8, self.comm, s), "ncclAllGather")
         _nccl_check(lib.ncclGroupEnd(), "ncclGroupEnd")
 
+    def all_gather(self, out, mine):
+        """ncclAllGather of equal byte counts (mine = this rank's slot of out, in place) on
+        the current stream, through this communicator (the windowed exchange's packets)."""
+        import ctypes as C
+
+        import torch
+
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _nccl_check(self.lib.ncclAllGather(C.c_void_p(mine.data_ptr()), C.c_void_p(out.data_ptr()), C.c_size_t(mine.numel()), self.NCCL_UINT8, self.comm, s),
+                    "ncclAllGather")
+
     def async_error(self) -> int:
         import ctypes as C
 
@@ -147,6 +158,81 @@ class RcclBandExchange:
         if self.comm:
             self.lib.ncclCommDestroy(self.comm)
             self.comm = None
+
+
+class WindowExchange:
+    """The windowed Z-slab exchange (SURVEY §8e option (a); ark_ddgi.h
+    ark_ddgi_window_exchange_info): with a rolling window (K < N) every rank packs the
+    tiles its update wrote (one 2,096-B packet per window probe of its slab, in slot
+    order), the packets of all ranks are all-gathered (equal counts, padded to the
+    largest slab share), and every rank writes the other slabs' packets into their
+    tiles. A window that covers the grid (K = N) exchanges the row bands instead
+    (`band`, e.g. RcclBandExchange.exchange). exchange() enqueues on the current stream,
+    as OverlappedSlabExchange calls it between exchange_begin and exchange_end.
+
+    source: window_exchange_info() / pack_window(tensor, stream) / unpack_window(tensor,
+    stream) - WindowSource(DDGIContext) on the GPU; the CPU tests pass an oracle-backed
+    twin. gather(out, mine): all-gather of mine (this rank's slot of out) into out."""
+
+    def __init__(self, source, band, gather, rank: int, world: int, max_probes_per_rank: int, device):
+        import torch
+
+        from . import abi
+
+        self.source, self.band, self.gather = source, band, gather
+        self.rank, self.world = rank, world
+        # every window's packets fit: at most min(K_max, N / P) probes of one slab
+        self.recv = torch.empty(world * max_probes_per_rank * abi.ARK_DDGI_WINDOW_PACKET_BYTES, dtype=torch.uint8, device=device)
+        self.last_bytes_per_rank = 0  # received per frame: world - 1 of these (full bands: 0)
+
+    def exchange(self):
+        info = self.source.window_exchange_info()
+        if info.full_bands:
+            self.last_bytes_per_rank = 0
+            self.band()
+            return
+        n = int(info.bytes_per_rank)
+        self.last_bytes_per_rank = n
+        if n == 0:
+            return
+        if n * self.world > self.recv.numel():
+            raise RuntimeError(f"WindowExchange: {n} B per rank exceeds the buffer sized at construction")
+        out = self.recv[:n * self.world]
+        mine = out[self.rank * n:(self.rank + 1) * n]
+        self.source.pack_window(mine)
+        self.gather(out, mine)
+        self.source.unpack_window(out)
+
+
+class WindowSource:
+    """WindowExchange's view of a DDGIContext: pack / unpack on the current stream."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def window_exchange_info(self):
+        return self.ctx.window_exchange_info()
+
+    def pack_window(self, t):
+        import torch
+
+        self.ctx.pack_window(t.data_ptr(), t.numel(), torch.cuda.current_stream().cuda_stream)
+
+    def unpack_window(self, t):
+        import torch
+
+        self.ctx.unpack_window(t.data_ptr(), t.numel(), torch.cuda.current_stream().cuda_stream)
+
+
+def torch_all_gather(group=None):
+    """WindowExchange's gather through a torch.distributed group (gloo on CPU, nccl = RCCL)."""
+
+    def gather(out, mine):
+        import torch.distributed as dist
+
+        dist.all_gather_into_tensor(out, mine, group=group)
+
+    return gather
 
 
 def _nccl_unique_id_type():

@@ -317,6 +317,7 @@ struct ArkDdgiCtx {
     bool countersPending = false;
     uint64_t lastRays = 0, lastProbes = 0;
     uint32_t nextProbeIndex = 0; // (first + K) % N of the last update, or of a loaded state
+    uint32_t lastFirst = 0, lastK = 0; // the last update's window (ark_ddgi_window_exchange_info)
 
     int fail(int code, const char* fmt, ...)
     {
@@ -1494,6 +1495,63 @@ int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* hipStream)
     return ARK_DDGI_OK;
 }
 
+static ArkDdgiWindowExchange windowExchangeInfo(const ArkDdgiCtx* ctx)
+{
+    ArkDdgiWindowExchange w {};
+    w.struct_size = sizeof(w);
+    w.first_probe = ctx->lastFirst;
+    w.probe_updates = ctx->lastK;
+    const uint32_t P = static_cast<uint32_t>(ctx->desc.shard_count), Zs = static_cast<uint32_t>(ctx->Z) / P;
+    w.full_bands = ctx->lastK == static_cast<uint32_t>(ctx->N) ? 1u : 0u;
+    for (uint32_t q = 0; q < P; ++q) {
+        const uint32_t n = slabRankOf(static_cast<uint32_t>(ctx->X), static_cast<uint32_t>(ctx->Y), static_cast<uint32_t>(ctx->Z), q * Zs, (q + 1) * Zs, ctx->lastFirst,
+                                      ctx->lastK);
+        w.probes_per_rank = std::max(w.probes_per_rank, n);
+        if (q == static_cast<uint32_t>(ctx->desc.shard_rank)) w.my_probes = n;
+    }
+    w.bytes_per_rank = w.full_bands ? 0u : static_cast<uint64_t>(w.probes_per_rank) * kWindowPacketBytes;
+    return w;
+}
+
+int ark_ddgi_window_exchange_info(const ArkDdgiCtx* ctx, ArkDdgiWindowExchange* out)
+{
+    if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    *out = windowExchangeInfo(ctx);
+    return ARK_DDGI_OK;
+}
+
+static int windowPack(ArkDdgiCtx* ctx, void* buf, uint64_t bytes, void* hipStream, bool unpack)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const ArkDdgiWindowExchange w = windowExchangeInfo(ctx);
+    if (w.full_bands) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "window exchange: the last window covered the grid (exchange the bands)");
+    const uint64_t need = unpack ? w.bytes_per_rank * static_cast<uint64_t>(ctx->desc.shard_count) : w.bytes_per_rank;
+    if (bytes != need) return ctx->fail(ARK_DDGI_E_SIZE_MISMATCH, "window exchange: %llu bytes, the window needs %llu", (unsigned long long)bytes, (unsigned long long)need);
+    if (need && !buf) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "window exchange: null buffer");
+    ARK_HIP(hipSetDevice(ctx->device));
+    WindowExchangeArgs a {};
+    a.X = ctx->X; a.Y = ctx->Y; a.Z = ctx->Z; a.N = ctx->N;
+    a.first = ctx->lastFirst;
+    a.K = ctx->lastK;
+    a.Wi = ctx->Wi; a.Wv = ctx->Wv;
+    a.slabDepth = static_cast<uint32_t>(ctx->Z / ctx->desc.shard_count);
+    a.rank = static_cast<uint32_t>(ctx->desc.shard_rank);
+    a.world = static_cast<uint32_t>(ctx->desc.shard_count);
+    a.bytesPerRank = w.bytes_per_rank;
+    a.irr = ctx->irr.as<uint16_t>();
+    a.vis = ctx->vis.as<uint16_t>();
+    a.buf = static_cast<uint8_t*>(buf);
+    if (need) ARK_HIP(launch_window_pack(a, unpack, streamOf(hipStream)));
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_pack_window(ArkDdgiCtx* ctx, void* dst, uint64_t bytes, void* hipStream) { return windowPack(ctx, dst, bytes, hipStream, false); }
+
+int ark_ddgi_unpack_window(ArkDdgiCtx* ctx, const void* src, uint64_t bytes, void* hipStream)
+{
+    return windowPack(ctx, const_cast<void*>(src), bytes, hipStream, true);
+}
+
 // The caller's stream s waits for the traversal stream's part of a pipelined frame
 // (slot table, traversal, offsets): device-side sequencing, or an event.
 static hipError_t tracedSync(ArkDdgiCtx* ctx, bool seq, uint32_t seqN, hipStream_t ts, hipStream_t s)
@@ -1693,6 +1751,8 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     ctx->lastRays = f.window_rays;
     ctx->lastProbes = f.window_probes;
     ctx->nextProbeIndex = (f.first + K) % N;
+    ctx->lastFirst = f.first;
+    ctx->lastK = K;
     return ARK_DDGI_OK;
 }
 

@@ -292,6 +292,25 @@ hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInsta
 // one level: nodes order[0 .. count), boxes [node][6] (lo, hi) of the deeper levels in, this level's out
 hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, float inflateAbs, hipStream_t s);
 
+// Windowed Z-slab exchange (ddgi_exchange.hip, ark_ddgi_pack_window / _unpack_window):
+// one packet per updated probe, its irradiance tile (10 x 10 RGBA16F, border included)
+// then its visibility tile (18 x 18 RG16F), in the rank's slot order (slabRankOf)
+struct WindowExchangeArgs {
+    uint32_t X, Y, Z, N;
+    uint32_t first, K;       // the window of the update exchanged
+    uint32_t Wi, Wv;         // atlas widths (texels)
+    uint32_t slabDepth;      // probe layers per rank (Z / world)
+    uint32_t rank, world;
+    uint64_t bytesPerRank;   // the all-gather's count per rank (max window probes of a slab x packet)
+    uint16_t* irr;
+    uint16_t* vis;
+    uint8_t* buf;            // pack: this rank's packets; unpack: all ranks' (world x bytesPerRank)
+};
+constexpr uint32_t kIrrTileTexels = (ARK_DDGI_IRRADIANCE_RES + 2 * ARK_DDGI_ATLAS_PADDING) * (ARK_DDGI_IRRADIANCE_RES + 2 * ARK_DDGI_ATLAS_PADDING);
+constexpr uint32_t kVisTileTexels = (ARK_DDGI_VISIBILITY_RES + 2 * ARK_DDGI_ATLAS_PADDING) * (ARK_DDGI_VISIBILITY_RES + 2 * ARK_DDGI_ATLAS_PADDING);
+constexpr uint32_t kWindowPacketBytes = kIrrTileTexels * 8u + kVisTileTexels * 4u; // 2,096
+hipError_t launch_window_pack(const WindowExchangeArgs& a, bool unpack, hipStream_t s);
+
 hipError_t launch_probe_slots(const FrameArgs& f, hipStream_t s);
 // stage 0: parameterization raster, 1: barycentrics + work list, 2: AO rays
 hipError_t launch_bake(const SceneArgs& sc, const BakeArgs& b, uint32_t blocks, int stage, hipStream_t s);

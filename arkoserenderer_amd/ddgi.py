@@ -193,6 +193,22 @@ class DDGIContext:
         """ark_ddgi_exchange_end: the exchange enqueued on comm_stream so far completes the frame."""
         self.check(self.lib.ark_ddgi_exchange_end(self.h, C.c_void_p(comm_stream) if comm_stream else None), "ark_ddgi_exchange_end")
 
+    def window_exchange_info(self) -> abi.ArkDdgiWindowExchange:
+        """ark_ddgi_window_exchange_info: the packet layout of the last update's window."""
+        w = abi.ArkDdgiWindowExchange()
+        self.check(self.lib.ark_ddgi_window_exchange_info(self.h, C.byref(w)), "ark_ddgi_window_exchange_info")
+        return w
+
+    def pack_window(self, dst_ptr: int, nbytes: int, comm_stream: int | None):
+        """ark_ddgi_pack_window: this rank's updated tiles -> dst (bytes_per_rank) on comm_stream."""
+        self.check(self.lib.ark_ddgi_pack_window(self.h, C.c_void_p(dst_ptr), nbytes, C.c_void_p(comm_stream) if comm_stream else None),
+                   "ark_ddgi_pack_window")
+
+    def unpack_window(self, src_ptr: int, nbytes: int, comm_stream: int | None):
+        """ark_ddgi_unpack_window: every rank's packets (world x bytes_per_rank) -> the other slabs' tiles."""
+        self.check(self.lib.ark_ddgi_unpack_window(self.h, C.c_void_p(src_ptr), nbytes, C.c_void_p(comm_stream) if comm_stream else None),
+                   "ark_ddgi_unpack_window")
+
     def synchronize(self):
         self.check(self.lib.ark_ddgi_synchronize(self.h), "ark_ddgi_synchronize")
 

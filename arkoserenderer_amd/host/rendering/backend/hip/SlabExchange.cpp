@@ -89,6 +89,7 @@ bool SlabBands::fromContext(ArkDdgiCtx* ctx, int rank, int world, SlabBands& out
         error = "the context's Z-slab bands are not rank " + std::to_string(rank) + " of " + std::to_string(world) + " equal bands";
         return false;
     }
+    out.ctx = ctx;
     out.irradiance = static_cast<uint8_t*>(v.irradiance_atlas);
     out.visibility = static_cast<uint8_t*>(v.visibility_atlas);
     out.irradianceBand = v.irradiance_slab_bytes;
@@ -106,8 +107,25 @@ bool RcclSlabExchange::createUniqueId(std::vector<uint8_t>& out)
     return true;
 }
 
+// A receive buffer of at least `bytes` (grown once the exchanges using it are done)
+static bool ensureRecv(uint8_t*& buf, size_t& have, size_t bytes, hipStream_t s)
+{
+    if (have >= bytes) return true;
+    if (buf) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(buf);
+        buf = nullptr;
+        have = 0;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return false;
+    buf = static_cast<uint8_t*>(p);
+    have = bytes;
+    return true;
+}
+
 RcclSlabExchange::RcclSlabExchange(int device, int rank, int world, const void* uniqueId, const SlabBands& bands, double timeoutSeconds)
-    : m_rank(rank), m_bands(bands), m_watchdog(timeoutSeconds)
+    : m_rank(rank), m_bands(bands), m_world(world), m_watchdog(timeoutSeconds)
 {
     if (hipSetDevice(device) != hipSuccess) {
         m_error = "hipSetDevice failed";
@@ -144,6 +162,7 @@ RcclSlabExchange::~RcclSlabExchange()
     if (m_ok) (void)drain();
     if (m_stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(m_stream));
     if (m_comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(m_comm));
+    if (m_recv) (void)hipFree(m_recv);
     for (void* e : m_done)
         if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
     if (m_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(m_stream));
@@ -167,16 +186,39 @@ void* RcclSlabExchange::exchange(int rank, void* updateDone)
     // frame n - kRing's all-gather (the last record of this slot) must be complete
     if (m_frames >= kRing && !m_watchdog.wait(slot, m_comm, "RcclSlabExchange frame n-3")) return nullptr;
     if (updateDone) (void)hipStreamWaitEvent(s, static_cast<hipEvent_t>(updateDone), 0);
-    // in place: this rank's band already sits at recvbuff + rank * count
-    ncclResult_t r = ncclGroupStart();
-    if (r == ncclSuccess)
-        r = ncclAllGather(m_bands.irradiance + m_rank * m_bands.irradianceBand, m_bands.irradiance, m_bands.irradianceBand, ncclUint8, comm, s);
-    if (r == ncclSuccess)
-        r = ncclAllGather(m_bands.visibility + m_rank * m_bands.visibilityBand, m_bands.visibility, m_bands.visibilityBand, ncclUint8, comm, s);
-    const ncclResult_t g = ncclGroupEnd();
-    if (r != ncclSuccess || g != ncclSuccess) {
-        ARKOSE_LOG(Error, "RcclSlabExchange: all-gather failed: %s", ncclGetErrorString(r != ncclSuccess ? r : g));
-        return nullptr;
+    ArkDdgiWindowExchange w {};
+    if (!m_bands.ctx || ark_ddgi_window_exchange_info(m_bands.ctx, &w) != ARK_DDGI_OK) w.full_bands = 1;
+    if (w.full_bands) {
+        // in place: this rank's band already sits at recvbuff + rank * count
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess)
+            r = ncclAllGather(m_bands.irradiance + m_rank * m_bands.irradianceBand, m_bands.irradiance, m_bands.irradianceBand, ncclUint8, comm, s);
+        if (r == ncclSuccess)
+            r = ncclAllGather(m_bands.visibility + m_rank * m_bands.visibilityBand, m_bands.visibility, m_bands.visibilityBand, ncclUint8, comm, s);
+        const ncclResult_t g = ncclGroupEnd();
+        if (r != ncclSuccess || g != ncclSuccess) {
+            ARKOSE_LOG(Error, "RcclSlabExchange: all-gather failed: %s", ncclGetErrorString(r != ncclSuccess ? r : g));
+            return nullptr;
+        }
+    } else if (w.bytes_per_rank) {
+        // the window's tiles only: pack, one all-gather of the packets, unpack
+        const size_t n = w.bytes_per_rank;
+        if (!ensureRecv(m_recv, m_recvBytes, n * m_world, s)) {
+            ARKOSE_LOG(Error, "RcclSlabExchange: receive buffer of %zu bytes", n * m_world);
+            return nullptr;
+        }
+        if (ark_ddgi_pack_window(m_bands.ctx, m_recv + m_rank * n, n, s) != ARK_DDGI_OK) {
+            ARKOSE_LOG(Error, "RcclSlabExchange: ark_ddgi_pack_window: %s", ark_ddgi_last_error(m_bands.ctx));
+            return nullptr;
+        }
+        if (const ncclResult_t r = ncclAllGather(m_recv + m_rank * n, m_recv, n, ncclUint8, comm, s); r != ncclSuccess) {
+            ARKOSE_LOG(Error, "RcclSlabExchange: all-gather failed: %s", ncclGetErrorString(r));
+            return nullptr;
+        }
+        if (ark_ddgi_unpack_window(m_bands.ctx, m_recv, n * m_world, s) != ARK_DDGI_OK) {
+            ARKOSE_LOG(Error, "RcclSlabExchange: ark_ddgi_unpack_window: %s", ark_ddgi_last_error(m_bands.ctx));
+            return nullptr;
+        }
     }
     (void)hipEventRecord(static_cast<hipEvent_t>(slot), s);
     ++m_frames;
@@ -199,6 +241,7 @@ DeviceCopySlabExchange::DeviceCopySlabExchange(std::vector<SlabBands> ranks)
 DeviceCopySlabExchange::~DeviceCopySlabExchange()
 {
     (void)hipStreamSynchronize(static_cast<hipStream_t>(m_stream));
+    if (m_recv) (void)hipFree(m_recv);
     (void)hipEventDestroy(static_cast<hipEvent_t>(m_done));
     (void)hipStreamDestroy(static_cast<hipStream_t>(m_stream));
 }
@@ -220,6 +263,21 @@ void* DeviceCopySlabExchange::exchange(int rank, void* updateDone)
     for (void* e : m_ready)
         if (e) (void)hipStreamWaitEvent(s, static_cast<hipEvent_t>(e), 0);
     const size_t P = m_ranks.size();
+    ArkDdgiWindowExchange w {};
+    if (!m_ranks[0].ctx || ark_ddgi_window_exchange_info(m_ranks[0].ctx, &w) != ARK_DDGI_OK) w.full_bands = 1;
+    if (!w.full_bands) {
+        // the windowed exchange: every rank packs into its region, every rank unpacks
+        const size_t n = w.bytes_per_rank;
+        if (n && !ensureRecv(m_recv, m_recvBytes, n * P, s)) ARKOSE_LOG(Fatal, "DeviceCopySlabExchange: receive buffer of %zu bytes", n * P);
+        for (size_t r = 0; n && r < P; ++r)
+            if (ark_ddgi_pack_window(m_ranks[r].ctx, m_recv + r * n, n, s) != ARK_DDGI_OK)
+                ARKOSE_LOG(Fatal, "DeviceCopySlabExchange: ark_ddgi_pack_window: %s", ark_ddgi_last_error(m_ranks[r].ctx));
+        for (size_t r = 0; n && r < P; ++r)
+            if (ark_ddgi_unpack_window(m_ranks[r].ctx, m_recv, n * P, s) != ARK_DDGI_OK)
+                ARKOSE_LOG(Fatal, "DeviceCopySlabExchange: ark_ddgi_unpack_window: %s", ark_ddgi_last_error(m_ranks[r].ctx));
+        (void)hipEventRecord(static_cast<hipEvent_t>(m_done), s);
+        return m_done;
+    }
     for (size_t src = 0; src < P; ++src)
         for (size_t dst = 0; dst < P; ++dst) {
             if (src == dst) continue;

@@ -19,6 +19,7 @@
 
 // Band geometry of one context's atlases under P ranks.
 struct SlabBands {
+    ArkDdgiCtx* ctx { nullptr }; // the windowed exchange packs / unpacks through it
     uint8_t* irradiance { nullptr };
     uint8_t* visibility { nullptr };
     size_t irradianceBand { 0 };  // bytes of one rank's band
@@ -73,7 +74,10 @@ private:
 };
 
 // One process per GPU: ncclAllGather (RCCL over xGMI) of each band in place, on a
-// side stream of this rank's device. Both calls in one ncclGroup.
+// side stream of this rank's device. Both calls in one ncclGroup. When the update's
+// window did not cover the grid (K < N: ark_ddgi_window_exchange_info), only the tiles
+// it wrote travel: ark_ddgi_pack_window into this rank's region of a receive buffer,
+// one ncclAllGather of the packets, ark_ddgi_unpack_window (ark_ddgi.h).
 class RcclSlabExchange final : public SlabExchange {
 public:
     // `uniqueId` = the 128-byte ncclUniqueId all ranks share (rank 0 creates it,
@@ -104,6 +108,9 @@ private:
     static constexpr uint32_t kRing = 3;
     void* m_done[kRing] {}; // completion of frame n in slot n % kRing
     uint64_t m_frames { 0 };
+    int m_world { 1 };
+    uint8_t* m_recv { nullptr }; // windowed exchange: world x bytes_per_rank
+    size_t m_recvBytes { 0 };
     bool m_ok { false };
     std::string m_error;
     ExchangeWatchdog m_watchdog;
@@ -126,6 +133,8 @@ public:
 
 private:
     std::vector<SlabBands> m_ranks;
+    uint8_t* m_recv { nullptr }; // windowed exchange: every rank's packets
+    size_t m_recvBytes { 0 };
     std::vector<void*> m_ready;
     std::vector<bool> m_hasArrived;
     int m_arrived { 0 };

@@ -182,7 +182,7 @@ def main(argv=None):
     # frame N+1's primary traversal (collective.OverlappedSlabExchange)
     exch = None
     if world > 1:
-        from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange
+        from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange, WindowExchange, WindowSource, torch_all_gather
 
         # the two bands as one RCCL group on the exchange stream itself (RcclBandExchange);
         # ARK_BENCH_TORCH_PG=1: through torch's process group instead
@@ -194,7 +194,13 @@ def main(argv=None):
                 print(f"warning: RcclBandExchange unavailable ({e}); using torch.distributed all-gather", file=sys.stderr)
         if band is None:
             band = SlabExchange.from_views(ctx.device_views(), rank, world, device)
-        exch = OverlappedSlabExchange(node, band.exchange, device)
+            gather = torch_all_gather()
+        else:
+            gather = band.all_gather
+        # K < N: only the window's tiles travel (WindowExchange); K = N: the row bands
+        window = WindowExchange(WindowSource(ctx), band.exchange, gather, rank, world, min(K, N // world), device)
+        exch = OverlappedSlabExchange(node, window.exchange, device)
+        exch.watchdog.rccl = band if isinstance(band, RcclBandExchange) else None
     setup_s = time.time() - t_setup
 
     frame = 0

@@ -435,6 +435,39 @@ int ark_ddgi_update_exchanged(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* params,
 int ark_ddgi_exchange_begin(ArkDdgiCtx* ctx, void* comm_stream);
 int ark_ddgi_exchange_end(ArkDdgiCtx* ctx, void* comm_stream);
 
+/* Windowed exchange (SURVEY §8e option (a); DDGINode.cpp:138-140 rolling window). When
+ * the last update's window does not cover the grid (K < N), a rank's update wrote only
+ * the tiles of its window probes, so instead of the row bands the ranks all-gather one
+ * packet per updated probe: its irradiance tile (10 x 10 RGBA16F incl. border) and its
+ * visibility tile (18 x 18 RG16F), ARK_DDGI_WINDOW_PACKET_BYTES = 2,096 B. Packets are in
+ * each rank's slot order (the rank of the probe among its slab's window probes), which
+ * every rank derives from the window alone, so no index travels. Every rank contributes
+ * bytes_per_rank (its packets, padded to the largest slab's share), in rank order.
+ *   ark_ddgi_window_exchange_info(ctx, &info)        of the last update (after it)
+ *   ark_ddgi_exchange_begin(ctx, comm_stream)
+ *   info.full_bands ? the band all-gather (ark_ddgi_get_device_views) :
+ *     ark_ddgi_pack_window(ctx, recv + rank * info.bytes_per_rank, info.bytes_per_rank, comm_stream)
+ *     all-gather of bytes_per_rank per rank into recv (in place) on comm_stream
+ *     ark_ddgi_unpack_window(ctx, recv, world * info.bytes_per_rank, comm_stream)
+ *   ark_ddgi_exchange_end(ctx, comm_stream)
+ * C4 at P = 8 and the reference's K = 2,048: 256 probes x 2,096 B = 0.54 MB per rank
+ * instead of 8.6 MB of bands (a rank receives 3.8 MB instead of 60 MB). Replaces the
+ * reference's single-GPU atlas writes (probeUpdateIrradiance.comp:77-78 and
+ * probeUpdateVisibility.comp:61-62 store into the one shared image). */
+#define ARK_DDGI_WINDOW_PACKET_BYTES 2096
+typedef struct ArkDdgiWindowExchange {
+    uint32_t struct_size;
+    uint32_t full_bands;      /* 1: the window covered every probe (K = N): exchange the row bands */
+    uint32_t probes_per_rank; /* the largest slab share of the window (packets per rank, padded) */
+    uint32_t my_probes;       /* this rank's window probes */
+    uint32_t first_probe;     /* the window exchanged: first probe index and count */
+    uint32_t probe_updates;
+    uint64_t bytes_per_rank;  /* probes_per_rank x ARK_DDGI_WINDOW_PACKET_BYTES (0 with full_bands) */
+} ArkDdgiWindowExchange;
+int ark_ddgi_window_exchange_info(const ArkDdgiCtx* ctx, ArkDdgiWindowExchange* out);
+int ark_ddgi_pack_window(ArkDdgiCtx* ctx, void* dst, uint64_t bytes, void* comm_stream);
+int ark_ddgi_unpack_window(ArkDdgiCtx* ctx, const void* src, uint64_t bytes, void* comm_stream);
+
 /* Resource geometry and transfers (blocking, for tests / state save-load). */
 int ark_ddgi_resource_size(const ArkDdgiCtx* ctx, int which, uint64_t* out_bytes);
 int ark_ddgi_read(ArkDdgiCtx* ctx, int which, void* host_dst, uint64_t bytes);

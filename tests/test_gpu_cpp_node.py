@@ -65,14 +65,17 @@ def _headless(tmp_path, tag, extra):
     return out, r.stdout
 
 
+@pytest.mark.parametrize("updates", [100, 144])
 @pytest.mark.parametrize("shards", [2, 3])
-def test_cpp_zslab_device_copy_exchange_equals_unsharded(tmp_path, shards):
+def test_cpp_zslab_device_copy_exchange_equals_unsharded(tmp_path, shards, updates):
     """C++ Z-slab ranks (DDGINode::setSlabExchange + ark_ddgi_update_overlapped):
-    P contexts in one process, bands exchanged by device copies on a side stream;
-    every context ends with the unsharded atlases, bit for bit, and the owners'
-    offsets merge to the unsharded offsets."""
-    ref, _ = _headless(tmp_path, "ref", [])
-    got, log = _headless(tmp_path, f"s{shards}", ["--shards", str(shards)])
+    P contexts in one process, exchanging on a side stream: a rolling window of 100 of
+    the 144 probes moves only the window's tiles (ark_ddgi_pack_window / _unpack_window),
+    the whole grid (144) the row bands by device copies; every context ends with the
+    unsharded atlases, bit for bit, and the owners' offsets merge to the unsharded
+    offsets."""
+    ref, _ = _headless(tmp_path, f"ref{updates}", ["--updates", str(updates)])
+    got, log = _headless(tmp_path, f"s{shards}_{updates}", ["--shards", str(shards), "--updates", str(updates)])
     assert f"{shards} Z-slab ranks, device-copy exchange" in log
     for k, dt in (("irr", np.uint16), ("vis", np.uint16), ("off", np.float32)):
         assert np.array_equal(np.fromfile(got + "." + k, dtype=dt), np.fromfile(ref + "." + k, dtype=dt)), k
