@@ -137,7 +137,16 @@ inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 // The probe update's dot with its last product contracted, (ax*bx + ay*by) + az*bz
 // as one fma, the form a shader compiler emits for GLSL dot() (SPIR-V without
 // NoContraction); k_probe_update evaluates the same expression.
-inline float dotFma(V3 a, V3 b) { return fmaf(a.z, b.z, a.x * b.x + a.y * b.y); }
+// The contraction choices the GLSL leaves open (VERDICT r05 "do this" #5): the default
+// build fuses them as the kernels do; -DARK_ORACLE_NOCONTRACT (libddgi_oracle_nocontract.so)
+// rounds every product and sum separately, as SPIR-V NoContraction decorations would,
+// the witness of how far that freedom moves results (tests/libm_parity.py).
+#ifdef ARK_ORACLE_NOCONTRACT
+inline float orcFma(float a, float b, float c) { return a * b + c; } // -ffp-contract=off: two roundings
+#else
+inline float orcFma(float a, float b, float c) { return fmaf(a, b, c); }
+#endif
+inline float dotFma(V3 a, V3 b) { return orcFma(a.z, b.z, a.x * b.x + a.y * b.y); }
 inline V3 cross(V3 a, V3 b) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x }; }
 inline float length(V3 a) { return sqrtf_(dot(a, a)); }
 // GLSL normalize(v) = v * inversesqrt(dot(v,v)); restated as v * (1/sqrt(dot)).
@@ -583,9 +592,9 @@ struct Ray {
 // origin, Vulkan/DXR algebraic convention).
 inline V3 crossFma(V3 a, V3 b)
 {
-    return { std::fma(a.y, b.z, -(a.z * b.y)), std::fma(a.z, b.x, -(a.x * b.z)), std::fma(a.x, b.y, -(a.y * b.x)) };
+    return { orcFma(a.y, b.z, -(a.z * b.y)), orcFma(a.z, b.x, -(a.x * b.z)), orcFma(a.x, b.y, -(a.y * b.x)) };
 }
-inline float dotFma3(V3 a, V3 b) { return std::fma(a.x, b.x, std::fma(a.y, b.y, a.z * b.z)); }
+inline float dotFma3(V3 a, V3 b) { return orcFma(a.x, b.x, orcFma(a.y, b.y, a.z * b.z)); }
 
 inline bool intersectTri(const Ray& r, const WTri& t, float tmax, float* outT, float* outU, float* outV, bool* backface)
 {
@@ -1455,7 +1464,7 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                     float weight = fmaxf_(0.0f, dotFma(texelDirection, dirs[s]));
                     V3 rad = v3(f16_to_f32(sf[s * 4 + 0]), f16_to_f32(sf[s * 4 + 1]), f16_to_f32(sf[s * 4 + 2]));
                     // newIrr += weight * rad, contracted (fma per component)
-                    newIrr = v3(fmaf(weight, rad.x, newIrr.x), fmaf(weight, rad.y, newIrr.y), fmaf(weight, rad.z, newIrr.z));
+                    newIrr = v3(orcFma(weight, rad.x, newIrr.x), orcFma(weight, rad.y, newIrr.y), orcFma(weight, rad.z, newIrr.z));
                     totalWeight += weight;
                 }
                 newIrr = newIrr / fmaxf_(totalWeight, epsilon);
@@ -1482,8 +1491,8 @@ int oracle_update(void* ctx, const ArkDdgiFrameParams* p, int threads)
                     float weight = om::powf_(fmaxf_(0.0f, dotFma(texelDirection, dirs[s])), p->visibility_sharpness);
                     float d = f16_to_f32(sf[s * 4 + 3]);
                     d = fminf_(fabsf_(d), maxDistance);
-                    nv0 = fmaf(weight, d, nv0);
-                    nv1 = fmaf(weight, square(d), nv1);
+                    nv0 = orcFma(weight, d, nv0);
+                    nv1 = orcFma(weight, square(d), nv1);
                     totalWeight += weight;
                 }
                 float den = fmaxf_(totalWeight, epsilon);
@@ -1961,6 +1970,15 @@ void oracle_f16_to_f32(const uint16_t* in, float* out, uint64_t n)
 }
 // 1 for the -DARK_ORACLE_LIBM build (glibc transcendentals), 0 for the default build
 int oracle_math_is_libm() { return om::kLibm ? 1 : 0; }
+// 1 for the -DARK_ORACLE_NOCONTRACT build (no fused multiply-adds), 0 otherwise
+int oracle_math_is_nocontract()
+{
+#ifdef ARK_ORACLE_NOCONTRACT
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 // ark_fmath.h on the host (both builds): op: 0 sin 1 cos 2 acos 3 atan2 4 log2 5 exp2 6 pow
 void oracle_fmath(int op, const float* x, const float* y, float* out, uint64_t n)

@@ -17,15 +17,24 @@ ORACLE_PATH = os.path.join(ROOT, "oracle", "build", "libddgi_oracle.so")
 # the -DARK_ORACLE_LIBM build: glibc transcendentals instead of ark_fmath.h (the
 # independent witness, oracle/Makefile)
 ORACLE_LIBM_PATH = os.path.join(ROOT, "oracle", "build", "libddgi_oracle_libm.so")
+# the witnesses of the contraction choices (oracle/Makefile): -DARK_ORACLE_NOCONTRACT
+# (no fused multiply-add, ark_fmath.h math) and both freedoms at once (+ glibc math)
+VARIANTS = {
+    "exact": (ORACLE_PATH, 0, 0),
+    "libm": (ORACLE_LIBM_PATH, 1, 0),
+    "nocontract": (os.path.join(ROOT, "oracle", "build", "libddgi_oracle_nocontract.so"), 0, 1),
+    "witness": (os.path.join(ROOT, "oracle", "build", "libddgi_oracle_witness.so"), 1, 1),
+}
 
 _libs = {}
 
 
-def load(libm: bool = False):
-    """The oracle library: the bit-exact build (ark_fmath.h), or with libm=True the
-    glibc-math build."""
-    if libm not in _libs:
-        path = ORACLE_LIBM_PATH if libm else ORACLE_PATH
+def load(libm: bool = False, variant: str | None = None):
+    """The oracle library: the bit-exact build (ark_fmath.h), with libm=True the
+    glibc-math build, or a named variant (VARIANTS)."""
+    variant = variant or ("libm" if libm else "exact")
+    if variant not in _libs:
+        path, want_libm, want_noc = VARIANTS[variant]
         if not os.path.exists(path):
             raise RuntimeError(f"oracle not built: {path} (run __graft_entry__.build())")
         lib = C.CDLL(path)
@@ -58,17 +67,19 @@ def load(libm: bool = False):
         lib.oracle_rt_reflections.argtypes = [C.c_void_p, C.POINTER(abi.ArkReflectionsDesc), C.c_int]
         lib.oracle_probe_debug.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.oracle_math_is_libm.restype = C.c_int
-        if lib.oracle_math_is_libm() != int(libm):
-            raise RuntimeError(f"{path}: oracle_math_is_libm() = {lib.oracle_math_is_libm()}, expected {int(libm)}")
-        _libs[libm] = lib
-    return _libs[libm]
+        lib.oracle_math_is_nocontract.restype = C.c_int
+        if lib.oracle_math_is_libm() != want_libm or lib.oracle_math_is_nocontract() != want_noc:
+            raise RuntimeError(f"{path}: oracle_math_is_libm/nocontract() = {lib.oracle_math_is_libm()}/{lib.oracle_math_is_nocontract()}, "
+                               f"expected {want_libm}/{want_noc}")
+        _libs[variant] = lib
+    return _libs[variant]
 
 
 class Oracle:
     """CPU restatement of the DDGI node; same inputs as the C-ABI."""
 
-    def __init__(self, desc: abi.ArkDdgiDesc, libm: bool = False):
-        self.lib = load(libm)
+    def __init__(self, desc: abi.ArkDdgiDesc, libm: bool = False, variant: str | None = None):
+        self.lib = load(libm, variant)
         self.desc = desc
         self.h = self.lib.oracle_create(C.byref(desc))
         if not self.h:

@@ -10,6 +10,12 @@ probeSampling.glsl:40,108,149, lighting.glsl:32-35 (IES atan/acos),
 probeUpdateOffset.comp:93 (exp2). Frame-local, at SURVEY §8(d)'s tolerances, with the
 flipped-ray accounting of tests/libm_parity.py. Each case prints its statistics
 (pytest -s; DESIGN.md §4 quotes them).
+
+VERDICT r05 "do this" #5: the same cases against the -DARK_ORACLE_NOCONTRACT oracle
+(every product and sum rounded separately, as SPIR-V NoContraction would give, where
+the default oracle fuses as the kernels do: dotFma, the probe update's accumulations,
+the cross and dot products of intersectTri) and against both freedoms at once
+(-DARK_ORACLE_LIBM -DARK_ORACLE_NOCONTRACT, the "witness" build).
 """
 import json
 
@@ -29,11 +35,15 @@ pytestmark = pytest.mark.gpu
 ST = (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS)
 
 
+VARIANTS = ["libm", "nocontract", "witness"]
+
+
 def _report(name, frame, st):
     """The full statistics, then one line with the clean-probe and all-probe atlas
     figures side by side (the all-probe ones include the probes with a
     flipped ray, where no tolerance is asserted)."""
     print(f"LIBM {name} frame {frame}: " + json.dumps(st), flush=True)
+    # name: "<case>[<variant>]"
     c, a = st["clean"], st["all"]
     print(f"LIBM-SUMMARY {name} frame {frame}: flipped {st['flipped_rays']}/{st['rays']} rays; "
           f"irradiance L-inf clean {c['irradiance']['linf']:.3g} / all {a['irradiance']['linf']:.3g}, "
@@ -42,15 +52,16 @@ def _report(name, frame, st):
           f"(probes clean {c['probes']} / all {a['probes']})", flush=True)
 
 
-def _whole_grid(name, sc, grid, cfg, frames, z_far, exposure):
+def _whole_grid(name, sc, grid, cfg, frames, z_far, exposure, variant="libm"):
     """Every frame: the libm oracle starts from the HIP context's state, both run the
     frame, the whole window is compared."""
     ctx = D.DDGIContext(grid, z_far, cfg)
     ctx.set_scene(sc)
-    orc = O.Oracle(ctx.desc, libm=True)
+    orc = O.Oracle(ctx.desc, variant=variant)
     orc.set_scene(sc, threads=16)
     N, R = grid.probe_count(), cfg.rays_per_probe
     first, flipped = 0, 0
+    name = f"{name}[{variant}]"
     for f in range(frames):
         for w in ST:
             orc.write(w, ctx.read(w))
@@ -73,14 +84,15 @@ def _whole_grid(name, sc, grid, cfg, frames, z_far, exposure):
     return flipped
 
 
-def test_cornell_c2_vs_libm_oracle():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_cornell_c2_vs_libm_oracle(variant):
     """C2: Cornell 8^3 x 64, the level's exposure, offsets off, 4 frames."""
     sc, ex = S.cornell_box()
     grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
     cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=False,
                        max_rays_per_probe=64, max_probe_updates=512)
     _whole_grid("C2", sc, grid, cfg, 4, ex["z_far"], dict(light_pre_exposure=ex["light_pre_exposure"],
-                                                           environment_brightness=ex["environment_brightness"]))
+                                                           environment_brightness=ex["environment_brightness"]), variant)
 
 
 # Drift bounds of the free-running C2 run (not SURVEY §8(d)'s one-frame tolerances,
@@ -130,7 +142,8 @@ def test_cornell_c2_free_running_drift():
         assert ulp >= DRIFT_WITHIN_1ULP, rows
 
 
-def test_features_scene_vs_libm_oracle():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_features_scene_vs_libm_oracle(variant):
     """Masked alpha test, translucent shadow-only geometry, mirrored instance,
     textures, sun + 2 IES spots (atan/acos LUT lookups), HDR environment, offsets on
     (exp2), 4 frames."""
@@ -138,10 +151,10 @@ def test_features_scene_vs_libm_oracle():
     grid = D.ProbeGrid((6, 4, 6), (0.7, 0.7, 0.7), (-1.75, 0.25, -1.75))
     cfg = D.DDGIConfig(rays_per_probe=128, probe_updates_per_frame=144, compute_probe_offsets=True,
                        max_rays_per_probe=128, max_probe_updates=144)
-    _whole_grid("features", sc, grid, cfg, 4, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05, environment_brightness=0.5))
+    _whole_grid("features", sc, grid, cfg, 4, 100.0, dict(light_pre_exposure=1.0, ambient_illuminance=0.05, environment_brightness=0.5), variant)
 
 
-def _windows_full_size(name, scene, dims, spacing, origin, R, z_far, exposure, windows):
+def _windows_full_size(name, scene, dims, spacing, origin, R, z_far, exposure, windows, variant="libm"):
     """The HIP path on the whole grid (K = N, as bench.py); the libm oracle on windows
     of 32 probes over every Z-slab: frame 0 from a reset oracle, frame 1 from the HIP
     path's frame-0 atlases and offsets (test_gpu_fullsize.py's method)."""
@@ -151,9 +164,10 @@ def _windows_full_size(name, scene, dims, spacing, origin, R, z_far, exposure, w
     ctx = D.DDGIContext(grid, z_far, cfg)
     ctx.set_scene(scene)
     ocfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=32, max_rays_per_probe=R, max_probe_updates=32, compute_probe_offsets=True)
-    orc = O.Oracle(D.desc_for(grid, z_far, ocfg), libm=True)
+    orc = O.Oracle(D.desc_for(grid, z_far, ocfg), variant=variant)
     orc.set_scene(scene, threads=16)
     start = None
+    name = f"{name}[{variant}]"
     for frame in range(2):
         p = D.frame_params(cfg, grid, D.AppState(frame), 0, **exposure)
         ctx.update(p)
@@ -188,18 +202,20 @@ def _windows_full_size(name, scene, dims, spacing, origin, R, z_far, exposure, w
     orc.close()
 
 
-def test_c4_full_size_vs_libm_oracle():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_c4_full_size_vs_libm_oracle(variant):
     """C4 as bench.py runs it: 10 M triangles, 32^3 x 256, sun, offsets on; 8 windows
     of 32 probes (one x row per Z-slab of 4), frames 0 and 1."""
     dims = (32, 32, 32)
     _windows_full_size("C4", S.soup(10_000_000), dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), 256, 10000.0,
-                       dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), _windows(dims, 8))
+                       dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), _windows(dims, 8), variant)
 
 
-def test_c5_substitute_full_size_vs_libm_oracle():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_c5_substitute_full_size_vs_libm_oracle(variant):
     """C5 substitute: the instanced city block (~3 M triangles), 48x16x48 x 512, sun +
     4 IES spot lights (the IES LUT's atan/acos on every lit spot sample); 8 windows of
     32 probes over every Z-slab, frames 0 and 1."""
     dims = (48, 16, 48)
     _windows_full_size("C5", S.city_block(), dims, (5.0, 2.5, 5.0), (2.5, 0.5, 2.5), 512, 1000.0,
-                       dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), _windows(dims, 8))
+                       dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0), _windows(dims, 8), variant)
