@@ -449,6 +449,7 @@ EXPORTS = {
     "ark_ddgi_share_scene": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ark_ddgi_set_lights": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ark_ddgi_set_instances": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "ark_ddgi_set_instances_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "ark_ddgi_mark_external_write": (C.c_int, [C.c_void_p]),
     "ark_ddgi_get_next_probe_index": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "ark_ddgi_update": (C.c_int, [C.c_void_p, C.POINTER(ArkDdgiFrameParams), C.c_void_p]),

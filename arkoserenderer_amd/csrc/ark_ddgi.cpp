@@ -130,29 +130,105 @@ void sampleTraversalOrder(uint32_t R, std::vector<uint32_t>& order)
 
 } // namespace
 
+// The nodes of a BVH8 by depth, deepest first (a node's internal children are one level
+// deeper): the refit's launch order, order[offsets[i] .. offsets[i + 1]) one level.
+static bool bvhLevelOrder(const GpuBvh8Node* h, uint64_t n, const int32_t* roots, int nRoots, std::vector<uint32_t>& order, std::vector<uint32_t>& offsets)
+{
+    std::vector<std::vector<uint32_t>> byDepth;
+    std::vector<std::pair<uint32_t, uint32_t>> work; // (node, depth)
+    for (int r = 0; r < nRoots; ++r)
+        if (roots[r] >= 0) work.push_back({ static_cast<uint32_t>(roots[r]), 0u });
+    while (!work.empty()) {
+        const auto [node, d] = work.back();
+        work.pop_back();
+        if (node >= n) return false;
+        if (byDepth.size() <= d) byDepth.resize(d + 1);
+        byDepth[d].push_back(node);
+        const uint32_t internal = static_cast<uint32_t>(__builtin_popcount(h[node].imask));
+        for (uint32_t k = 0; k < internal; ++k) work.push_back({ h[node].child_base + k, d + 1 });
+    }
+    order.clear();
+    order.reserve(n);
+    offsets.assign(1, 0u);
+    for (size_t d = byDepth.size(); d-- > 0;) {
+        std::sort(byDepth[d].begin(), byDepth[d].end());
+        order.insert(order.end(), byDepth[d].begin(), byDepth[d].end());
+        offsets.push_back(static_cast<uint32_t>(order.size()));
+    }
+    return true;
+}
+
 // The scene of a context on the device (ark_ddgi_set_scene): BVH nodes + triangles,
 // shading records, RT mesh data, materials, textures, lights. Reference-counted:
 // ark_ddgi_share_scene lets the Z-slab contexts of one GPU use one copy.
 // A background rebuild of the sun's light-space BVH (sunRebuildStep): a host thread
-// downloads the world BVHs' triangle records, builds the BVH for `dir` and uploads it
+// waits for a device snapshot of the world BVHs' triangle records (taken in stream
+// order behind the refits, `snap` / `evSnap`), builds the BVH for `dir` and uploads it
 // into `buf`; `done` set last (release).
 struct SunJob {
     std::thread t;
     std::atomic<bool> done { false };
     float dir[3] {};
-    uint32_t version = 0; // SceneStore::version when started (a refit since: discarded)
+    uint32_t version = 0; // SceneStore::version of the snapshot
+    uint32_t refitsAt = 0; // SceneStore::refitCount of the snapshot (later refits: refitted forward at install)
+    DeviceBuffer snap;    // the records it builds from
+    hipEvent_t evSnap = nullptr;
     DeviceBuffer buf;     // nodes, then the triangle records at triOffset
     size_t triOffset = 0;
-    uint64_t nodes = 0;
+    uint64_t nodes = 0, triRecords = 0;
     uint32_t depth = 0;
     float frame[9] {};
+    double frameD[9] {};
+    float inflateAbs = 0.0f;
+    std::vector<uint32_t> levelOrder, levelOffsets;
     float ms = 0.0f;
     bool ok = false;
     ~SunJob()
     {
         if (t.joinable()) t.join();
         buf.release(); // not installed (an installed buffer was moved to the scene)
+        snap.release();
+        if (evSnap) (void)hipEventDestroy(evSnap);
     }
+};
+
+// A background rebuild of the world BVHs after refits (worldRebuildStep; the reference
+// rebuilds its TLAS in full every 60 frames, GpuScene.cpp:998-1010): a host thread takes
+// a device snapshot of the refitted triangle records, builds the three hit-mask classes'
+// BVHs anew from them (set_scene's builder), keeps every record's words as they were
+// (so hits stay bit-identical) and uploads nodes + records, the new record order's
+// source indices (perm, for the shading records) and the refit's level order.
+struct WorldJob {
+    std::thread t;
+    std::atomic<bool> done { false };
+    uint32_t version = 0, refitsAt = 0;
+    DeviceBuffer snap;
+    hipEvent_t evSnap = nullptr;
+    uint64_t snapRecords = 0;
+    std::vector<int> classOf; // instance -> hit-mask class (0 opaque, 1 masked, 2 blend)
+    DeviceBuffer buf, perm, order;
+    size_t triOffset = 0;
+    uint64_t nodes = 0, triRecords = 0, triangles = 0;
+    int32_t roots[3] { -1, -1, -1 };
+    uint32_t opaqueNodes = 0, depth = 0, maxLeaf = 0;
+    float sah = 0.0f;
+    std::vector<uint32_t> levelOffsets;
+    float ms = 0.0f;
+    bool ok = false;
+    std::string error;
+    ~WorldJob()
+    {
+        if (t.joinable()) t.join();
+        for (DeviceBuffer* b : { &buf, &perm, &order, &snap }) b->release();
+        if (evSnap) (void)hipEventDestroy(evSnap);
+    }
+};
+
+// A buffer replaced while launches enqueued before may still read it: freed once `done`
+// (recorded behind them) has completed.
+struct Retired {
+    DeviceBuffer buf;
+    hipEvent_t done = nullptr;
 };
 
 struct SceneStore {
@@ -172,16 +248,30 @@ struct SceneStore {
     std::vector<GpuSpotLight> spotsScene;
     ArkDdgiBvhStats bvhStats {};
     uint32_t bvhMaxDepth = 0; // deepest of the world BVHs and the sun's (traversal spill)
-    float boundsLo[3] { 0, 0, 0 }, boundsHi[3] { 0, 0, 0 }; // world AABB of all triangles
-    // ark_ddgi_set_instances: bumped by every refit (a sharing context re-derives its
-    // SceneArgs); the builder's absolute inflation; the refit's buffers, built on first use
+    uint32_t worldDepth = 0, sunDepth = 0;
+    // ark_ddgi_set_instances: bumped by every refit and install (a sharing context
+    // re-derives its SceneArgs); the builder's absolute inflation; the refit's buffers
     uint32_t version = 0;
     float inflateAbs = 0.0f;
     uint64_t triRecords = 0; // triangle records of the world BVHs (holes included)
     DeviceBuffer refitInst, refitBoxes, refitOrder, refitBounds;
     std::vector<uint32_t> levelOffsets; // refitOrder[levelOffsets[i] .. [i + 1]): the nodes of one depth, deepest first
+    // the light-space BVH follows the motion: refitted with the world BVHs (its records
+    // re-transformed, its boxes of their light coordinates)
+    DeviceBuffer sunRefitOrder, sunRefitBoxes;
+    std::vector<uint32_t> sunLevelOffsets;
+    uint64_t sunTriRecords = 0;
+    float sunInflateAbs = 0.0f;
+    double sunFrameD[9] {};
+    // the refit's transforms: the last ones uploaded (dirty = changed since the records
+    // were written); pinned staging of the stream-ordered uploads, two sets in turn
+    std::vector<RefitInstance> refitHost;
+    void* stage[2] { nullptr, nullptr };
+    size_t stageBytes[2] { 0, 0 };
+    hipEvent_t stageDone[2] { nullptr, nullptr };
+    int stageNext = 0;
     // the light-space BVH follows the sun: set_scene chose it (sunWanted), and after a
-    // sun-direction change or a refit it is rebuilt in the background (sunRebuildStep)
+    // sun-direction change it is rebuilt in the background (sunRebuildStep)
     bool sunWanted = false;
     int buildThreads = 16;
     std::unique_ptr<SunJob> sunJob;
@@ -197,15 +287,31 @@ struct SceneStore {
     float sunFailedDir[3] { 0, 0, 0 };
     uint32_t sunFailedVersion = 0;
     uint32_t sunFailures = 0;
+    // the world BVHs' background rebuild (worldRebuildStep): refits since the installed
+    // BVHs were built, the running job, rebuilds installed
+    uint32_t refitsSinceBuild = 0, sunRefitsSinceBuild = 0;
+    std::unique_ptr<WorldJob> worldJob;
+    uint32_t worldRebuilds = 0, refitCount = 0;
+    std::vector<Retired> retired;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
     SceneStore& operator=(const SceneStore&) = delete;
     ~SceneStore()
     {
         (void)hipSetDevice(device);
-        sunJob.reset(); // joins it: the job reads the triangle records freed below
+        sunJob.reset(); // joins them: the jobs read snapshots freed below
+        worldJob.reset();
+        (void)hipDeviceSynchronize();
+        for (Retired& r : retired) {
+            r.buf.release();
+            if (r.done) (void)hipEventDestroy(r.done);
+        }
+        for (int i = 0; i < 2; ++i) {
+            if (stage[i]) (void)hipHostFree(stage[i]);
+            if (stageDone[i]) (void)hipEventDestroy(stageDone[i]);
+        }
         for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
-                                 &refitBoxes, &refitOrder, &refitBounds })
+                                 &refitBoxes, &refitOrder, &refitBounds, &sunRefitOrder, &sunRefitBoxes })
             b->release();
     }
 };
@@ -318,6 +424,10 @@ struct ArkDdgiCtx {
     uint64_t lastRays = 0, lastProbes = 0;
     uint32_t nextProbeIndex = 0; // (first + K) % N of the last update, or of a loaded state
     uint32_t lastFirst = 0, lastK = 0; // the last update's window (ark_ddgi_window_exchange_info)
+    // a refit or an installed rebuild enqueued on a caller's stream (ark_ddgi_set_instances_async,
+    // worldRebuildStep): the next update's traversal on the traversal stream waits for it
+    hipEvent_t evRefit = nullptr;
+    bool refitPending = false;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -559,17 +669,151 @@ hipError_t drainContext(ArkDdgiCtx* ctx)
     return e;
 }
 
-// The background rebuild's thread: the world records from the device, the light-space
-// BVH of job->dir on the host (as set_scene builds it, from the same records), the
-// result uploaded into job->buf on a stream of its own.
-void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t count, int threads)
+// --- scene maintenance: stream-ordered refits, background rebuilds ------------------
+
+// A buffer the launches enqueued so far on `s` (and, through orderBegin, everything the
+// context enqueued before) may read: freed by collectRetired once they are done.
+hipError_t retireBuffer(SceneStore& st, DeviceBuffer& b, hipStream_t s)
+{
+    if (!b.ptr) return hipSuccess;
+    Retired r;
+    hipError_t e = hipEventCreateWithFlags(&r.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(r.done, s);
+    if (e != hipSuccess) {
+        if (r.done) (void)hipEventDestroy(r.done);
+        (void)hipStreamSynchronize(s); // cannot defer: wait, then free
+        b.release();
+        return e;
+    }
+    r.buf = b;
+    b = DeviceBuffer {};
+    st.retired.push_back(r);
+    return hipSuccess;
+}
+
+void collectRetired(SceneStore& st)
+{
+    for (size_t i = 0; i < st.retired.size();) {
+        Retired& r = st.retired[i];
+        if (hipEventQuery(r.done) == hipSuccess) {
+            r.buf.release();
+            (void)hipEventDestroy(r.done);
+            st.retired[i] = st.retired.back();
+            st.retired.pop_back();
+        } else {
+            ++i;
+        }
+    }
+}
+
+// `bytes` of host data into `dst` in stream order on `s`, through the store's pinned
+// staging (two sets in turn; a set is reused once its previous copy has run).
+hipError_t stagedUpload(SceneStore& st, void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+    if (bytes == 0) return hipSuccess;
+    const int i = st.stageNext;
+    st.stageNext ^= 1;
+    hipError_t e = hipSuccess;
+    if (!st.stageDone[i] && (e = hipEventCreateWithFlags(&st.stageDone[i], hipEventDisableTiming)) != hipSuccess) return e;
+    if (st.stageBytes[i]) (void)hipEventSynchronize(st.stageDone[i]); // its last copy (an earlier frame's) has run
+    if (st.stageBytes[i] < bytes) {
+        if (st.stage[i]) (void)hipHostFree(st.stage[i]);
+        st.stage[i] = nullptr;
+        st.stageBytes[i] = 0;
+        if ((e = hipHostMalloc(&st.stage[i], bytes, hipHostMallocDefault)) != hipSuccess) return e;
+        st.stageBytes[i] = bytes;
+    }
+    std::memcpy(st.stage[i], src, bytes);
+    if ((e = hipMemcpyAsync(dst, st.stage[i], bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    return hipEventRecord(st.stageDone[i], s);
+}
+
+// The refit of every BVH of the scene on `s`: the records of dirty instances re-transformed
+// (st.refitInst), the world BVHs' boxes level by level, and the light-space sun BVH's
+// records and light-space boxes. Inflations from the device-side bounds.
+int enqueueRefit(ArkDdgiCtx* ctx, SceneStore& st, hipStream_t s)
+{
+    uint32_t* bounds = st.refitBounds.as<uint32_t>();
+    ARK_HIP(launch_refit_bounds_reset(bounds, s));
+    GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(static_cast<char*>(st.nodes.ptr) + st.args.tri_byte_offset);
+    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(),
+                              bounds, s));
+    RefitBoxArgs world {};
+    world.inflate_min = st.inflateAbs;
+    world.light = 0;
+    const uint32_t* order = st.refitOrder.as<uint32_t>();
+    for (size_t l = 0; l + 1 < st.levelOffsets.size(); ++l)
+        ARK_HIP(launch_refit_nodes(st.nodes.as<GpuBvh8Node>(), tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l], st.levelOffsets[l + 1] - st.levelOffsets[l],
+                                   world, bounds, s));
+    if (st.sunArgs.sun_root >= 0 && st.sunTriRecords && !st.sunLevelOffsets.empty()) {
+        GpuTriangle* stris = const_cast<GpuTriangle*>(st.sunArgs.sun_tris);
+        ARK_HIP(launch_refit_tris(stris, static_cast<uint32_t>(st.sunTriRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(),
+                                  st.positions.as<float>(), bounds, s));
+        RefitBoxArgs light {};
+        std::memcpy(light.frame, st.sunFrameD, sizeof(light.frame));
+        light.inflate_min = st.sunInflateAbs;
+        light.light = 1;
+        ARK_HIP(launch_refit_light_bounds(stris, static_cast<uint32_t>(st.sunTriRecords), light, bounds, s));
+        const uint32_t* so = st.sunRefitOrder.as<uint32_t>();
+        for (size_t l = 0; l + 1 < st.sunLevelOffsets.size(); ++l)
+            ARK_HIP(launch_refit_nodes(const_cast<GpuBvh8Node*>(st.sunArgs.sun_nodes), stris, st.sunRefitBoxes.as<float>(), so + st.sunLevelOffsets[l],
+                                       st.sunLevelOffsets[l + 1] - st.sunLevelOffsets[l], light, bounds, s));
+    }
+    return ARK_DDGI_OK;
+}
+
+// The refit's transforms of `instances` on the device (stream-ordered), every one dirty
+// (allDirty: the records are of an older version, an installed rebuild) or those whose
+// transform changed since the last upload.
+int uploadRefitInstances(ArkDdgiCtx* ctx, SceneStore& st, const ArkRTInstance* instances, uint32_t count, bool allDirty, hipStream_t s)
+{
+    if (st.refitHost.size() != count) {
+        st.refitHost.assign(count, RefitInstance {});
+        allDirty = true;
+    }
+    if (!st.refitInst.ptr || st.refitInst.bytes < std::max<size_t>(16, count * sizeof(RefitInstance))) ARK_HIP(st.refitInst.alloc(std::max<size_t>(16, count * sizeof(RefitInstance))));
+    if (!st.refitBounds.ptr) ARK_HIP(st.refitBounds.alloc(kRefitBoundsWords * sizeof(uint32_t)));
+    for (uint32_t ii = 0; ii < count; ++ii) {
+        const float* M = instances[ii].object_to_world;
+        const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
+        const ArkRTTriangleMesh& mesh = st.meshHost[instances[ii].rt_mesh_index];
+        RefitInstance& q = st.refitHost[ii];
+        const bool moved = allDirty || std::memcmp(q.m, M, sizeof(q.m)) != 0;
+        std::memcpy(q.m, M, sizeof(q.m));
+        q.first_vertex = mesh.first_vertex;
+        q.first_index = static_cast<uint32_t>(mesh.first_index);
+        q.flip = det < 0.0f ? 1u : 0u;
+        q.dirty = moved ? 1u : 0u;
+    }
+    ARK_HIP(stagedUpload(st, st.refitInst.ptr, st.refitHost.data(), count * sizeof(RefitInstance), s));
+    return ARK_DDGI_OK;
+}
+
+// Background builds' host-thread inputs: a snapshot of the world records on `s` behind
+// every refit enqueued so far (the refits run on the callers' streams; a thread reading
+// the live records could see a half-refitted set).
+hipError_t snapshotRecords(SceneStore& st, DeviceBuffer& snap, hipEvent_t& ev, hipStream_t s)
+{
+    const size_t bytes = st.triRecords * sizeof(GpuTriangle);
+    hipError_t e = snap.alloc(std::max<size_t>(bytes, 16));
+    if (e == hipSuccess && bytes)
+        e = hipMemcpyAsync(snap.ptr, static_cast<const char*>(st.nodes.ptr) + st.args.tri_byte_offset, bytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess && !ev) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, s);
+    return e;
+}
+
+// The sun rebuild's thread: the snapshot of the world records, the light-space BVH of
+// job->dir on the host (as set_scene builds it), uploaded into job->buf.
+void runSunJob(SunJob* job, int device, uint64_t count, int threads)
 {
     const auto t0 = std::chrono::steady_clock::now();
     bool ok = hipSetDevice(device) == hipSuccess;
     hipStream_t s = nullptr;
     ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventSynchronize(job->evSnap) == hipSuccess;
     std::vector<GpuTriangle> rec(ok ? count : 0);
-    ok = ok && hipMemcpyAsync(rec.data(), records, count * sizeof(GpuTriangle), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    ok = ok && hipMemcpyAsync(rec.data(), job->snap.ptr, count * sizeof(GpuTriangle), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
     Bvh8BuildResult r;
     if (ok) {
         SunBvhInput in;
@@ -582,11 +826,18 @@ void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t cou
         copt.threads = threads;
         ok = build_sun_bvh(in, opt, copt, r) && !r.nodes.empty();
         for (int i = 0; i < 3; ++i)
-            for (int k = 0; k < 3; ++k) job->frame[i * 3 + k] = static_cast<float>(in.frame[i][k]);
+            for (int k = 0; k < 3; ++k) {
+                job->frame[i * 3 + k] = static_cast<float>(in.frame[i][k]);
+                job->frameD[i * 3 + k] = in.frame[i][k];
+            }
+        job->inflateAbs = in.inflateAbs;
+        const int32_t root = 0;
+        ok = ok && bvhLevelOrder(r.nodes.data(), r.nodes.size(), &root, 1, job->levelOrder, job->levelOffsets);
     }
     if (ok) {
         const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
         job->triOffset = (nb + 255) & ~static_cast<size_t>(255);
+        job->triRecords = r.tris.size();
         r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
         ok = job->buf.alloc(job->triOffset + r.tris.size() * sizeof(GpuTriangle)) == hipSuccess &&
              hipMemcpyAsync(job->buf.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice, s) == hipSuccess &&
@@ -601,15 +852,192 @@ void runSunJob(SunJob* job, int device, const GpuTriangle* records, uint64_t cou
     job->done.store(true, std::memory_order_release);
 }
 
+// Structural check of a BVH8 before anything reaches the GPU: every node is
+// referenced once from a root-reachable parent (no cycles, no sharing), every leaf's
+// triangles lie inside the triangle array and every triangle (every record but the
+// holes of the rows) is covered once.
+bool checkBvh8Structure(const std::vector<GpuBvh8Node>& allNodes, const std::vector<GpuTriangle>& allTris, const int32_t* roots, int nRoots, std::string& why)
+{
+    char buf[128];
+    auto bad = [&](const char* fmt, uint64_t v) {
+        std::snprintf(buf, sizeof(buf), fmt, static_cast<unsigned long long>(v));
+        why = buf;
+        return false;
+    };
+    std::vector<uint8_t> seenNode(allNodes.size(), 0);
+    std::vector<uint8_t> seenTri(allTris.size(), 0);
+    std::vector<uint32_t> work;
+    for (int c = 0; c < nRoots; ++c)
+        if (roots[c] >= 0) work.push_back(static_cast<uint32_t>(roots[c]));
+    while (!work.empty()) {
+        const uint32_t n = work.back();
+        work.pop_back();
+        if (n >= allNodes.size() || seenNode[n]) return bad("BVH invalid: node %llu", n);
+        seenNode[n] = 1;
+        const GpuBvh8Node& nd = allNodes[n];
+        uint32_t internal = 0;
+        if ((nd.leaf_tris >> 24) || (nd.leaf_mask & nd.imask)) return bad("BVH invalid: node %llu leaf rows", n);
+        for (int sl = 0; sl < 8; ++sl) {
+            const bool isInternal = (nd.imask >> sl) & 1u;
+            uint32_t slotTris[kBvh8MaxLeafSize];
+            const int cnt = bvh8SlotTriangles(nd, sl, slotTris);
+            if (cnt < 0) return bad("BVH invalid: node %llu slot", n);
+            if (isInternal) work.push_back(nd.child_base + internal++);
+            for (int i = 0; i < cnt; ++i) {
+                const uint32_t t = slotTris[i];
+                if (t >= allTris.size() || isHoleTriangle(allTris[t])) return bad("BVH invalid: leaf range%.0llu", 0);
+                if (seenTri[t]) return bad("BVH invalid: triangle %llu in two leaves", t);
+                seenTri[t] = 1;
+            }
+            for (int a = 0; a < 3; ++a)
+                if ((isInternal || cnt > 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return bad("BVH invalid: child box%.0llu", 0);
+        }
+    }
+    for (size_t t = 0; t < seenTri.size(); ++t)
+        if (!seenTri[t] && !isHoleTriangle(allTris[t])) return bad("BVH invalid: triangle %llu unreachable", t);
+    return true;
+}
+
+
+// The world rebuild's thread: the three classes' BVHs from the snapshot's records (their
+// vertices v0, v0 + e1, v0 + e2; each leaf record then replaced by its source record,
+// bit for bit), the record order's source indices and the refit's level order.
+void runWorldJob(WorldJob* job, int device, int threads)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    bool ok = hipSetDevice(device) == hipSuccess;
+    hipStream_t s = nullptr;
+    ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventSynchronize(job->evSnap) == hipSuccess;
+    std::vector<GpuTriangle> rec(ok ? job->snapRecords : 0);
+    ok = ok && hipMemcpyAsync(rec.data(), job->snap.ptr, rec.size() * sizeof(GpuTriangle), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    if (!ok) job->error = "snapshot download failed";
+    std::vector<BuildTriangle> cls[3];
+    if (ok) {
+        for (size_t i = 0; i < rec.size(); ++i) {
+            const GpuTriangle& g = rec[i];
+            if (isHoleTriangle(g)) continue;
+            uint32_t inst, flip;
+            std::memcpy(&inst, &g.t2[1], 4);
+            std::memcpy(&flip, &g.t2[3], 4);
+            if (inst >= job->classOf.size()) {
+                ok = false;
+                job->error = "record of an unknown instance";
+                break;
+            }
+            BuildTriangle t;
+            const float e1[3] = { g.t0[3], g.t1[0], g.t1[1] }, e2[3] = { g.t1[2], g.t1[3], g.t2[0] };
+            for (int a = 0; a < 3; ++a) {
+                t.v0[a] = g.t0[a];
+                t.v1[a] = g.t0[a] + e1[a];
+                t.v2[a] = g.t0[a] + e2[a];
+            }
+            t.instance = inst;
+            t.primitive = static_cast<uint32_t>(i); // the source record (replaced below)
+            t.flip_facing = flip;
+            cls[job->classOf[inst]].push_back(t);
+        }
+    }
+    std::vector<GpuBvh8Node> allNodes;
+    std::vector<GpuTriangle> allTris;
+    if (ok) {
+        BvhBuildOptions opt;
+        opt.max_leaf_size = kBvh8MaxLeafSize;
+        opt.threads = threads;
+        {
+            float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+            for (int c = 0; c < 3; ++c)
+                for (const BuildTriangle& t : cls[c])
+                    for (const float* v : { t.v0, t.v1, t.v2 })
+                        for (int a = 0; a < 3; ++a) {
+                            lo[a] = std::min(lo[a], v[a]);
+                            hi[a] = std::max(hi[a], v[a]);
+                        }
+            opt.inflate_abs = bvh8_inflation_box(lo, hi);
+        }
+        Bvh8CollapseOptions copt;
+        copt.threads = threads;
+        for (int c = 0; c < 3 && ok; ++c) {
+            if (cls[c].empty()) continue;
+            BvhBuildResult r2 = build_bvh(cls[c], opt, 0u, 0u);
+            std::vector<BuildTriangle>().swap(cls[c]);
+            if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) {
+                ok = false;
+                job->error = "BVH2 leaf over the leaf size";
+                break;
+            }
+            if (c == 0) job->sah = r2.sah_cost;
+            job->maxLeaf = std::max(job->maxLeaf, r2.max_leaf);
+            Bvh8BuildResult r = collapse_bvh8(r2, static_cast<uint32_t>(allNodes.size()), static_cast<uint32_t>(allTris.size()), copt);
+            job->roots[c] = static_cast<int32_t>(allNodes.size());
+            if (c == 0) job->opaqueNodes = static_cast<uint32_t>(r.nodes.size());
+            job->depth = std::max(job->depth, r.max_depth);
+            job->triangles += r.triangles;
+            allNodes.insert(allNodes.end(), r.nodes.begin(), r.nodes.end());
+            allTris.insert(allTris.end(), r.tris.begin(), r.tris.end());
+        }
+    }
+    std::vector<uint32_t> perm;
+    if (ok) {
+        perm.assign(allTris.size(), 0xffffffffu);
+        for (size_t i = 0; i < allTris.size(); ++i) {
+            GpuTriangle& g = allTris[i];
+            if (isHoleTriangle(g)) continue;
+            uint32_t src;
+            std::memcpy(&src, &g.t2[2], 4);
+            perm[i] = src;
+            g = rec[src];
+        }
+        ok = checkBvh8Structure(allNodes, allTris, job->roots, 3, job->error);
+    }
+    std::vector<uint32_t> order;
+    ok = ok && bvhLevelOrder(allNodes.data(), allNodes.size(), job->roots, 3, order, job->levelOffsets);
+    if (ok) {
+        const size_t nb = allNodes.size() * sizeof(GpuBvh8Node);
+        job->triOffset = (nb + 255) & ~static_cast<size_t>(255);
+        job->triRecords = allTris.size();
+        job->nodes = allNodes.size();
+        allTris.push_back(GpuTriangle {}); // padding record (five-load fetch)
+        ok = job->triOffset + allTris.size() * sizeof(GpuTriangle) < (1ull << 32) &&
+             job->buf.alloc(job->triOffset + allTris.size() * sizeof(GpuTriangle)) == hipSuccess &&
+             job->perm.alloc(std::max<size_t>(16, perm.size() * 4)) == hipSuccess && job->order.alloc(std::max<size_t>(16, order.size() * 4)) == hipSuccess &&
+             hipMemcpyAsync(job->buf.ptr, allNodes.data(), nb, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(static_cast<char*>(job->buf.ptr) + job->triOffset, allTris.data(), allTris.size() * sizeof(GpuTriangle), hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(job->perm.ptr, perm.data(), perm.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(job->order.ptr, order.data(), order.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+        if (!ok && job->error.empty()) job->error = "upload failed";
+    }
+    if (s) (void)hipStreamDestroy(s);
+    job->ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    job->ok = ok;
+    job->done.store(true, std::memory_order_release);
+}
+
+// Frames in flight may read what an install replaces: a shared scene waits for the
+// device (every context's work); otherwise the caller's stream `s` waits for the
+// context's earlier operations (orderBegin) and the old buffers are retired behind it.
+hipError_t installBarrier(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (ctx->sceneStore.use_count() > 1) return hipDeviceSynchronize();
+    return orderBegin(ctx, s);
+}
+
+// The end of a refit or an install on `s`: with a shared scene the other contexts'
+// next traversals do not wait for this context's streams, so the work completes here.
+hipError_t installDone(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (ctx->sceneStore.use_count() > 1) return hipStreamSynchronize(s);
+    return hipSuccess;
+}
+
 // The light-space sun BVH follows the context's sun (called by every update and by
-// set_lights / set_instances): a finished rebuild is installed - once the frames that
-// may read the old one are done, and only if no refit came in between - and a new one
-// is started when the scene chose the light-space BVH at set_scene but holds none for
-// this direction (a direction change, or a refit dropped it). Until it is installed the
-// sun's shadow rays traverse the world BVHs (deriveSceneArgs), with the same results.
-// One rebuild at a time per scene; with contexts that share a scene under different
-// suns, the scene follows the context that asked last.
-int sunRebuildStep(ArkDdgiCtx* ctx)
+// set_lights / set_instances, on the stream `s` of the call): a finished rebuild for
+// this context's sun is installed - stream-ordered behind the frames that may read the
+// old one, and refitted forward when refits came in between - and a new one is started
+// when the scene chose the light-space BVH at set_scene but holds none for this
+// direction. Until it is installed the sun's shadow rays traverse the world BVHs
+// (deriveSceneArgs), with the same results. One rebuild at a time per scene.
+int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
 {
     SceneStore& st = *ctx->sceneStore;
     auto sameDir = [](const float* a, const float* b) { return std::memcmp(a, b, 3 * sizeof(float)) == 0; };
@@ -631,46 +1059,161 @@ int sunRebuildStep(ArkDdgiCtx* ctx)
             st.bvhStats.sun_rebuild_failures = ++st.sunFailures;
             j.t.join();
             st.sunJob.reset();
-        } else if (j.version != st.version || (st.sunReqStreak >= 2 && !sameDir(j.dir, st.sunReqDir))) {
-            // stale: a refit came in between, or the scene's contexts settled on another sun
+        } else if (st.sunReqStreak >= 2 && !sameDir(j.dir, st.sunReqDir)) {
+            // stale: the scene's contexts settled on another sun
             j.t.join();
             st.sunJob.reset();
         } else if (ctx->hasSun && sameDir(j.dir, ctx->sunDir)) {
             std::unique_ptr<SunJob> job = std::move(st.sunJob);
             job->t.join();
-            // frames in flight may traverse the old one (any context, when shared)
-            if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
-            else ARK_HIP(drainContext(ctx));
-            st.sunNodes.release();
+            ARK_HIP(installBarrier(ctx, s));
+            ARK_HIP(retireBuffer(st, st.sunNodes, s));
+            ARK_HIP(retireBuffer(st, st.sunRefitOrder, s));
             st.sunNodes = job->buf;
             job->buf = DeviceBuffer {};
             st.sunArgs.sun_nodes = st.sunNodes.as<GpuBvh8Node>();
             st.sunArgs.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.sunNodes.ptr) + job->triOffset);
             st.sunArgs.sun_root = 0;
             std::memcpy(st.sunArgs.sun_frame, job->frame, sizeof(job->frame));
+            std::memcpy(st.sunFrameD, job->frameD, sizeof(job->frameD));
             std::memcpy(st.sunDirBuilt, job->dir, sizeof(job->dir));
+            st.sunInflateAbs = job->inflateAbs;
+            st.sunTriRecords = job->triRecords;
+            st.sunLevelOffsets = job->levelOffsets;
+            ARK_HIP(st.sunRefitOrder.alloc(std::max<size_t>(16, job->levelOrder.size() * 4)));
+            ARK_HIP(hipMemcpy(st.sunRefitOrder.ptr, job->levelOrder.data(), job->levelOrder.size() * 4, hipMemcpyHostToDevice));
+            if (st.sunRefitBoxes.bytes < job->nodes * 6 * sizeof(float)) {
+                ARK_HIP(retireBuffer(st, st.sunRefitBoxes, s));
+                ARK_HIP(st.sunRefitBoxes.alloc(std::max<size_t>(16, job->nodes * 6 * sizeof(float) * 5 / 4)));
+            }
             st.sunBvhNodes = job->nodes;
+            st.sunDepth = job->depth;
             st.bvhMaxDepth = std::max(st.bvhMaxDepth, job->depth);
             st.bvhStats.max_depth = st.bvhMaxDepth;
             st.bvhStats.sun_node_count = job->nodes;
             st.bvhStats.sun_max_depth = job->depth;
             st.bvhStats.sun_rebuilds = ++st.sunRebuilds;
             st.bvhStats.sun_build_ms = job->ms;
+            st.sunRefitsSinceBuild = st.refitCount - job->refitsAt;
+            if (st.sunRefitsSinceBuild) {
+                // refits came in while it was built: its records follow them (every
+                // instance re-transformed, the light-space boxes refitted)
+                if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), true, s)) return rc;
+                if (const int rc = enqueueRefit(ctx, st, s)) return rc;
+            }
+            ARK_HIP(retireBuffer(st, job->snap, s));
+            ARK_HIP(hipEventRecord(ctx->evRefit, s));
+            ARK_HIP(installDone(ctx, s));
+            ctx->refitPending = true;
             ++st.version;
             if (const int rc = refreshScene(ctx)) return rc;
         }
         // else: built for another context's sun; that context installs it
     }
     if (!st.sunWanted || !ctx->hasSun || st.sunJob || st.sunReqStreak < 2 || !sameDir(st.sunReqDir, ctx->sunDir)) return ARK_DDGI_OK;
-    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt)) return ARK_DDGI_OK;
+    // installed for this sun and not loosened by refits since it was built: nothing to do
+    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt) && st.sunRefitsSinceBuild == 0) return ARK_DDGI_OK;
     if (st.sunFailed && st.sunFailedVersion == st.version && sameDir(st.sunFailedDir, ctx->sunDir)) return ARK_DDGI_OK;
     auto job = std::make_unique<SunJob>();
     std::memcpy(job->dir, ctx->sunDir, sizeof(job->dir));
     job->version = st.version;
-    const GpuTriangle* records = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.nodes.ptr) + st.args.tri_byte_offset);
-    job->t = std::thread(runSunJob, job.get(), st.device, records, st.triRecords, st.buildThreads);
+    job->refitsAt = st.refitCount;
+    ARK_HIP(orderBegin(ctx, s));
+    ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
+    job->t = std::thread(runSunJob, job.get(), st.device, st.triRecords, st.buildThreads);
     st.sunJob = std::move(job);
     return ARK_DDGI_OK;
+}
+
+// The world BVHs' background rebuild after refits (the reference's full TLAS build every
+// 60 frames restores tightness, GpuScene.cpp:998-1010; a refit keeps the old topology,
+// whose boxes loosen as instances move): a finished rebuild is installed on `s` -
+// behind the frames that may read the old BVHs, its shading records gathered into its
+// record order, and refitted forward when refits came in while it was built - and,
+// while refits have loosened the installed one, a new one is started.
+int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    SceneStore& st = *ctx->sceneStore;
+    if (st.worldJob && st.worldJob->done.load(std::memory_order_acquire)) {
+        std::unique_ptr<WorldJob> job = std::move(st.worldJob);
+        job->t.join();
+        if (!job->ok) return ctx->fail(ARK_DDGI_E_DEVICE, "background BVH rebuild failed: %s", job->error.c_str());
+        ARK_HIP(installBarrier(ctx, s));
+        // the shading records in the new record order (before the old ones are retired)
+        DeviceBuffer tn;
+        ARK_HIP(tn.alloc(std::max<size_t>(64, job->triRecords * 64)));
+        ARK_HIP(launch_gather_records(tn.as<float4>(), st.triNormals.as<float4>(), job->perm.as<uint32_t>(), job->triRecords, s));
+        ARK_HIP(retireBuffer(st, st.triNormals, s));
+        ARK_HIP(retireBuffer(st, st.nodes, s));
+        ARK_HIP(retireBuffer(st, st.refitOrder, s));
+        ARK_HIP(retireBuffer(st, job->perm, s));
+        ARK_HIP(retireBuffer(st, job->snap, s));
+        st.triNormals = tn;
+        st.nodes = job->buf;
+        job->buf = DeviceBuffer {};
+        st.refitOrder = job->order;
+        job->order = DeviceBuffer {};
+        st.levelOffsets = job->levelOffsets;
+        if (st.refitBoxes.bytes < job->nodes * 6 * sizeof(float)) {
+            ARK_HIP(retireBuffer(st, st.refitBoxes, s));
+            ARK_HIP(st.refitBoxes.alloc(std::max<size_t>(16, job->nodes * 6 * sizeof(float) * 5 / 4)));
+        }
+        SceneArgs& sc = st.args;
+        sc.nodes = st.nodes.as<GpuBvh8Node>();
+        sc.tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.nodes.ptr) + job->triOffset);
+        sc.tri_byte_offset = static_cast<uint32_t>(job->triOffset);
+        sc.tri_normals = st.triNormals.as<float4>();
+        sc.root_opaque = job->roots[0];
+        sc.root_masked = job->roots[1];
+        sc.root_blend = job->roots[2];
+        sc.opaque_nodes = job->opaqueNodes;
+        st.triRecords = job->triRecords;
+        st.worldDepth = job->depth;
+        st.bvhMaxDepth = std::max(job->depth, st.sunArgs.sun_root >= 0 ? st.sunDepth : 0u);
+        st.bvhStats.node_count = job->nodes;
+        st.bvhStats.max_depth = st.bvhMaxDepth;
+        st.bvhStats.max_leaf_size = job->maxLeaf;
+        st.bvhStats.sah_cost = job->sah;
+        st.bvhStats.node_bytes = job->nodes * sizeof(GpuBvh8Node);
+        st.bvhStats.triangle_bytes = job->triRecords * sizeof(GpuTriangle);
+        st.bvhStats.bvh_rebuilds = ++st.worldRebuilds;
+        st.bvhStats.bvh_rebuild_ms = job->ms;
+        st.refitsSinceBuild = st.refitCount - job->refitsAt; // refits since its snapshot
+        if (st.refitsSinceBuild) {
+            if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), true, s)) return rc;
+            if (const int rc = enqueueRefit(ctx, st, s)) return rc;
+        }
+        ARK_HIP(hipEventRecord(ctx->evRefit, s));
+        ARK_HIP(installDone(ctx, s));
+        ctx->refitPending = true;
+        ++st.version;
+        if (const int rc = refreshScene(ctx)) return rc;
+    }
+    if (st.worldJob || st.refitsSinceBuild == 0) return ARK_DDGI_OK;
+    auto job = std::make_unique<WorldJob>();
+    job->version = st.version;
+    job->refitsAt = st.refitCount;
+    job->snapRecords = st.triRecords;
+    job->classOf.resize(st.instHost.size());
+    for (size_t i = 0; i < st.instHost.size(); ++i) {
+        const uint32_t m = st.instHost[i].hit_mask;
+        job->classOf[i] = (m & ARK_RT_HIT_MASK_OPAQUE) ? 0 : (m & ARK_RT_HIT_MASK_MASKED) ? 1 : 2;
+    }
+    ARK_HIP(orderBegin(ctx, s));
+    ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
+    job->t = std::thread(runWorldJob, job.get(), st.device, st.buildThreads);
+    st.worldJob = std::move(job);
+    st.refitsSinceBuild = 0;
+    return ARK_DDGI_OK;
+}
+
+// Everything an operation on `s` does to the scene first: buffers retired by earlier
+// installs freed, finished rebuilds installed, new ones started.
+int sceneMaintenance(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    collectRetired(*ctx->sceneStore);
+    if (const int rc = worldRebuildStep(ctx, s)) return rc;
+    return sunRebuildStep(ctx, s);
 }
 
 // Makes `st` the context's scene with the scene's lights: the per-context work sets
@@ -761,6 +1304,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipEventCreateWithFlags(&ctx->evTraced, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeSrc, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeDone, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evRefit, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->evFrameDone)
         if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
@@ -833,6 +1377,7 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (ctx->evTraced) (void)hipEventDestroy(ctx->evTraced);
     if (ctx->evExchangeSrc) (void)hipEventDestroy(ctx->evExchangeSrc);
     if (ctx->evExchangeDone) (void)hipEventDestroy(ctx->evExchangeDone);
+    if (ctx->evRefit) (void)hipEventDestroy(ctx->evRefit);
     for (auto& ev : ctx->evFrameDone)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
@@ -843,43 +1388,10 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
 
 const char* ark_ddgi_last_error(const ArkDdgiCtx* ctx) { return ctx ? ctx->lastError.c_str() : "null context"; }
 
-// Structural check of a BVH8 before anything reaches the GPU: every node is
-// referenced once from a root-reachable parent (no cycles, no sharing), every leaf's
-// triangles lie inside the triangle array and every triangle (every record but the
-// holes of the rows) is covered once.
 static int checkBvh8(ArkDdgiCtx* ctx, const std::vector<GpuBvh8Node>& allNodes, const std::vector<GpuTriangle>& allTris, const int32_t* roots, int nRoots)
 {
-    std::vector<uint8_t> seenNode(allNodes.size(), 0);
-    std::vector<uint8_t> seenTri(allTris.size(), 0);
-    std::vector<uint32_t> work;
-    for (int c = 0; c < nRoots; ++c)
-        if (roots[c] >= 0) work.push_back(static_cast<uint32_t>(roots[c]));
-    while (!work.empty()) {
-        const uint32_t n = work.back();
-        work.pop_back();
-        if (n >= allNodes.size() || seenNode[n]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u", n);
-        seenNode[n] = 1;
-        const GpuBvh8Node& nd = allNodes[n];
-        uint32_t internal = 0;
-        if ((nd.leaf_tris >> 24) || (nd.leaf_mask & nd.imask)) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u leaf rows", n);
-        for (int sl = 0; sl < 8; ++sl) {
-            const bool isInternal = (nd.imask >> sl) & 1u;
-            uint32_t slotTris[kBvh8MaxLeafSize];
-            const int cnt = bvh8SlotTriangles(nd, sl, slotTris);
-            if (cnt < 0) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: node %u slot %d", n, sl);
-            if (isInternal) work.push_back(nd.child_base + internal++);
-            for (int i = 0; i < cnt; ++i) {
-                const uint32_t t = slotTris[i];
-                if (t >= allTris.size() || isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: leaf range");
-                if (seenTri[t]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %u in two leaves", t);
-                seenTri[t] = 1;
-            }
-            for (int a = 0; a < 3; ++a)
-                if ((isInternal || cnt > 0) && nd.qlo[a][sl] > nd.qhi[a][sl]) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: child box");
-        }
-    }
-    for (size_t t = 0; t < seenTri.size(); ++t)
-        if (!seenTri[t] && !isHoleTriangle(allTris[t])) return ctx->fail(ARK_DDGI_E_DEVICE, "BVH invalid: triangle %zu unreachable", t);
+    std::string why;
+    if (!checkBvh8Structure(allNodes, allTris, roots, nRoots, why)) return ctx->fail(ARK_DDGI_E_DEVICE, "%s", why.c_str());
     return ARK_DDGI_OK;
 }
 
@@ -957,10 +1469,6 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
                         hi[a] = std::max(hi[a], v[a]);
                     }
         opt.inflate_abs = bvh8_inflation_box(lo, hi); // one inflation for all classes (shadow rays test all)
-        for (int a = 0; a < 3; ++a) {
-            st->boundsLo[a] = lo[a] <= hi[a] ? lo[a] : 0.0f;
-            st->boundsHi[a] = lo[a] <= hi[a] ? hi[a] : 0.0f;
-        }
     }
     // host threads for the build (ArkDdgiDesc.build_threads; 0: the box's CPU share per
     // GPU, 16 cores)
@@ -1094,9 +1602,24 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
         st->sunCostWorld = static_cast<float>(sun_shadow_cost(allNodes, allTris, roots, 3, nullptr, L, origins));
         st->sunCostLight = static_cast<float>(sun_shadow_cost(r.nodes, r.tris, &sroot, 1, sunIn.frame, L, origins));
     }
+    const uint32_t worldDepth = maxDepth;
     if (sunBuilt && (ctx->sunBvh == 1 || sun_bvh_pays(st->sunCostWorld, st->sunCostLight))) {
         const size_t nb = r.nodes.size() * sizeof(GpuBvh8Node);
         sunTriOffset = (nb + 255) & ~static_cast<size_t>(255);
+        // what its refits need (enqueueRefit): the level order, the build's inflation and
+        // frame, the record count (padding excluded)
+        {
+            const int32_t sroot = 0;
+            std::vector<uint32_t> order;
+            if (!bvhLevelOrder(r.nodes.data(), r.nodes.size(), &sroot, 1, order, st->sunLevelOffsets)) return ctx->fail(ARK_DDGI_E_DEVICE, "sun BVH: a node outside it");
+            if ((rc = upload(ctx, st->sunRefitOrder, order.data(), order.size())) != 0) return rc;
+            ARK_HIP(st->sunRefitBoxes.alloc(std::max<size_t>(16, r.nodes.size() * 6 * sizeof(float) * 5 / 4)));
+            st->sunTriRecords = r.tris.size();
+            st->sunInflateAbs = sunIn.inflateAbs;
+            for (int i = 0; i < 3; ++i)
+                for (int k = 0; k < 3; ++k) st->sunFrameD[i * 3 + k] = sunIn.frame[i][k];
+            st->sunDepth = r.max_depth;
+        }
         r.tris.push_back(GpuTriangle {}); // padding record (five-load fetch)
         ARK_HIP(st->sunNodes.alloc(sunTriOffset + r.tris.size() * sizeof(GpuTriangle)));
         ARK_HIP(hipMemcpy(st->sunNodes.ptr, r.nodes.data(), nb, hipMemcpyHostToDevice));
@@ -1182,6 +1705,7 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     st->sunWanted = sunNodeCount > 0;
     st->buildThreads = opt.threads;
     st->bvhMaxDepth = maxDepth;
+    st->worldDepth = worldDepth;
     st->inflateAbs = opt.inflate_abs;
     st->triRecords = allTris.size();
     const auto t1 = std::chrono::steady_clock::now();
@@ -1255,50 +1779,42 @@ int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* L)
         ctx->lightsDirty = true;
     }
     if (const int rc = refreshScene(ctx)) return rc;
-    return sunRebuildStep(ctx);
+    // a sun rebuild to start or install: on the context's internal stream, in call order
+    // (orderBegin / orderEnd) only when one is, so that a frame with no rebuild costs the
+    // next update no cross-stream wait
+    SceneStore& st = *ctx->sceneStore;
+    const bool sunWork = st.sunWanted && ctx->hasSun && (st.sunJob ? st.sunJob->done.load(std::memory_order_acquire) : true);
+    if (!sunWork) return sunRebuildStep(ctx, nullptr);
+    const uint32_t v = st.version;
+    const bool hadJob = static_cast<bool>(st.sunJob);
+    ARK_HIP(orderBegin(ctx, ctx->stream));
+    if (const int rc = sunRebuildStep(ctx, ctx->stream)) return rc;
+    if (st.version != v || static_cast<bool>(st.sunJob) != hadJob) ARK_HIP(orderEnd(ctx, ctx->stream));
+    return ARK_DDGI_OK;
 }
 
 namespace {
 // ark_ddgi_set_instances' first use of a scene: the world BVHs' nodes by depth, deepest
-// first (a node's internal children are one level deeper), its work buffers.
+// first, and the refit's work buffers (a topology download: refits never change it)
 int prepareRefit(ArkDdgiCtx* ctx, SceneStore& st)
 {
     const uint64_t n = st.bvhStats.node_count;
     std::vector<GpuBvh8Node> h(n);
     if (n) ARK_HIP(hipMemcpy(h.data(), st.nodes.ptr, n * sizeof(GpuBvh8Node), hipMemcpyDeviceToHost));
-    std::vector<std::vector<uint32_t>> byDepth;
-    std::vector<std::pair<uint32_t, uint32_t>> work; // (node, depth)
-    for (int32_t root : { st.args.root_opaque, st.args.root_masked, st.args.root_blend })
-        if (root >= 0) work.push_back({ static_cast<uint32_t>(root), 0u });
-    while (!work.empty()) {
-        const auto [node, d] = work.back();
-        work.pop_back();
-        if (node >= n) return ctx->fail(ARK_DDGI_E_DEVICE, "refit: node %u outside the BVH", node);
-        if (byDepth.size() <= d) byDepth.resize(d + 1);
-        byDepth[d].push_back(node);
-        const uint32_t internal = static_cast<uint32_t>(__builtin_popcount(h[node].imask));
-        for (uint32_t k = 0; k < internal; ++k) work.push_back({ h[node].child_base + k, d + 1 });
-    }
+    const int32_t roots[3] = { st.args.root_opaque, st.args.root_masked, st.args.root_blend };
     std::vector<uint32_t> order;
-    order.reserve(n);
-    st.levelOffsets.assign(1, 0u);
-    for (size_t d = byDepth.size(); d-- > 0;) {
-        std::sort(byDepth[d].begin(), byDepth[d].end());
-        order.insert(order.end(), byDepth[d].begin(), byDepth[d].end());
-        st.levelOffsets.push_back(static_cast<uint32_t>(order.size()));
-    }
+    if (!bvhLevelOrder(h.data(), n, roots, 3, order, st.levelOffsets)) return ctx->fail(ARK_DDGI_E_DEVICE, "refit: a node outside the BVH");
     int rc;
     if ((rc = upload(ctx, st.refitOrder, order.data(), order.size())) != 0) return rc;
     ARK_HIP(st.refitBoxes.alloc(std::max<size_t>(16, n * 6 * sizeof(float))));
-    ARK_HIP(st.refitInst.alloc(std::max<size_t>(16, st.instHost.size() * sizeof(RefitInstance))));
-    ARK_HIP(st.refitBounds.alloc(6 * sizeof(uint32_t)));
+    if (!st.refitBounds.ptr) ARK_HIP(st.refitBounds.alloc(kRefitBoundsWords * sizeof(uint32_t)));
     return ARK_DDGI_OK;
 }
-
-float fromOrderedBits(uint32_t u) { return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
 } // namespace
 
-int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count)
+static int checkSequencing(ArkDdgiCtx* ctx);
+
+int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count, void* hipStream)
 {
     if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
     if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "ark_ddgi_set_instances before ark_ddgi_set_scene");
@@ -1313,19 +1829,30 @@ int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint
             if (!std::isfinite(v)) return ctx->fail(ARK_DDGI_E_INVALID_ARGUMENT, "set_instances: instance %u: non-finite transform", i);
     }
     const auto t0 = std::chrono::steady_clock::now();
+    const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
-    // every launch in flight may read the scene: this context's, or with a shared scene
-    // every context's on the device
+    if (const int r = checkSequencing(ctx)) return r;
+    // every launch in flight may read the scene: with a shared scene every context's on
+    // the device (waited for here); otherwise this context's, which the refit follows in
+    // stream order (orderBegin: its earlier operations, their traversals included)
     if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
-    else ARK_HIP(drainContext(ctx));
+    ARK_HIP(orderBegin(ctx, s));
     int rc;
     if (st.levelOffsets.empty() && (rc = prepareRefit(ctx, st)) != 0) return rc;
-    // the instance table of the shading kernels and the refit's transforms
+    // a light-space sun BVH without a refit order (none recorded) cannot follow: dropped
+    if (st.sunArgs.sun_root >= 0 && st.sunLevelOffsets.empty()) {
+        st.sunArgs.sun_root = -1;
+        st.sunArgs.sun_nodes = nullptr;
+        st.sunArgs.sun_tris = nullptr;
+        ARK_HIP(retireBuffer(st, st.sunNodes, s));
+        st.sunBvhNodes = 0;
+        st.bvhStats.sun_node_count = 0;
+        st.bvhStats.sun_max_depth = 0;
+    }
+    // the instance table of the shading kernels (set_scene's determinant and rows)
     std::vector<GpuInstance> ginst(count);
-    std::vector<RefitInstance> rinst(count);
     for (uint32_t ii = 0; ii < count; ++ii) {
         const float* M = instances[ii].object_to_world;
-        // set_scene's determinant and normal-matrix rows
         const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
         const ArkRTTriangleMesh& mesh = st.meshHost[instances[ii].rt_mesh_index];
         GpuInstance& g = ginst[ii];
@@ -1336,57 +1863,37 @@ int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint
         g.flip_facing = det < 0.0f ? 1 : 0;
         g.hit_mask = static_cast<int32_t>(instances[ii].hit_mask);
         g.material_index = mesh.material_index;
-        RefitInstance& q = rinst[ii];
-        std::memset(&q, 0, sizeof(q));
-        std::memcpy(q.m, M, sizeof(q.m));
-        q.first_vertex = mesh.first_vertex;
-        q.first_index = static_cast<uint32_t>(mesh.first_index);
-        q.flip = g.flip_facing ? 1u : 0u;
     }
-    if (count) {
-        ARK_HIP(hipMemcpy(st.instances.ptr, ginst.data(), count * sizeof(GpuInstance), hipMemcpyHostToDevice));
-        ARK_HIP(hipMemcpy(st.refitInst.ptr, rinst.data(), count * sizeof(RefitInstance), hipMemcpyHostToDevice));
-    }
-    const uint32_t initBounds[6] = { 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u };
-    ARK_HIP(hipMemcpy(st.refitBounds.ptr, initBounds, sizeof(initBounds), hipMemcpyHostToDevice));
-    GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(static_cast<char*>(st.nodes.ptr) + st.args.tri_byte_offset);
-    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(),
-                              st.refitBounds.as<uint32_t>(), ctx->stream));
-    uint32_t b[6];
-    ARK_HIP(hipMemcpyAsync(b, st.refitBounds.ptr, sizeof(b), hipMemcpyDeviceToHost, ctx->stream));
-    ARK_HIP(hipStreamSynchronize(ctx->stream));
-    // the builder's absolute inflation (1e-6 of the scene diagonal), never below set_scene's
-    float lo[3], hi[3];
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = fromOrderedBits(b[a]);
-        hi[a] = fromOrderedBits(b[3 + a]);
-    }
-    const float inflate = std::max(st.inflateAbs, bvh8_inflation_box(lo, hi));
-    const uint32_t* order = st.refitOrder.as<uint32_t>();
-    for (size_t l = 0; l + 1 < st.levelOffsets.size(); ++l)
-        ARK_HIP(launch_refit_nodes(st.nodes.as<GpuBvh8Node>(), tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l],
-                                   st.levelOffsets[l + 1] - st.levelOffsets[l], inflate, ctx->stream));
-    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    ARK_HIP(stagedUpload(st, st.instances.ptr, ginst.data(), count * sizeof(GpuInstance), s));
+    if ((rc = uploadRefitInstances(ctx, st, instances, count, false, s)) != 0) return rc;
+    if ((rc = enqueueRefit(ctx, st, s)) != 0) return rc;
+    ARK_HIP(hipEventRecord(ctx->evRefit, s));
+    ARK_HIP(installDone(ctx, s));
+    ctx->refitPending = true;
     for (uint32_t ii = 0; ii < count; ++ii) std::memcpy(st.instHost[ii].object_to_world, instances[ii].object_to_world, sizeof(float) * 12);
-    for (int a = 0; a < 3; ++a) {
-        st.boundsLo[a] = lo[a] <= hi[a] ? lo[a] : 0.0f;
-        st.boundsHi[a] = lo[a] <= hi[a] ? hi[a] : 0.0f;
-    }
-    // the light-space sun BVH holds the old world-space records: the sun's shadow rays
-    // traverse the world BVHs from now on (a set_scene builds a new one)
-    st.sunArgs.sun_root = -1;
-    st.sunArgs.sun_nodes = nullptr;
-    st.sunArgs.sun_tris = nullptr;
-    st.sunNodes.release();
-    st.sunBvhNodes = 0;
-    st.bvhStats.sun_node_count = 0;
-    st.bvhStats.sun_max_depth = 0;
-    st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     ++st.version;
-    if (const int rc2 = refreshScene(ctx)) return rc2;
-    return sunRebuildStep(ctx); // a new light-space BVH of the refitted records, in the background
+    ++st.refitsSinceBuild;
+    ++st.sunRefitsSinceBuild;
+    st.bvhStats.refit_version = ++st.refitCount;
+    if ((rc = refreshScene(ctx)) != 0) return rc;
+    // background rebuilds of the loosened BVHs (world and light-space), from a snapshot
+    // taken on s behind this refit
+    if ((rc = sceneMaintenance(ctx, s)) != 0) return rc;
+    ARK_HIP(orderEnd(ctx, s));
+    st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return ARK_DDGI_OK;
 }
 
+int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count)
+{
+    if (!ctx) return ARK_DDGI_E_INVALID_ARGUMENT;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (const int rc = ark_ddgi_set_instances_async(ctx, instances, count, ctx->stream)) return rc;
+    ARK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->sceneStore->bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->bvhStats = ctx->sceneStore->bvhStats;
+    return ARK_DDGI_OK;
+}
 
 static uint32_t countSlabProbes(const ArkDdgiCtx* ctx, uint32_t first, uint32_t K)
 {
@@ -1578,9 +2085,6 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     const hipStream_t s = streamOf(hipStream);
     if (const int r = checkSequencing(ctx)) return r;
     ARK_HIP(hipSetDevice(ctx->device));
-    if (ctx->sceneVersion != ctx->sceneStore->version) // another context refitted the shared scene or installed a sun BVH
-        if (const int rc = refreshScene(ctx)) return rc;
-    if (const int rc = sunRebuildStep(ctx)) return rc;
     FrameArgs f {};
     f.abort_word = ctx->seqWords.as<uint32_t>() + 64;
     f.X = ctx->X; f.Y = ctx->Y; f.Z = ctx->Z;
@@ -1625,6 +2129,10 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     f.fib = ctx->fib.as<float4>() + b * Rmax;
     RoctxRange ddgiZone("DDGI");
     ARK_HIP(orderBegin(ctx, s));
+    // finished background rebuilds installed (and refitted forward) on s, new ones started
+    if (const int rc = sceneMaintenance(ctx, s)) return rc;
+    if (ctx->sceneVersion != ctx->sceneStore->version) // another context refitted the shared scene or installed a BVH
+        if (const int rc = refreshScene(ctx)) return rc;
     // lights changed since the last update: stored ahead of this frame's shadow rays and
     // shading on s (the traversal on the traversal stream reads no light)
     ARK_HIP(flushLights(ctx, s));
@@ -1677,6 +2185,12 @@ static int updateImpl(ArkDdgiCtx* ctx, const ArkDdgiFrameParams* p, void* hipStr
     else if (pipe && ctx->frameDoneValid[b]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b], 0));
     // a serial previous frame wrote its offsets on the caller's stream
     if (pipe && !ctx->prevPipelined && ctx->frameDoneValid[b ^ 1u]) ARK_HIP(hipStreamWaitEvent(ts, ctx->evFrameDone[b ^ 1u], 0));
+    // a refit or an installed rebuild enqueued since the last update (on any stream): the
+    // traversal reads the BVH it writes
+    if (ctx->refitPending) {
+        if (ts != s) ARK_HIP(hipStreamWaitEvent(ts, ctx->evRefit, 0));
+        ctx->refitPending = false;
+    }
     if (count) ARK_HIP(hipMemsetAsync(ctx->counters.ptr, 0, ctx->counters.bytes, s));
     // (k_probe_slots zeroes f.ray_counter)
     if (timing) ARK_HIP(hipEventRecord(ctx->ev[0], s));
@@ -2012,7 +2526,7 @@ int ark_ddgi_get_last_timings(ArkDdgiCtx* ctx, float* out, int count)
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out)
 {
     if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
-    *out = ctx->bvhStats;
+    *out = ctx->hasScene ? ctx->sceneStore->bvhStats : ctx->bvhStats; // the store's: installs and refits of any sharing context
     return ARK_DDGI_OK;
 }
 

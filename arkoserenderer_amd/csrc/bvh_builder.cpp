@@ -1383,6 +1383,7 @@ bool build_sun_bvh(SunBvhInput& in, const BvhBuildOptions& opt, const Bvh8Collap
     BvhBuildOptions lopt = opt;
     lopt.max_leaf_size = kBvh8MaxLeafSize;
     lopt.inflate_abs = 2.0f * bvh8_inflation_box(lo, hi) + 2e-6f * in.maxAbs;
+    in.inflateAbs = lopt.inflate_abs;
     BvhBuildResult r2 = build_bvh(in.tris, lopt, 0u, 0u);
     std::vector<BuildTriangle>().swap(in.tris);
     if (r2.max_leaf > static_cast<uint32_t>(kBvh8MaxLeafSize)) return false;

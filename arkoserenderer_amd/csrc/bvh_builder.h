@@ -108,6 +108,7 @@ struct SunBvhInput {
     std::vector<GpuTriangle> world;   // world-space records (make_gpu_triangle)
     double frame[3][3] = {};          // rows u, v, w
     float maxAbs = 0.0f;              // largest |world coordinate|
+    float inflateAbs = 0.0f;          // out (build_sun_bvh): the boxes' absolute inflation (the refit's floor)
 };
 void sun_frame(const float sun_dir[3], double frame[3][3]);
 void sun_add_triangles(SunBvhInput& in, const std::vector<BuildTriangle>& world_tris, int threads = 0);

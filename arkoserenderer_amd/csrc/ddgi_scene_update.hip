@@ -13,7 +13,13 @@
 //                    from their triangle records, internal children from the level below
 //                    - inflated as the builder inflates them (bvh_builder.cpp writeNode),
 //                    the node's quantization grid and outward-rounded child planes
-//                    recomputed (quantGrid, collapse_bvh8).
+//                    recomputed (quantGrid, collapse_bvh8). The world BVHs box world
+//                    coordinates; the sun's light-space BVH its records' light
+//                    coordinates (k_refit_light_bounds first), so it follows the motion
+//                    instead of being dropped.
+//   k_gather_records the shading records in an installed background rebuild's order.
+// Every launch is stream-ordered behind the context's earlier work (ark_ddgi_set_instances_async):
+// the boxes' inflation is derived on the device from the refit's bounds, no host round trip.
 // Refitting never changes a hit: hits do not depend on the BVH's shape (the (instance,
 // primitive) tie rule and conservative boxes), only on the triangle records,
 // which equal a fresh set_scene's bit for bit.
@@ -37,6 +43,12 @@ __device__ __forceinline__ uint32_t orderedBits(float f)
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+__global__ void __launch_bounds__(32) k_refit_bounds_reset(uint32_t* __restrict__ bounds)
+{
+    const uint32_t i = threadIdx.x;
+    if (i < kRefitBoundsWords) bounds[i] = (i < 3 || (i >= 6 && i < 9)) ? 0xffffffffu : 0u;
+}
+
 __global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tris, uint32_t count, const RefitInstance* __restrict__ inst,
                                                     const uint32_t* __restrict__ indices, const float* __restrict__ positions, uint32_t* __restrict__ bounds)
 {
@@ -46,28 +58,39 @@ __global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tr
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i < count) {
         float4* rec = reinterpret_cast<float4*>(tris + i);
-        float4 t2 = rec[2];
+        float4 t0 = rec[0], t1 = rec[1], t2 = rec[2];
         const uint32_t id = __float_as_uint(t2.y), prim = __float_as_uint(t2.z);
         if (id != kHoleInstance) {
             const RefitInstance I = inst[id];
-            const float* M = I.m;
             float w[3][3];
-            for (int k = 0; k < 3; ++k) {
-                const uint32_t idx = indices[static_cast<size_t>(I.first_index) + 3u * prim + k];
-                const float* P = positions + (static_cast<uint64_t>(static_cast<int64_t>(I.first_vertex)) + idx) * 3u;
-                // ark_ddgi_set_scene's expression, left to right, no contraction
-                w[k][0] = M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3];
-                w[k][1] = M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7];
-                w[k][2] = M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11];
+            if (I.dirty) {
+                const float* M = I.m;
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t idx = indices[static_cast<size_t>(I.first_index) + 3u * prim + k];
+                    const float* P = positions + (static_cast<uint64_t>(static_cast<int64_t>(I.first_vertex)) + idx) * 3u;
+                    // ark_ddgi_set_scene's expression, left to right, no contraction
+                    w[k][0] = M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3];
+                    w[k][1] = M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7];
+                    w[k][2] = M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11];
+                }
+                // make_gpu_triangle: e1 = v1 - v0, e2 = v2 - v0
+                const float e1x = w[1][0] - w[0][0], e1y = w[1][1] - w[0][1], e1z = w[1][2] - w[0][2];
+                const float e2x = w[2][0] - w[0][0], e2y = w[2][1] - w[0][1], e2z = w[2][2] - w[0][2];
+                rec[0] = make_float4(w[0][0], w[0][1], w[0][2], e1x);
+                rec[1] = make_float4(e1y, e1z, e2x, e2y);
+                t2.x = e2z;
+                t2.w = __uint_as_float(I.flip);
+                rec[2] = t2;
+            } else {
+                // an unmoved instance: its record stays; its vertices (v0, v0 + e1, v0 + e2)
+                // still bound the scene
+                const float v0[3] = { t0.x, t0.y, t0.z }, e1[3] = { t0.w, t1.x, t1.y }, e2[3] = { t1.z, t1.w, t2.x };
+                for (int a = 0; a < 3; ++a) {
+                    w[0][a] = v0[a];
+                    w[1][a] = v0[a] + e1[a];
+                    w[2][a] = v0[a] + e2[a];
+                }
             }
-            // make_gpu_triangle: e1 = v1 - v0, e2 = v2 - v0
-            const float e1x = w[1][0] - w[0][0], e1y = w[1][1] - w[0][1], e1z = w[1][2] - w[0][2];
-            const float e2x = w[2][0] - w[0][0], e2y = w[2][1] - w[0][1], e2z = w[2][2] - w[0][2];
-            rec[0] = make_float4(w[0][0], w[0][1], w[0][2], e1x);
-            rec[1] = make_float4(e1y, e1z, e2x, e2y);
-            t2.x = e2z;
-            t2.w = __uint_as_float(I.flip);
-            rec[2] = t2;
             for (int a = 0; a < 3; ++a) {
                 const float lo = fminf(fminf(w[0][a], w[1][a]), w[2][a]), hi = fmaxf(fmaxf(w[0][a], w[1][a]), w[2][a]);
                 atomicMin(&red[a], orderedBits(lo));
@@ -78,6 +101,63 @@ __global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tr
     __syncthreads();
     if (threadIdx.x < 3) atomicMin(&bounds[threadIdx.x], red[threadIdx.x]);
     else if (threadIdx.x < 6) atomicMax(&bounds[threadIdx.x], red[threadIdx.x]);
+}
+
+// The light coordinates of a record's three vertices as build_sun_bvh computes them
+// (bvh_builder.cpp sunAddRecords: v0, v0 + e1, v0 + e2 in double, each rotated into the
+// frame in double and rounded to fp32), and the largest |world coordinate|.
+__device__ __forceinline__ void lightVertices(const float4 t0, const float4 t1, const float4 t2, const double* F, float L[3][3], float& maxAbs)
+{
+    double V[3][3];
+    const double e1[3] = { t0.w, t1.x, t1.y }, e2[3] = { t1.z, t1.w, t2.x };
+    V[0][0] = t0.x;
+    V[0][1] = t0.y;
+    V[0][2] = t0.z;
+    maxAbs = 0.0f;
+    for (int a = 0; a < 3; ++a) {
+        V[1][a] = V[0][a] + e1[a];
+        V[2][a] = V[0][a] + e2[a];
+        maxAbs = fmaxf(maxAbs, static_cast<float>(fmax(fabs(V[0][a]), fmax(fabs(V[1][a]), fabs(V[2][a])))));
+    }
+    for (int k = 0; k < 3; ++k)
+        for (int r = 0; r < 3; ++r) L[k][r] = static_cast<float>(F[3 * r + 0] * V[k][0] + F[3 * r + 1] * V[k][1] + F[3 * r + 2] * V[k][2]);
+}
+
+__global__ void __launch_bounds__(256) k_refit_light_bounds(const GpuTriangle* __restrict__ tris, uint32_t count, RefitBoxArgs a, uint32_t* __restrict__ bounds)
+{
+    __shared__ uint32_t red[7];
+    if (threadIdx.x < 7) red[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < count) {
+        const float4* rec = reinterpret_cast<const float4*>(tris + i);
+        const float4 t0 = rec[0], t1 = rec[1], t2 = rec[2];
+        if (__float_as_uint(t2.y) != kHoleInstance) {
+            float L[3][3], m;
+            lightVertices(t0, t1, t2, a.frame, L, m);
+            for (int ax = 0; ax < 3; ++ax) {
+                atomicMin(&red[ax], orderedBits(fminf(fminf(L[0][ax], L[1][ax]), L[2][ax])));
+                atomicMax(&red[3 + ax], orderedBits(fmaxf(fmaxf(L[0][ax], L[1][ax]), L[2][ax])));
+            }
+            atomicMax(&red[6], orderedBits(m));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) atomicMin(&bounds[6 + threadIdx.x], red[threadIdx.x]);
+    else if (threadIdx.x < 7) atomicMax(&bounds[6 + threadIdx.x], red[threadIdx.x]);
+}
+
+__device__ __forceinline__ float fromOrderedBits(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+
+// bvh8_inflation_box of bounds lo = b[0..2], hi = b[3..5] (double, as on the host)
+__device__ __forceinline__ float inflationBox(const uint32_t* b)
+{
+    double d2 = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double lo = fromOrderedBits(b[a]), hi = fromOrderedBits(b[3 + a]);
+        if (hi >= lo) d2 += (hi - lo) * (hi - lo);
+    }
+    return static_cast<float>(1e-6 * sqrt(d2));
 }
 
 // bvh_builder.cpp writeNode's inflation of a child box: relative to its magnitude and
@@ -114,11 +194,14 @@ __device__ __forceinline__ void quantGrid(float L, float H, int& e, double& p)
 }
 
 __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ nodes, const GpuTriangle* __restrict__ tris, float* __restrict__ boxes,
-                                                     const uint32_t* __restrict__ order, uint32_t count, float inflateAbs)
+                                                     const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra, const uint32_t* __restrict__ bounds)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint32_t n = order[i];
+    // the inflation of this BVH's boxes from the refit's bounds (RefitBoxArgs)
+    const float inflateAbs = ra.light ? fmaxf(ra.inflate_min, 2.0f * inflationBox(bounds + 6) + 2e-6f * fromOrderedBits(bounds[12]))
+                                      : fmaxf(ra.inflate_min, inflationBox(bounds));
     GpuBvh8Node nd = nodes[n];
     float clo[8][3], chi[8][3];
     float nlo[3] = { INFINITY, INFINITY, INFINITY }, nhi[3] = { -INFINITY, -INFINITY, -INFINITY };
@@ -139,6 +222,16 @@ __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ n
                 if (pos >= 24u || !((nd.leaf_tris >> pos) & 1u)) break;
                 const float4* rec = reinterpret_cast<const float4*>(tris + nd.tri_base + pos);
                 const float4 a = rec[0], b = rec[1], c = rec[2];
+                if (ra.light) {
+                    // the light coordinates build_sun_bvh boxed
+                    float L[3][3], m;
+                    lightVertices(a, b, c, ra.frame, L, m);
+                    for (int ax = 0; ax < 3; ++ax) {
+                        lo[ax] = fminf(lo[ax], fminf(L[0][ax], fminf(L[1][ax], L[2][ax])));
+                        hi[ax] = fmaxf(hi[ax], fmaxf(L[0][ax], fmaxf(L[1][ax], L[2][ax])));
+                    }
+                    continue;
+                }
                 // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2
                 const float v0[3] = { a.x, a.y, a.z }, e1[3] = { a.w, b.x, b.y }, e2[3] = { b.z, b.w, c.x };
                 for (int ax = 0; ax < 3; ++ax) {
@@ -191,12 +284,28 @@ __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ n
     }
 }
 
+// an installed rebuild's shading records in its record order: dst record i = src record
+// perm[i] (holes: zeros), one float4 per thread
+__global__ void __launch_bounds__(256) k_gather_records(float4* __restrict__ dst, const float4* __restrict__ src, const uint32_t* __restrict__ perm, uint64_t words)
+{
+    const uint64_t w = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (w >= words) return;
+    const uint32_t from = perm[w >> 2];
+    dst[w] = from == 0xffffffffu ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : src[static_cast<uint64_t>(from) * 4u + (w & 3u)];
+}
+
 } // namespace dev
 
 hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream_t s)
 {
     if (b.count == 0) return hipSuccess;
     hipLaunchKernelGGL(dev::k_store_lights, dim3(1), dim3(256), 0, s, b, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_refit_bounds_reset(uint32_t* bounds, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_refit_bounds_reset, dim3(1), dim3(32), 0, s, bounds);
     return hipGetLastError();
 }
 
@@ -208,10 +317,26 @@ hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInsta
     return hipGetLastError();
 }
 
-hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, float inflateAbs, hipStream_t s)
+hipError_t launch_refit_light_bounds(const GpuTriangle* tris, uint32_t count, const RefitBoxArgs& a, uint32_t* bounds, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_refit_nodes, dim3((count + 127u) / 128u), dim3(128), 0, s, nodes, tris, boxes, order, count, inflateAbs);
+    hipLaunchKernelGGL(dev::k_refit_light_bounds, dim3((count + 255u) / 256u), dim3(256), 0, s, tris, count, a, bounds);
+    return hipGetLastError();
+}
+
+hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
+                              const uint32_t* bounds, hipStream_t s)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::k_refit_nodes, dim3((count + 127u) / 128u), dim3(128), 0, s, nodes, tris, boxes, order, count, a, bounds);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_records(float4* dst, const float4* src, const uint32_t* perm, uint64_t count, hipStream_t s)
+{
+    if (count == 0) return hipSuccess;
+    const uint64_t words = count * 4u; // four float4 per 64-B record
+    hipLaunchKernelGGL(dev::k_gather_records, dim3(static_cast<uint32_t>((words + 255u) / 256u)), dim3(256), 0, s, dst, src, perm, words);
     return hipGetLastError();
 }
 

@@ -160,6 +160,12 @@ class DDGIContext:
         a = np.ascontiguousarray(instances)
         self.check(self.lib.ark_ddgi_set_instances(self.h, C.c_void_p(a.ctypes.data), int(a.size)), "ark_ddgi_set_instances")
 
+    def set_instances_async(self, instances: np.ndarray, stream: int | None):
+        """ark_ddgi_set_instances_async: the same refit enqueued on `stream` (no host wait)."""
+        a = np.ascontiguousarray(instances)
+        self.check(self.lib.ark_ddgi_set_instances_async(self.h, C.c_void_p(a.ctypes.data), int(a.size), C.c_void_p(stream) if stream else None),
+                   "ark_ddgi_set_instances_async")
+
     def share_scene(self, src: "DDGIContext"):
         """ark_ddgi_share_scene: use src's device scene and BVH (same GPU), no copy."""
         self.check(self.lib.ark_ddgi_share_scene(self.h, src.h), "ark_ddgi_share_scene")

@@ -138,14 +138,14 @@ RenderPipelineNode::ExecuteCallback DDGINode::construct(GpuScene& scene, Registr
         // the SceneLightSet and the TLAS: the light buffers with this frame's
         // pre-exposure (GpuScene.cpp:792-858; the context keeps its device copy when
         // nothing changed), and the TLAS instance data + build when a transform moved
-        // (:872-1009; here a device refit of the flattened BVHs - the reference's full
-        // build every 60 frames only restores tightness, which construct()'s set_scene
-        // does on a pipeline rebuild)
+        // (:872-1009; here a device refit of the flattened BVHs, and a background rebuild
+        // installed when ready - the reference's full build every 60 frames)
         if (int rc = ark_ddgi_set_lights(ctx, &scene.rtLights()); rc != ARK_DDGI_OK)
             ARKOSE_LOG(Error, "DDGINode: ark_ddgi_set_lights failed (%d): %s", rc, ark_ddgi_last_error(ctx));
         if (scene.instanceVersion() != m_instanceVersion) {
             const std::vector<ArkRTInstance>& instances = scene.rtInstances();
-            int rc = ark_ddgi_set_instances(ctx, instances.data(), static_cast<uint32_t>(instances.size()));
+            // enqueued on this frame's stream ahead of the update (no host wait)
+            int rc = ark_ddgi_set_instances_async(ctx, instances.data(), static_cast<uint32_t>(instances.size()), cmdList.hipStream());
             if (rc != ARK_DDGI_OK) {
                 // a refit cannot follow this change (the topology changed: another mesh,
                 // triangle count or hit mask): build the scene anew, as construct() does

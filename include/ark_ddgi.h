@@ -22,7 +22,7 @@
  *                           device: the Z-slab contexts of a GPU share it.
  *   ark_ddgi_set_lights  <- the per-frame light upload of GpuScene::update
  *                           (GpuScene.cpp:790-858, pre-exposure from :792).
- *   ark_ddgi_set_instances <- the per-frame TLAS instance update + build
+ *   ark_ddgi_set_instances(_async) <- the per-frame TLAS instance update + build
  *                           (GpuScene.cpp:872-1009), as a device refit.
  *   ark_ddgi_update      <- the DDGINode execute lambda (DDGINode.cpp:132-259):
  *                           traceRays -> irradiance update -> visibility update ->
@@ -348,16 +348,22 @@ int ark_ddgi_set_lights(ArkDdgiCtx* ctx, const ArkDdgiLights* lights);
  * is the scene's instance list with new object_to_world transforms: the same count, RT
  * meshes, triangle counts and hit masks as the last set_scene (else
  * ARK_DDGI_E_INVALID_ARGUMENT and nothing changes). The flattened world-space BVHs are
- * refitted on the device - every triangle record re-transformed in the fp32 operation
- * order set_scene uses, every node box recomputed bottom-up and re-quantized outward -
- * so the hits equal those of a set_scene with the same instances (they never depend on
- * the BVH's shape); only the node boxes' tightness can degrade with large motions, which
- * a set_scene (the full build) restores. The sun's light-space BVH holds the old
- * records: it is dropped (the sun's shadow rays traverse the world BVHs) and rebuilt in
- * the background from the refitted records, as after a sun-direction change
- * (ark_ddgi_set_lights). Blocking: waits for the context's (a shared scene: the
- * device's) work in flight, refits, returns when the scene is updated; the cost is in
- * ArkDdgiBvhStats.refit_ms. */
+ * refitted on the device - the triangle records of every moved instance re-transformed
+ * in the fp32 operation order set_scene uses, every node box recomputed bottom-up and
+ * re-quantized outward - so the hits equal those of a set_scene with the same
+ * instances (they never depend on the BVH's shape). The sun's light-space BVH is
+ * refitted with them (its records re-transformed, its boxes of their light
+ * coordinates). The refitted boxes loosen as instances move: after a refit a host
+ * thread rebuilds the world BVHs (and the light-space one) from a device snapshot of
+ * the refitted records, and the first update after a build is done installs it,
+ * refitted forward when more refits came in meanwhile (the reference's full build every
+ * 60 frames; ArkDdgiBvhStats.bvh_rebuilds / sun_rebuilds).
+ * _async: enqueued on `hip_stream` behind the context's earlier operations (no host
+ * wait; the next update's traversal waits for it on the device); a shared scene
+ * (ark_ddgi_share_scene) first waits for the device, whose other contexts may be
+ * reading it. The blocking form runs it on the context's internal stream and returns
+ * when the scene is updated; ArkDdgiBvhStats.refit_ms is the call's host time. */
+int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count, void* hip_stream);
 int ark_ddgi_set_instances(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count);
 
 /* One DDGI update (DDGINode.cpp:132-259) enqueued on `hip_stream` (NULL = the null

@@ -5,6 +5,13 @@ before and after - one instance moved by 0.5 m, then every instance rotated by 2
 about y (the refit keeps the topology, so the boxes loosen with the motion).
 
     python tools/refit_cost.py [--config c4 c3] [--steps 5]
+    python tools/refit_cost.py --continuous [--frames 300] [--config c4 c3]
+
+--continuous (VERDICT r05 "do this" #3): the static rate, then `frames` frames that each
+move one instance (ark_ddgi_set_instances_async on the update's stream, no host wait)
+- the rate under motion, the background rebuilds installed meanwhile - then static
+frames until the rebuilds of the final state (world BVHs and the light-space sun BVH)
+are installed, and the rate again: it should be back at the static rate.
 """
 import argparse
 import json
@@ -30,6 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", nargs="+", default=["c4", "c3"])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--continuous", action="store_true", help="one instance moved every frame for --frames frames, then back to static")
+    ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--sun-turn", action="store_true", help="instead of refits: turn the sun by 10 deg, wait for the background rebuild, turn it back, wait again")
     args = ap.parse_args()
     import torch
@@ -59,6 +68,53 @@ def main():
         had_sun_bvh = node.ctx.bvh_stats().sun_node_count > 0
         out = {"config": name, "triangles": int(sc.triangle_count), "instances": int(sc.instances.size),
                "build_ms": round(node.ctx.bvh_stats().build_ms, 1), "mrays_per_s_static": round(rate(), 1)}
+        if args.continuous:
+            sptr = torch.cuda.current_stream().cuda_stream
+            static = [out["mrays_per_s_static"], round(rate(), 1)]
+            inst0 = sc.instances.copy()
+            n = len(inst0)
+            st0 = node.ctx.bvh_stats()
+            node.ctx.synchronize()
+            t = time.perf_counter()
+            for f in range(args.frames):
+                inst = inst0.copy()
+                m = inst["object_to_world"].reshape(-1, 3, 4)
+                m[f % n, 0, 3] += np.float32(0.3 * np.sin(0.1 * f))  # one instance a frame, back and forth
+                m[(f // n) % n, 2, 3] += np.float32(0.2)               # and one left displaced for n frames
+                inst["object_to_world"] = m.reshape(-1, 12)
+                node.ctx.set_instances_async(inst, sptr)
+                node.execute(app[0], sptr)
+                app[0] = D.AppState(app[0].frame_index + 1)
+                if f % 50 == 49:
+                    print(json.dumps({"frame": f + 1, "elapsed_s": round(time.perf_counter() - t, 2)}), flush=True)
+            node.ctx.synchronize()
+            motion_s = time.perf_counter() - t
+            st1 = node.ctx.bvh_stats()
+            # static again: until rebuilds started after the last refit are installed
+            t = time.perf_counter()
+            w0, s0 = st1.bvh_rebuilds, st1.sun_rebuilds
+            while time.perf_counter() - t < 120.0:
+                st = node.ctx.bvh_stats()
+                if st.bvh_rebuilds >= w0 + 1 and (not had_sun_bvh or st.sun_rebuilds >= s0 + 1):
+                    break
+                node.execute(app[0], sptr)
+                app[0] = D.AppState(app[0].frame_index + 1)
+                node.ctx.synchronize()
+                time.sleep(0.01)
+            settle_s = time.perf_counter() - t
+            st2 = node.ctx.bvh_stats()
+            after = [round(rate(), 1) for _ in range(2)]
+            out["continuous"] = {
+                "frames": args.frames, "mrays_per_s_moving": round(N * R * args.frames / motion_s / 1e6, 1),
+                "ms_per_frame_moving": round(motion_s / args.frames * 1e3, 4),
+                "installs_while_moving": {"world": int(st1.bvh_rebuilds - st0.bvh_rebuilds), "sun": int(st1.sun_rebuilds - st0.sun_rebuilds)},
+                "world_rebuild_ms": round(st2.bvh_rebuild_ms, 1), "sun_rebuild_ms": round(st2.sun_build_ms, 1),
+                "settled_after_s": round(settle_s, 2), "sun_bvh_installed": bool(st2.sun_node_count > 0),
+                "mrays_per_s_static_before": static, "mrays_per_s_static_after": after,
+                "after_vs_before": round(max(after) / max(static), 4)}
+            print(json.dumps(out), flush=True)
+            node.ctx.close()
+            continue
         if args.sun_turn:
             turns = []
             base = node.ctx.bvh_stats().sun_rebuilds
