@@ -79,13 +79,14 @@ def main():
 
             def gather(out, mine):  # the other ranks' packets (a device copy stands in for the all-gather)
                 n = mine.numel()
-                for q in range(s):
-                    if q != rank:
-                        out[q * n:(q + 1) * n].copy_(others[:n])
+                if rank > 0:
+                    out[:rank * n].copy_(others[:rank * n])
+                if rank + 1 < s:
+                    out[(rank + 1) * n:s * n].copy_(others[:(s - rank - 1) * n])
 
             wx = WindowExchange(WindowSource(node.ctx), band, gather, rank, s, min(K, G ** 3 // s), dev)
             wx.recv.zero_()
-            others = wx.recv[:wx.recv.numel() // s].clone()
+            others = wx.recv.clone()
             loop = OverlappedSlabExchange(node, wx.exchange, dev)
             run = loop.step
             received = (s - 1) * (sum(b[3] for b in bands)) if K == G ** 3 else None
