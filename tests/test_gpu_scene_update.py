@@ -395,3 +395,119 @@ def test_continuous_motion_installs_rebuilds():
     finally:
         ctx.close()
         orc.close()
+
+
+def _install_sun_on_a(a, b, sc, grid, cfg, exposure, sun):
+    """Two contexts share a scene; A asks twice for a new sun (a stable request starts
+    the background rebuild) and updates until it installs the light-space BVH; B has
+    not seen the new version yet."""
+    import time
+
+    a.set_lights(sun, ())
+    a.set_lights(sun, ())
+    t0, f = time.time(), 0
+    while a.bvh_stats().sun_rebuilds == 0:
+        assert time.time() - t0 < 90, "no light-space BVH installed within 90 s"
+        a.update(D.frame_params(cfg, grid, D.AppState(f), 0, **exposure))
+        a.synchronize()
+        f += 1
+        time.sleep(0.02)
+    return f
+
+
+def test_shared_scene_set_lights_after_other_context_installs():
+    """B shares A's scene; A installs a (possibly deeper) light-space
+    sun BVH; B then calls set_lights - which re-derives its scene view and must size its
+    traversal spill for the new depth - and updates. B's frames stay bit-exact against
+    an oracle fed the same lights."""
+    sc = S.soup(96_000, extent=7.0)
+    grid = D.ProbeGrid((6, 6, 6), (1.2, 1.2, 1.2), (0.5, 0.5, 0.5))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=216, compute_probe_offsets=False,
+                       max_rays_per_probe=64, max_probe_updates=216, sun_bvh=abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE)
+    exposure = dict(light_pre_exposure=1.0, environment_brightness=1.0)
+    a = D.DDGIContext(grid, 10000.0, cfg)
+    b = D.DDGIContext(grid, 10000.0, cfg)
+    a.set_scene(sc)
+    b.share_scene(a)
+    orc = O.Oracle(b.desc)
+    orc.set_scene(sc)
+    try:
+        for f in range(2):
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            b.update(p)
+            orc.update(p)
+        b.synchronize()
+        _compare(b, orc, 1, "before the install")
+        d = np.array([-0.6, -1.0, 0.3], np.float32)
+        sun = (sc.sun[0], tuple(float(x) for x in d / np.linalg.norm(d)))
+        _install_sun_on_a(a, b, sc, grid, cfg, exposure, sun)
+        b.set_lights(sun, ())
+        orc.set_lights(sun, ())
+        assert b.bvh_stats().max_depth >= b.bvh_stats().sun_max_depth
+        for f in range(2, 4):
+            p = D.frame_params(cfg, grid, D.AppState(f), 0, **exposure)
+            b.update(p)
+            orc.update(p)
+            b.synchronize()
+            _compare(b, orc, f, "B after A installed a sun BVH")
+    finally:
+        a.close()
+        b.close()
+        orc.close()
+
+
+def test_shared_scene_reflections_after_other_context_installs():
+    """B shares A's scene; A installs a light-space sun BVH; B's next
+    operation is rt_reflections, which must size (and only then point into) its spill
+    area for the scene's new depth. B's reflections equal the oracle's bit for bit."""
+    import torch
+
+    import reflection_inputs as RI
+
+    sc = scenes.features_scene()
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=144, max_rays_per_probe=64, max_probe_updates=144,
+                       sun_bvh=abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE)
+    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.05, environment_brightness=0.5)
+    a = D.DDGIContext(GRID, 100.0, cfg)
+    b = D.DDGIContext(GRID, 100.0, cfg)
+    a.set_scene(sc)
+    b.share_scene(a)
+    orc = O.Oracle(b.desc)
+    orc.set_scene(sc)
+    try:
+        d = np.array([0.4, -1.0, -0.5], np.float32)
+        sun = (sc.sun[0], tuple(float(x) for x in d / np.linalg.norm(d)))
+        for ctx in (b,):
+            ctx.set_lights(sun, list(sc.spots))
+        orc.set_lights(sun, list(sc.spots))
+        for f in range(2):
+            p = D.frame_params(cfg, GRID, D.AppState(f), 0, **exposure)
+            b.update(p)
+            orc.update(p)
+        b.synchronize()
+        a.set_lights(sun, list(sc.spots))
+        a.set_lights(sun, list(sc.spots))
+        import time
+
+        t0, f = time.time(), 0
+        while a.bvh_stats().sun_rebuilds == 0:
+            assert time.time() - t0 < 90, "no light-space BVH installed within 90 s"
+            a.update(D.frame_params(cfg, GRID, D.AppState(f), 0, **exposure))
+            a.synchronize()
+            f += 1
+            time.sleep(0.02)
+        W, H = 64, 48
+        cam = RI.camera(W, H)
+        g, _ = RI.gbuffer(W, H, cam, seed=3)
+        kw = dict(environment_multiplier=0.5, ambient_amount=0.05)
+        want_rad, want_dir = orc.rt_reflections(W, H, cam, g, **kw)
+        dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in g.items()}
+        rad = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+        dirs = torch.zeros((H, W, 4), dtype=torch.int16, device="cuda")
+        D.RTReflectionsNode().execute(b, cam, {k: dev[k] for k in ("depth", "material", "normal_velocity")}, dev["blue_noise"], rad, dirs, **kw)
+        assert np.array_equal(rad.cpu().numpy().view(np.uint16), want_rad)
+        assert np.array_equal(dirs.cpu().numpy().view(np.uint16), want_dir)
+    finally:
+        a.close()
+        b.close()
+        orc.close()

@@ -14,4 +14,4 @@ for v in shipped c32 c64; do
   env TMPDIR=/tmp $L timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/cf_$v -o run --output-format csv -- python3 tools/compose_bench.py > $OUT/cf_$v.log 2>&1 || { echo "fetch $v failed"; exit 1; }
   env TMPDIR=/tmp $L timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/cw_$v -o run --output-format csv -- python3 tools/compose_bench.py > $OUT/cw_$v.log 2>&1 || { echo "write $v failed"; exit 1; }
 done
-echo done
+echo done1
