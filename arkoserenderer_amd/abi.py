@@ -51,6 +51,7 @@ ARK_DDGI_SUN_BVH_AUTO = 0
 ARK_DDGI_SUN_BVH_WORLD = 1
 ARK_DDGI_SUN_BVH_LIGHT_SPACE = 2
 ARK_DDGI_FLAG_SERIAL_FRAMES = 0x1
+ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD = 0x2
 
 ARK_TEX_RGBA8_UNORM = 0
 ARK_TEX_RGBA8_SRGB = 1
@@ -284,6 +285,8 @@ class ArkDdgiBvhStats(C.Structure):
         ("bvh_rebuilds", C.c_uint32),
         ("bvh_rebuild_ms", C.c_float),
         ("refit_version", C.c_uint32),
+        ("bvh_built_refit_version", C.c_uint32),
+        ("sun_built_refit_version", C.c_uint32),
     ]
 
 

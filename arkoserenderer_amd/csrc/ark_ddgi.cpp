@@ -1095,6 +1095,7 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
             st.bvhStats.sun_rebuilds = ++st.sunRebuilds;
             st.bvhStats.sun_build_ms = job->ms;
             st.sunRefitsSinceBuild = st.refitCount - job->refitsAt;
+            st.bvhStats.sun_built_refit_version = job->refitsAt;
             if (st.sunRefitsSinceBuild) {
                 // refits came in while it was built: its records follow them (every
                 // instance re-transformed, the light-space boxes refitted)
@@ -1111,8 +1112,11 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         // else: built for another context's sun; that context installs it
     }
     if (!st.sunWanted || !ctx->hasSun || st.sunJob || st.sunReqStreak < 2 || !sameDir(st.sunReqDir, ctx->sunDir)) return ARK_DDGI_OK;
-    // installed for this sun and not loosened by refits since it was built: nothing to do
-    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt) && st.sunRefitsSinceBuild == 0) return ARK_DDGI_OK;
+    // installed for this sun: rebuilt only when refits loosened it, one background build
+    // at a time (the world BVHs' first), and not with ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD
+    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt) &&
+        (st.sunRefitsSinceBuild == 0 || st.worldJob || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)))
+        return ARK_DDGI_OK;
     if (st.sunFailed && st.sunFailedVersion == st.version && sameDir(st.sunFailedDir, ctx->sunDir)) return ARK_DDGI_OK;
     auto job = std::make_unique<SunJob>();
     std::memcpy(job->dir, ctx->sunDir, sizeof(job->dir));
@@ -1120,7 +1124,7 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     job->refitsAt = st.refitCount;
     ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
-    job->t = std::thread(runSunJob, job.get(), st.device, st.triRecords, st.buildThreads);
+    job->t = std::thread(runSunJob, job.get(), st.device, st.triRecords, std::max(1, st.buildThreads / 2));
     st.sunJob = std::move(job);
     return ARK_DDGI_OK;
 }
@@ -1179,6 +1183,7 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         st.bvhStats.bvh_rebuilds = ++st.worldRebuilds;
         st.bvhStats.bvh_rebuild_ms = job->ms;
         st.refitsSinceBuild = st.refitCount - job->refitsAt; // refits since its snapshot
+        st.bvhStats.bvh_built_refit_version = job->refitsAt;
         if (st.refitsSinceBuild) {
             if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), true, s)) return rc;
             if (const int rc = enqueueRefit(ctx, st, s)) return rc;
@@ -1189,7 +1194,7 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         ++st.version;
         if (const int rc = refreshScene(ctx)) return rc;
     }
-    if (st.worldJob || st.refitsSinceBuild == 0) return ARK_DDGI_OK;
+    if (st.worldJob || st.refitsSinceBuild == 0 || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) return ARK_DDGI_OK;
     auto job = std::make_unique<WorldJob>();
     job->version = st.version;
     job->refitsAt = st.refitCount;
@@ -1201,7 +1206,8 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     }
     ARK_HIP(orderBegin(ctx, s));
     ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
-    job->t = std::thread(runWorldJob, job.get(), st.device, st.buildThreads);
+    // half the host threads: the other half stays with the frames being enqueued meanwhile
+    job->t = std::thread(runWorldJob, job.get(), st.device, std::max(1, st.buildThreads / 2));
     st.worldJob = std::move(job);
     st.refitsSinceBuild = 0;
     return ARK_DDGI_OK;
@@ -1259,7 +1265,7 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     ctx->Kmax = desc->max_probe_updates > 0 ? desc->max_probe_updates : ARK_DDGI_REFERENCE_MAX_PROBE_UPDATES;
     const int shards = desc->shard_count > 0 ? desc->shard_count : 1;
     if (ctx->Rmax > ARK_DDGI_MAX_RAYS_PER_PROBE || ctx->Z % shards != 0 || desc->shard_rank < 0 || desc->shard_rank >= shards ||
-        desc->sun_bvh < ARK_DDGI_SUN_BVH_AUTO || desc->sun_bvh > ARK_DDGI_SUN_BVH_LIGHT_SPACE || (desc->flags & ~ARK_DDGI_FLAG_SERIAL_FRAMES) ||
+        desc->sun_bvh < ARK_DDGI_SUN_BVH_AUTO || desc->sun_bvh > ARK_DDGI_SUN_BVH_LIGHT_SPACE || (desc->flags & ~(ARK_DDGI_FLAG_SERIAL_FRAMES | ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) ||
         desc->build_threads < 0) {
         delete ctx;
         return ARK_DDGI_E_INVALID_ARGUMENT;

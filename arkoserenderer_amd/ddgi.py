@@ -70,6 +70,7 @@ class DDGIConfig:
     # structure, serial frames (no frames in flight), host threads of the BVH builds
     sun_bvh: int = abi.ARK_DDGI_SUN_BVH_AUTO
     serial_frames: bool = False
+    background_rebuild: bool = True
     build_threads: int = 0
 
 
@@ -106,7 +107,7 @@ def desc_for(grid: ProbeGrid, z_far: float, config: DDGIConfig, device: int = 0,
     d.shard_rank = int(shard_rank)
     d.shard_count = int(shard_count)
     d.sun_bvh = int(config.sun_bvh)
-    d.flags = abi.ARK_DDGI_FLAG_SERIAL_FRAMES if config.serial_frames else 0
+    d.flags = (abi.ARK_DDGI_FLAG_SERIAL_FRAMES if config.serial_frames else 0) | (0 if config.background_rebuild else abi.ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)
     d.build_threads = int(config.build_threads)
     return d
 

@@ -160,8 +160,11 @@ typedef struct ArkDdgiDesc {
 #define ARK_DDGI_SUN_BVH_WORLD 1
 #define ARK_DDGI_SUN_BVH_LIGHT_SPACE 2
 /* ArkDdgiDesc.flags. SERIAL_FRAMES: every update runs in line on the caller's stream
- * (no traversal stream, no frames in flight); results are the same. */
+ * (no traversal stream, no frames in flight); results are the same. NO_BACKGROUND_REBUILD:
+ * after ark_ddgi_set_instances the BVHs are only refitted, never rebuilt in the background
+ * (a set_scene restores their tightness); results are the same. */
 #define ARK_DDGI_FLAG_SERIAL_FRAMES 0x1u
+#define ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD 0x2u
 
 /* RTVertex, scalar layout, 36 B (RTData.h:9-13 / NonPositionVertex SceneData.h). */
 typedef struct ArkRTVertex {
@@ -537,6 +540,8 @@ typedef struct ArkDdgiBvhStats {
     uint32_t bvh_rebuilds;  /* world BVHs rebuilt in the background after refits and installed */
     float bvh_rebuild_ms;   /* host time of the last such rebuild (0 = none) */
     uint32_t refit_version; /* refits (ark_ddgi_set_instances) since set_scene */
+    uint32_t bvh_built_refit_version; /* refit_version of the records the installed world BVHs were built from */
+    uint32_t sun_built_refit_version; /* the same for the installed light-space sun BVH */
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 

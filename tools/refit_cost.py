@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--continuous", action="store_true", help="one instance moved every frame for --frames frames, then back to static")
     ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--no-background", action="store_true", help="ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD: refits only (isolates the rebuild threads' cost)")
     ap.add_argument("--sun-turn", action="store_true", help="instead of refits: turn the sun by 10 deg, wait for the background rebuild, turn it back, wait again")
     args = ap.parse_args()
     import torch
@@ -48,7 +49,8 @@ def main():
     for name in args.config:
         sc, grid, R, zf = build(name)
         N = grid.probe_count()
-        cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+        cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True,
+                           background_rebuild=not args.no_background)
         node = D.DDGINode(cfg)
         node.construct(sc, grid, zf, light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
         app = [D.AppState(0)]
@@ -75,6 +77,9 @@ def main():
             n = len(inst0)
             st0 = node.ctx.bvh_stats()
             node.ctx.synchronize()
+            stream = torch.cuda.current_stream()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.frames)]
+            host_refit = 0.0
             t = time.perf_counter()
             for f in range(args.frames):
                 inst = inst0.copy()
@@ -82,7 +87,11 @@ def main():
                 m[f % n, 0, 3] += np.float32(0.3 * np.sin(0.1 * f))  # one instance a frame, back and forth
                 m[(f // n) % n, 2, 3] += np.float32(0.2)               # and one left displaced for n frames
                 inst["object_to_world"] = m.reshape(-1, 12)
+                ev[f][0].record(stream)
+                th = time.perf_counter()
                 node.ctx.set_instances_async(inst, sptr)
+                host_refit += time.perf_counter() - th
+                ev[f][1].record(stream)
                 node.execute(app[0], sptr)
                 app[0] = D.AppState(app[0].frame_index + 1)
                 if f % 50 == 49:
@@ -90,12 +99,13 @@ def main():
             node.ctx.synchronize()
             motion_s = time.perf_counter() - t
             st1 = node.ctx.bvh_stats()
-            # static again: until rebuilds started after the last refit are installed
+            refit_dev = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+            # static again: until BVHs built from the final records (after the last refit)
+            # are installed - the world BVHs and the light-space sun BVH
             t = time.perf_counter()
-            w0, s0 = st1.bvh_rebuilds, st1.sun_rebuilds
-            while time.perf_counter() - t < 120.0:
+            while time.perf_counter() - t < 120.0 and not args.no_background:
                 st = node.ctx.bvh_stats()
-                if st.bvh_rebuilds >= w0 + 1 and (not had_sun_bvh or st.sun_rebuilds >= s0 + 1):
+                if st.bvh_built_refit_version == st.refit_version and (not had_sun_bvh or st.sun_built_refit_version == st.refit_version):
                     break
                 node.execute(app[0], sptr)
                 app[0] = D.AppState(app[0].frame_index + 1)
@@ -107,6 +117,9 @@ def main():
             out["continuous"] = {
                 "frames": args.frames, "mrays_per_s_moving": round(N * R * args.frames / motion_s / 1e6, 1),
                 "ms_per_frame_moving": round(motion_s / args.frames * 1e3, 4),
+                "refit_device_ms": {"median": round(refit_dev[len(refit_dev) // 2], 4), "max": round(refit_dev[-1], 4)},
+                "refit_host_enqueue_ms": round(host_refit / args.frames * 1e3, 4), "background_rebuild": not args.no_background,
+                "built_refit_version": {"world": int(st2.bvh_built_refit_version), "sun": int(st2.sun_built_refit_version), "refits": int(st2.refit_version)},
                 "installs_while_moving": {"world": int(st1.bvh_rebuilds - st0.bvh_rebuilds), "sun": int(st1.sun_rebuilds - st0.sun_rebuilds)},
                 "world_rebuild_ms": round(st2.bvh_rebuild_ms, 1), "sun_rebuild_ms": round(st2.sun_build_ms, 1),
                 "settled_after_s": round(settle_s, 2), "sun_bvh_installed": bool(st2.sun_node_count > 0),
