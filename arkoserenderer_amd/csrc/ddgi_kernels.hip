@@ -2422,7 +2422,7 @@ hipError_t launch_rt_reflections(const SceneArgs& sc, const FrameArgs& f, const 
 hipError_t launch_lighting_compose(const FrameArgs& f, const ArkComposeDesc& c, hipStream_t s)
 {
     if (c.width == 0 || c.height == 0) return hipSuccess;
-    const uint64_t tiles = static_cast<uint64_t>((c.width + 15u) / 16u) * ((c.height + 15u) / 16u);
+    const uint64_t tiles = static_cast<uint64_t>((c.width + 63u) / 64u) * ((c.height + 3u) / 4u); // 64 x 4 tiles (ddgi_compose.inc)
     if (tiles > (1ull << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dev::k_lighting_compose, dim3(static_cast<uint32_t>((tiles + 7u) / 8u * 8u)), dim3(256), 0, s, f, c);
     return hipGetLastError();

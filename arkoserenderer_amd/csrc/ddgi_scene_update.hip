@@ -253,19 +253,20 @@ __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ n
         }
     }
     // the node's grid and its children's planes, rounded outward (collapse_bvh8)
-    double step[3], p[3];
+    double step[3], p[3], inv[3];
     for (int a = 0; a < 3; ++a) {
         int e;
         quantGrid(nlo[a], nhi[a], e, p[a]);
         step[a] = ldexp(1.0, e);
+        inv[a] = ldexp(1.0, -e); // exact: the step is a power of two (no double divide per plane)
         nd.p[a] = static_cast<float>(p[a]);
         nd.e[a] = static_cast<uint8_t>(e + 127);
     }
     for (int s = 0; s < 8; ++s) {
         if (!((used >> s) & 1u)) continue;
         for (int a = 0; a < 3; ++a) {
-            double ql = floor((static_cast<double>(clo[s][a]) - p[a]) / step[a]);
-            double qh = ceil((static_cast<double>(chi[s][a]) - p[a]) / step[a]);
+            double ql = floor((static_cast<double>(clo[s][a]) - p[a]) * inv[a]);
+            double qh = ceil((static_cast<double>(chi[s][a]) - p[a]) * inv[a]);
             ql = fmin(255.0, fmax(0.0, ql));
             qh = fmin(255.0, fmax(0.0, qh));
             while (ql > 0.0 && static_cast<double>(static_cast<float>(p[a] + ql * step[a])) > clo[s][a]) ql -= 1.0;
