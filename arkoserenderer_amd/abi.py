@@ -287,6 +287,7 @@ class ArkDdgiBvhStats(C.Structure):
         ("refit_version", C.c_uint32),
         ("bvh_built_refit_version", C.c_uint32),
         ("sun_built_refit_version", C.c_uint32),
+        ("bvh_rebuild_failures", C.c_uint32),
     ]
 
 

@@ -292,6 +292,7 @@ struct SceneStore {
     uint32_t refitsSinceBuild = 0, sunRefitsSinceBuild = 0;
     std::unique_ptr<WorldJob> worldJob;
     uint32_t worldRebuilds = 0, refitCount = 0;
+    bool worldRebuildFailed = false;
     std::vector<Retired> retired;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
@@ -1141,7 +1142,15 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     if (st.worldJob && st.worldJob->done.load(std::memory_order_acquire)) {
         std::unique_ptr<WorldJob> job = std::move(st.worldJob);
         job->t.join();
-        if (!job->ok) return ctx->fail(ARK_DDGI_E_DEVICE, "background BVH rebuild failed: %s", job->error.c_str());
+        if (!job->ok) {
+            // the refitted BVHs stay (results do not depend on the tree); no more
+            // background rebuilds of this scene (a set_scene builds anew), reported in
+            // the stats and last_error, the update goes on
+            st.worldRebuildFailed = true;
+            st.bvhStats.bvh_rebuild_failures++;
+            ctx->lastError = "background BVH rebuild failed: " + job->error;
+            return ARK_DDGI_OK;
+        }
         ARK_HIP(installBarrier(ctx, s));
         // the shading records in the new record order (before the old ones are retired)
         DeviceBuffer tn;
@@ -1194,7 +1203,7 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         ++st.version;
         if (const int rc = refreshScene(ctx)) return rc;
     }
-    if (st.worldJob || st.refitsSinceBuild == 0 || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) return ARK_DDGI_OK;
+    if (st.worldJob || st.refitsSinceBuild == 0 || st.worldRebuildFailed || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) return ARK_DDGI_OK;
     auto job = std::make_unique<WorldJob>();
     job->version = st.version;
     job->refitsAt = st.refitCount;

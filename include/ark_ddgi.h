@@ -542,6 +542,8 @@ typedef struct ArkDdgiBvhStats {
     uint32_t refit_version; /* refits (ark_ddgi_set_instances) since set_scene */
     uint32_t bvh_built_refit_version; /* refit_version of the records the installed world BVHs were built from */
     uint32_t sun_built_refit_version; /* the same for the installed light-space sun BVH */
+    uint32_t bvh_rebuild_failures;    /* background world rebuilds that failed (the refitted BVHs stay; no more
+                                       * background rebuilds of this scene) */
 } ArkDdgiBvhStats;
 int ark_ddgi_get_bvh_stats(ArkDdgiCtx* ctx, ArkDdgiBvhStats* out_stats);
 
