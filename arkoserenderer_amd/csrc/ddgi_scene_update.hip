@@ -193,95 +193,100 @@ __device__ __forceinline__ void quantGrid(float L, float H, int& e, double& p)
     }
 }
 
+// One level of the refit, eight lanes per node - lane s owns child slot s: its box (the
+// child node's from the level below, or its leaf triangles'), the node's box by a
+// reduction over the eight lanes, the node's grid (every lane alike), then the slot's
+// outward-rounded planes. (One thread per node walked the eight slots and up to 24
+// triangle records in a row: C4 refits took 4.0 ms, profiles/r06_f_refit_continuous_bg.log.)
 __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ nodes, const GpuTriangle* __restrict__ tris, float* __restrict__ boxes,
                                                      const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra, const uint32_t* __restrict__ bounds)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const uint32_t n = order[i];
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = t >> 3, s = t & 7u;
+    const bool live = i < count; // a node's eight lanes are live or not together (count nodes = 8 count lanes)
+    if (!__any(live)) return;
+    const uint32_t n = live ? order[i] : 0u;
     // the inflation of this BVH's boxes from the refit's bounds (RefitBoxArgs)
     const float inflateAbs = ra.light ? fmaxf(ra.inflate_min, 2.0f * inflationBox(bounds + 6) + 2e-6f * fromOrderedBits(bounds[12]))
                                       : fmaxf(ra.inflate_min, inflationBox(bounds));
-    GpuBvh8Node nd = nodes[n];
-    float clo[8][3], chi[8][3];
-    float nlo[3] = { INFINITY, INFINITY, INFINITY }, nhi[3] = { -INFINITY, -INFINITY, -INFINITY };
-    uint32_t used = 0, internal = 0;
-    for (int s = 0; s < 8; ++s) {
-        float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
-        if ((nd.imask >> s) & 1u) {
-            // the child node's box (its level ran before this one), already inflated
-            const float* b = boxes + 6u * static_cast<size_t>(nd.child_base + internal++);
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = b[a];
-                hi[a] = b[3 + a];
-            }
-        } else if ((nd.leaf_mask >> s) & 1u) {
-            // triangle i of the slot at tri_base + s + stride i, its row's consecutive bits
-            for (uint32_t k = 0; k < static_cast<uint32_t>(kBvh8MaxLeafSize); ++k) {
-                const uint32_t pos = static_cast<uint32_t>(s) + nd.tri_stride * k;
-                if (pos >= 24u || !((nd.leaf_tris >> pos) & 1u)) break;
-                const float4* rec = reinterpret_cast<const float4*>(tris + nd.tri_base + pos);
-                const float4 a = rec[0], b = rec[1], c = rec[2];
-                if (ra.light) {
-                    // the light coordinates build_sun_bvh boxed
-                    float L[3][3], m;
-                    lightVertices(a, b, c, ra.frame, L, m);
-                    for (int ax = 0; ax < 3; ++ax) {
-                        lo[ax] = fminf(lo[ax], fminf(L[0][ax], fminf(L[1][ax], L[2][ax])));
-                        hi[ax] = fmaxf(hi[ax], fmaxf(L[0][ax], fmaxf(L[1][ax], L[2][ax])));
-                    }
-                    continue;
-                }
-                // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2
-                const float v0[3] = { a.x, a.y, a.z }, e1[3] = { a.w, b.x, b.y }, e2[3] = { b.z, b.w, c.x };
-                for (int ax = 0; ax < 3; ++ax) {
-                    const float p1 = v0[ax] + e1[ax], p2 = v0[ax] + e2[ax];
-                    lo[ax] = fminf(lo[ax], fminf(v0[ax], fminf(p1, p2)));
-                    hi[ax] = fmaxf(hi[ax], fmaxf(v0[ax], fmaxf(p1, p2)));
-                }
-            }
-            inflateBox(lo, hi, inflateAbs);
-        } else {
-            continue;
-        }
-        used |= 1u << s;
+    const uint4 hdr = live ? reinterpret_cast<const uint4*>(nodes + n)[1] : make_uint4(0u, 0u, 0u, 0u); // child_base, tri_base, leaf_tris, stride | leaf_mask << 8
+    const uint32_t imask = live ? (reinterpret_cast<const uint32_t*>(nodes + n)[3] >> 24) : 0u;
+    const uint32_t childBase = hdr.x, triBase = hdr.y, leafTris = hdr.z, stride = hdr.w & 0xffu, leafMask = (hdr.w >> 8) & 0xffu;
+    float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    bool used = false;
+    if ((imask >> s) & 1u) {
+        // the child node's box (its level ran before this one), already inflated
+        const float* b = boxes + 6u * static_cast<size_t>(childBase + static_cast<uint32_t>(__builtin_popcount(imask & ((1u << s) - 1u))));
         for (int a = 0; a < 3; ++a) {
-            clo[s][a] = lo[a];
-            chi[s][a] = hi[a];
-            nlo[a] = fminf(nlo[a], lo[a]);
-            nhi[a] = fmaxf(nhi[a], hi[a]);
+            lo[a] = b[a];
+            hi[a] = b[3 + a];
         }
+        used = true;
+    } else if ((leafMask >> s) & 1u) {
+        // triangle k of the slot at tri_base + s + stride k, its row's consecutive bits
+        for (uint32_t k = 0; k < static_cast<uint32_t>(kBvh8MaxLeafSize); ++k) {
+            const uint32_t pos = s + stride * k;
+            if (pos >= 24u || !((leafTris >> pos) & 1u)) break;
+            const float4* rec = reinterpret_cast<const float4*>(tris + triBase + pos);
+            const float4 a = rec[0], b = rec[1], c = rec[2];
+            if (ra.light) {
+                // the light coordinates build_sun_bvh boxed
+                float L[3][3], m;
+                lightVertices(a, b, c, ra.frame, L, m);
+                for (int ax = 0; ax < 3; ++ax) {
+                    lo[ax] = fminf(lo[ax], fminf(L[0][ax], fminf(L[1][ax], L[2][ax])));
+                    hi[ax] = fmaxf(hi[ax], fmaxf(L[0][ax], fmaxf(L[1][ax], L[2][ax])));
+                }
+                continue;
+            }
+            // the triangle Möller–Trumbore tests: v0, v0 + e1, v0 + e2
+            const float v0[3] = { a.x, a.y, a.z }, e1[3] = { a.w, b.x, b.y }, e2[3] = { b.z, b.w, c.x };
+            for (int ax = 0; ax < 3; ++ax) {
+                const float p1 = v0[ax] + e1[ax], p2 = v0[ax] + e2[ax];
+                lo[ax] = fminf(lo[ax], fminf(v0[ax], fminf(p1, p2)));
+                hi[ax] = fmaxf(hi[ax], fmaxf(v0[ax], fmaxf(p1, p2)));
+            }
+        }
+        inflateBox(lo, hi, inflateAbs);
+        used = true;
     }
-    // the node's grid and its children's planes, rounded outward (collapse_bvh8)
-    double step[3], p[3], inv[3];
+    // the node's box over its eight lanes (an unused slot contributes +-inf)
+    float nlo[3] = { lo[0], lo[1], lo[2] }, nhi[3] = { hi[0], hi[1], hi[2] };
+    for (int m = 1; m < 8; m <<= 1)
+        for (int a = 0; a < 3; ++a) {
+            nlo[a] = fminf(nlo[a], __shfl_xor(nlo[a], m, 8));
+            nhi[a] = fmaxf(nhi[a], __shfl_xor(nhi[a], m, 8));
+        }
+    if (!live) return;
+    // the node's grid (each lane alike) and this slot's planes, rounded outward (collapse_bvh8)
+    GpuBvh8Node* nd = nodes + n;
     for (int a = 0; a < 3; ++a) {
         int e;
-        quantGrid(nlo[a], nhi[a], e, p[a]);
-        step[a] = ldexp(1.0, e);
-        inv[a] = ldexp(1.0, -e); // exact: the step is a power of two (no double divide per plane)
-        nd.p[a] = static_cast<float>(p[a]);
-        nd.e[a] = static_cast<uint8_t>(e + 127);
-    }
-    for (int s = 0; s < 8; ++s) {
-        if (!((used >> s) & 1u)) continue;
-        for (int a = 0; a < 3; ++a) {
-            double ql = floor((static_cast<double>(clo[s][a]) - p[a]) * inv[a]);
-            double qh = ceil((static_cast<double>(chi[s][a]) - p[a]) * inv[a]);
-            ql = fmin(255.0, fmax(0.0, ql));
-            qh = fmin(255.0, fmax(0.0, qh));
-            while (ql > 0.0 && static_cast<double>(static_cast<float>(p[a] + ql * step[a])) > clo[s][a]) ql -= 1.0;
-            while (qh < 255.0 && static_cast<double>(static_cast<float>(p[a] + qh * step[a])) < chi[s][a]) qh += 1.0;
-            nd.qlo[a][s] = static_cast<uint8_t>(ql);
-            nd.qhi[a][s] = static_cast<uint8_t>(qh);
+        double p;
+        quantGrid(nlo[a], nhi[a], e, p);
+        const double step = ldexp(1.0, e), inv = ldexp(1.0, -e); // exact: the step is a power of two
+        if (s == 0) {
+            nd->p[a] = static_cast<float>(p);
+            nd->e[a] = static_cast<uint8_t>(e + 127);
         }
+        if (!used) continue;
+        double ql = floor((static_cast<double>(lo[a]) - p) * inv);
+        double qh = ceil((static_cast<double>(hi[a]) - p) * inv);
+        ql = fmin(255.0, fmax(0.0, ql));
+        qh = fmin(255.0, fmax(0.0, qh));
+        while (ql > 0.0 && static_cast<double>(static_cast<float>(p + ql * step)) > lo[a]) ql -= 1.0;
+        while (qh < 255.0 && static_cast<double>(static_cast<float>(p + qh * step)) < hi[a]) qh += 1.0;
+        nd->qlo[a][s] = static_cast<uint8_t>(ql);
+        nd->qhi[a][s] = static_cast<uint8_t>(qh);
     }
-    nodes[n] = nd;
-    // this node's box as its parent's child box (inflated, as writeNode does per level)
-    inflateBox(nlo, nhi, inflateAbs);
-    float* b = boxes + 6u * static_cast<size_t>(n);
-    for (int a = 0; a < 3; ++a) {
-        b[a] = nlo[a];
-        b[3 + a] = nhi[a];
+    if (s == 0) {
+        // this node's box as its parent's child box (inflated, as writeNode does per level)
+        inflateBox(nlo, nhi, inflateAbs);
+        float* b = boxes + 6u * static_cast<size_t>(n);
+        for (int a = 0; a < 3; ++a) {
+            b[a] = nlo[a];
+            b[3 + a] = nhi[a];
+        }
     }
 }
 
@@ -329,7 +334,8 @@ hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float
                               const uint32_t* bounds, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_refit_nodes, dim3((count + 127u) / 128u), dim3(128), 0, s, nodes, tris, boxes, order, count, a, bounds);
+    const uint64_t lanes = 8ull * count; // eight lanes per node
+    hipLaunchKernelGGL(dev::k_refit_nodes, dim3(static_cast<uint32_t>((lanes + 127u) / 128u)), dim3(128), 0, s, nodes, tris, boxes, order, count, a, bounds);
     return hipGetLastError();
 }
 
