@@ -293,6 +293,8 @@ struct SceneStore {
     std::unique_ptr<WorldJob> worldJob;
     uint32_t worldRebuilds = 0, refitCount = 0;
     bool worldRebuildFailed = false;
+    bool sunTurn = false;     // a loosened light-space BVH's rebuild goes before the next world one
+    uint32_t worldYields = 0; // world starts skipped for it since the last world start
     std::vector<Retired> retired;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
@@ -1127,6 +1129,7 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
     job->t = std::thread(runSunJob, job.get(), st.device, st.triRecords, std::max(1, st.buildThreads / 2));
     st.sunJob = std::move(job);
+    st.sunTurn = false;
     return ARK_DDGI_OK;
 }
 
@@ -1204,6 +1207,14 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         if (const int rc = refreshScene(ctx)) return rc;
     }
     if (st.worldJob || st.refitsSinceBuild == 0 || st.worldRebuildFailed || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) return ARK_DDGI_OK;
+    // one background build at a time, taking turns with a loosened light-space BVH's
+    // rebuild (it yields a few times at most: the sun's may wait on another context's sun)
+    if (st.sunJob) return ARK_DDGI_OK;
+    const bool sunLoosened = st.sunWanted && st.sunArgs.sun_root >= 0 && st.sunRefitsSinceBuild > 0;
+    if (st.sunTurn && sunLoosened && st.worldYields < 4) {
+        ++st.worldYields;
+        return ARK_DDGI_OK;
+    }
     auto job = std::make_unique<WorldJob>();
     job->version = st.version;
     job->refitsAt = st.refitCount;
@@ -1218,6 +1229,8 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     // half the host threads: the other half stays with the frames being enqueued meanwhile
     job->t = std::thread(runWorldJob, job.get(), st.device, std::max(1, st.buildThreads / 2));
     st.worldJob = std::move(job);
+    st.sunTurn = true;
+    st.worldYields = 0;
     st.refitsSinceBuild = 0;
     return ARK_DDGI_OK;
 }
