@@ -8,6 +8,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -16,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -192,7 +194,7 @@ struct SunJob {
     }
 };
 
-// A background rebuild of the world BVHs after refits (worldRebuildStep; the reference
+// A background rebuild of the world BVHs after refits (worldCollect / worldStart; the reference
 // rebuilds its TLAS in full every 60 frames, GpuScene.cpp:998-1010): a host thread takes
 // a device snapshot of the refitted triangle records, builds the three hit-mask classes'
 // BVHs anew from them (set_scene's builder), keeps every record's words as they were
@@ -254,7 +256,7 @@ struct SceneStore {
     uint32_t version = 0;
     float inflateAbs = 0.0f;
     uint64_t triRecords = 0; // triangle records of the world BVHs (holes included)
-    DeviceBuffer refitInst, refitBoxes, refitOrder, refitBounds;
+    DeviceBuffer refitInst, refitBoxes, refitOrder;
     std::vector<uint32_t> levelOffsets; // refitOrder[levelOffsets[i] .. [i + 1]): the nodes of one depth, deepest first
     // the light-space BVH follows the motion: refitted with the world BVHs (its records
     // re-transformed, its boxes of their light coordinates)
@@ -266,10 +268,18 @@ struct SceneStore {
     // the refit's transforms: the last ones uploaded (dirty = changed since the records
     // were written); pinned staging of the stream-ordered uploads, two sets in turn
     std::vector<RefitInstance> refitHost;
-    void* stage[2] { nullptr, nullptr };
-    size_t stageBytes[2] { 0, 0 };
-    hipEvent_t stageDone[2] { nullptr, nullptr };
+    // pinned staging of the per-frame uploads, a ring: a slot is reused once its copy (a
+    // few calls back) has run, so the host runs up to kStageSlots / 2 frames of
+    // set_instances_async ahead of the device (two slots: one frame, and every call
+    // waited for the previous frame's refit)
+    static constexpr int kStageSlots = 8;
+    void* stage[kStageSlots] {};
+    size_t stageBytes[kStageSlots] {};
+    hipEvent_t stageDone[kStageSlots] {};
     int stageNext = 0;
+    // object-space bounds of every instance's triangles (set_scene): the refit's world and
+    // light-space bounds, for its box inflation, from the instances' transforms on the host
+    std::vector<std::array<float, 6>> instObjBox;
     // the light-space BVH follows the sun: set_scene chose it (sunWanted), and after a
     // sun-direction change it is rebuilt in the background (sunRebuildStep)
     bool sunWanted = false;
@@ -287,14 +297,15 @@ struct SceneStore {
     float sunFailedDir[3] { 0, 0, 0 };
     uint32_t sunFailedVersion = 0;
     uint32_t sunFailures = 0;
-    // the world BVHs' background rebuild (worldRebuildStep): refits since the installed
+    // the world BVHs' background rebuild (worldCollect / worldStart): refits since the installed
     // BVHs were built, the running job, rebuilds installed
     uint32_t refitsSinceBuild = 0, sunRefitsSinceBuild = 0;
     std::unique_ptr<WorldJob> worldJob;
     uint32_t worldRebuilds = 0, refitCount = 0;
     bool worldRebuildFailed = false;
-    bool sunTurn = false;     // a loosened light-space BVH's rebuild goes before the next world one
-    uint32_t worldYields = 0; // world starts skipped for it since the last world start
+    // the background build started last (loosenedTurn: loosened BVHs take turns)
+    enum : uint8_t { kBackgroundNone, kBackgroundWorld, kBackgroundSun };
+    uint8_t lastBackground = kBackgroundNone;
     std::vector<Retired> retired;
     SceneStore() = default;
     SceneStore(const SceneStore&) = delete;
@@ -309,12 +320,12 @@ struct SceneStore {
             r.buf.release();
             if (r.done) (void)hipEventDestroy(r.done);
         }
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kStageSlots; ++i) {
             if (stage[i]) (void)hipHostFree(stage[i]);
             if (stageDone[i]) (void)hipEventDestroy(stageDone[i]);
         }
         for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
-                                 &refitBoxes, &refitOrder, &refitBounds, &sunRefitOrder, &sunRefitBoxes })
+                                 &refitBoxes, &refitOrder, &sunRefitOrder, &sunRefitBoxes })
             b->release();
     }
 };
@@ -428,7 +439,7 @@ struct ArkDdgiCtx {
     uint32_t nextProbeIndex = 0; // (first + K) % N of the last update, or of a loaded state
     uint32_t lastFirst = 0, lastK = 0; // the last update's window (ark_ddgi_window_exchange_info)
     // a refit or an installed rebuild enqueued on a caller's stream (ark_ddgi_set_instances_async,
-    // worldRebuildStep): the next update's traversal on the traversal stream waits for it
+    // worldCollect): the next update's traversal on the traversal stream waits for it
     hipEvent_t evRefit = nullptr;
     bool refitPending = false;
 
@@ -710,12 +721,12 @@ void collectRetired(SceneStore& st)
 }
 
 // `bytes` of host data into `dst` in stream order on `s`, through the store's pinned
-// staging (two sets in turn; a set is reused once its previous copy has run).
+// staging ring (a slot is reused once its previous copy has run).
 hipError_t stagedUpload(SceneStore& st, void* dst, const void* src, size_t bytes, hipStream_t s)
 {
     if (bytes == 0) return hipSuccess;
     const int i = st.stageNext;
-    st.stageNext ^= 1;
+    st.stageNext = (i + 1) % SceneStore::kStageSlots;
     hipError_t e = hipSuccess;
     if (!st.stageDone[i] && (e = hipEventCreateWithFlags(&st.stageDone[i], hipEventDisableTiming)) != hipSuccess) return e;
     if (st.stageBytes[i]) (void)hipEventSynchronize(st.stageDone[i]); // its last copy (an earlier frame's) has run
@@ -731,36 +742,79 @@ hipError_t stagedUpload(SceneStore& st, void* dst, const void* src, size_t bytes
     return hipEventRecord(st.stageDone[i], s);
 }
 
+// The boxes' absolute inflations of a refit, as set_scene and build_sun_bvh derive them
+// from the records' bounds (world: bvh8_inflation_box, 1e-6 |diagonal|; light space:
+// 2 x 1e-6 |light diagonal| + 2e-6 max |world coordinate|), here from bounds that
+// contain the records: every instance's object-space box (st.instObjBox) through its
+// current transform (st.refitHost), corner by corner in double, and those corners in the
+// sun's frame. Never less than the build's (st.inflateAbs, st.sunInflateAbs). Larger
+// bounds only loosen the boxes; the hits do not depend on them.
+void refitInflations(const SceneStore& st, float& world, float& light)
+{
+    double lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    double llo[3] = { INFINITY, INFINITY, INFINITY }, lhi[3] = { -INFINITY, -INFINITY, -INFINITY };
+    double maxAbs = 0.0;
+    const size_t n = std::min(st.instObjBox.size(), st.refitHost.size());
+    for (size_t i = 0; i < n; ++i) {
+        const std::array<float, 6>& b = st.instObjBox[i];
+        if (!(b[0] <= b[3])) continue; // no triangles
+        const float* M = st.refitHost[i].m;
+        for (int c = 0; c < 8; ++c) {
+            const double P[3] = { b[(c & 1) ? 3 : 0], b[(c & 2) ? 4 : 1], b[(c & 4) ? 5 : 2] };
+            double w[3];
+            for (int r = 0; r < 3; ++r) {
+                w[r] = double(M[4 * r]) * P[0] + double(M[4 * r + 1]) * P[1] + double(M[4 * r + 2]) * P[2] + double(M[4 * r + 3]);
+                lo[r] = std::min(lo[r], w[r]);
+                hi[r] = std::max(hi[r], w[r]);
+                maxAbs = std::max(maxAbs, std::fabs(w[r]));
+            }
+            for (int r = 0; r < 3; ++r) {
+                const double L = st.sunFrameD[3 * r] * w[0] + st.sunFrameD[3 * r + 1] * w[1] + st.sunFrameD[3 * r + 2] * w[2];
+                llo[r] = std::min(llo[r], L);
+                lhi[r] = std::max(lhi[r], L);
+            }
+        }
+    }
+    auto box = [](const double* l, const double* h) {
+        double d2 = 0.0;
+        for (int a = 0; a < 3; ++a)
+            if (h[a] >= l[a]) d2 += (h[a] - l[a]) * (h[a] - l[a]);
+        return 1e-6 * std::sqrt(d2);
+    };
+    // rounded up to fp32 (the bounds' own rounding to fp32 in the builds is within it)
+    world = std::max(st.inflateAbs, std::nextafter(static_cast<float>(box(lo, hi)), INFINITY));
+    light = std::max(st.sunInflateAbs, std::nextafter(static_cast<float>(2.0 * box(llo, lhi) + 2e-6 * maxAbs), INFINITY));
+}
+
 // The refit of every BVH of the scene on `s`: the records of dirty instances re-transformed
 // (st.refitInst), the world BVHs' boxes level by level, and the light-space sun BVH's
-// records and light-space boxes. Inflations from the device-side bounds.
+// records and light-space boxes. The boxes' inflations from the instances' bounds
+// (refitInflations, host).
 int enqueueRefit(ArkDdgiCtx* ctx, SceneStore& st, hipStream_t s)
 {
-    uint32_t* bounds = st.refitBounds.as<uint32_t>();
-    ARK_HIP(launch_refit_bounds_reset(bounds, s));
+    float inflateWorld = 0.0f, inflateLight = 0.0f;
+    refitInflations(st, inflateWorld, inflateLight);
     GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(static_cast<char*>(st.nodes.ptr) + st.args.tri_byte_offset);
-    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(),
-                              bounds, s));
+    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(), s));
     RefitBoxArgs world {};
-    world.inflate_min = st.inflateAbs;
+    world.inflate = inflateWorld;
     world.light = 0;
     const uint32_t* order = st.refitOrder.as<uint32_t>();
     for (size_t l = 0; l + 1 < st.levelOffsets.size(); ++l)
         ARK_HIP(launch_refit_nodes(st.nodes.as<GpuBvh8Node>(), tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l], st.levelOffsets[l + 1] - st.levelOffsets[l],
-                                   world, bounds, s));
+                                   world, s));
     if (st.sunArgs.sun_root >= 0 && st.sunTriRecords && !st.sunLevelOffsets.empty()) {
         GpuTriangle* stris = const_cast<GpuTriangle*>(st.sunArgs.sun_tris);
         ARK_HIP(launch_refit_tris(stris, static_cast<uint32_t>(st.sunTriRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(),
-                                  st.positions.as<float>(), bounds, s));
+                                  st.positions.as<float>(), s));
         RefitBoxArgs light {};
         std::memcpy(light.frame, st.sunFrameD, sizeof(light.frame));
-        light.inflate_min = st.sunInflateAbs;
+        light.inflate = inflateLight;
         light.light = 1;
-        ARK_HIP(launch_refit_light_bounds(stris, static_cast<uint32_t>(st.sunTriRecords), light, bounds, s));
         const uint32_t* so = st.sunRefitOrder.as<uint32_t>();
         for (size_t l = 0; l + 1 < st.sunLevelOffsets.size(); ++l)
             ARK_HIP(launch_refit_nodes(const_cast<GpuBvh8Node*>(st.sunArgs.sun_nodes), stris, st.sunRefitBoxes.as<float>(), so + st.sunLevelOffsets[l],
-                                       st.sunLevelOffsets[l + 1] - st.sunLevelOffsets[l], light, bounds, s));
+                                       st.sunLevelOffsets[l + 1] - st.sunLevelOffsets[l], light, s));
     }
     return ARK_DDGI_OK;
 }
@@ -775,7 +829,6 @@ int uploadRefitInstances(ArkDdgiCtx* ctx, SceneStore& st, const ArkRTInstance* i
         allDirty = true;
     }
     if (!st.refitInst.ptr || st.refitInst.bytes < std::max<size_t>(16, count * sizeof(RefitInstance))) ARK_HIP(st.refitInst.alloc(std::max<size_t>(16, count * sizeof(RefitInstance))));
-    if (!st.refitBounds.ptr) ARK_HIP(st.refitBounds.alloc(kRefitBoundsWords * sizeof(uint32_t)));
     for (uint32_t ii = 0; ii < count; ++ii) {
         const float* M = instances[ii].object_to_world;
         const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
@@ -1039,8 +1092,9 @@ hipError_t installDone(ArkDdgiCtx* ctx, hipStream_t s)
 // old one, and refitted forward when refits came in between - and a new one is started
 // when the scene chose the light-space BVH at set_scene but holds none for this
 // direction. Until it is installed the sun's shadow rays traverse the world BVHs
-// (deriveSceneArgs), with the same results. One rebuild at a time per scene.
-int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
+// (deriveSceneArgs), with the same results. sunCollect: the request streak and a
+// finished rebuild; sunStartKind / sunStart: a new one.
+int sunCollect(ArkDdgiCtx* ctx, hipStream_t s)
 {
     SceneStore& st = *ctx->sceneStore;
     auto sameDir = [](const float* a, const float* b) { return std::memcmp(a, b, 3 * sizeof(float)) == 0; };
@@ -1114,13 +1168,38 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         }
         // else: built for another context's sun; that context installs it
     }
-    if (!st.sunWanted || !ctx->hasSun || st.sunJob || st.sunReqStreak < 2 || !sameDir(st.sunReqDir, ctx->sunDir)) return ARK_DDGI_OK;
-    // installed for this sun: rebuilt only when refits loosened it, one background build
-    // at a time (the world BVHs' first), and not with ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD
-    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt) &&
-        (st.sunRefitsSinceBuild == 0 || st.worldJob || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)))
-        return ARK_DDGI_OK;
-    if (st.sunFailed && st.sunFailedVersion == st.version && sameDir(st.sunFailedDir, ctx->sunDir)) return ARK_DDGI_OK;
+    return ARK_DDGI_OK;
+}
+
+// The sun rebuild this context's sun asks for: kSunNone; kSunMissing when the scene holds
+// no light-space BVH for it (started at once, even beside a world rebuild); kSunLoosened
+// when the installed one was built for it and refits have loosened it since (a
+// background rebuild like the world BVHs', one at a time with them, not with
+// ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD). Only on a stable request, and not again after a
+// failure for the same direction and scene version.
+enum SunStart { kSunNone, kSunLoosened, kSunMissing };
+SunStart sunStartKind(const ArkDdgiCtx* ctx)
+{
+    const SceneStore& st = *ctx->sceneStore;
+    auto sameDir = [](const float* a, const float* b) { return std::memcmp(a, b, 3 * sizeof(float)) == 0; };
+    if (!st.sunWanted || !ctx->hasSun || st.sunJob || st.sunReqStreak < 2 || !sameDir(st.sunReqDir, ctx->sunDir)) return kSunNone;
+    if (st.sunFailed && st.sunFailedVersion == st.version && sameDir(st.sunFailedDir, ctx->sunDir)) return kSunNone;
+    if (st.sunArgs.sun_root >= 0 && sameDir(ctx->sunDir, st.sunDirBuilt))
+        return (st.sunRefitsSinceBuild == 0 || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) ? kSunNone : kSunLoosened;
+    return kSunMissing;
+}
+
+// A world rebuild is wanted while refits have loosened the installed BVHs (and none
+// failed, and background rebuilds are on).
+bool worldStartWanted(const ArkDdgiCtx* ctx)
+{
+    const SceneStore& st = *ctx->sceneStore;
+    return !st.worldJob && st.refitsSinceBuild != 0 && !st.worldRebuildFailed && !(ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD);
+}
+
+int sunStart(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    SceneStore& st = *ctx->sceneStore;
     auto job = std::make_unique<SunJob>();
     std::memcpy(job->dir, ctx->sunDir, sizeof(job->dir));
     job->version = st.version;
@@ -1129,7 +1208,27 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     ARK_HIP(snapshotRecords(st, job->snap, job->evSnap, s));
     job->t = std::thread(runSunJob, job.get(), st.device, st.triRecords, std::max(1, st.buildThreads / 2));
     st.sunJob = std::move(job);
-    st.sunTurn = false;
+    st.lastBackground = SceneStore::kBackgroundSun;
+    return ARK_DDGI_OK;
+}
+
+// A loosened BVH's rebuild starts when no other background build runs; when both the
+// world BVHs and the light-space one are loosened they take turns (under continuous
+// motion each would otherwise start again the moment its last one is installed).
+bool loosenedTurn(const SceneStore& st, uint8_t mine, bool otherWanted)
+{
+    if (st.worldJob || st.sunJob) return false;
+    return !otherWanted || st.lastBackground != mine;
+}
+
+// sunCollect, then a sun rebuild to start (set_lights: the world BVHs' rebuilds are
+// left to the next update or set_instances)
+int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    if (const int rc = sunCollect(ctx, s)) return rc;
+    const SunStart k = sunStartKind(ctx);
+    if (k == kSunMissing || (k == kSunLoosened && loosenedTurn(*ctx->sceneStore, SceneStore::kBackgroundSun, worldStartWanted(ctx))))
+        return sunStart(ctx, s);
     return ARK_DDGI_OK;
 }
 
@@ -1138,8 +1237,8 @@ int sunRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
 // whose boxes loosen as instances move): a finished rebuild is installed on `s` -
 // behind the frames that may read the old BVHs, its shading records gathered into its
 // record order, and refitted forward when refits came in while it was built - and,
-// while refits have loosened the installed one, a new one is started.
-int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
+// while refits have loosened the installed one, a new one is started (worldStart).
+int worldCollect(ArkDdgiCtx* ctx, hipStream_t s)
 {
     SceneStore& st = *ctx->sceneStore;
     if (st.worldJob && st.worldJob->done.load(std::memory_order_acquire)) {
@@ -1206,15 +1305,12 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
         ++st.version;
         if (const int rc = refreshScene(ctx)) return rc;
     }
-    if (st.worldJob || st.refitsSinceBuild == 0 || st.worldRebuildFailed || (ctx->desc.flags & ARK_DDGI_FLAG_NO_BACKGROUND_REBUILD)) return ARK_DDGI_OK;
-    // one background build at a time, taking turns with a loosened light-space BVH's
-    // rebuild (it yields a few times at most: the sun's may wait on another context's sun)
-    if (st.sunJob) return ARK_DDGI_OK;
-    const bool sunLoosened = st.sunWanted && st.sunArgs.sun_root >= 0 && st.sunRefitsSinceBuild > 0;
-    if (st.sunTurn && sunLoosened && st.worldYields < 4) {
-        ++st.worldYields;
-        return ARK_DDGI_OK;
-    }
+    return ARK_DDGI_OK;
+}
+
+int worldStart(ArkDdgiCtx* ctx, hipStream_t s)
+{
+    SceneStore& st = *ctx->sceneStore;
     auto job = std::make_unique<WorldJob>();
     job->version = st.version;
     job->refitsAt = st.refitCount;
@@ -1229,8 +1325,7 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
     // half the host threads: the other half stays with the frames being enqueued meanwhile
     job->t = std::thread(runWorldJob, job.get(), st.device, std::max(1, st.buildThreads / 2));
     st.worldJob = std::move(job);
-    st.sunTurn = true;
-    st.worldYields = 0;
+    st.lastBackground = SceneStore::kBackgroundWorld;
     st.refitsSinceBuild = 0;
     return ARK_DDGI_OK;
 }
@@ -1240,8 +1335,16 @@ int worldRebuildStep(ArkDdgiCtx* ctx, hipStream_t s)
 int sceneMaintenance(ArkDdgiCtx* ctx, hipStream_t s)
 {
     collectRetired(*ctx->sceneStore);
-    if (const int rc = worldRebuildStep(ctx, s)) return rc;
-    return sunRebuildStep(ctx, s);
+    if (const int rc = worldCollect(ctx, s)) return rc;
+    if (const int rc = sunCollect(ctx, s)) return rc;
+    const SunStart k = sunStartKind(ctx);
+    if (k == kSunMissing) {
+        if (const int rc = sunStart(ctx, s)) return rc;
+    }
+    const bool world = worldStartWanted(ctx), sun = k == kSunLoosened;
+    if (world && loosenedTurn(*ctx->sceneStore, SceneStore::kBackgroundWorld, sun)) return worldStart(ctx, s);
+    if (sun && loosenedTurn(*ctx->sceneStore, SceneStore::kBackgroundSun, world)) return sunStart(ctx, s);
+    return ARK_DDGI_OK;
 }
 
 // Makes `st` the context's scene with the scene's lights: the per-context work sets
@@ -1664,6 +1767,29 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, st->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
     st->instHost.assign(s->instances, s->instances + s->instance_count);
     st->meshHost.assign(s->meshes, s->meshes + s->mesh_count);
+    // every instance's object-space box (refitInflations)
+    st->instObjBox.assign(s->instance_count, { INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY });
+    for (uint32_t ii = 0; ii < s->instance_count; ++ii) {
+        const ArkRTInstance& in = s->instances[ii];
+        const ArkRTTriangleMesh& mesh = s->meshes[in.rt_mesh_index];
+        std::array<float, 6>& box = st->instObjBox[ii];
+        std::mutex mu;
+        parallelFor(static_cast<size_t>(in.triangle_count) * 3u, opt.threads, [&](size_t b, size_t e) {
+            float lo[3] = { INFINITY, INFINITY, INFINITY }, hi[3] = { -INFINITY, -INFINITY, -INFINITY };
+            for (size_t k = b; k < e; ++k) {
+                const float* P = s->positions + (static_cast<int64_t>(mesh.first_vertex) + s->indices[static_cast<size_t>(mesh.first_index) + k]) * 3;
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min(lo[a], P[a]);
+                    hi[a] = std::max(hi[a], P[a]);
+                }
+            }
+            std::lock_guard<std::mutex> g(mu);
+            for (int a = 0; a < 3; ++a) {
+                box[a] = std::min(box[a], lo[a]);
+                box[3 + a] = std::max(box[3 + a], hi[a]);
+            }
+        });
+    }
     if ((rc = upload(ctx, st->meshes, s->meshes, s->mesh_count)) != 0) return rc;
     if ((rc = upload(ctx, st->materials, s->materials, s->material_count)) != 0) return rc;
     if ((rc = upload(ctx, st->instances, ginst.data(), ginst.size())) != 0) return rc;
@@ -1835,7 +1961,6 @@ int prepareRefit(ArkDdgiCtx* ctx, SceneStore& st)
     int rc;
     if ((rc = upload(ctx, st.refitOrder, order.data(), order.size())) != 0) return rc;
     ARK_HIP(st.refitBoxes.alloc(std::max<size_t>(16, n * 6 * sizeof(float))));
-    if (!st.refitBounds.ptr) ARK_HIP(st.refitBounds.alloc(kRefitBoundsWords * sizeof(uint32_t)));
     return ARK_DDGI_OK;
 }
 } // namespace

@@ -284,30 +284,22 @@ struct alignas(16) RefitInstance {
     uint32_t flip;         // det(object_to_world) < 0
     uint32_t dirty;        // its transform changed since the records were last written
 };
-// The refit's scene bounds (order-preserving bits; atomicMin / atomicMax): [0..2] lo,
-// [3..5] hi of the world coordinates; the light-space BVH's: [6..8] lo, [9..11] hi of
-// the light coordinates, [12] the largest |world coordinate|
-constexpr uint32_t kRefitBoundsWords = 13;
-// The inflation of the refitted boxes, derived on the device from the bounds (no host
-// round trip): world BVHs max(inflate_min, 1e-6 |diagonal|) (bvh8_inflation_box, as
-// set_scene); the light-space BVH max(inflate_min, 2 x 1e-6 |light diagonal| + 2e-6
-// max |world coordinate|) (build_sun_bvh)
+// The refitted boxes' absolute inflation, from the host (enqueueRefit / refitInflations:
+// the instances' transformed bounds, never less than the build's): world BVHs 1e-6
+// |diagonal| (bvh8_inflation_box, as set_scene); the light-space BVH 2 x 1e-6 |light
+// diagonal| + 2e-6 max |world coordinate| (build_sun_bvh)
 struct RefitBoxArgs {
     double frame[9];     // light-space rows u, v, w (sun_frame); unused for the world BVHs
-    float inflate_min;   // the inflation of the build (never less)
+    float inflate;       // the inflation of this BVH's boxes
     uint32_t light;      // 1: the light-space BVH (boxes of the light coordinates)
 };
 hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream_t s);
-hipError_t launch_refit_bounds_reset(uint32_t* bounds, hipStream_t s);
-// every record of a dirty instance re-transformed (the others kept); bounds [0..5] of
-// every record's world coordinates
-hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, uint32_t* bounds,
-                             hipStream_t s);
-// the light-space bounds [6..12] of every record (after launch_refit_tris on the light-space BVH's records)
-hipError_t launch_refit_light_bounds(const GpuTriangle* tris, uint32_t count, const RefitBoxArgs& a, uint32_t* bounds, hipStream_t s);
+// every record of a dirty instance re-transformed; the others are not touched beyond
+// their instance word
+hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s);
 // one level: nodes order[0 .. count), boxes [node][6] (lo, hi) of the deeper levels in, this level's out
 hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
-                              const uint32_t* bounds, hipStream_t s);
+                              hipStream_t s);
 // dst[i] = src[perm[i]] (64-B shading records), perm ~0: zeros (an installed rebuild's record order)
 hipError_t launch_gather_records(float4* dst, const float4* src, const uint32_t* perm, uint64_t count, hipStream_t s);
 

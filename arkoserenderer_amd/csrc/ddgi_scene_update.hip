@@ -7,19 +7,18 @@
 //                    reuse could race a copy still queued).
 //   k_refit_tris     every world-space triangle record re-transformed from the object-
 //                    space pools with the new instance transform, in set_scene's fp32
-//                    operation order (ark_ddgi.cpp), + the scene bounds (for the boxes'
-//                    absolute inflation).
+//                    operation order (ark_ddgi.cpp), the dirty instances' records only.
 //   k_refit_nodes    one BVH8 level (deepest first): each node's child boxes - leaf slots
 //                    from their triangle records, internal children from the level below
 //                    - inflated as the builder inflates them (bvh_builder.cpp writeNode),
 //                    the node's quantization grid and outward-rounded child planes
 //                    recomputed (quantGrid, collapse_bvh8). The world BVHs box world
 //                    coordinates; the sun's light-space BVH its records' light
-//                    coordinates (k_refit_light_bounds first), so it follows the motion
-//                    instead of being dropped.
+//                    coordinates, so it follows the motion instead of being dropped.
 //   k_gather_records the shading records in an installed background rebuild's order.
 // Every launch is stream-ordered behind the context's earlier work (ark_ddgi_set_instances_async):
-// the boxes' inflation is derived on the device from the refit's bounds, no host round trip.
+// the boxes' inflation comes from the host with the launch (refitInflations: the
+// instances' object-space boxes through their new transforms), no device round trip.
 // Refitting never changes a hit: hits do not depend on the BVH's shape (the (instance,
 // primitive) tie rule and conservative boxes), only on the triangle records,
 // which equal a fresh set_scene's bit for bit.
@@ -36,29 +35,18 @@ __global__ void __launch_bounds__(256) k_store_lights(LightBlock b, GpuSpotLight
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(b.spots)[i];
 }
 
-// order-preserving float <-> u32 (for atomicMin / atomicMax of the scene bounds)
-__device__ __forceinline__ uint32_t orderedBits(float f)
-{
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-__global__ void __launch_bounds__(32) k_refit_bounds_reset(uint32_t* __restrict__ bounds)
-{
-    const uint32_t i = threadIdx.x;
-    if (i < kRefitBoundsWords) bounds[i] = (i < 3 || (i >= 6 && i < 9)) ? 0xffffffffu : 0u;
-}
-
+// One thread per record: a dirty instance's record re-transformed from its mesh's
+// vertices, the others left as they are (their third 16 B read for the instance id).
+// (It also reduced the scene bounds with LDS atomics over every record, for the
+// inflation: 1.1 ms per C4 refit, and 1.5 ms for the light-space copy; the bounds now
+// come from the instances' boxes on the host, refitInflations.)
 __global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tris, uint32_t count, const RefitInstance* __restrict__ inst,
-                                                    const uint32_t* __restrict__ indices, const float* __restrict__ positions, uint32_t* __restrict__ bounds)
+                                                    const uint32_t* __restrict__ indices, const float* __restrict__ positions)
 {
-    __shared__ uint32_t red[6];
-    if (threadIdx.x < 6) red[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i < count) {
         float4* rec = reinterpret_cast<float4*>(tris + i);
-        float4 t0 = rec[0], t1 = rec[1], t2 = rec[2];
+        float4 t2 = rec[2];
         const uint32_t id = __float_as_uint(t2.y), prim = __float_as_uint(t2.z);
         if (id != kHoleInstance) {
             const RefitInstance I = inst[id];
@@ -81,26 +69,9 @@ __global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tr
                 t2.x = e2z;
                 t2.w = __uint_as_float(I.flip);
                 rec[2] = t2;
-            } else {
-                // an unmoved instance: its record stays; its vertices (v0, v0 + e1, v0 + e2)
-                // still bound the scene
-                const float v0[3] = { t0.x, t0.y, t0.z }, e1[3] = { t0.w, t1.x, t1.y }, e2[3] = { t1.z, t1.w, t2.x };
-                for (int a = 0; a < 3; ++a) {
-                    w[0][a] = v0[a];
-                    w[1][a] = v0[a] + e1[a];
-                    w[2][a] = v0[a] + e2[a];
-                }
-            }
-            for (int a = 0; a < 3; ++a) {
-                const float lo = fminf(fminf(w[0][a], w[1][a]), w[2][a]), hi = fmaxf(fmaxf(w[0][a], w[1][a]), w[2][a]);
-                atomicMin(&red[a], orderedBits(lo));
-                atomicMax(&red[3 + a], orderedBits(hi));
             }
         }
     }
-    __syncthreads();
-    if (threadIdx.x < 3) atomicMin(&bounds[threadIdx.x], red[threadIdx.x]);
-    else if (threadIdx.x < 6) atomicMax(&bounds[threadIdx.x], red[threadIdx.x]);
 }
 
 // The light coordinates of a record's three vertices as build_sun_bvh computes them
@@ -121,43 +92,6 @@ __device__ __forceinline__ void lightVertices(const float4 t0, const float4 t1, 
     }
     for (int k = 0; k < 3; ++k)
         for (int r = 0; r < 3; ++r) L[k][r] = static_cast<float>(F[3 * r + 0] * V[k][0] + F[3 * r + 1] * V[k][1] + F[3 * r + 2] * V[k][2]);
-}
-
-__global__ void __launch_bounds__(256) k_refit_light_bounds(const GpuTriangle* __restrict__ tris, uint32_t count, RefitBoxArgs a, uint32_t* __restrict__ bounds)
-{
-    __shared__ uint32_t red[7];
-    if (threadIdx.x < 7) red[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < count) {
-        const float4* rec = reinterpret_cast<const float4*>(tris + i);
-        const float4 t0 = rec[0], t1 = rec[1], t2 = rec[2];
-        if (__float_as_uint(t2.y) != kHoleInstance) {
-            float L[3][3], m;
-            lightVertices(t0, t1, t2, a.frame, L, m);
-            for (int ax = 0; ax < 3; ++ax) {
-                atomicMin(&red[ax], orderedBits(fminf(fminf(L[0][ax], L[1][ax]), L[2][ax])));
-                atomicMax(&red[3 + ax], orderedBits(fmaxf(fmaxf(L[0][ax], L[1][ax]), L[2][ax])));
-            }
-            atomicMax(&red[6], orderedBits(m));
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) atomicMin(&bounds[6 + threadIdx.x], red[threadIdx.x]);
-    else if (threadIdx.x < 7) atomicMax(&bounds[6 + threadIdx.x], red[threadIdx.x]);
-}
-
-__device__ __forceinline__ float fromOrderedBits(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
-
-// bvh8_inflation_box of bounds lo = b[0..2], hi = b[3..5] (double, as on the host)
-__device__ __forceinline__ float inflationBox(const uint32_t* b)
-{
-    double d2 = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        const double lo = fromOrderedBits(b[a]), hi = fromOrderedBits(b[3 + a]);
-        if (hi >= lo) d2 += (hi - lo) * (hi - lo);
-    }
-    return static_cast<float>(1e-6 * sqrt(d2));
 }
 
 // bvh_builder.cpp writeNode's inflation of a child box: relative to its magnitude and
@@ -199,16 +133,14 @@ __device__ __forceinline__ void quantGrid(float L, float H, int& e, double& p)
 // outward-rounded planes. (One thread per node walked the eight slots and up to 24
 // triangle records in a row: C4 refits took 4.0 ms, profiles/r06_f_refit_continuous_bg.log.)
 __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ nodes, const GpuTriangle* __restrict__ tris, float* __restrict__ boxes,
-                                                     const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra, const uint32_t* __restrict__ bounds)
+                                                     const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t i = t >> 3, s = t & 7u;
     const bool live = i < count; // a node's eight lanes are live or not together (count nodes = 8 count lanes)
     if (!__any(live)) return;
     const uint32_t n = live ? order[i] : 0u;
-    // the inflation of this BVH's boxes from the refit's bounds (RefitBoxArgs)
-    const float inflateAbs = ra.light ? fmaxf(ra.inflate_min, 2.0f * inflationBox(bounds + 6) + 2e-6f * fromOrderedBits(bounds[12]))
-                                      : fmaxf(ra.inflate_min, inflationBox(bounds));
+    const float inflateAbs = ra.inflate;
     const uint4 hdr = live ? reinterpret_cast<const uint4*>(nodes + n)[1] : make_uint4(0u, 0u, 0u, 0u); // child_base, tri_base, leaf_tris, stride | leaf_mask << 8
     const uint32_t imask = live ? (reinterpret_cast<const uint32_t*>(nodes + n)[3] >> 24) : 0u;
     const uint32_t childBase = hdr.x, triBase = hdr.y, leafTris = hdr.z, stride = hdr.w & 0xffu, leafMask = (hdr.w >> 8) & 0xffu;
@@ -309,33 +241,19 @@ hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_refit_bounds_reset(uint32_t* bounds, hipStream_t s)
-{
-    hipLaunchKernelGGL(dev::k_refit_bounds_reset, dim3(1), dim3(32), 0, s, bounds);
-    return hipGetLastError();
-}
-
-hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, uint32_t* bounds,
-                             hipStream_t s)
+hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_refit_tris, dim3((count + 255u) / 256u), dim3(256), 0, s, tris, count, inst, indices, positions, bounds);
-    return hipGetLastError();
-}
-
-hipError_t launch_refit_light_bounds(const GpuTriangle* tris, uint32_t count, const RefitBoxArgs& a, uint32_t* bounds, hipStream_t s)
-{
-    if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_refit_light_bounds, dim3((count + 255u) / 256u), dim3(256), 0, s, tris, count, a, bounds);
+    hipLaunchKernelGGL(dev::k_refit_tris, dim3((count + 255u) / 256u), dim3(256), 0, s, tris, count, inst, indices, positions);
     return hipGetLastError();
 }
 
 hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
-                              const uint32_t* bounds, hipStream_t s)
+                              hipStream_t s)
 {
     if (count == 0) return hipSuccess;
     const uint64_t lanes = 8ull * count; // eight lanes per node
-    hipLaunchKernelGGL(dev::k_refit_nodes, dim3(static_cast<uint32_t>((lanes + 127u) / 128u)), dim3(128), 0, s, nodes, tris, boxes, order, count, a, bounds);
+    hipLaunchKernelGGL(dev::k_refit_nodes, dim3(static_cast<uint32_t>((lanes + 127u) / 128u)), dim3(128), 0, s, nodes, tris, boxes, order, count, a);
     return hipGetLastError();
 }
 

@@ -389,7 +389,8 @@ def test_continuous_motion_installs_rebuilds():
             f += 1
             if st.bvh_rebuilds >= 2 and st.sun_rebuilds >= 1:
                 break
-            assert time.time() - t0 < 120, f"rebuilds not installed within 120 s (world {st.bvh_rebuilds}, sun {st.sun_rebuilds})"
+            assert time.time() - t0 < 120, (f"rebuilds not installed within 120 s (world {st.bvh_rebuilds}, failed {st.bvh_rebuild_failures}; "
+                                                 f"sun {st.sun_rebuilds}, failed {st.sun_rebuild_failures})")
         assert st.refit_version == f and st.sun_node_count > 0
         print(f"continuous motion: {f} frames, world rebuilds {st.bvh_rebuilds} ({st.bvh_rebuild_ms:.1f} ms), sun rebuilds {st.sun_rebuilds}")
     finally:
