@@ -188,7 +188,8 @@ def test_overlapped_update_two_slabs_one_gpu(device_seq):
             assert r["mismatch"] == 0, (which, r)
 
 
-@pytest.mark.parametrize("mode,port", [("torch_pg_events", 29541), ("torch_pg_seq", 29542), ("rccl_seq", 29543)])
+@pytest.mark.parametrize("mode,port", [("torch_pg_events", 29541), ("torch_pg_seq", 29542), ("rccl_seq", 29543),
+                                       ("window_full", 29544), ("window_k100", 29545)])
 def test_bench_frame_loop_over_one_rank_rccl(mode, port):
     """bench.py's N > 1 frame loop as it runs on every rank: DDGINode.execute_overlapped
     driven by OverlappedSlabExchange (torch events, a side stream, the in-place RCCL
@@ -196,15 +197,18 @@ def test_bench_frame_loop_over_one_rank_rccl(mode, port):
     enqueued without host synchronisation: the atlases and offsets equal a plain
     node's (the exchange of one rank moves nothing, so only the event plumbing and
     stream order are under test). torch_pg_seq: device-side sequence words instead
-    of events; rccl_seq: also the bench's direct RCCL group (RcclBandExchange)."""
+    of events; rccl_seq: also the bench's direct RCCL group (RcclBandExchange);
+    window_full / window_k100: bench.py's composition exactly - WindowExchange over the
+    RCCL group, the whole grid (row bands) and a 100-probe window (packets)."""
     import torch
     import torch.distributed as dist
 
-    from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange, SlabExchange
+    from arkoserenderer_amd.collective import OverlappedSlabExchange, RcclBandExchange, SlabExchange, WindowExchange, WindowSource
 
     sc, ex = S.cornell_box()
     grid = D.ProbeGrid((8, 8, 8), (0.257, 0.257, 0.257), (-0.9, 0.1, -0.9))
-    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=512, compute_probe_offsets=True,
+    K = 100 if mode == "window_k100" else 512
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=K, compute_probe_offsets=True,
                        max_rays_per_probe=64, max_probe_updates=512)
     exposure = dict(light_pre_exposure=ex["light_pre_exposure"], environment_brightness=ex["environment_brightness"])
     dev = torch.device("cuda", 0)
@@ -217,9 +221,12 @@ def test_bench_frame_loop_over_one_rank_rccl(mode, port):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     band = None
     try:
-        Ex = RcclBandExchange if mode == "rccl_seq" else SlabExchange
+        Ex = RcclBandExchange if mode in ("rccl_seq", "window_full", "window_k100") else SlabExchange
         band = Ex.from_views(ranked.ctx.device_views(), 0, 1, dev)
-        exch = OverlappedSlabExchange(ranked, band.exchange, dev, device_seq=mode != "torch_pg_events")
+        exchange = band.exchange
+        if mode.startswith("window"):
+            exchange = WindowExchange(WindowSource(ranked.ctx), band.exchange, band.all_gather, 0, 1, min(K, 512), dev).exchange
+        exch = OverlappedSlabExchange(ranked, exchange, dev, device_seq=mode != "torch_pg_events")
         sptr = torch.cuda.current_stream(dev).cuda_stream
         for f in range(6):
             plain.execute(D.AppState(f), sptr)

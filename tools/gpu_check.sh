@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT/profiles
 export TMPDIR=/tmp
 if [[ " $* " != *" --no-tests "* ]]; then
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 \
     || { echo "gpu tests failed rc=$?"; tail -30 $OUT/pytest.log; exit 1; }
   tail -3 $OUT/pytest.log
 fi
