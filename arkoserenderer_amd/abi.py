@@ -503,6 +503,7 @@ EXPORTS = {
     "ark_ddgi_debug_bvh8_check_opts": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int, C.c_float, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_sun_bvh_check": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_float, C.POINTER(C.c_uint64)]),
     "ark_ddgi_debug_sun_choice": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
+    "ark_ddgi_debug_scene_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

@@ -280,6 +280,29 @@ struct SceneStore {
     // object-space bounds of every instance's triangles (set_scene): the refit's world and
     // light-space bounds, for its box inflation, from the instances' transforms on the host
     std::vector<std::array<float, 6>> instObjBox;
+    // The geometry a refit writes comes in three copies: the front one (nodes, sunNodes,
+    // instances above: what the kernels read) and two spares. A refit brings the next
+    // spare from the transforms it holds (xf[slot]) to the new ones on the context's
+    // refit stream and makes it the front one: it waits only for the operations that read
+    // that copy while it was the front one, two refits before (the frame before last),
+    // so that it runs beside the frame in flight's traversal and the next traversal does
+    // not wait for it (with two copies it waited for the previous frame's shading, and
+    // the frames ran one after the other: C4 4.3 ms per moving frame, static 3.3). An
+    // install (a new topology) drops the spares; the next refit copies the front one.
+    struct Spare {
+        DeviceBuffer nodes, sunNodes, instances;
+        bool valid = false;
+        int slot = 0;
+    };
+    Spare spare[2]; // spare[0]: the next refit's target
+    // the refit's node masks (k_node_masks: per topology) and the inflations each copy's
+    // boxes hold; refitFull: the next refit reaches every node (a new topology, or boxes
+    // scratch not of this one)
+    DeviceBuffer nodeMasks, sunNodeMasks;
+    bool masksValid = false, sunMasksValid = false, refitFull = true;
+    float inflCopy[3][2] {};
+    int front = 0; // slot of the front copy (xf index)
+    std::vector<std::array<float, 12>> xf[3];
     // the light-space BVH follows the sun: set_scene chose it (sunWanted), and after a
     // sun-direction change it is rebuilt in the background (sunRebuildStep)
     bool sunWanted = false;
@@ -325,7 +348,9 @@ struct SceneStore {
             if (stageDone[i]) (void)hipEventDestroy(stageDone[i]);
         }
         for (DeviceBuffer* b : { &nodes, &triNormals, &indices, &vertices, &positions, &meshes, &materials, &instances, &texInfos, &texels, &sunNodes, &refitInst,
-                                 &refitBoxes, &refitOrder, &sunRefitOrder, &sunRefitBoxes })
+                                 &refitBoxes, &refitOrder, &sunRefitOrder, &sunRefitBoxes, &spare[0].nodes, &spare[0].sunNodes,
+                                 &spare[0].instances, &spare[1].nodes, &spare[1].sunNodes, &spare[1].instances,
+                                 &nodeMasks, &sunNodeMasks })
             b->release();
     }
 };
@@ -442,6 +467,16 @@ struct ArkDdgiCtx {
     // worldCollect): the next update's traversal on the traversal stream waits for it
     hipEvent_t evRefit = nullptr;
     bool refitPending = false;
+    // ark_ddgi_set_instances_async's refits run on refitStream (SceneStore::spare):
+    // evFree[slot] ends with the operations that read that slot's copy while it was the
+    // front one (recorded when a refit swapped it out, on the stream of the last
+    // operation, which follows the others); evInstalled with the last install (a rebuild
+    // installed on a caller's stream writes the front copy)
+    hipStream_t refitStream = nullptr;
+    hipEvent_t evFree[3] = {};
+    bool freeValid[3] = { false, false, false };
+    hipEvent_t evInstalled = nullptr;
+    bool installValid = false;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -790,51 +825,97 @@ void refitInflations(const SceneStore& st, float& world, float& light)
 // (st.refitInst), the world BVHs' boxes level by level, and the light-space sun BVH's
 // records and light-space boxes. The boxes' inflations from the instances' bounds
 // (refitInflations, host).
-int enqueueRefit(ArkDdgiCtx* ctx, SceneStore& st, hipStream_t s)
+struct RefitTarget {
+    GpuBvh8Node* nodes;
+    GpuBvh8Node* sunNodes; // the light-space BVH's buffer (its records at the front copy's offset)
+};
+RefitTarget frontTarget(SceneStore& st) { return { st.nodes.as<GpuBvh8Node>(), st.sunNodes.as<GpuBvh8Node>() }; }
+RefitTarget spareTarget(SceneStore::Spare& c) { return { c.nodes.as<GpuBvh8Node>(), c.sunNodes.as<GpuBvh8Node>() }; }
+
+// The instance masks of a BVH's nodes (k_node_masks), level by level on `s`, into `masks`
+int computeMasks(ArkDdgiCtx* ctx, SceneStore& st, DeviceBuffer& masks, const GpuBvh8Node* nodes, const GpuTriangle* tris, uint64_t nodeCount,
+                 const DeviceBuffer& order, const std::vector<uint32_t>& offsets, hipStream_t s)
+{
+    if (masks.bytes < std::max<uint64_t>(8, nodeCount * 8)) {
+        ARK_HIP(retireBuffer(st, masks, s));
+        ARK_HIP(masks.alloc(std::max<uint64_t>(8, nodeCount * 8)));
+    }
+    for (size_t l = 0; l + 1 < offsets.size(); ++l)
+        ARK_HIP(launch_node_masks(nodes, tris, masks.as<uint64_t>(), order.as<uint32_t>() + offsets[l], offsets[l + 1] - offsets[l], s));
+    return ARK_DDGI_OK;
+}
+
+// The inflation of the refitted boxes rounded up to a power of two: it changes only when
+// the scene's extent crosses one, so that a refit rarely has to touch the nodes of the
+// instances that did not move (a change refits every node).
+float inflationStep(float x) { return x > 0.0f ? std::ldexp(1.0f, static_cast<int>(std::ceil(std::log2(static_cast<double>(x))))) : x; }
+
+// The refit of the copy `t` (slot: the transforms and inflations it holds) of every BVH
+// of the scene on `s`, level by level, the nodes with a moved instance below them
+// (st.refitInst's dirty flags: the instances whose transform differs from the copy's):
+// their moved records re-transformed, their boxes and planes recomputed. Every node after
+// an install or a new scene (refitFull) or a change of the inflation.
+int enqueueRefit(ArkDdgiCtx* ctx, SceneStore& st, hipStream_t s, const RefitTarget& t, int slot)
 {
     float inflateWorld = 0.0f, inflateLight = 0.0f;
     refitInflations(st, inflateWorld, inflateLight);
-    GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(static_cast<char*>(st.nodes.ptr) + st.args.tri_byte_offset);
-    ARK_HIP(launch_refit_tris(tris, static_cast<uint32_t>(st.triRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(), st.positions.as<float>(), s));
+    inflateWorld = inflationStep(inflateWorld);
+    inflateLight = inflationStep(inflateLight);
+    uint64_t dirty = 0;
+    for (size_t i = 0; i < st.refitHost.size(); ++i)
+        if (st.refitHost[i].dirty) dirty |= 1ull << (i & 63u);
+    GpuTriangle* tris = reinterpret_cast<GpuTriangle*>(reinterpret_cast<char*>(t.nodes) + st.args.tri_byte_offset);
+    const RefitInstance* inst = st.refitInst.as<RefitInstance>();
+    if (!st.masksValid) {
+        if (const int rc = computeMasks(ctx, st, st.nodeMasks, t.nodes, tris, st.bvhStats.node_count, st.refitOrder, st.levelOffsets, s)) return rc;
+        st.masksValid = true;
+    }
     RefitBoxArgs world {};
     world.inflate = inflateWorld;
     world.light = 0;
+    world.dirty = (st.refitFull || inflateWorld != st.inflCopy[slot][0]) ? ~0ull : dirty;
     const uint32_t* order = st.refitOrder.as<uint32_t>();
     for (size_t l = 0; l + 1 < st.levelOffsets.size(); ++l)
-        ARK_HIP(launch_refit_nodes(st.nodes.as<GpuBvh8Node>(), tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l], st.levelOffsets[l + 1] - st.levelOffsets[l],
-                                   world, s));
+        ARK_HIP(launch_refit_nodes(t.nodes, tris, st.refitBoxes.as<float>(), order + st.levelOffsets[l], st.levelOffsets[l + 1] - st.levelOffsets[l],
+                                   world, st.nodeMasks.as<uint64_t>(), inst, st.indices.as<uint32_t>(), st.positions.as<float>(), s));
+    st.inflCopy[slot][0] = inflateWorld;
     if (st.sunArgs.sun_root >= 0 && st.sunTriRecords && !st.sunLevelOffsets.empty()) {
-        GpuTriangle* stris = const_cast<GpuTriangle*>(st.sunArgs.sun_tris);
-        ARK_HIP(launch_refit_tris(stris, static_cast<uint32_t>(st.sunTriRecords), st.refitInst.as<RefitInstance>(), st.indices.as<uint32_t>(),
-                                  st.positions.as<float>(), s));
+        const size_t sunTriOffset = reinterpret_cast<const char*>(st.sunArgs.sun_tris) - static_cast<const char*>(st.sunNodes.ptr);
+        GpuTriangle* stris = reinterpret_cast<GpuTriangle*>(reinterpret_cast<char*>(t.sunNodes) + sunTriOffset);
+        if (!st.sunMasksValid) {
+            if (const int rc = computeMasks(ctx, st, st.sunNodeMasks, t.sunNodes, stris, st.sunBvhNodes, st.sunRefitOrder, st.sunLevelOffsets, s)) return rc;
+            st.sunMasksValid = true;
+        }
         RefitBoxArgs light {};
         std::memcpy(light.frame, st.sunFrameD, sizeof(light.frame));
         light.inflate = inflateLight;
         light.light = 1;
+        light.dirty = (st.refitFull || inflateLight != st.inflCopy[slot][1]) ? ~0ull : dirty;
         const uint32_t* so = st.sunRefitOrder.as<uint32_t>();
         for (size_t l = 0; l + 1 < st.sunLevelOffsets.size(); ++l)
-            ARK_HIP(launch_refit_nodes(const_cast<GpuBvh8Node*>(st.sunArgs.sun_nodes), stris, st.sunRefitBoxes.as<float>(), so + st.sunLevelOffsets[l],
-                                       st.sunLevelOffsets[l + 1] - st.sunLevelOffsets[l], light, s));
+            ARK_HIP(launch_refit_nodes(t.sunNodes, stris, st.sunRefitBoxes.as<float>(), so + st.sunLevelOffsets[l], st.sunLevelOffsets[l + 1] - st.sunLevelOffsets[l],
+                                       light, st.sunNodeMasks.as<uint64_t>(), inst, st.indices.as<uint32_t>(), st.positions.as<float>(), s));
+        st.inflCopy[slot][1] = inflateLight;
     }
+    st.refitFull = false;
     return ARK_DDGI_OK;
 }
 
 // The refit's transforms of `instances` on the device (stream-ordered), every one dirty
-// (allDirty: the records are of an older version, an installed rebuild) or those whose
-// transform changed since the last upload.
-int uploadRefitInstances(ArkDdgiCtx* ctx, SceneStore& st, const ArkRTInstance* instances, uint32_t count, bool allDirty, hipStream_t s)
+// (have = nullptr: the records are of an older version, an installed rebuild) or those
+// whose transform differs from the one the target copy's records hold (`have`).
+int uploadRefitInstances(ArkDdgiCtx* ctx, SceneStore& st, const ArkRTInstance* instances, uint32_t count, const std::vector<std::array<float, 12>>* have,
+                         hipStream_t s)
 {
-    if (st.refitHost.size() != count) {
-        st.refitHost.assign(count, RefitInstance {});
-        allDirty = true;
-    }
+    bool allDirty = !have || have->size() != count;
+    if (st.refitHost.size() != count) st.refitHost.assign(count, RefitInstance {});
     if (!st.refitInst.ptr || st.refitInst.bytes < std::max<size_t>(16, count * sizeof(RefitInstance))) ARK_HIP(st.refitInst.alloc(std::max<size_t>(16, count * sizeof(RefitInstance))));
     for (uint32_t ii = 0; ii < count; ++ii) {
         const float* M = instances[ii].object_to_world;
         const float det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) + M[2] * (M[4] * M[9] - M[5] * M[8]);
         const ArkRTTriangleMesh& mesh = st.meshHost[instances[ii].rt_mesh_index];
         RefitInstance& q = st.refitHost[ii];
-        const bool moved = allDirty || std::memcmp(q.m, M, sizeof(q.m)) != 0;
+        const bool moved = allDirty || std::memcmp((*have)[ii].data(), M, sizeof(q.m)) != 0;
         std::memcpy(q.m, M, sizeof(q.m));
         q.first_vertex = mesh.first_vertex;
         q.first_index = static_cast<uint32_t>(mesh.first_index);
@@ -843,6 +924,42 @@ int uploadRefitInstances(ArkDdgiCtx* ctx, SceneStore& st, const ArkRTInstance* i
     }
     ARK_HIP(stagedUpload(st, st.refitInst.ptr, st.refitHost.data(), count * sizeof(RefitInstance), s));
     return ARK_DDGI_OK;
+}
+
+// A BVH of the scene was replaced (an install): its node masks are recomputed and the
+// next refit reaches every node.
+void markTopologyChanged(SceneStore& st)
+{
+    st.masksValid = false;
+    st.sunMasksValid = false;
+    st.refitFull = true;
+}
+
+// The spare geometry copies retired behind everything enqueued on `s` so far.
+hipError_t dropSpares(SceneStore& st, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+    for (SceneStore::Spare& c : st.spare) {
+        for (DeviceBuffer* b : { &c.nodes, &c.sunNodes, &c.instances })
+            if (e == hipSuccess) e = retireBuffer(st, *b, s);
+        c.valid = false;
+    }
+    return e;
+}
+
+// An install replaced a BVH of the front copy (a new topology, refitted forward on `s`):
+// the back copy is dropped - retired behind everything enqueued so far - and copied anew
+// from the front one by the next refit, which waits for the install (evInstalled).
+hipError_t installedGeometry(ArkDdgiCtx* ctx, SceneStore& st, hipStream_t s)
+{
+    hipError_t e = dropSpares(st, s);
+    markTopologyChanged(st); // (again: the boxes scratch is of the old topology without a forward refit)
+    std::vector<std::array<float, 12>>& xf = st.xf[st.front];
+    xf.resize(st.instHost.size());
+    for (size_t i = 0; i < st.instHost.size(); ++i) std::memcpy(xf[i].data(), st.instHost[i].object_to_world, sizeof(float) * 12);
+    if (e == hipSuccess) e = hipEventRecord(ctx->evInstalled, s);
+    ctx->installValid = e == hipSuccess;
+    return e;
 }
 
 // Background builds' host-thread inputs: a snapshot of the world records on `s` behind
@@ -1153,13 +1270,15 @@ int sunCollect(ArkDdgiCtx* ctx, hipStream_t s)
             st.bvhStats.sun_build_ms = job->ms;
             st.sunRefitsSinceBuild = st.refitCount - job->refitsAt;
             st.bvhStats.sun_built_refit_version = job->refitsAt;
+            markTopologyChanged(st);
             if (st.sunRefitsSinceBuild) {
                 // refits came in while it was built: its records follow them (every
                 // instance re-transformed, the light-space boxes refitted)
-                if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), true, s)) return rc;
-                if (const int rc = enqueueRefit(ctx, st, s)) return rc;
+                if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), nullptr, s)) return rc;
+                if (const int rc = enqueueRefit(ctx, st, s, frontTarget(st), st.front)) return rc;
             }
             ARK_HIP(retireBuffer(st, job->snap, s));
+            ARK_HIP(installedGeometry(ctx, st, s));
             ARK_HIP(hipEventRecord(ctx->evRefit, s));
             ARK_HIP(installDone(ctx, s));
             ctx->refitPending = true;
@@ -1295,10 +1414,12 @@ int worldCollect(ArkDdgiCtx* ctx, hipStream_t s)
         st.bvhStats.bvh_rebuild_ms = job->ms;
         st.refitsSinceBuild = st.refitCount - job->refitsAt; // refits since its snapshot
         st.bvhStats.bvh_built_refit_version = job->refitsAt;
+        markTopologyChanged(st);
         if (st.refitsSinceBuild) {
-            if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), true, s)) return rc;
-            if (const int rc = enqueueRefit(ctx, st, s)) return rc;
+            if (const int rc = uploadRefitInstances(ctx, st, st.instHost.data(), static_cast<uint32_t>(st.instHost.size()), nullptr, s)) return rc;
+            if (const int rc = enqueueRefit(ctx, st, s, frontTarget(st), st.front)) return rc;
         }
+        ARK_HIP(installedGeometry(ctx, st, s));
         ARK_HIP(hipEventRecord(ctx->evRefit, s));
         ARK_HIP(installDone(ctx, s));
         ctx->refitPending = true;
@@ -1436,6 +1557,16 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeSrc, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evExchangeDone, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->evRefit, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->evInstalled, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (auto& ev : ctx->evFree)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    {
+        // the refit stream at the device's highest priority: its per-level launches are
+        // dispatched ahead of the frame in flight's work when both wait for a CU
+        int lo = 0, hi = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return bad(e, "hipDeviceGetStreamPriorityRange");
+        if ((e = hipStreamCreateWithPriority(&ctx->refitStream, hipStreamNonBlocking, hi)) != hipSuccess) return bad(e, "hipStreamCreateWithPriority");
+    }
     for (auto& ev : ctx->evFrameDone)
         if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
@@ -1509,6 +1640,10 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     if (ctx->evExchangeSrc) (void)hipEventDestroy(ctx->evExchangeSrc);
     if (ctx->evExchangeDone) (void)hipEventDestroy(ctx->evExchangeDone);
     if (ctx->evRefit) (void)hipEventDestroy(ctx->evRefit);
+    if (ctx->evInstalled) (void)hipEventDestroy(ctx->evInstalled);
+    for (auto& ev : ctx->evFree)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->refitStream) (void)hipStreamDestroy(ctx->refitStream);
     for (auto& ev : ctx->evFrameDone)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
@@ -1766,6 +1901,12 @@ int ark_ddgi_set_scene(ArkDdgiCtx* ctx, const ArkDdgiScene* s)
     if ((rc = upload(ctx, st->vertices, reinterpret_cast<const float*>(s->vertices), s->vertex_count * 9)) != 0) return rc;
     if ((rc = upload(ctx, st->positions, s->positions, s->vertex_count * 3)) != 0) return rc;
     st->instHost.assign(s->instances, s->instances + s->instance_count);
+    // the transforms both geometry copies hold (the back one is made at the first refit)
+    st->xf[0].resize(s->instance_count);
+    for (uint32_t ii = 0; ii < s->instance_count; ++ii) std::memcpy(st->xf[0][ii].data(), s->instances[ii].object_to_world, sizeof(float) * 12);
+    st->xf[1] = st->xf[2] = st->xf[0];
+    st->spare[0].slot = 1;
+    st->spare[1].slot = 2;
     st->meshHost.assign(s->meshes, s->meshes + s->mesh_count);
     // every instance's object-space box (refitInflations)
     st->instObjBox.assign(s->instance_count, { INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY });
@@ -1965,6 +2106,35 @@ int prepareRefit(ArkDdgiCtx* ctx, SceneStore& st)
 }
 } // namespace
 
+namespace {
+// The refitted spare becomes the front copy (SceneStore::spare), the front one the last
+// spare: the kernel views follow.
+void rotateGeometry(SceneStore& st)
+{
+    const bool sun = st.sunArgs.sun_root >= 0 && st.sunNodes.ptr;
+    const size_t sunTriOffset = sun ? static_cast<size_t>(reinterpret_cast<const char*>(st.sunArgs.sun_tris) - static_cast<const char*>(st.sunNodes.ptr)) : 0;
+    SceneStore::Spare old;
+    old.nodes = st.nodes;
+    old.sunNodes = st.sunNodes;
+    old.instances = st.instances;
+    old.valid = true;
+    old.slot = st.front;
+    st.nodes = st.spare[0].nodes;
+    st.sunNodes = st.spare[0].sunNodes;
+    st.instances = st.spare[0].instances;
+    st.front = st.spare[0].slot;
+    st.spare[0] = st.spare[1];
+    st.spare[1] = old;
+    st.args.nodes = st.nodes.as<GpuBvh8Node>();
+    st.args.tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.nodes.ptr) + st.args.tri_byte_offset);
+    st.args.instances = st.instances.as<GpuInstance>();
+    if (sun) {
+        st.sunArgs.sun_nodes = st.sunNodes.as<GpuBvh8Node>();
+        st.sunArgs.sun_tris = reinterpret_cast<const GpuTriangle*>(static_cast<const char*>(st.sunNodes.ptr) + sunTriOffset);
+    }
+}
+} // namespace
+
 static int checkSequencing(ArkDdgiCtx* ctx);
 
 int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances, uint32_t count, void* hipStream)
@@ -1985,22 +2155,58 @@ int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances
     const hipStream_t s = streamOf(hipStream);
     ARK_HIP(hipSetDevice(ctx->device));
     if (const int r = checkSequencing(ctx)) return r;
-    // every launch in flight may read the scene: with a shared scene every context's on
-    // the device (waited for here); otherwise this context's, which the refit follows in
-    // stream order (orderBegin: its earlier operations, their traversals included)
-    if (ctx->sceneStore.use_count() > 1) ARK_HIP(hipDeviceSynchronize());
-    ARK_HIP(orderBegin(ctx, s));
+    // with a shared scene every context's launches may read either copy: all of them end
+    // first (and the refit below before returning)
+    const bool shared = ctx->sceneStore.use_count() > 1;
+    if (shared) ARK_HIP(hipDeviceSynchronize());
     int rc;
     if (st.levelOffsets.empty() && (rc = prepareRefit(ctx, st)) != 0) return rc;
+    // everything this context enqueued so far ends with its last operation's stream
+    // (orderBegin chains the others into it): the front copy's readers among them
+    const hipStream_t last = ctx->orderValid ? ctx->orderStream : s;
     // a light-space sun BVH without a refit order (none recorded) cannot follow: dropped
     if (st.sunArgs.sun_root >= 0 && st.sunLevelOffsets.empty()) {
         st.sunArgs.sun_root = -1;
         st.sunArgs.sun_nodes = nullptr;
         st.sunArgs.sun_tris = nullptr;
-        ARK_HIP(retireBuffer(st, st.sunNodes, s));
+        ARK_HIP(retireBuffer(st, st.sunNodes, last));
+        ARK_HIP(dropSpares(st, last));
         st.sunBvhNodes = 0;
         st.bvhStats.sun_node_count = 0;
         st.bvhStats.sun_max_depth = 0;
+    }
+    // The refit writes the next spare copy on the refit stream, after the operations that
+    // read it (while it was the front one: evFree) and the last install; the frames in
+    // flight keep reading the front copy. The copy swapped out here is free once the
+    // operations enqueued so far are done.
+    SceneStore::Spare& tgt = st.spare[0];
+    const int fs = st.front, ts = tgt.slot;
+    const hipStream_t rs = ctx->refitStream;
+    ARK_HIP(hipEventRecord(ctx->evFree[fs], last));
+    ctx->freeValid[fs] = true;
+    if (ctx->freeValid[ts]) ARK_HIP(hipStreamWaitEvent(rs, ctx->evFree[ts], 0));
+    if (ctx->installValid) {
+        ARK_HIP(hipStreamWaitEvent(rs, ctx->evInstalled, 0));
+        ctx->installValid = false;
+    }
+    if (!tgt.valid) {
+        // a copy of the front one (a new scene or an installed rebuild)
+        auto copy = [&](DeviceBuffer& dst, const DeviceBuffer& src) -> hipError_t {
+            if (!src.ptr) return retireBuffer(st, dst, last);
+            hipError_t e = hipSuccess;
+            if (dst.bytes != src.bytes) {
+                if ((e = retireBuffer(st, dst, last)) != hipSuccess) return e;
+                if ((e = dst.alloc(src.bytes)) != hipSuccess) return e;
+            }
+            return hipMemcpyAsync(dst.ptr, src.ptr, src.bytes, hipMemcpyDeviceToDevice, rs);
+        };
+        ARK_HIP(copy(tgt.nodes, st.nodes));
+        ARK_HIP(copy(tgt.sunNodes, st.sunNodes));
+        ARK_HIP(copy(tgt.instances, st.instances));
+        st.xf[ts] = st.xf[fs];
+        st.inflCopy[ts][0] = st.inflCopy[fs][0];
+        st.inflCopy[ts][1] = st.inflCopy[fs][1];
+        tgt.valid = true;
     }
     // the instance table of the shading kernels (set_scene's determinant and rows)
     std::vector<GpuInstance> ginst(count);
@@ -2017,11 +2223,18 @@ int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances
         g.hit_mask = static_cast<int32_t>(instances[ii].hit_mask);
         g.material_index = mesh.material_index;
     }
-    ARK_HIP(stagedUpload(st, st.instances.ptr, ginst.data(), count * sizeof(GpuInstance), s));
-    if ((rc = uploadRefitInstances(ctx, st, instances, count, false, s)) != 0) return rc;
-    if ((rc = enqueueRefit(ctx, st, s)) != 0) return rc;
-    ARK_HIP(hipEventRecord(ctx->evRefit, s));
-    ARK_HIP(installDone(ctx, s));
+    ARK_HIP(stagedUpload(st, tgt.instances.ptr, ginst.data(), count * sizeof(GpuInstance), rs));
+    if ((rc = uploadRefitInstances(ctx, st, instances, count, &st.xf[ts], rs)) != 0) return rc;
+    if ((rc = enqueueRefit(ctx, st, rs, spareTarget(tgt), ts)) != 0) return rc;
+    ARK_HIP(hipEventRecord(ctx->evRefit, rs));
+    if (shared) ARK_HIP(hipStreamSynchronize(rs));
+    // the refitted copy becomes the front one
+    st.xf[ts].resize(count);
+    for (uint32_t ii = 0; ii < count; ++ii) std::memcpy(st.xf[ts][ii].data(), instances[ii].object_to_world, sizeof(float) * 12);
+    rotateGeometry(st);
+    // the caller's stream follows the refit (what it runs next sees the new geometry); the
+    // next update's traversal on the traversal stream waits for it too (refitPending)
+    ARK_HIP(hipStreamWaitEvent(s, ctx->evRefit, 0));
     ctx->refitPending = true;
     for (uint32_t ii = 0; ii < count; ++ii) std::memcpy(st.instHost[ii].object_to_world, instances[ii].object_to_world, sizeof(float) * 12);
     ++st.version;
@@ -2034,6 +2247,30 @@ int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances
     if ((rc = sceneMaintenance(ctx, s)) != 0) return rc;
     ARK_HIP(orderEnd(ctx, s));
     st.bvhStats.refit_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return ARK_DDGI_OK;
+}
+
+int ark_ddgi_debug_scene_digest(ArkDdgiCtx* ctx, uint64_t* out)
+{
+    if (!ctx || !out) return ARK_DDGI_E_INVALID_ARGUMENT;
+    if (!ctx->hasScene) return ctx->fail(ARK_DDGI_E_NO_SCENE, "scene digest before ark_ddgi_set_scene");
+    ARK_HIP(hipSetDevice(ctx->device));
+    ARK_HIP(hipDeviceSynchronize());
+    const SceneStore& st = *ctx->sceneStore;
+    auto digest = [&](const void* dev, size_t bytes, uint64_t& h) -> hipError_t {
+        h = 1469598103934665603ull;
+        if (!dev || !bytes) return hipSuccess;
+        std::vector<unsigned char> b(bytes);
+        const hipError_t e = hipMemcpy(b.data(), dev, bytes, hipMemcpyDeviceToHost);
+        for (unsigned char c : b) h = (h ^ c) * 1099511628211ull;
+        return e;
+    };
+    ARK_HIP(digest(st.args.nodes, st.bvhStats.node_count * sizeof(GpuBvh8Node), out[0]));
+    ARK_HIP(digest(st.args.tris, st.triRecords * sizeof(GpuTriangle), out[1]));
+    const bool sun = st.sunArgs.sun_root >= 0;
+    ARK_HIP(digest(sun ? st.sunArgs.sun_nodes : nullptr, st.sunBvhNodes * sizeof(GpuBvh8Node), out[2]));
+    ARK_HIP(digest(sun ? st.sunArgs.sun_tris : nullptr, st.sunTriRecords * sizeof(GpuTriangle), out[3]));
+    if (!sun) out[2] = out[3] = 0;
     return ARK_DDGI_OK;
 }
 

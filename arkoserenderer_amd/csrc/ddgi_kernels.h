@@ -292,14 +292,15 @@ struct RefitBoxArgs {
     double frame[9];     // light-space rows u, v, w (sun_frame); unused for the world BVHs
     float inflate;       // the inflation of this BVH's boxes
     uint32_t light;      // 1: the light-space BVH (boxes of the light coordinates)
+    uint64_t dirty;      // bits (id mod 64) of the instances moved since the target copy's version; all: every node
 };
 hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream_t s);
-// every record of a dirty instance re-transformed; the others are not touched beyond
-// their instance word
-hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s);
-// one level: nodes order[0 .. count), boxes [node][6] (lo, hi) of the deeper levels in, this level's out
-hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
-                              hipStream_t s);
+// one level (order[0 .. count)): masks[node] = the instance bits below it (children's masks from the deeper levels)
+hipError_t launch_node_masks(const GpuBvh8Node* nodes, const GpuTriangle* tris, uint64_t* masks, const uint32_t* order, uint32_t count, hipStream_t s);
+// one level: nodes order[0 .. count) whose mask meets a.dirty - their leaf slots' records of
+// dirty instances re-transformed (inst), boxes [node][6] (lo, hi) of the deeper levels in, this level's out
+hipError_t launch_refit_nodes(GpuBvh8Node* nodes, GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
+                              const uint64_t* masks, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s);
 // dst[i] = src[perm[i]] (64-B shading records), perm ~0: zeros (an installed rebuild's record order)
 hipError_t launch_gather_records(float4* dst, const float4* src, const uint32_t* perm, uint64_t count, hipStream_t s);
 

@@ -5,10 +5,11 @@
 //   k_store_lights   the context's spot lights from a by-value kernel argument into its
 //                    device light buffer, in stream order (no host staging buffer whose
 //                    reuse could race a copy still queued).
-//   k_refit_tris     every world-space triangle record re-transformed from the object-
-//                    space pools with the new instance transform, in set_scene's fp32
-//                    operation order (ark_ddgi.cpp), the dirty instances' records only.
-//   k_refit_nodes    one BVH8 level (deepest first): each node's child boxes - leaf slots
+//   k_node_masks     the instances below each node (bit id mod 64), once per topology.
+//   k_refit_nodes    one BVH8 level (deepest first), the nodes with a moved instance below
+//                    them: the moved instances' records of their leaf slots re-transformed
+//                    from the object-space pools in set_scene's fp32 operation order
+//                    (ark_ddgi.cpp), each node's child boxes - leaf slots
 //                    from their triangle records, internal children from the level below
 //                    - inflated as the builder inflates them (bvh_builder.cpp writeNode),
 //                    the node's quantization grid and outward-rounded child planes
@@ -35,43 +36,57 @@ __global__ void __launch_bounds__(256) k_store_lights(LightBlock b, GpuSpotLight
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(b.spots)[i];
 }
 
-// One thread per record: a dirty instance's record re-transformed from its mesh's
-// vertices, the others left as they are (their third 16 B read for the instance id).
-// (It also reduced the scene bounds with LDS atomics over every record, for the
-// inflation: 1.1 ms per C4 refit, and 1.5 ms for the light-space copy; the bounds now
-// come from the instances' boxes on the host, refitInflations.)
-__global__ void __launch_bounds__(256) k_refit_tris(GpuTriangle* __restrict__ tris, uint32_t count, const RefitInstance* __restrict__ inst,
-                                                    const uint32_t* __restrict__ indices, const float* __restrict__ positions)
+// A dirty instance's triangle record re-transformed from its mesh's vertices in place
+// (k_refit_nodes, for the triangles of the leaf slots it refits).
+__device__ __forceinline__ void refitRecord(float4* rec, float4& t0, float4& t1, float4& t2, const RefitInstance& I, uint32_t prim,
+                                            const uint32_t* __restrict__ indices, const float* __restrict__ positions)
+{
+    const float* M = I.m;
+    float w[3][3];
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t idx = indices[static_cast<size_t>(I.first_index) + 3u * prim + k];
+        const float* P = positions + (static_cast<uint64_t>(static_cast<int64_t>(I.first_vertex)) + idx) * 3u;
+        // ark_ddgi_set_scene's expression, left to right, no contraction
+        w[k][0] = M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3];
+        w[k][1] = M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7];
+        w[k][2] = M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11];
+    }
+    // make_gpu_triangle: e1 = v1 - v0, e2 = v2 - v0
+    const float e1x = w[1][0] - w[0][0], e1y = w[1][1] - w[0][1], e1z = w[1][2] - w[0][2];
+    const float e2x = w[2][0] - w[0][0], e2y = w[2][1] - w[0][1], e2z = w[2][2] - w[0][2];
+    t0 = make_float4(w[0][0], w[0][1], w[0][2], e1x);
+    t1 = make_float4(e1y, e1z, e2x, e2y);
+    t2.x = e2z;
+    t2.w = __uint_as_float(I.flip);
+    rec[0] = t0;
+    rec[1] = t1;
+    rec[2] = t2;
+}
+
+// The instances below each node (bit id mod 64 of every triangle's instance), one level
+// per launch, deepest first, one thread per node: k_refit_nodes skips the nodes none of
+// whose instances moved.
+__global__ void __launch_bounds__(256) k_node_masks(const GpuBvh8Node* __restrict__ nodes, const GpuTriangle* __restrict__ tris, uint64_t* __restrict__ masks,
+                                                    const uint32_t* __restrict__ order, uint32_t count)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < count) {
-        float4* rec = reinterpret_cast<float4*>(tris + i);
-        float4 t2 = rec[2];
-        const uint32_t id = __float_as_uint(t2.y), prim = __float_as_uint(t2.z);
-        if (id != kHoleInstance) {
-            const RefitInstance I = inst[id];
-            float w[3][3];
-            if (I.dirty) {
-                const float* M = I.m;
-                for (int k = 0; k < 3; ++k) {
-                    const uint32_t idx = indices[static_cast<size_t>(I.first_index) + 3u * prim + k];
-                    const float* P = positions + (static_cast<uint64_t>(static_cast<int64_t>(I.first_vertex)) + idx) * 3u;
-                    // ark_ddgi_set_scene's expression, left to right, no contraction
-                    w[k][0] = M[0] * P[0] + M[1] * P[1] + M[2] * P[2] + M[3];
-                    w[k][1] = M[4] * P[0] + M[5] * P[1] + M[6] * P[2] + M[7];
-                    w[k][2] = M[8] * P[0] + M[9] * P[1] + M[10] * P[2] + M[11];
-                }
-                // make_gpu_triangle: e1 = v1 - v0, e2 = v2 - v0
-                const float e1x = w[1][0] - w[0][0], e1y = w[1][1] - w[0][1], e1z = w[1][2] - w[0][2];
-                const float e2x = w[2][0] - w[0][0], e2y = w[2][1] - w[0][1], e2z = w[2][2] - w[0][2];
-                rec[0] = make_float4(w[0][0], w[0][1], w[0][2], e1x);
-                rec[1] = make_float4(e1y, e1z, e2x, e2y);
-                t2.x = e2z;
-                t2.w = __uint_as_float(I.flip);
-                rec[2] = t2;
+    if (i >= count) return;
+    const uint32_t n = order[i];
+    const GpuBvh8Node& nd = nodes[n];
+    uint64_t m = 0;
+    for (int s = 0; s < 8; ++s) {
+        if ((nd.imask >> s) & 1u) {
+            m |= masks[nd.child_base + static_cast<uint32_t>(__builtin_popcount(nd.imask & ((1u << s) - 1u)))];
+        } else if ((nd.leaf_mask >> s) & 1u) {
+            for (uint32_t k = 0; k < static_cast<uint32_t>(kBvh8MaxLeafSize); ++k) {
+                const uint32_t pos = s + nd.tri_stride * k;
+                if (pos >= 24u || !((nd.leaf_tris >> pos) & 1u)) break;
+                const uint32_t id = __float_as_uint(reinterpret_cast<const float4*>(tris + nd.tri_base + pos)[2].y);
+                m |= 1ull << (id & 63u);
             }
         }
     }
+    masks[n] = m;
 }
 
 // The light coordinates of a record's three vertices as build_sun_bvh computes them
@@ -132,14 +147,23 @@ __device__ __forceinline__ void quantGrid(float L, float H, int& e, double& p)
 // reduction over the eight lanes, the node's grid (every lane alike), then the slot's
 // outward-rounded planes. (One thread per node walked the eight slots and up to 24
 // triangle records in a row: C4 refits took 4.0 ms, profiles/r06_f_refit_continuous_bg.log.)
-__global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ nodes, const GpuTriangle* __restrict__ tris, float* __restrict__ boxes,
-                                                     const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra)
+__global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ nodes, GpuTriangle* __restrict__ tris, float* __restrict__ boxes,
+                                                     const uint32_t* __restrict__ order, uint32_t count, RefitBoxArgs ra, const uint64_t* __restrict__ masks,
+                                                     const RefitInstance* __restrict__ inst, const uint32_t* __restrict__ indices,
+                                                     const float* __restrict__ positions)
 {
+    // the refit runs beside the frame in flight's persistent kernels (the refit stream):
+    // its few waves take the SIMDs' issue slots first, so that its chain of per-level
+    // launches, which the next frame's traversal waits for, is not starved
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t i = t >> 3, s = t & 7u;
-    const bool live = i < count; // a node's eight lanes are live or not together (count nodes = 8 count lanes)
+    const uint32_t n0 = i < count ? order[i] : 0u;
+    // a node none of whose instances moved keeps its planes and its box (boxes[]) from
+    // the last refit that reached it (the same transforms and inflation: RefitBoxArgs.dirty)
+    const bool live = i < count && (masks[n0] & ra.dirty) != 0; // a node's eight lanes alike
     if (!__any(live)) return;
-    const uint32_t n = live ? order[i] : 0u;
+    const uint32_t n = live ? n0 : 0u;
     const float inflateAbs = ra.inflate;
     const uint4 hdr = live ? reinterpret_cast<const uint4*>(nodes + n)[1] : make_uint4(0u, 0u, 0u, 0u); // child_base, tri_base, leaf_tris, stride | leaf_mask << 8
     const uint32_t imask = live ? (reinterpret_cast<const uint32_t*>(nodes + n)[3] >> 24) : 0u;
@@ -159,8 +183,11 @@ __global__ void __launch_bounds__(128) k_refit_nodes(GpuBvh8Node* __restrict__ n
         for (uint32_t k = 0; k < static_cast<uint32_t>(kBvh8MaxLeafSize); ++k) {
             const uint32_t pos = s + stride * k;
             if (pos >= 24u || !((leafTris >> pos) & 1u)) break;
-            const float4* rec = reinterpret_cast<const float4*>(tris + triBase + pos);
-            const float4 a = rec[0], b = rec[1], c = rec[2];
+            float4* rec = reinterpret_cast<float4*>(tris + triBase + pos);
+            float4 a = rec[0], b = rec[1], c = rec[2];
+            // the record of a moved instance re-transformed here (each record is in one leaf slot)
+            const RefitInstance& I = inst[__float_as_uint(c.y)];
+            if (I.dirty) refitRecord(rec, a, b, c, I, __float_as_uint(c.z), indices, positions);
             if (ra.light) {
                 // the light coordinates build_sun_bvh boxed
                 float L[3][3], m;
@@ -241,19 +268,20 @@ hipError_t launch_store_lights(const LightBlock& b, GpuSpotLight* dst, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_refit_tris(GpuTriangle* tris, uint32_t count, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s)
+hipError_t launch_node_masks(const GpuBvh8Node* nodes, const GpuTriangle* tris, uint64_t* masks, const uint32_t* order, uint32_t count, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::k_refit_tris, dim3((count + 255u) / 256u), dim3(256), 0, s, tris, count, inst, indices, positions);
+    hipLaunchKernelGGL(dev::k_node_masks, dim3((count + 255u) / 256u), dim3(256), 0, s, nodes, tris, masks, order, count);
     return hipGetLastError();
 }
 
-hipError_t launch_refit_nodes(GpuBvh8Node* nodes, const GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
-                              hipStream_t s)
+hipError_t launch_refit_nodes(GpuBvh8Node* nodes, GpuTriangle* tris, float* boxes, const uint32_t* order, uint32_t count, const RefitBoxArgs& a,
+                              const uint64_t* masks, const RefitInstance* inst, const uint32_t* indices, const float* positions, hipStream_t s)
 {
     if (count == 0) return hipSuccess;
     const uint64_t lanes = 8ull * count; // eight lanes per node
-    hipLaunchKernelGGL(dev::k_refit_nodes, dim3(static_cast<uint32_t>((lanes + 127u) / 128u)), dim3(128), 0, s, nodes, tris, boxes, order, count, a);
+    hipLaunchKernelGGL(dev::k_refit_nodes, dim3(static_cast<uint32_t>((lanes + 127u) / 128u)), dim3(128), 0, s, nodes, tris, boxes, order, count, a, masks, inst, indices,
+                       positions);
     return hipGetLastError();
 }
 

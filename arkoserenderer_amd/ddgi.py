@@ -345,6 +345,13 @@ class DDGIContext:
         self.check(self.lib.ark_ddgi_get_bvh_stats(self.h, C.byref(s)), "ark_ddgi_get_bvh_stats")
         return s
 
+    def scene_digest(self) -> tuple:
+        """ark_ddgi_debug_scene_digest: digests of the world BVH nodes, world records, sun
+        BVH nodes, sun records the kernels read now (tests of the refit)."""
+        out = (C.c_uint64 * 4)()
+        self.check(self.lib.ark_ddgi_debug_scene_digest(self.h, out), "ark_ddgi_debug_scene_digest")
+        return tuple(int(v) for v in out)
+
 
 def frame_params(config: DDGIConfig, grid: ProbeGrid, app: AppState, first_probe_index: int,
                  light_pre_exposure: float = 1.0, ambient_illuminance: float = 0.0,

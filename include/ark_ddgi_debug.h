@@ -71,6 +71,13 @@ int ark_ddgi_debug_sun_bvh_check(const float* triangles, uint64_t n, const float
  * is chosen, samples}. No GPU. */
 int ark_ddgi_debug_sun_choice(const float* triangles, uint64_t n, const float* sun_dir, uint32_t n_samples, double* out);
 
+/* FNV-1a 64 digests of the geometry the context's kernels read now (the front copy,
+ * after everything it enqueued): out[4] = {world BVH8 nodes, world triangle records,
+ * light-space sun BVH8 nodes, its records} (the sun's 0 without one). For the refit
+ * tests: refits that reach only the nodes of moved instances leave the same bytes as
+ * one that reaches every node. Synchronous. */
+int ark_ddgi_debug_scene_digest(struct ArkDdgiCtx* ctx, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

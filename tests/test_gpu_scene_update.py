@@ -398,6 +398,89 @@ def test_continuous_motion_installs_rebuilds():
         orc.close()
 
 
+def test_partial_refits_equal_full_refit():
+    """Refits reach only the nodes with a moved instance below them (node instance masks,
+    the back copy brought from its own transforms): after a sequence of moves - one
+    instance, then another, one back, a mirrored one, and a pause - the geometry the
+    kernels read (world and light-space BVH nodes and records) is byte-identical to a
+    context that refits every node once to the final transforms (no background rebuilds:
+    the topology stays)."""
+    sc = S.soup(64_000, extent=7.0)
+    grid = D.ProbeGrid((4, 4, 4), (2.0, 2.0, 2.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=32, probe_updates_per_frame=64, max_rays_per_probe=32, max_probe_updates=64,
+                       sun_bvh=abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE, background_rebuild=False)
+    a = D.DDGIContext(grid, 10000.0, cfg)
+    a.set_scene(sc)
+    inst = sc.instances.copy()
+    M = inst["object_to_world"].reshape(-1, 3, 4)
+    p = D.frame_params(cfg, grid, D.AppState(0), 0, light_pre_exposure=1.0, environment_brightness=1.0)
+    moves = [(3, 0.1), (5, -0.2), (3, -0.1), (7, 0.05), (None, 0.0), (5, 0.3), (9, 0.0)]
+    for f, (i, dx) in enumerate(moves):
+        if i == 9:
+            M[i, :, 0] *= -1.0  # mirrored
+        elif i is not None:
+            M[i, 1, 3] += np.float32(dx)
+        inst["object_to_world"] = M.reshape(-1, 12)
+        a.set_instances(inst)
+        a.update(p)
+    a.synchronize()
+    b = D.DDGIContext(grid, 10000.0, cfg)
+    b.set_scene(sc)
+    b.set_instances(inst)
+    b.synchronize()
+    da, db = a.scene_digest(), b.scene_digest()
+    assert da[2] != 0, "no light-space sun BVH"
+    assert da == db, (da, db)
+    a.close()
+    b.close()
+
+
+def test_motion_frames_in_flight_unsynchronized():
+    """Refits overlapping the frames in flight (the double-buffered geometry of
+    ark_ddgi_set_instances_async): 48 frames, each moving instances and updating on one
+    stream with no host wait in between - frame n's refit writes the back copy while
+    frame n - 1 still traces and shades the front one, and background rebuilds install
+    on the way - then the atlases and offsets against the oracle fed the same sequence.
+    Any frame that read a half-refitted copy, or a refit that overwrote geometry a frame
+    still read, shows in the final atlases (each frame blends into them)."""
+    import torch
+
+    sc = S.soup(64_000, extent=7.0)
+    grid = D.ProbeGrid((8, 8, 8), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    cfg = D.DDGIConfig(rays_per_probe=64, probe_updates_per_frame=300, compute_probe_offsets=True,
+                       max_rays_per_probe=64, max_probe_updates=300, sun_bvh=abi.ARK_DDGI_SUN_BVH_LIGHT_SPACE)
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
+    ctx.set_scene(sc)
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(sc)
+    stream = torch.cuda.Stream()
+    exposure = dict(light_pre_exposure=1.0, environment_brightness=1.0)
+    inst0 = sc.instances.copy()
+    first = 0
+    try:
+        for f in range(48):
+            inst = inst0.copy()
+            M = inst["object_to_world"].reshape(-1, 3, 4).copy()
+            M[f % len(inst), :, 3] += np.float32(0.05 * ((f % 5) + 1))
+            M[2, :, :3] = _rot_y(0.03 * f) @ M[2, :, :3]
+            inst["object_to_world"] = M.reshape(len(inst), 12)
+            ctx.set_instances_async(inst, stream.cuda_stream)
+            orc.set_instances(inst)
+            p = D.frame_params(cfg, grid, D.AppState(f), first, **exposure)
+            ctx.update(p, stream.cuda_stream)
+            orc.update(p)
+            first = (first + p.probe_updates) % grid.probe_count()
+        stream.synchronize()
+        ctx.synchronize()
+        _compare(ctx, orc, 47, "48 frames in flight with a refit each")
+        st = ctx.bvh_stats()
+        assert st.refit_version == 48
+        print(f"frames in flight: world rebuilds {st.bvh_rebuilds}, sun rebuilds {st.sun_rebuilds}")
+    finally:
+        ctx.close()
+        orc.close()
+
+
 def _install_sun_on_a(a, b, sc, grid, cfg, exposure, sun):
     """Two contexts share a scene; A asks twice for a new sun (a stable request starts
     the background rebuild) and updates until it installs the light-space BVH; B has
