@@ -28,6 +28,12 @@ whole-update figures (roofline()).
 when fewer than N GPUs are visible. `--dry-run` prints that decision without any
 GPU call.
 
+ARK_BENCH_REHEARSAL=1 (test infrastructure, never a measurement): the N > 1 frame loop
+on ONE GPU - every rank on cuda:0, a gloo process group, the atlas all-gather staged
+through host memory - so that the Z-slab ranks' code path (rendezvous, slab contexts,
+overlapped exchange, barrier and max-over-ranks timing) runs on a one-GPU box; RCCL
+itself refuses two ranks on one device.
+
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -150,11 +156,15 @@ def main(argv=None):
 
     world = int(env.get("WORLD_SIZE", "1"))
     rank = int(env.get("RANK", "0"))
-    local_rank = int(env.get("LOCAL_RANK", "0"))
+    rehearsal = env.get("ARK_BENCH_REHEARSAL") == "1"
+    local_rank = 0 if rehearsal else int(env.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from arkoserenderer_amd import abi
     from arkoserenderer_amd import ddgi as D
@@ -187,7 +197,11 @@ def main(argv=None):
         # the two bands as one RCCL group on the exchange stream itself (RcclBandExchange);
         # ARK_BENCH_TORCH_PG=1: through torch's process group instead
         band = None
-        if os.environ.get("ARK_BENCH_TORCH_PG") != "1":
+        if rehearsal:
+            band = SlabExchange.from_views(ctx.device_views(), rank, world, device)
+            band.exchange = _host_staged(band)
+            gather = _host_gather
+        elif os.environ.get("ARK_BENCH_TORCH_PG") != "1":
             try:
                 band = RcclBandExchange.from_views(ctx.device_views(), rank, world, device)
             except (RuntimeError, OSError, AttributeError) as e:  # no direct RCCL: the process group's all-gather
@@ -195,7 +209,7 @@ def main(argv=None):
         if band is None:
             band = SlabExchange.from_views(ctx.device_views(), rank, world, device)
             gather = torch_all_gather()
-        else:
+        elif not rehearsal:
             gather = band.all_gather
         # K < N: only the window's tiles travel (WindowExchange); K = N: the row bands
         window = WindowExchange(WindowSource(ctx), band.exchange, gather, rank, world, min(K, N // world), device)
@@ -325,6 +339,26 @@ def main(argv=None):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _host_gather(out, mine):
+    """ARK_BENCH_REHEARSAL: the all-gather through host memory over gloo (in order on the
+    current stream: the copies synchronise it)."""
+    import torch.distributed as dist
+
+    parts = list(out.cpu().chunk(dist.get_world_size()))
+    dist.all_gather(parts, mine.cpu())
+    out.copy_(__import__("torch").cat(parts).to(out.device))
+
+
+def _host_staged(band):
+    """ARK_BENCH_REHEARSAL: SlabExchange's band all-gathers through host memory."""
+
+    def exchange():
+        for full, mine in band.bufs:
+            _host_gather(full, mine)
+
+    return exchange
 
 
 def library_sha16() -> str:
