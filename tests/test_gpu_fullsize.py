@@ -107,6 +107,37 @@ def test_c4_full_size_probe_subset():
     assert n == 2 * 256
 
 
+def test_c4_full_size_every_probe():
+    """C4 exactly as bench.py runs it - 10 M triangles, 32^3 probes x 256 rays, the whole
+    grid in one window (K = N), sun, offsets on - against the oracle on EVERY probe, two
+    frames (frame 1's indirect term reads frame 0's full atlases): whole irradiance and
+    visibility atlases and offsets bit for bit (16 host threads: about 15 s per oracle
+    frame). The subset test above runs the same comparison on 256 probes."""
+    scene = S.soup(10_000_000)
+    dims = (32, 32, 32)
+    grid = D.ProbeGrid(dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    N = grid.probe_count()
+    cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=N, max_rays_per_probe=256, max_probe_updates=N, compute_probe_offsets=True)
+    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    ctx = D.DDGIContext(grid, 10000.0, cfg)
+    ctx.set_scene(scene)
+    orc = O.Oracle(ctx.desc)
+    orc.set_scene(scene, threads=16)
+    try:
+        for frame in range(2):
+            p = D.frame_params(cfg, grid, D.AppState(frame), 0, **exposure)
+            ctx.update(p)
+            orc.update(p, threads=16)
+            ctx.synchronize()
+            for w in (abi.ARK_DDGI_ATLAS_IRRADIANCE, abi.ARK_DDGI_ATLAS_VISIBILITY, abi.ARK_DDGI_PROBE_OFFSETS):
+                g, o = np.ascontiguousarray(ctx.read(w)).reshape(-1).view(np.uint8), np.ascontiguousarray(orc.read(w)).reshape(-1).view(np.uint8)
+                assert g.size == o.size and np.array_equal(g, o), f"frame {frame} resource {w}: {int(np.count_nonzero(g != o)) if g.size == o.size else 'size'} bytes differ"
+            assert np.count_nonzero(ctx.read(abi.ARK_DDGI_ATLAS_IRRADIANCE)) > 0
+    finally:
+        ctx.close()
+        orc.close()
+
+
 def test_c3_substitute_full_grid_probe_subset():
     """C3 substitute at its full 24x12x24 grid x 256 rays with the sun and 3 IES spot
     lights (4 shadow rays per lit hit), offsets on; 8 windows of 24 probes."""
