@@ -107,18 +107,24 @@ def test_c4_full_size_probe_subset():
     assert n == 2 * 256
 
 
-def test_c4_full_size_every_probe():
+@pytest.mark.parametrize("config", ["c4", "c3"])
+def test_full_size_every_probe(config):
     """C4 exactly as bench.py runs it - 10 M triangles, 32^3 probes x 256 rays, the whole
-    grid in one window (K = N), sun, offsets on - against the oracle on EVERY probe, two
+    grid in one window (K = N), sun, offsets on - and the C3 substitute as its config line
+    runs it (24x12x24 x 256, sun + 3 IES spots), against the oracle on EVERY probe, two
     frames (frame 1's indirect term reads frame 0's full atlases): whole irradiance and
-    visibility atlases and offsets bit for bit (16 host threads: about 15 s per oracle
-    frame). The subset test above runs the same comparison on 256 probes."""
-    scene = S.soup(10_000_000)
-    dims = (32, 32, 32)
-    grid = D.ProbeGrid(dims, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+    visibility atlases and offsets bit for bit (16 host threads: about 15 s per C4
+    oracle frame). The subset tests run the same comparison on a few hundred probes."""
+    if config == "c4":
+        scene = S.soup(10_000_000)
+        grid = D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+        exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    else:
+        scene = S.sponza_substitute()
+        grid = D.ProbeGrid(*S.sponza_substitute_grid())
+        exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
     N = grid.probe_count()
     cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=N, max_rays_per_probe=256, max_probe_updates=N, compute_probe_offsets=True)
-    exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
     ctx = D.DDGIContext(grid, 10000.0, cfg)
     ctx.set_scene(scene)
     orc = O.Oracle(ctx.desc)

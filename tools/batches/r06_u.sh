@@ -1,4 +1,4 @@
-# C4 full size, every probe, two frames, against the oracle
+# C4 and the C3 substitute at full size, every probe, two frames, against the oracle
 set -o pipefail
 OUT=gpurun_out/r06_u
 mkdir -p $OUT
