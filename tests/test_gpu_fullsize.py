@@ -107,25 +107,37 @@ def test_c4_full_size_probe_subset():
     assert n == 2 * 256
 
 
-@pytest.mark.parametrize("config", ["c4", "c3"])
+@pytest.mark.parametrize("config", ["c4", "c3", "c5"])
 def test_full_size_every_probe(config):
     """C4 exactly as bench.py runs it - 10 M triangles, 32^3 probes x 256 rays, the whole
     grid in one window (K = N), sun, offsets on - and the C3 substitute as its config line
     runs it (24x12x24 x 256, sun + 3 IES spots), against the oracle on EVERY probe, two
     frames (frame 1's indirect term reads frame 0's full atlases): whole irradiance and
     visibility atlases and offsets bit for bit (16 host threads: about 15 s per C4
-    oracle frame). The subset tests run the same comparison on a few hundred probes."""
+    oracle frame). The subset tests run the same comparison on a few hundred probes.
+    c5 (the city block, 48x16x48 x 512, sun + 4 IES spots: several minutes of oracle
+    work) runs only with ARK_SLOW_TESTS=1."""
+    import os
+
+    if config == "c5" and os.environ.get("ARK_SLOW_TESTS") != "1":
+        pytest.skip("C5 every probe: ARK_SLOW_TESTS=1")
     if config == "c4":
         scene = S.soup(10_000_000)
         grid = D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
         exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
-    else:
+    elif config == "c3":
         scene = S.sponza_substitute()
         grid = D.ProbeGrid(*S.sponza_substitute_grid())
         exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
+    else:
+        scene = S.city_block()
+        grid = D.ProbeGrid((48, 16, 48), (5.0, 2.5, 5.0), (2.5, 0.5, 2.5))
+        exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
     N = grid.probe_count()
-    cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=N, max_rays_per_probe=256, max_probe_updates=N, compute_probe_offsets=True)
-    ctx = D.DDGIContext(grid, 10000.0, cfg)
+    R = 512 if config == "c5" else 256
+    z_far = 1000.0 if config == "c5" else 10000.0
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, max_rays_per_probe=R, max_probe_updates=N, compute_probe_offsets=True)
+    ctx = D.DDGIContext(grid, z_far, cfg)
     ctx.set_scene(scene)
     orc = O.Oracle(ctx.desc)
     orc.set_scene(scene, threads=16)
