@@ -211,23 +211,29 @@ def test_c4_full_size_vs_libm_oracle(variant):
                        dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), _windows(dims, 8), variant)
 
 
+@pytest.mark.parametrize("config", ["c4", "c5"])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_c4_whole_grid_vs_libm_oracle(variant):
-    """C4 on EVERY probe (the whole 32^3 x 256 window, 8.4 M rays a frame), frames 0 and
-    1, against each witness oracle: the subset above, all probes. About a minute of
-    oracle work per variant: runs with ARK_SLOW_TESTS=1."""
+def test_whole_grid_vs_libm_oracle(variant, config):
+    """C4 (the whole 32^3 x 256 window, 8.4 M rays a frame) and the C5 substitute (48x16x48
+    x 512, sun + 4 IES spots, 18.9 M rays) on EVERY probe, frames 0 and 1, against each
+    witness oracle: the subsets above, all probes. About a minute of oracle work per
+    case: runs with ARK_SLOW_TESTS=1."""
     import os
 
     if os.environ.get("ARK_SLOW_TESTS") != "1":
-        pytest.skip("C4 whole grid against the witnesses: ARK_SLOW_TESTS=1")
-    grid = D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0))
+        pytest.skip("whole grids against the witnesses: ARK_SLOW_TESTS=1")
+    if config == "c4":
+        sc, grid, R, z_far = S.soup(10_000_000), D.ProbeGrid((32, 32, 32), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0)), 256, 10000.0
+        exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0)
+    else:
+        sc, grid, R, z_far = S.city_block(), D.ProbeGrid((48, 16, 48), (5.0, 2.5, 5.0), (2.5, 0.5, 2.5)), 512, 1000.0
+        exposure = dict(light_pre_exposure=1.0, ambient_illuminance=0.02, environment_brightness=1.0)
     N = grid.probe_count()
-    cfg = D.DDGIConfig(rays_per_probe=256, probe_updates_per_frame=N, compute_probe_offsets=True, max_rays_per_probe=256, max_probe_updates=N)
+    cfg = D.DDGIConfig(rays_per_probe=R, probe_updates_per_frame=N, compute_probe_offsets=True, max_rays_per_probe=R, max_probe_updates=N)
     # SURVEY §8(d)'s atlas tolerances and the flip fraction asserted; the largest
-    # unflipped surfel difference reported (11 fp16 ulp once, nocontract frame 1:
+    # unflipped surfel difference reported (11 fp16 ulp once at C4, nocontract frame 1:
     # profiles/r06_za_c4_whole_grid_witness.log), not held to the windows' 8
-    _whole_grid("C4-whole", S.soup(10_000_000), grid, cfg, 2, 10000.0,
-                dict(light_pre_exposure=1.0, ambient_illuminance=0.0, environment_brightness=1.0), variant, surfel_ulp=None)
+    _whole_grid(f"{config.upper()}-whole", sc, grid, cfg, 2, z_far, exposure, variant, surfel_ulp=None)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
