@@ -473,7 +473,6 @@ struct ArkDdgiCtx {
     // operation, which follows the others); evInstalled with the last install (a rebuild
     // installed on a caller's stream writes the front copy)
     hipStream_t refitStream = nullptr;
-    hipStream_t markStream = nullptr; // records "after everything so far" (evFree, retirements)
     hipEvent_t evFree[3] = {};
     bool freeValid[3] = { false, false, false };
     hipEvent_t evInstalled = nullptr;
@@ -1568,7 +1567,6 @@ int ark_ddgi_create(const ArkDdgiDesc* desc, ArkDdgiCtx** outCtx)
         if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return bad(e, "hipDeviceGetStreamPriorityRange");
         if ((e = hipStreamCreateWithPriority(&ctx->refitStream, hipStreamNonBlocking, hi)) != hipSuccess) return bad(e, "hipStreamCreateWithPriority");
     }
-    if ((e = hipStreamCreateWithFlags(&ctx->markStream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     for (auto& ev : ctx->evFrameDone)
         if ((e = hipEventCreateWithFlags(&ev, syncFlags)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto& ev : ctx->ev)
@@ -1646,7 +1644,6 @@ void ark_ddgi_destroy(ArkDdgiCtx* ctx)
     for (auto& ev : ctx->evFree)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->refitStream) (void)hipStreamDestroy(ctx->refitStream);
-    if (ctx->markStream) (void)hipStreamDestroy(ctx->markStream);
     for (auto& ev : ctx->evFrameDone)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->traceStream) (void)hipStreamDestroy(ctx->traceStream);
@@ -2165,11 +2162,13 @@ int ark_ddgi_set_instances_async(ArkDdgiCtx* ctx, const ArkRTInstance* instances
     int rc;
     if (st.levelOffsets.empty() && (rc = prepareRefit(ctx, st)) != 0) return rc;
     // everything this context enqueued so far ends with its last operation (orderBegin
-    // chains the others into it; evOrder): the front copy's readers among them. Events
-    // that mark that point are recorded on the context's own mark stream behind evOrder,
-    // not on the last operation's stream, which the caller may have destroyed since.
-    const hipStream_t last = ctx->markStream;
-    if (ctx->orderValid) ARK_HIP(hipStreamWaitEvent(last, ctx->evOrder, 0));
+    // chains the others into it): the front copy's readers among them. Events that mark
+    // that point are recorded on `s` behind it (orderBegin) - not on the last operation's
+    // stream, which the caller may have destroyed since, nor on a stream of the
+    // context's own (one more stream on the process's few hardware queues; measured no
+    // better under motion, profiles/r06_ab2_refit_ordering/)
+    ARK_HIP(orderBegin(ctx, s));
+    const hipStream_t last = s;
     // a light-space sun BVH without a refit order (none recorded) cannot follow: dropped
     if (st.sunArgs.sun_root >= 0 && st.sunLevelOffsets.empty()) {
         st.sunArgs.sun_root = -1;
